@@ -1,0 +1,411 @@
+"""CPU ORACLE for the SPAI-via-GFlowNet hot path — TEST INFRASTRUCTURE ONLY.
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline``
+leg may import this module, and only as the checker / the timed CPU baseline.
+The product (``gflownet_spai_amd``) never imports it and has no CPU fallback.
+
+It is a plain restatement (numpy / scipy / torch-CPU) of the reference's
+algorithm for the hot path, each function citing the reference file:line it
+follows (reference = tonylizza/gflownet-spai @ 2024-10-24), plus the
+north-star extensions that have no reference counterpart (marked
+"PARITY UNPINNED BY THE REFERENCE": pinned instead by numpy ``lstsq`` /
+stacked Householder QR and by the reference's own ``calculate_residual`` via the
+symmetric-A identity ||AM-I|| = ||M^T A - I||).
+
+Pinning: ``tests/test_oracle_golden.py`` checks every function here against the
+golden vectors captured from the reference itself (``tests/golden/make_golden.py``).
+
+Contents
+  * pattern layout: raw COO -> action ids / lines      (preconditioner.py:12-25)
+  * reference-parity rollout (sequential, torch noise)  (gflownet/gflownet.py:125-197, log.py:24-121)
+  * throughput rollout (Gumbel-top-k, Philox4x32-10)   (distributional restatement of gflownet.py:148)
+  * copy fill + ||MA-I||_F                             (utils.py:295-356, 89-126; preconditioner.py:79-93)
+  * reward                                              (preconditioner.py:55-66, 68-77, 137-165)
+  * least-squares fill + ||AM-I||_F                    (north-star extension; parity unpinned by the reference)
+  * trajectory balance loss                             (gflownet/utils.py:228-278)
+"""
+from __future__ import annotations
+
+import numpy as np
+import scipy.sparse as sp
+import torch
+
+# --------------------------------------------------------------------------------------
+# Pattern / layout
+# --------------------------------------------------------------------------------------
+
+
+def lines_from_coo(rows, cols, vals, n, orient, width=None):
+    """Line-major ELL view of a raw COO matrix.
+
+    orient == "row": line i lists (col k, value, action id) of row i    (MA side, CSR)
+    orient == "col": line j lists (row r, value, action id) of column j (AM side, CSC)
+    The action id of an entry is its position in the raw COO order
+    (preconditioner.py:23-25: edge_index = matrix._indices()).
+    Entries inside a line are sorted by the other index.  Raises on duplicates.
+    """
+    rows = np.asarray(rows, np.int64)
+    cols = np.asarray(cols, np.int64)
+    vals = np.asarray(vals)
+    line, other = (rows, cols) if orient == "row" else (cols, rows)
+    order = np.lexsort((other, line))
+    ls, os_ = line[order], other[order]
+    if ls.size and np.any((ls[1:] == ls[:-1]) & (os_[1:] == os_[:-1])):
+        raise ValueError("duplicate (row, col) entries are not supported")
+    counts = np.bincount(ls, minlength=n)
+    w = int(counts.max()) if counts.size else 0
+    if width is None:
+        width = max(w, 1)
+    if w > width:
+        raise ValueError(f"line width {w} exceeds {width}")
+    start = np.concatenate([[0], np.cumsum(counts)[:-1]])
+    slot = np.arange(ls.size) - start[ls]
+    idx = np.full((n, width), -1, np.int32)
+    act = np.full((n, width), -1, np.int32)
+    val = np.zeros((n, width), vals.dtype)
+    idx[ls, slot] = os_
+    act[ls, slot] = order
+    val[ls, slot] = vals[order]
+    return idx, act, val
+
+
+def poisson2d(grid, dtype=np.float32):
+    t = sp.diags([-np.ones(grid - 1), 2 * np.ones(grid), -np.ones(grid - 1)], [-1, 0, 1])
+    i = sp.identity(grid)
+    a = (sp.kron(i, t) + sp.kron(t, i)).tocoo().astype(dtype)
+    order = np.lexsort((a.col, a.row))
+    return a.row[order].astype(np.int64), a.col[order].astype(np.int64), a.data[order], grid * grid
+
+
+def poisson3d(grid, dtype=np.float64):
+    t = sp.diags([-np.ones(grid - 1), 2 * np.ones(grid), -np.ones(grid - 1)], [-1, 0, 1])
+    i = sp.identity(grid)
+    a = (sp.kron(sp.kron(i, i), t) + sp.kron(sp.kron(i, t), i) + sp.kron(sp.kron(t, i), i)).tocoo().astype(dtype)
+    order = np.lexsort((a.col, a.row))
+    return a.row[order].astype(np.int64), a.col[order].astype(np.int64), a.data[order], grid ** 3
+
+
+# --------------------------------------------------------------------------------------
+# Reference-parity rollout (gflownet/gflownet.py:125-197 with the fixed-logit policy
+# contract of policy.py:63-73; log.py:24-89)
+# --------------------------------------------------------------------------------------
+
+
+def parity_rollout(logits, B, generator=None):
+    """Sequential rollout with exactly the reference's torch ops and noise stream.
+
+    Per step: each sample's probs = softmax(logits masked by its history)
+    (policy.py:65-73) -> stack [B,1,E+1] -> row renormalisation when B > 1
+    (gflownet.py:116-120) -> Categorical(probs).sample() (gflownet.py:148) which is
+    argmax(p / q), q ~ Exp(1) drawn B*(E+1) per step from the default generator.
+    Returns actions [T,B] int64 (-1 after done), fwd_probs [B,T] fp32 (1 after done).
+    """
+    logits = torch.as_tensor(logits, dtype=torch.float32).view(1, -1)
+    A1 = logits.shape[1]
+    E = A1 - 1
+    done = torch.zeros(B, dtype=torch.bool)
+    hist = []  # list of [B] int64 (log._actions)
+    fwd = []
+    while not bool(done.all()):
+        acts = torch.stack(hist, 1) if hist else torch.empty(B, 0, dtype=torch.long)
+        probs = []
+        for b in range(B):
+            x = logits
+            if acts.shape[1] > 0:
+                mask = torch.ones_like(x, dtype=torch.bool)
+                mask[:, acts[b]] = 0
+                x = x.masked_fill(~mask, float("-inf"))
+            probs.append(torch.softmax(x, dim=1))
+        probs_all = torch.stack(probs, 0)  # [B,1,E+1]
+        if B > 1:
+            s = probs_all.sum(2)
+            s[s == 0] = 1
+            probs_all = probs_all / s.unsqueeze(1)
+        # torch.distributions.Categorical(probs).sample() == multinomial(p/sum, 1, True)
+        p2 = probs_all.reshape(-1, A1)
+        p2 = p2 / p2.sum(-1, keepdim=True)
+        q = torch.empty_like(p2).exponential_(1, generator=generator)
+        a_all = torch.argmax(p2 / q, dim=-1).view(B, 1)
+        mask_active = ~done
+        fp = torch.ones(B)
+        gathered = probs_all.gather(2, a_all.unsqueeze(1)).view(B)
+        fp[mask_active] = gathered[mask_active]
+        fwd.append(fp)
+        la = -torch.ones(B, dtype=torch.long)
+        la[mask_active] = a_all.view(B)[mask_active]
+        hist.append(la)
+        term = (a_all.view(B) == E)
+        done[mask_active] = term[mask_active]
+    return torch.stack(hist, 0), torch.stack(fwd, 0).t().contiguous()
+
+
+# --------------------------------------------------------------------------------------
+# Throughput rollout: Gumbel-top-k with counter-based Philox4x32-10.
+# Distributionally identical to the sequential process of gflownet.py:148 (sampling
+# without replacement until the terminal id is drawn == Plackett-Luce order of
+# keys l_a + Gumbel_a; removed set = {a : key_a > key_E}); not pathwise identical.
+# Everything below is defined bit-for-bit so that the HIP kernels reproduce it.
+# --------------------------------------------------------------------------------------
+
+_PHILOX_M0, _PHILOX_M1 = np.uint64(0xD2511F53), np.uint64(0xCD9E8D57)
+_PHILOX_W0, _PHILOX_W1 = 0x9E3779B9, 0xBB67AE85
+_MASK32 = np.uint64(0xFFFFFFFF)
+
+
+def philox4x32_10(c0, c1, c2, c3, k0, k1):
+    """Random123 Philox4x32-10 on uint32 arrays (returned as uint64 arrays < 2^32)."""
+    c0, c1, c2, c3 = (np.asarray(x, np.uint64) & _MASK32 for x in (c0, c1, c2, c3))
+    k0, k1 = int(k0) & 0xFFFFFFFF, int(k1) & 0xFFFFFFFF
+    for r in range(10):
+        p0 = _PHILOX_M0 * c0
+        p1 = _PHILOX_M1 * c2
+        hi0, lo0 = p0 >> np.uint64(32), p0 & _MASK32
+        hi1, lo1 = p1 >> np.uint64(32), p1 & _MASK32
+        c0, c1, c2, c3 = hi1 ^ c1 ^ np.uint64(k0), lo1, hi0 ^ c3 ^ np.uint64(k1), lo0
+        k0 = (k0 + _PHILOX_W0) & 0xFFFFFFFF
+        k1 = (k1 + _PHILOX_W1) & 0xFFFFFFFF
+    return c0, c1, c2, c3
+
+
+_LOG_C = np.array([0x3f800000, 0xbefffffc, 0x3eaaabc8, 0xbe8002d3, 0x3e4c5c05,
+                   0xbe2994df, 0x3e191428, 0xbe13394f, 0x3db31375], np.uint32).view(np.float32)
+_LN2F = np.array([0x3f317218], np.uint32).view(np.float32)[0]
+
+
+def det_logf(x):
+    """Deterministic natural log of positive normal float32 values.
+
+    Exponent/mantissa split by bit operations, m in [sqrt(.5), sqrt(2)), t = m - 1
+    (exact), ln(1+t) = t * Q(t) with a degree-8 Q evaluated by Horner using only
+    separately rounded fp32 multiplies and adds (no FMA), then e*ln2 + that.
+    The HIP kernel (rollout.hip: det_logf) performs the identical op sequence.
+    """
+    x = np.asarray(x, np.float32)
+    bits = x.view(np.uint32)
+    e = (bits >> np.uint32(23)).astype(np.int32) - 127
+    mb = (bits & np.uint32(0x7FFFFF)) | np.uint32(0x3F800000)
+    big = mb > np.uint32(0x3FB504F3)
+    mb = np.where(big, mb - np.uint32(0x00800000), mb).astype(np.uint32)
+    e = e + big.astype(np.int32)
+    t = mb.view(np.float32) - np.float32(1.0)
+    p = np.full_like(t, _LOG_C[8])
+    for c in _LOG_C[7::-1]:
+        p = p * t
+        p = p + c
+    p = p * t
+    return e.astype(np.float32) * _LN2F + p
+
+
+def gumbel_keys(logits, b_global, seed, stream):
+    """key_a = l_a - ln(-ln u_a) in fp32 for a = 0..E (E = terminal).
+
+    Counter = (a >> 2, b_global, stream_lo, stream_hi), key = (seed_lo, seed_hi),
+    output word a & 3; u = (2*(w >> 9) + 1) * 2^-24 in (0, 1), exact in fp32.
+    """
+    logits = np.asarray(logits, np.float32)
+    a = np.arange(logits.size, dtype=np.uint64)
+    w = philox4x32_10(a >> np.uint64(2), np.full_like(a, b_global), np.full_like(a, stream & 0xFFFFFFFF),
+                      np.full_like(a, (stream >> 32) & 0xFFFFFFFF), seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF)
+    sel = (a & np.uint64(3)).astype(np.int64)
+    word = np.choose(sel, w).astype(np.uint64)
+    k = (word >> np.uint64(9)).astype(np.uint32)
+    u = (np.float32(2.0) * k.astype(np.float32) + np.float32(1.0)) * np.float32(2.0 ** -24)
+    q = -det_logf(u)
+    key = logits - det_logf(q)
+    return key + np.float32(0.0)  # -0 -> +0
+
+
+def throughput_rollout(logits, B, seed, stream, sample_base=0):
+    """Removed sets, ordered trajectories and forward probabilities for B samples.
+
+    Returns (removed [B,E] bool, actions [T,B] int64, fwd_probs [B,T] fp32, counts [B]).
+    Order: key descending, ties by action id ascending; trajectory = winners then E.
+    fwd_probs[t] = w_{a_t} / (Z - sum_{s<t} w_{a_s}) with w = exp(l - lmax) in fp64
+    (the probability the sequential reference assigns to that step, log.py:70).
+    """
+    logits = np.asarray(logits, np.float32)
+    E = logits.size - 1
+    lmax = np.float64(logits.max())
+    w = np.exp(logits.astype(np.float64) - lmax)
+    Z = w.sum()
+    removed = np.zeros((B, E), np.bool_)
+    orders, probs = [], []
+    for b in range(B):
+        key = gumbel_keys(logits, sample_base + b, seed, stream)
+        win = np.flatnonzero(key[:E] > key[E])
+        removed[b, win] = True
+        o = win[np.lexsort((win, -key[win]))]
+        ww = w[o]
+        pref = np.concatenate([[0.0], np.cumsum(ww)])
+        p = np.concatenate([ww / (Z - pref[:-1]), [w[E] / (Z - pref[-1])]])
+        orders.append(np.concatenate([o, [E]]))
+        probs.append(p)
+    counts = np.array([len(o) - 1 for o in orders])
+    T = int(counts.max()) + 1
+    actions = -np.ones((T, B), np.int64)
+    fwd = np.ones((B, T), np.float32)
+    for b in range(B):
+        actions[:len(orders[b]), b] = orders[b]
+        fwd[b, :len(probs[b])] = probs[b].astype(np.float32)
+    return removed, actions, fwd, counts
+
+
+def removal_from_actions(actions_bt, E):
+    """Removed-set bitmap from a [B,T] action list (preconditioner.py:37-43, utils.py:315-323)."""
+    a = np.asarray(actions_bt)
+    B = a.shape[0]
+    removed = np.zeros((B, E), np.bool_)
+    for b in range(B):
+        x = a[b]
+        x = x[(x >= 0) & (x < E)]
+        removed[b, x] = True
+    return removed
+
+
+# --------------------------------------------------------------------------------------
+# Copy fill + residual + reward (reference parity)
+# --------------------------------------------------------------------------------------
+
+
+def copy_fill_coo(rows, cols, vals, removed_b, n):
+    """M = initial matrix minus removed edges, values copied as fp32 (utils.py:331-353)."""
+    keep = ~np.asarray(removed_b, bool)
+    return rows[keep], cols[keep], np.asarray(vals)[keep].astype(np.float32)
+
+
+def residual_ma_torch(m_rows, m_cols, m_vals, a_rows, a_cols, a_vals, n):
+    """||M A - I||_F with the reference's torch ops (preconditioner.py:79-93)."""
+    M = torch.sparse_coo_tensor(torch.from_numpy(np.stack([m_rows, m_cols]).astype(np.int64)),
+                                torch.from_numpy(np.asarray(m_vals, np.float32)), (n, n)).coalesce()
+    A = torch.sparse_coo_tensor(torch.from_numpy(np.stack([a_rows, a_cols]).astype(np.int64)),
+                                torch.from_numpy(np.asarray(a_vals)), (n, n))
+    i = torch.arange(n)
+    eye = torch.sparse_coo_tensor(torch.stack([i, i]), torch.ones(n, dtype=torch.float64), (n, n))
+    return float(torch.norm(torch.mm(M, A) - eye))
+
+
+def residual_fro_fp64(X: sp.spmatrix, Y: sp.spmatrix):
+    """||X Y - I||_F with fp64 products and sums (scipy)."""
+    P = (X.astype(np.float64) @ Y.astype(np.float64)).tocsr()
+    P = P - sp.identity(P.shape[0], format="csr")
+    return float(np.sqrt((P.data.astype(np.float64) ** 2).sum()))
+
+
+def reward(residual, nnz_m, alpha, r0, f0, n):
+    """preconditioner.py:55-66 + 68-77 + 137-165, with alpha taken from the argument.
+
+    Mirrors torch's type promotion exactly: alpha is a 0-d fp32 tensor, the
+    residual ratio a 0-d fp64 tensor, the flop ratio a python float, so
+    (1 - alpha) * (1 - flop_ratio) is computed in fp32 and the sum in fp64.
+    """
+    alpha = torch.as_tensor(alpha, dtype=torch.float32)
+    res = torch.as_tensor(residual, dtype=torch.float64)
+    r0 = torch.as_tensor(r0, dtype=torch.float64)
+    rr = res / r0 if float(r0) != 0 else float("inf")
+    flops = int(nnz_m) * n * 2
+    cr = flops / f0 if f0 != 0 else float("inf")
+    perf = alpha * (1 - rr) + (1 - alpha) * (1 - cr)
+    return float(perf.to(torch.float64) * 1000)
+
+
+# --------------------------------------------------------------------------------------
+# Least-squares fill (north-star extension) — PARITY UNPINNED BY THE REFERENCE.
+# m_j = argmin || A[:, J_j] m - e_j ||_2, J_j = kept pattern rows of column j.
+# Oracle: stacked Householder QR in fp64 (numpy), cross-checked by lstsq.
+# --------------------------------------------------------------------------------------
+
+
+def lsq_fill(pat_idx, keep, a_idx, a_val, line_ids=None):
+    """Column-wise LS fill.  pat_idx [N,W] (rows of each column, -1 pad), keep [N,W] bool,
+    a_idx/a_val [N,WA]: column lines of A.  Returns m [len(line_ids), W] fp64 (0 where not kept).
+
+    Uses stacked dense Householder QR over the local row set I_j = union of rows of
+    A[:, J_j]; singular systems are not expected (A nonsingular => columns independent).
+    """
+    N, W = pat_idx.shape
+    WA = a_idx.shape[1]
+    if line_ids is None:
+        line_ids = np.arange(N)
+    line_ids = np.asarray(line_ids)
+    n = line_ids.size
+    J = np.where(keep[line_ids], pat_idx[line_ids], -1)  # [n, W]
+    Jc = np.where(J >= 0, J, 0)
+    rows = a_idx[Jc]  # [n, W, WA]
+    vals = a_val[Jc].astype(np.float64)
+    valid = (J[:, :, None] >= 0) & (rows >= 0)
+    rows = np.where(valid, rows, -1)
+    vals = np.where(valid, vals, 0.0)
+    flat = rows.reshape(n, W * WA)
+    srt = np.sort(np.where(flat >= 0, flat, np.iinfo(np.int32).max), axis=1)
+    first = np.ones_like(srt, bool)
+    first[:, 1:] = srt[:, 1:] != srt[:, :-1]
+    first &= srt != np.iinfo(np.int32).max
+    IMAX = max(int(first.sum(1).max()) if n else 1, 1)
+    uniq = np.full((n, IMAX), -1, np.int64)
+    pos = np.cumsum(first, 1) - 1
+    r_i, c_i = np.nonzero(first)
+    uniq[r_i, pos[r_i, c_i]] = srt[r_i, c_i]
+    # local row index of each (p, s) entry
+    dense = np.zeros((n, IMAX, W))
+    for p in range(W):
+        for s in range(WA):
+            r = rows[:, p, s]
+            ok = r >= 0
+            loc = np.argmax(uniq == r[:, None], axis=1)
+            dense[np.nonzero(ok)[0], loc[ok], p] += vals[ok, p, s]
+    rhs = (uniq == line_ids[:, None]).astype(np.float64)
+    # columns not kept are zero columns; replace by unit vectors on an extra row so QR
+    # stays nonsingular, and force their coefficients to 0 afterwards.
+    kept = J >= 0
+    ext = np.zeros((n, IMAX + W, W))
+    ext[:, :IMAX, :] = dense
+    ii = np.arange(W)
+    ext[:, IMAX + ii, ii] = np.where(kept, 0.0, 1.0)
+    rhs_ext = np.zeros((n, IMAX + W))
+    rhs_ext[:, :IMAX] = rhs
+    q, r = np.linalg.qr(ext)
+    qtb = np.einsum("nij,ni->nj", q, rhs_ext)
+    m = np.linalg.solve(r, qtb[..., None])[..., 0]
+    m = np.where(kept, m, 0.0)
+    return m
+
+
+def lsq_fill_lstsq(pat_idx, keep, A_csc: sp.csc_matrix, j):
+    """Per-column numpy lstsq cross-check of lsq_fill (small cases only)."""
+    J = pat_idx[j][keep[j] & (pat_idx[j] >= 0)]
+    if J.size == 0:
+        return np.zeros(0), J
+    sub = A_csc[:, J].toarray().astype(np.float64)
+    e = np.zeros(A_csc.shape[0])
+    e[j] = 1.0
+    m, *_ = np.linalg.lstsq(sub, e, rcond=None)
+    return m, J
+
+
+def m_to_csc(pat_idx, m, n, dtype=np.float32):
+    """Assemble M (column lines of values aligned with pat_idx) as a scipy CSC matrix."""
+    N, W = pat_idx.shape
+    cols = np.repeat(np.arange(N), W)
+    rows = pat_idx.reshape(-1)
+    v = np.asarray(m, dtype).reshape(-1)
+    ok = rows >= 0
+    return sp.csc_matrix((v[ok], (rows[ok], cols[ok])), shape=(n, n))
+
+
+# --------------------------------------------------------------------------------------
+# Trajectory balance loss (gflownet/utils.py:228-278)
+# --------------------------------------------------------------------------------------
+
+
+def trajectory_balance_loss(total_flow, rewards, fwd_probs, back_probs):
+    eps = 1e-9
+    total_flow = total_flow.to(fwd_probs.device).to(fwd_probs.dtype)
+    rewards = rewards.to(fwd_probs.device).to(fwd_probs.dtype)
+    back_probs = back_probs.to(fwd_probs.device).to(fwd_probs.dtype)
+    lf = torch.log(fwd_probs + eps).sum(dim=-1)
+    lb = torch.log(back_probs + eps).sum(dim=-1)
+    lf = lf - lf.max(dim=0, keepdim=True)[0]
+    lb = lb - lb.max(dim=0, keepdim=True)[0]
+    lhs = torch.log(total_flow + eps) + lf
+    rhs = torch.log(rewards + eps) + lb
+    return ((lhs - rhs) ** 2).mean()

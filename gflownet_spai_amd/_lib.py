@@ -1,0 +1,106 @@
+"""ctypes binding of libspai_hip.so (the C ABI declared in include/spai_hip.h).
+
+The shared library is built in-tree (``gflownet_spai_amd/libspai_hip.so``) by
+``__graft_entry__.build()`` / ``make -C gflownet_spai_amd/csrc``.  There is no
+CPU fallback: if the library is missing or no GPU is present, every compute entry
+point raises.  Status codes map to the exception types the reference raises
+(ValueError for bad input, ``gflownet/utils.py:100-121``; RuntimeError otherwise).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libspai_hip.so")
+
+SPAI_OK, SPAI_ERR_INVALID, SPAI_ERR_HIP, SPAI_ERR_UNSUPPORTED = 0, 1, 2, 3
+FILL_COPY, FILL_LSQ = 0, 1
+DTYPE_F32, DTYPE_F64 = 0, 1
+ABI_VERSION = 1
+
+_c_i32, _c_i64, _c_u64, _c_sz, _c_p = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_size_t, ctypes.c_void_p
+
+# name -> (restype, argtypes); mirrors include/spai_hip.h one-to-one.
+SIGNATURES = {
+    "spai_abi_version": (ctypes.c_int, []),
+    "spai_last_error": (ctypes.c_char_p, []),
+    "spai_logits_stats_workspace_bytes": (_c_sz, [_c_i32, _c_i32]),
+    "spai_logits_stats": (ctypes.c_int, [_c_p, _c_i64, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_sz, _c_p]),
+    "spai_parity_step_workspace_bytes": (_c_sz, [_c_i32, _c_i32]),
+    "spai_parity_step": (ctypes.c_int, [_c_p, _c_i64, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_i32, _c_p, _c_p,
+                                        _c_p, _c_p, _c_p, _c_sz, _c_p]),
+    "spai_rollout_workspace_bytes": (_c_sz, [_c_i32, _c_i32]),
+    "spai_rollout_select": (ctypes.c_int, [_c_p, _c_i64, _c_i32, _c_i32, _c_u64, _c_u64, _c_i32, _c_p, _c_i32,
+                                           _c_p, _c_p, _c_sz, _c_p]),
+    "spai_rollout_order": (ctypes.c_int, [_c_p, _c_i64, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_i64, _c_i32, _c_i64,
+                                          _c_p, _c_p, _c_p, _c_sz, _c_p]),
+    "spai_actions_to_removed": (ctypes.c_int, [_c_p, _c_i64, _c_i64, _c_i32, _c_i32, _c_i32, _c_p, _c_i32, _c_p,
+                                               _c_p]),
+    "spai_fill_workspace_bytes": (_c_sz, [_c_i32, _c_i32]),
+    "spai_fill_residual": (ctypes.c_int, [_c_i32, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_i32, _c_p, _c_p,
+                                          _c_i32, _c_i32, _c_p, _c_i32, _c_p, _c_i32, _c_p, _c_p, _c_sz, _c_p]),
+}
+
+_lib = None
+
+
+class SpaiUnavailable(RuntimeError):
+    """libspai_hip.so is missing or cannot run here (no GPU)."""
+
+
+def load():
+    """Load and type the library (no GPU needed just to load)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise SpaiUnavailable(f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'` "
+                              "or `make -C gflownet_spai_amd/csrc`")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.spai_abi_version() != ABI_VERSION:
+        raise SpaiUnavailable(f"libspai_hip ABI {lib.spai_abi_version()} != expected {ABI_VERSION}")
+    _lib = lib
+    return lib
+
+
+def require_device(t: torch.Tensor):
+    if not t.is_cuda:
+        raise SpaiUnavailable("gflownet_spai_amd runs on the MI355X only (tensor on %s); there is no CPU path" % t.device)
+
+
+def check(status: int, where: str):
+    if status == SPAI_OK:
+        return
+    msg = f"{where}: {load().spai_last_error().decode(errors='replace')}"
+    if status == SPAI_ERR_INVALID:
+        raise ValueError(msg)
+    if status == SPAI_ERR_UNSUPPORTED:
+        raise NotImplementedError(msg)
+    raise RuntimeError(msg)
+
+
+def ptr(t: torch.Tensor | None):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def stream_ptr(device=None):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+_ws_cache: dict = {}
+
+
+def workspace(nbytes: int, device, tag: str) -> torch.Tensor:
+    """Caller-owned workspace (a byte tensor from torch's caching allocator), reused per tag."""
+    key = (tag, str(device))
+    ws = _ws_cache.get(key)
+    if ws is None or ws.numel() < nbytes:
+        ws = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
+        _ws_cache[key] = ws
+    return ws

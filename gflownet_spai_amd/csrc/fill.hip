@@ -1,0 +1,259 @@
+// Fill + residual kernel for gfx950: builds M from the pattern and the per-sample removal
+// bitmaps (copy fill of gflownet/utils.py:331-353, or the north-star per-line least-squares
+// fill) and accumulates ||M A - I||_F^2 (row lines, preconditioner.py:79-93) or
+// ||A M - I||_F^2 (column lines) without materialising the product.
+//
+// Identity used (one line l of M with slots p -> other index k_p, values m_p):
+//     || sum_p m_p A_line(k_p) - e_l ||^2 = m^T G m - 2 c^T m + 1
+// with G_pq = <A_line(k_p), A_line(k_q)> and c_p = A_line(k_p)[l].  G and c depend only on
+// the pattern, so one thread per line computes them ONCE from the W x WA entries it
+// gathers and then loops over all B samples: per sample it reads W mask bits, solves the
+// masked W x W normal equations in fp64 (LSQ) or copies (COPY), stores m in the target
+// precision and evaluates the quadratic form on the STORED values.  HBM traffic per
+// launch is the pattern + A lines once and B x (mask bits + M values); the B-fold
+// re-reads of A that an SpGEMM per sample would make never happen.
+#include "spai_device.h"
+#include "spai_status.h"
+
+namespace spai {
+namespace {
+
+constexpr int kNT = 256;
+
+template <int W, int WA, typename TA, typename TM, bool LSQ>
+__global__ __launch_bounds__(kNT) void k_line(int32_t line_begin, int32_t line_end, int32_t wrt, int32_t wart,
+                                              const int32_t* __restrict__ pat_idx,
+                                              const int32_t* __restrict__ pat_act,
+                                              const float* __restrict__ pat_val, const int32_t* __restrict__ a_idx,
+                                              const TA* __restrict__ a_val, int32_t B,
+                                              const uint32_t* __restrict__ removed, int32_t words,
+                                              TM* __restrict__ m_out, double* __restrict__ partials) {
+  __shared__ double sred[kNT / 64];
+  const int j = line_begin + blockIdx.x * kNT + threadIdx.x;
+  const bool valid = j < line_end;
+  const int64_t nloc = line_end - line_begin;
+
+  int idx[W], act[W];
+  float val[W];
+#pragma unroll
+  for (int p = 0; p < W; ++p) {
+    idx[p] = -1;
+    act[p] = 0;
+    val[p] = 0.0f;
+    if (valid && p < wrt) {
+      const int64_t o = (int64_t)j * wrt + p;
+      idx[p] = pat_idx[o];
+      act[p] = pat_act[o];
+      val[p] = pat_val[o];
+    }
+  }
+
+  double G[W][W];
+  double c[W];
+  {
+    int ai[W][WA];
+    TA av[W][WA];
+#pragma unroll
+    for (int p = 0; p < W; ++p) {
+#pragma unroll
+      for (int q = 0; q < WA; ++q) {
+        ai[p][q] = -1;
+        av[p][q] = (TA)0;
+        if (idx[p] >= 0 && q < wart) {
+          const int64_t o = (int64_t)idx[p] * wart + q;
+          ai[p][q] = a_idx[o];
+          av[p][q] = a_val[o];
+        }
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < W; ++p) {
+      double cp = 0.0, gpp = 0.0;
+#pragma unroll
+      for (int s = 0; s < WA; ++s) {
+        const double v = (double)av[p][s];
+        gpp += v * v;
+        cp += (ai[p][s] == j) ? v : 0.0;
+      }
+      c[p] = cp;
+      G[p][p] = gpp;
+#pragma unroll
+      for (int q = p + 1; q < W; ++q) {
+        double g = 0.0;
+#pragma unroll
+        for (int s = 0; s < WA; ++s) {
+#pragma unroll
+          for (int t = 0; t < WA; ++t) {
+            g += (ai[p][s] >= 0 && ai[p][s] == ai[q][t]) ? (double)av[p][s] * (double)av[q][t] : 0.0;
+          }
+        }
+        G[p][q] = g;
+      }
+    }
+  }
+
+  for (int b = 0; b < B; ++b) {
+    const uint32_t* rb = removed + (int64_t)b * words;
+    bool keep[W];
+#pragma unroll
+    for (int p = 0; p < W; ++p) keep[p] = idx[p] >= 0 && !((rb[act[p] >> 5] >> (act[p] & 31)) & 1u);
+
+    double mr[W];
+    if constexpr (!LSQ) {
+#pragma unroll
+      for (int p = 0; p < W; ++p) mr[p] = keep[p] ? (double)val[p] : 0.0;
+    } else {
+      // masked LDL^T of the normal equations: removed slots become identity rows, rhs 0
+      double L[W][W], D[W], iD[W], y[W];
+#pragma unroll
+      for (int k = 0; k < W; ++k) {
+        double dk = keep[k] ? G[k][k] : 1.0;
+        const double ref = dk;
+#pragma unroll
+        for (int s = 0; s < k; ++s) dk -= L[k][s] * L[k][s] * D[s];
+        D[k] = dk;
+        iD[k] = (dk > 1e-13 * ref) ? 1.0 / dk : 0.0;
+#pragma unroll
+        for (int i = k + 1; i < W; ++i) {
+          double v = (keep[k] && keep[i]) ? G[k][i] : 0.0;
+#pragma unroll
+          for (int s = 0; s < k; ++s) v -= L[i][s] * L[k][s] * D[s];
+          L[i][k] = v * iD[k];
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < W; ++k) {
+        double v = keep[k] ? c[k] : 0.0;
+#pragma unroll
+        for (int s = 0; s < k; ++s) v -= L[k][s] * y[s];
+        y[k] = v;
+      }
+#pragma unroll
+      for (int k = W - 1; k >= 0; --k) {
+        double v = y[k] * iD[k];
+#pragma unroll
+        for (int s = k + 1; s < W; ++s) v -= L[s][k] * mr[s];
+        mr[k] = v;
+      }
+#pragma unroll
+      for (int p = 0; p < W; ++p) mr[p] = keep[p] ? (double)(TM)mr[p] : 0.0;  // stored precision
+    }
+
+    if (m_out != nullptr && valid) {
+      TM* dst = m_out + ((int64_t)b * nloc + (j - line_begin)) * wrt;
+#pragma unroll
+      for (int p = 0; p < W; ++p)
+        if (p < wrt) dst[p] = (TM)mr[p];
+    }
+
+    double r2 = 0.0;
+    if (valid) {
+      r2 = 1.0;
+#pragma unroll
+      for (int p = 0; p < W; ++p) {
+        double acc = mr[p] * G[p][p] - 2.0 * c[p];
+#pragma unroll
+        for (int q = p + 1; q < W; ++q) acc += 2.0 * mr[q] * G[p][q];
+        r2 += mr[p] * acc;
+      }
+    }
+    r2 = block_sum<kNT>(r2, sred);
+    if (threadIdx.x == 0) partials[(int64_t)b * gridDim.x + blockIdx.x] = r2;
+  }
+}
+
+__global__ __launch_bounds__(kNT) void k_reduce(const double* __restrict__ partials, int32_t nparts,
+                                                double* __restrict__ out) {
+  __shared__ double sred[kNT / 64];
+  const int b = blockIdx.x;
+  double s = 0.0;
+  for (int i = threadIdx.x; i < nparts; i += kNT) s += partials[(int64_t)b * nparts + i];
+  s = block_sum<kNT>(s, sred);
+  if (threadIdx.x == 0) out[b] = s;
+}
+
+template <int W, int WA, typename TA, typename TM, bool LSQ>
+hipError_t launch_line(int32_t lb, int32_t le, int32_t wrt, int32_t wart, const int32_t* pi, const int32_t* pa,
+                       const float* pv, const int32_t* ai, const void* av, int32_t B, const uint32_t* rm,
+                       int32_t words, void* mo, double* partials, int32_t nparts, hipStream_t s) {
+  k_line<W, WA, TA, TM, LSQ><<<nparts, kNT, 0, s>>>(lb, le, wrt, wart, pi, pa, pv, ai, static_cast<const TA*>(av), B,
+                                                     rm, words, static_cast<TM*>(mo), partials);
+  return hipGetLastError();
+}
+
+using LaunchFn = hipError_t (*)(int32_t, int32_t, int32_t, int32_t, const int32_t*, const int32_t*, const float*,
+                                const int32_t*, const void*, int32_t, const uint32_t*, int32_t, void*, double*,
+                                int32_t, hipStream_t);
+
+struct Variant {
+  int W, WA, a_dtype, m_dtype, mode;
+  LaunchFn fn;
+};
+
+// Compiled (width, A dtype, M dtype, fill) combinations; dispatch takes the first that fits.
+static const Variant kVariants[] = {
+    {5, 5, SPAI_DTYPE_F32, SPAI_DTYPE_F32, SPAI_FILL_COPY, launch_line<5, 5, float, float, false>},
+    {7, 7, SPAI_DTYPE_F32, SPAI_DTYPE_F32, SPAI_FILL_COPY, launch_line<7, 7, float, float, false>},
+    {5, 5, SPAI_DTYPE_F64, SPAI_DTYPE_F32, SPAI_FILL_COPY, launch_line<5, 5, double, float, false>},
+    {7, 7, SPAI_DTYPE_F64, SPAI_DTYPE_F32, SPAI_FILL_COPY, launch_line<7, 7, double, float, false>},
+    {5, 5, SPAI_DTYPE_F32, SPAI_DTYPE_F32, SPAI_FILL_LSQ, launch_line<5, 5, float, float, true>},
+    {7, 7, SPAI_DTYPE_F32, SPAI_DTYPE_F32, SPAI_FILL_LSQ, launch_line<7, 7, float, float, true>},
+    {5, 5, SPAI_DTYPE_F64, SPAI_DTYPE_F64, SPAI_FILL_LSQ, launch_line<5, 5, double, double, true>},
+    {7, 7, SPAI_DTYPE_F64, SPAI_DTYPE_F64, SPAI_FILL_LSQ, launch_line<7, 7, double, double, true>},
+};
+
+}  // namespace
+}  // namespace spai
+
+using namespace spai;
+
+extern "C" size_t spai_fill_workspace_bytes(int32_t n_lines, int32_t B) {
+  const int64_t nparts = ((int64_t)std::max(n_lines, 1) + kNT - 1) / kNT;
+  Carve c(nullptr);
+  c.take<double>((size_t)nparts * std::max(B, 1));
+  return c.off;
+}
+
+extern "C" int spai_fill_residual(int32_t fill_mode, int32_t line_begin, int32_t line_end, int32_t W,
+                                  const int32_t* pat_idx, const int32_t* pat_act, const float* pat_val, int32_t WA,
+                                  const int32_t* a_idx, const void* a_val, int32_t a_dtype, int32_t B,
+                                  const uint32_t* removed, int32_t words, void* m_out, int32_t m_dtype,
+                                  double* res2_out, void* workspace, size_t workspace_bytes, void* stream) {
+  SPAI_CHECK_ARG(fill_mode == SPAI_FILL_COPY || fill_mode == SPAI_FILL_LSQ, "spai_fill_residual: bad fill_mode %d",
+                 fill_mode);
+  SPAI_CHECK_ARG(a_dtype == SPAI_DTYPE_F32 || a_dtype == SPAI_DTYPE_F64, "spai_fill_residual: bad a_dtype");
+  SPAI_CHECK_ARG(m_dtype == SPAI_DTYPE_F32 || m_dtype == SPAI_DTYPE_F64, "spai_fill_residual: bad m_dtype");
+  SPAI_CHECK_ARG(line_begin >= 0 && line_end >= line_begin && W >= 1 && WA >= 1 && B >= 1 && words >= 0,
+                 "spai_fill_residual: bad shape");
+  SPAI_CHECK_ARG(res2_out && workspace, "spai_fill_residual: null output/workspace");
+  hipStream_t s = (hipStream_t)stream;
+  const int32_t n = line_end - line_begin;
+  if (n == 0) {
+    SPAI_CHECK_HIP(hipMemsetAsync(res2_out, 0, sizeof(double) * B, s));
+    return SPAI_OK;
+  }
+  SPAI_CHECK_ARG(pat_idx && pat_act && pat_val && a_idx && a_val && removed, "spai_fill_residual: null input");
+  SPAI_CHECK_ARG(workspace_bytes >= spai_fill_workspace_bytes(n, B), "spai_fill_residual: workspace too small");
+  const int32_t want_m = fill_mode == SPAI_FILL_COPY ? SPAI_DTYPE_F32 : m_dtype;
+  SPAI_CHECK_ARG(fill_mode != SPAI_FILL_COPY || m_dtype == SPAI_DTYPE_F32,
+                 "spai_fill_residual: copy fill stores fp32 values (utils.py:350)");
+  const Variant* v = nullptr;
+  for (const Variant& cand : kVariants) {
+    if (cand.mode == fill_mode && cand.a_dtype == a_dtype && cand.m_dtype == want_m && cand.W >= W && cand.WA >= WA) {
+      v = &cand;
+      break;
+    }
+  }
+  if (!v) {
+    set_error("spai_fill_residual: no compiled kernel for W=%d WA=%d a_dtype=%d m_dtype=%d mode=%d", W, WA, a_dtype,
+              m_dtype, fill_mode);
+    return SPAI_ERR_UNSUPPORTED;
+  }
+  const int32_t nparts = (n + kNT - 1) / kNT;
+  double* partials = static_cast<double*>(workspace);
+  SPAI_CHECK_HIP(v->fn(line_begin, line_end, W, WA, pat_idx, pat_act, pat_val, a_idx, a_val, B, removed, words, m_out,
+                       partials, nparts, s));
+  k_reduce<<<B, kNT, 0, s>>>(partials, nparts, res2_out);
+  SPAI_CHECK_LAUNCH();
+  return SPAI_OK;
+}

@@ -1,0 +1,148 @@
+"""Thin host wrappers over the C ABI (include/spai_hip.h) taking torch device tensors.
+
+Each wrapper validates shapes on the host, allocates outputs with torch's caching
+allocator on the current stream, and launches through ctypes.  No CPU fallback.
+"""
+from __future__ import annotations
+
+import contextlib
+
+import torch
+
+from . import _lib
+from .layout import Lines
+
+_DT = {torch.float32: _lib.DTYPE_F32, torch.float64: _lib.DTYPE_F64}
+
+
+def _l():
+    return _lib.load()
+
+
+# Optional per-launch HIP-event timing (bench.py): name -> list of (start, end) events,
+# recorded on the stream the kernels are launched on (torch's current stream).
+TIMERS: dict | None = None
+
+
+@contextlib.contextmanager
+def _timed(name: str):
+    if TIMERS is None:
+        yield
+        return
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    yield
+    e.record()
+    TIMERS.setdefault(name, []).append((s, e))
+
+
+def timer_ms(name: str) -> list:
+    return [s.elapsed_time(e) for s, e in (TIMERS or {}).get(name, [])]
+
+
+def logits_stats(logits: torch.Tensor, B: int):
+    """lmax [B] fp32 and z [B] fp64 of logits [E+1] (shared) or [B, E+1]."""
+    _lib.require_device(logits)
+    shared = logits.dim() == 1
+    lg = logits.contiguous().float()
+    E1 = lg.shape[-1]
+    lmax = torch.empty(B, dtype=torch.float32, device=lg.device)
+    z = torch.empty(B, dtype=torch.float64, device=lg.device)
+    nb = _l().spai_logits_stats_workspace_bytes(E1, B)
+    ws = _lib.workspace(nb, lg.device, "stats")
+    with _timed("logits_stats"):
+        st = _l().spai_logits_stats(_lib.ptr(lg), 0 if shared else E1, E1, B, _lib.ptr(lmax), _lib.ptr(z),
+                                      _lib.ptr(ws), ws.numel(), _lib.stream_ptr(lg.device))
+    _lib.check(st, "spai_logits_stats")
+    return lg, lmax, z
+
+
+def parity_step(lg: torch.Tensor, B: int, noise: torch.Tensor, lmax, chosen, active, zrem):
+    E1 = lg.shape[-1]
+    out_a = torch.empty(B, dtype=torch.int64, device=lg.device)
+    out_p = torch.empty(B, dtype=torch.float32, device=lg.device)
+    noise = noise.to(lg.device, non_blocking=True).contiguous()
+    if noise.shape != (B, E1):
+        raise ValueError(f"noise shape {tuple(noise.shape)} != {(B, E1)}")
+    nb = _l().spai_parity_step_workspace_bytes(E1, B)
+    ws = _lib.workspace(nb, lg.device, "parity")
+    _lib.check(_l().spai_parity_step(_lib.ptr(lg), 0 if lg.dim() == 1 else E1, E1, B, _lib.ptr(noise),
+                                     _lib.ptr(lmax), _lib.ptr(chosen), chosen.shape[1], _lib.ptr(active),
+                                     _lib.ptr(zrem), _lib.ptr(out_a), _lib.ptr(out_p), _lib.ptr(ws), ws.numel(),
+                                     _lib.stream_ptr(lg.device)), "spai_parity_step")
+    return out_a, out_p
+
+
+def rollout_select(lg: torch.Tensor, B: int, seed: int, stream_id: int, sample_base: int = 0):
+    """Phase 1 of the throughput rollout: removal bitmaps [B, ceil(E/32)] and counts [B]."""
+    _lib.require_device(lg)
+    E = lg.shape[-1] - 1
+    words = (E + 31) // 32
+    removed = torch.empty(B, words, dtype=torch.int32, device=lg.device)
+    counts = torch.empty(B, dtype=torch.int32, device=lg.device)
+    nb = _l().spai_rollout_workspace_bytes(E, B)
+    if nb == 0:
+        raise RuntimeError("spai_rollout_workspace_bytes failed: " + _l().spai_last_error().decode())
+    ws = _lib.workspace(nb, lg.device, "rollout")
+    with _timed("rollout_select"):
+        st = _l().spai_rollout_select(_lib.ptr(lg), 0 if lg.dim() == 1 else E + 1, E, B, seed & (2**64 - 1),
+                                        stream_id & (2**64 - 1), sample_base, _lib.ptr(removed), words,
+                                        _lib.ptr(counts), _lib.ptr(ws), ws.numel(), _lib.stream_ptr(lg.device))
+    _lib.check(st, "spai_rollout_select")
+    return removed, counts, ws
+
+
+def rollout_order(lg, B, lmax, z, counts, counts_host, ws):
+    """Phase 2: ordered trajectories. Returns actions [B, T] int64, fwd_probs [B, T] fp32."""
+    E = lg.shape[-1] - 1
+    total = int(counts_host.sum())
+    T = int(counts_host.max()) + 1
+    actions = torch.empty(B, T, dtype=torch.int64, device=lg.device)
+    fwd = torch.empty(B, T, dtype=torch.float32, device=lg.device)
+    with _timed("rollout_order"):
+        st = _l().spai_rollout_order(_lib.ptr(lg), 0 if lg.dim() == 1 else E + 1, E, B, _lib.ptr(lmax),
+                                       _lib.ptr(z), _lib.ptr(counts), total, T, T, _lib.ptr(actions), _lib.ptr(fwd),
+                                       _lib.ptr(ws), ws.numel(), _lib.stream_ptr(lg.device))
+    _lib.check(st, "spai_rollout_order")
+    return actions, fwd
+
+
+def actions_to_removed(actions_bt: torch.Tensor, E: int):
+    """Removal bitmaps + unique counts from a [B, T] int64 action tensor (-1 padded)."""
+    _lib.require_device(actions_bt)
+    a = actions_bt.to(torch.int64)
+    B, T = a.shape
+    words = (E + 31) // 32
+    removed = torch.empty(B, words, dtype=torch.int32, device=a.device)
+    counts = torch.empty(B, dtype=torch.int32, device=a.device)
+    _lib.check(_l().spai_actions_to_removed(_lib.ptr(a), a.stride(0), a.stride(1), B, T, E, _lib.ptr(removed),
+                                            words, _lib.ptr(counts), _lib.stream_ptr(a.device)),
+               "spai_actions_to_removed")
+    return removed, counts
+
+
+def fill_residual(pattern: Lines, a_lines: Lines, removed: torch.Tensor, lsq: bool, line_begin: int = 0,
+                  line_end: int | None = None, store_m: bool = False, m_dtype=torch.float32):
+    """res2 [B] fp64 (= sum over lines [begin, end) of ||line residual||^2) and optional M values."""
+    _lib.require_device(removed)
+    if line_end is None:
+        line_end = pattern.n
+    B, words = removed.shape
+    if a_lines.val.dtype not in _DT:
+        raise ValueError(f"A dtype {a_lines.val.dtype} not supported (fp32/fp64)")
+    mode = _lib.FILL_LSQ if lsq else _lib.FILL_COPY
+    if not lsq:
+        m_dtype = torch.float32
+    n_loc = line_end - line_begin
+    res2 = torch.empty(B, dtype=torch.float64, device=removed.device)
+    m = torch.empty(B, n_loc, pattern.width, dtype=m_dtype, device=removed.device) if store_m else None
+    nb = _l().spai_fill_workspace_bytes(max(n_loc, 1), B)
+    ws = _lib.workspace(nb, removed.device, "fill")
+    with _timed("fill_residual"):
+        st = _l().spai_fill_residual(mode, line_begin, line_end, pattern.width, _lib.ptr(pattern.idx),
+                                       _lib.ptr(pattern.act), _lib.ptr(pattern.val), a_lines.width,
+                                       _lib.ptr(a_lines.idx), _lib.ptr(a_lines.val), _DT[a_lines.val.dtype], B,
+                                       _lib.ptr(removed), words, _lib.ptr(m), _DT[m_dtype], _lib.ptr(res2),
+                                       _lib.ptr(ws), ws.numel(), _lib.stream_ptr(removed.device))
+    _lib.check(st, "spai_fill_residual")
+    return res2, m

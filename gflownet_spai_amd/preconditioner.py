@@ -1,0 +1,174 @@
+"""Drop-in ``PreconditionerEnv`` (reference: preconditioner.py:11-165) on the MI355X path.
+
+Same constructor, attributes and methods as the reference; the work behind
+``update`` / ``calculate_residual`` runs in libspai_hip.so:
+
+  reference (per sample, Python)                 here (all samples, one launch each)
+  ------------------------------------------     --------------------------------------------
+  keep-list list-comp over E   utils.py:323      spai_actions_to_removed  -> removal bitmaps
+  COO rebuild + 2x coalesce    utils.py:343-353  (none: M = shared pattern lines + bitmap)
+                               utils.py:115-124
+  torch.mm(M, A) SpGEMM        preconditioner:88 spai_fill_residual -> ||M A - I||_F^2 per sample
+  sparse sub + norm            preconditioner:90   (fp64, never materialises M A)
+  reward formula               preconditioner:137-165, 55-66  (torch ops, same type promotion)
+
+Extensions (keyword-only, defaults = reference behaviour):
+  side="MA" | "AM"    which residual: ||M A - I|| (reference) or ||A M - I|| (column SPAI)
+  fill="copy" | "lsq" M = copied pattern values (reference) or per-line least squares
+  keep_m=False        keep the last batch's M values (LSQ) in ``self.last_m``
+Documented deviations: alpha is taken from the ``alpha`` argument (the reference reads
+the never-set ``self.alpha``, preconditioner.py:163); fp64 original matrices are
+accepted (the reference raises in torch.mm, utils.py:350); a raw COO pattern with
+duplicate entries raises ValueError (the reference's action ids are inconsistent then).
+"""
+from __future__ import annotations
+
+from typing import List, Tuple
+
+import torch
+from torch import Tensor
+
+from . import kernels
+from .env import Env
+from .layout import Lines, build_lines, lines_to_coo, raw_coo
+
+
+class Data:
+    """Keyword attribute bag standing in for torch_geometric.data.Data (preconditioner.py:25)."""
+
+    def __init__(self, **kw):
+        self.__dict__.update(kw)
+
+    def __contains__(self, k):
+        return k in self.__dict__
+
+
+def _default_device():
+    if not torch.cuda.is_available():
+        raise RuntimeError("PreconditionerEnv needs an MI355X (no CPU path)")
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+class PreconditionerEnv(Env):
+    def __init__(self, matrix_size: int, initial_matrix: Tensor, original_matrix: Tensor, *, side: str = "MA",
+                 fill: str = "copy", keep_m: bool = False, device=None):
+        if side not in ("MA", "AM"):
+            raise ValueError("side must be 'MA' or 'AM'")
+        if fill not in ("copy", "lsq"):
+            raise ValueError("fill must be 'copy' or 'lsq'")
+        self.device = torch.device(device) if device is not None else _default_device()
+        self.side, self.fill, self.keep_m = side, fill, keep_m
+        self.matrix_size = matrix_size
+        self.init_nnz = initial_matrix.coalesce().indices().size(1)
+        self.state_dim = self.init_nnz
+        self.num_actions = self.init_nnz + 1
+        self.matrix = initial_matrix.clone()
+        self.original_matrix = original_matrix.clone()
+        edge_index = self.matrix._indices()
+        edge_attr = self.matrix._values()
+        self.data = Data(edge_index=edge_index, edge_attr=edge_attr.float())
+
+        orient = "row" if side == "MA" else "col"
+        r, c, v = raw_coo(self.matrix)
+        if r.numel() != self.init_nnz:
+            raise ValueError("initial_matrix has duplicate raw entries; action ids would be ambiguous")
+        self.pattern: Lines = build_lines(r, c, v, matrix_size, orient, self.device, torch.float32)
+        a = self.original_matrix.coalesce()
+        a_dtype = torch.float64 if a.dtype == torch.float64 else torch.float32
+        ai = a.indices()
+        self.a_lines: Lines = build_lines(ai[0], ai[1], a.values(), matrix_size, orient, self.device, a_dtype)
+        self.last_m = None
+
+        self.orig_residual = self.calculate_residual(self.original_matrix, self.original_matrix)
+        self._r0 = float(self.orig_residual)  # host copy: no device sync inside the reward formula
+        self.orig_flops, _ = self.matrix_flops(self.original_matrix)
+
+    # ------------------------------------------------------------------ hot path
+    def update(self, sparse_matrices: List[Tensor], actions, alpha) -> List[Tensor]:
+        """preconditioner.py:32-52: one reward per row of ``actions`` ([B, T], -1 padded)."""
+        acts = torch.as_tensor(actions)
+        if acts.dim() == 1:
+            acts = acts.view(1, -1)
+        acts = acts.to(self.device, torch.int64)
+        removed, counts = kernels.actions_to_removed(acts, self.init_nnz)
+        return list(self.rewards_from_removed(removed, counts, alpha).unbind(0))
+
+    def rewards_from_removed(self, removed: Tensor, counts: Tensor, alpha, line_begin: int = 0,
+                             line_end: int | None = None, group=None) -> Tensor:
+        """[B] fp64 rewards from removal bitmaps; with ``group`` the lines are a shard and the
+        per-sample squared norms are summed across the process group (one all_reduce)."""
+        res2, m = kernels.fill_residual(self.pattern, self.a_lines, removed, self.fill == "lsq", line_begin,
+                                        line_end, store_m=self.keep_m, m_dtype=self.a_lines.val.dtype)
+        if group is not None:
+            import torch.distributed as dist
+            dist.all_reduce(res2, group=group)
+        if self.keep_m:
+            self.last_m = m
+        self.last_residual = torch.sqrt(res2)
+        nnz = self.init_nnz - counts.to(torch.int64)
+        return self._performance(self.last_residual, nnz, alpha).to(torch.float64) * 1000
+
+    def _performance(self, residual: Tensor, nnz: Tensor, alpha) -> Tensor:
+        """preconditioner.py:137-165 with the reference's type promotion: alpha 0-d fp32,
+        residual ratio fp64, flop ratio python-float -> fp32 product; sum in fp64."""
+        dev = residual.device
+        alpha = torch.as_tensor(alpha, dtype=torch.float32, device=dev) if not torch.is_tensor(alpha) else alpha.to(dev)
+        rr = residual / self.orig_residual.to(dev) if self._r0 != 0 else torch.full_like(residual, float("inf"))
+        flops = nnz.to(torch.float64) * (2.0 * self.matrix_size)
+        cr = flops / self.orig_flops if self.orig_flops != 0 else torch.full_like(flops, float("inf"))
+        t1 = alpha * (1 - rr)
+        t2 = (1 - alpha) * (1 - cr).to(torch.float32)
+        return t1 + t2
+
+    # ------------------------------------------------------------------ reference API
+    def reward(self, s: Tensor, traj_length: int, alpha) -> Tensor:
+        r = self.evaluate_preconditioner(s, self.original_matrix, self.orig_residual, self.orig_flops, alpha)
+        return r.to(torch.float64) * 1000
+
+    def matrix_flops(self, matrix: Tensor) -> Tuple[int, int]:
+        if matrix.is_sparse:
+            non_zeros = matrix._values().numel()
+            return non_zeros * matrix.shape[1] * 2, non_zeros
+        non_zeros = torch.nonzero(matrix).size(0)
+        return 2 * non_zeros, non_zeros
+
+    def calculate_residual(self, updated_matrix: Tensor, original_matrix: Tensor) -> Tensor:
+        """||M A - I||_F (or ||A M - I||_F for side='AM') of arbitrary sparse M, A on the GPU."""
+        orient = self.pattern.orient
+        n = self.matrix_size
+        if original_matrix is self.original_matrix:
+            a_lines = self.a_lines
+        else:
+            a = original_matrix.coalesce()
+            ai = a.indices()
+            a_lines = build_lines(ai[0], ai[1], a.values(), n, orient, self.device,
+                                  torch.float64 if a.dtype == torch.float64 else torch.float32)
+        m = updated_matrix.coalesce()
+        mi = m.indices()
+        pat = build_lines(mi[0], mi[1], m.values(), n, orient, self.device, torch.float32)
+        removed = torch.zeros(1, max((pat.n * pat.width + 31) // 32, 1), dtype=torch.int32, device=self.device)
+        res2, _ = kernels.fill_residual(pat, a_lines, removed, lsq=False)
+        return torch.sqrt(res2[0])
+
+    def mask(self, s: Tensor) -> Tensor:
+        return torch.ones(len(s), self.num_actions)
+
+    def evaluate_preconditioner(self, updated_matrix: Tensor, original_matrix: Tensor, orig_residual, orig_flops,
+                                alpha) -> Tensor:
+        residual = self.calculate_residual(updated_matrix, original_matrix)
+        _, non_zeros = self.matrix_flops(updated_matrix)
+        return self._performance(residual.view(1), torch.tensor([non_zeros], device=residual.device), alpha)[0]
+
+    # ------------------------------------------------------------------ products
+    def assemble(self, b: int = 0, removed: Tensor | None = None) -> Tensor:
+        """Sparse M of sample b of the last batch (LSQ: stored values; COPY: needs ``removed``)."""
+        if self.fill == "lsq":
+            if self.last_m is None:
+                raise ValueError("construct with keep_m=True to keep M")
+            return lines_to_coo(self.pattern, self.last_m[b], self.matrix_size)
+        if removed is None:
+            raise ValueError("copy fill: pass the removal bitmaps")
+        bits = removed[b]
+        act = self.pattern.act.long().clamp(min=0)
+        gone = ((bits[act >> 5] >> (act & 31)) & 1).bool() | (self.pattern.act < 0)
+        return lines_to_coo(self.pattern, torch.where(gone, 0.0, self.pattern.val), self.matrix_size)

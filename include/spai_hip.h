@@ -1,0 +1,135 @@
+/*
+ * spai_hip.h — C ABI of libspai_hip.so, the MI355X (gfx950) hot path of SPAI-via-GFlowNet.
+ *
+ * The reference (tonylizza/gflownet-spai @ 2024-10-24) is pure Python/PyTorch with no
+ * FFI; its hot path is the call chain
+ *     GFlowNet.sample_states  (gflownet/gflownet.py:125-197)
+ *       -> ForwardPolicy logits + Categorical sampling (policy.py:34-73, gflownet.py:148)
+ *       -> PreconditionerEnv.update (preconditioner.py:32-52)
+ *            -> update_edges_and_convert_to_sparse + resize (gflownet/utils.py:295-356, 89-126)
+ *            -> calculate_residual ||M A - I||_F (preconditioner.py:79-93)
+ *            -> evaluate_preconditioner / reward (preconditioner.py:55-66, 137-165)
+ * Each entry point below names the reference code it replaces.  The Python drop-ins
+ * (gflownet_spai_amd/{gflownet,preconditioner,log}.py) bind these through ctypes; the
+ * binding a maintainer would add to the reference is shown in INTEGRATION.md.
+ *
+ * Conventions
+ *   - Every pointer argument is a DEVICE pointer owned by the caller, unless noted.
+ *     No allocation crosses the ABI; the library uses only the caller's workspace.
+ *   - `stream` is a hipStream_t passed as void*; all calls are stream-ordered and
+ *     asynchronous (no host synchronisation inside any call).
+ *   - Return value: SPAI_OK (0) or an error code; spai_last_error() returns a
+ *     thread-local message for the last failing call.  Nothing throws across the ABI.
+ *   - Bitmaps are uint32 words, bit (a & 31) of word (a >> 5) <=> action / edge a.
+ *   - "Lines" are the ELL rows of a sparse matrix in one orientation: for the
+ *     ||M A - I|| side (reference) line i = row i (CSR), for the ||A M - I|| side
+ *     (north star) line j = column j (CSC).  A pattern line holds, per slot, the other
+ *     index (-1 = padding), the action id of that entry and its initial value.
+ */
+#ifndef SPAI_HIP_H
+#define SPAI_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SPAI_OK 0
+#define SPAI_ERR_INVALID 1     /* bad argument (maps to ValueError) */
+#define SPAI_ERR_HIP 2         /* HIP runtime / launch failure (RuntimeError) */
+#define SPAI_ERR_UNSUPPORTED 3 /* shape outside the compiled kernels (NotImplementedError) */
+
+#define SPAI_FILL_COPY 0 /* M = pattern values of kept entries (gflownet/utils.py:331-353) */
+#define SPAI_FILL_LSQ 1  /* m_j = argmin ||A[:,J_j] m - e_j||_2 (north-star extension) */
+
+#define SPAI_DTYPE_F32 0
+#define SPAI_DTYPE_F64 1
+
+/* ABI version (bumped on any signature change) and last error text. */
+int spai_abi_version(void);
+const char* spai_last_error(void);
+
+/* ---------------------------------------------------------------- logits statistics
+ * lmax[b] = max_a logits[b, a], z[b] = sum_a exp(logits[b, a] - lmax[b]) (fp64), over the
+ * E1 = E + 1 actions of each of B rows spaced `bstride` floats apart (bstride 0 = one row
+ * shared by all samples; outputs are still written for every b).
+ * Replaces the softmax normaliser of policy.py:73 (computed once per rollout because
+ * the reference's logits are state-independent within a rollout, gflownet.py:133,145). */
+size_t spai_logits_stats_workspace_bytes(int32_t E1, int32_t B);
+int spai_logits_stats(const float* logits, int64_t bstride, int32_t E1, int32_t B,
+                      float* lmax, double* z, void* workspace, size_t workspace_bytes, void* stream);
+
+/* ---------------------------------------------------------------- reference-parity step
+ * One step of the reference loop (gflownet.py:135-179): for every sample b,
+ *   a_b = argmax_a w_a / noise[b, a],  w_a = exp(l_a - lmax_b), w_a := 0 if chosen,
+ * i.e. Categorical(probs).sample() == argmax(p / q), q ~ Exp(1) (torch multinomial
+ * fast path; noise drawn on the host from the torch CPU generator, B*(E+1) per step).
+ * For active samples: sets the chosen bit, logs out_action[b] = a_b and
+ * out_prob[b] = w_a / zrem[b] (log.py:70), subtracts w_a from zrem[b] and clears
+ * active[b] when a_b == E (gflownet.py:177-179).  Inactive samples log -1 and 1.0.
+ * chosen: [B][words1] bitmap over E+1 actions. */
+size_t spai_parity_step_workspace_bytes(int32_t E1, int32_t B);
+int spai_parity_step(const float* logits, int64_t bstride, int32_t E1, int32_t B, const float* noise,
+                     const float* lmax, uint32_t* chosen, int32_t words1, uint8_t* active, double* zrem,
+                     int64_t* out_action, float* out_prob, void* workspace, size_t workspace_bytes,
+                     void* stream);
+
+/* ---------------------------------------------------------------- throughput rollout
+ * Whole trajectories in one pass (replaces the T-step loop of gflownet.py:135-179):
+ * Gumbel-top-k over key_a = l_a - ln(-ln u_a), u from Philox4x32-10 with counter
+ * (a >> 2, sample_base + b, stream_lo, stream_hi) and key (seed_lo, seed_hi); the
+ * removed set of sample b is {a < E : key_a > key_E}.  Distributionally identical to
+ * the reference's sequential sampling without replacement; bit-exact to oracle/.
+ *
+ * Phase 1 (spai_rollout_select): writes removed[B][words] (words = ceil(E/32)),
+ * counts[B] (= k_b, the number removed) and stages the winners in the workspace.
+ * Phase 2 (spai_rollout_order): total = sum_b counts[b] (read by the caller), T = max
+ * k_b + 1.  Sorts each sample's winners by key descending (ties: action ascending),
+ * then writes the trajectory log in [B][t_cap] layout (t_cap >= T):
+ *   actions[b][t] = t-th removed action, actions[b][k_b] = E, -1 after;
+ *   fwd_probs[b][t] = w_{a_t} / (Z_b - sum_{s<t} w_{a_s}), 1.0 after the terminal;
+ * (log.py:67-87 semantics: the Log's actions [T,B] is the transpose).  lmax/z come
+ * from spai_logits_stats.  One workspace serves both phases of one rollout. */
+size_t spai_rollout_workspace_bytes(int32_t E, int32_t B);
+int spai_rollout_select(const float* logits, int64_t bstride, int32_t E, int32_t B, uint64_t seed,
+                        uint64_t stream_id, int32_t sample_base, uint32_t* removed, int32_t words,
+                        int32_t* counts, void* workspace, size_t workspace_bytes, void* stream);
+int spai_rollout_order(const float* logits, int64_t bstride, int32_t E, int32_t B, const float* lmax,
+                       const double* z, const int32_t* counts, int64_t total, int32_t T, int64_t t_cap,
+                       int64_t* actions, float* fwd_probs, void* workspace, size_t workspace_bytes,
+                       void* stream);
+
+/* ---------------------------------------------------------------- actions -> removal sets
+ * removed[b] = { a : 0 <= a < E, a in actions[b, :] } (preconditioner.py:37-43 +
+ * utils.py:315-323: -1 padding and the terminal id E are ignored), and
+ * counts[b] = |removed[b]|, so nnz(M_b) = E - counts[b] (utils.py:343-353 coalesce). */
+int spai_actions_to_removed(const int64_t* actions, int64_t stride_b, int64_t stride_t, int32_t B,
+                            int32_t T, int32_t E, uint32_t* removed, int32_t words, int32_t* counts,
+                            void* stream);
+
+/* ---------------------------------------------------------------- fill + residual
+ * For lines [line_begin, line_end) of the pattern and every sample b:
+ *   keep_p = (pat_idx[l,p] >= 0) && !removed[b][pat_act[l,p]]
+ *   fill_mode COPY: m_p = keep_p ? (float)pat_val[l,p] : 0        (utils.py:331-353)
+ *   fill_mode LSQ : m = argmin ||A_lines[J] m - e_l||, J = kept p  (north star; fp64 solve)
+ *   res2_out[b]  = sum over the lines of || sum_p m_p A_line(pat_idx[l,p]) - e_l ||^2 (fp64)
+ * which is ||M A - I||_F^2 (row lines, CSR; preconditioner.py:79-93) or ||A M - I||_F^2
+ * (column lines, CSC) restricted to those lines; summing res2_out over a partition of
+ * the lines (e.g. the ranks of a column-sharded job) gives the full square norm.
+ * M is evaluated from its STORED precision (m_dtype).  m_out (may be NULL) receives
+ * [B][line_end - line_begin][W] values in m_dtype (0 where not kept).
+ * a_idx/a_val: [n_lines][WA] lines of the original matrix A in the same orientation.
+ * Shapes outside the compiled widths (W, WA <= 7) return SPAI_ERR_UNSUPPORTED. */
+size_t spai_fill_workspace_bytes(int32_t n_lines, int32_t B);
+int spai_fill_residual(int32_t fill_mode, int32_t line_begin, int32_t line_end, int32_t W,
+                       const int32_t* pat_idx, const int32_t* pat_act, const float* pat_val, int32_t WA,
+                       const int32_t* a_idx, const void* a_val, int32_t a_dtype, int32_t B,
+                       const uint32_t* removed, int32_t words, void* m_out, int32_t m_dtype,
+                       double* res2_out, void* workspace, size_t workspace_bytes, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SPAI_HIP_H */

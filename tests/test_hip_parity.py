@@ -1,0 +1,268 @@
+"""HIP path (through the C ABI) vs the reference's golden vectors and the CPU oracle.
+
+Bar: bit-exact for index work (sampled actions, removed sets, counts, orders); floats
+within 1e-6 relative (north-star tolerance) unless the arithmetic is exact (integer
+stencils in fp64: residuals of copy-filled Poisson matrices are exact).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+import scipy.sparse as sp
+import torch
+
+from oracle import spai_oracle as O
+
+from .conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def load(name):
+    return np.load(os.path.join(GOLDEN, name))
+
+
+def coo(rows, cols, vals, n):
+    return torch.sparse_coo_tensor(torch.from_numpy(np.stack([rows, cols]).astype(np.int64)), torch.from_numpy(vals),
+                                   (n, n))
+
+
+class FixedLogits(torch.nn.Module):
+    """Stand-in policy with the reference ForwardPolicy call contract (as in make_golden.py)."""
+
+    def __init__(self, logits):
+        super().__init__()
+        self.l = torch.nn.Parameter(torch.as_tensor(logits).view(1, -1).clone())
+        self.alpha = torch.nn.Parameter(torch.tensor(0.0))
+
+    def logits(self, data):
+        return self.l.to(DEV), torch.sigmoid(self.alpha).to(DEV)
+
+    def forward(self, data, actions):
+        x = self.l
+        if actions.numel():
+            m = torch.zeros_like(x, dtype=torch.bool)
+            m[:, actions] = True
+            x = x.masked_fill(m, float("-inf"))
+        return torch.softmax(x, 1), torch.sigmoid(self.alpha)
+
+
+def test_library_loaded_from_tree():
+    from gflownet_spai_amd import _lib
+    lib = _lib.load()
+    assert lib.spai_abi_version() == _lib.ABI_VERSION
+    assert os.path.dirname(_lib.LIB_PATH).endswith("gflownet_spai_amd")
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_parity_rollout_bit_exact_vs_reference(seed):
+    from gflownet_spai_amd import BackwardPolicy, GFlowNet, PreconditionerEnv, trajectory_balance_loss
+    d = load(f"c1_rollout_s{seed}.npz")
+    n, B = int(d["n"]), int(d["B"])
+    A = coo(d["rows"], d["cols"], d["vals"], n)
+    env = PreconditionerEnv(n, A, A)
+    E = env.num_actions - 1
+    pol = FixedLogits(d["logits"])
+    torch.manual_seed(0)
+    bwd = BackwardPolicy(1, 4, E + 1).to(DEV)
+    g = GFlowNet(pol, bwd, env, mode="parity")
+    torch.manual_seed(int(d["seed"]))
+    log = g.sample_states([A.clone() for _ in range(B)], return_log=True)
+    assert np.array_equal(log.actions.cpu().numpy(), d["actions"])
+    with torch.no_grad():
+        np.testing.assert_allclose(log.fwd_probs.cpu().numpy(), d["fwd_probs"], rtol=1e-6, atol=1e-9)
+    np.testing.assert_allclose(log.rewards.cpu().numpy(), d["rewards"], rtol=1e-6)
+    assert len(log._actions) == d["actions"].shape[0]
+    loss = trajectory_balance_loss(log.total_flow, log.rewards, log.fwd_probs, log.back_probs)
+    assert float(loss) == pytest.approx(float(d["loss"]), rel=1e-5)
+    loss.backward()
+    gref = d["logits_grad"]
+    np.testing.assert_allclose(pol.l.grad.view(-1).numpy(), gref, rtol=2e-4, atol=2e-6 * np.abs(gref).max())
+
+
+@pytest.mark.parametrize("name", ["c1_removal.npz", "c1p_removal.npz", "rand64_removal.npz"])
+def test_env_update_vs_reference(name):
+    """PreconditionerEnv.update (copy fill) on both sides vs the reference and the fp64 oracle."""
+    from gflownet_spai_amd import PreconditionerEnv
+    d = load(name)
+    n = int(d["n"])
+    A = coo(d["rows"], d["cols"], d["vals"], n)
+    Acsr = sp.csr_matrix((d["vals"].astype(np.float64), (d["rows"], d["cols"])), shape=(n, n))
+    symmetric = abs(Acsr - Acsr.T).max() == 0
+    exact = name != "rand64_removal.npz"  # integer stencils: every residual is exact in fp64
+    removed = d["removed"]
+    K = removed.shape[0]
+    for side in ("MA", "AM"):
+        env = PreconditionerEnv(n, A, A, side=side)
+        E = env.num_actions - 1
+        assert env.orig_flops == int(d["f0"]) and env.num_actions == int(d["num_actions"])
+        assert float(env.orig_residual) == pytest.approx(float(d["r0"]), rel=0 if exact else 1e-6)
+        T = max(int(removed.sum(1).max()), 1)
+        acts = -np.ones((K, T + 1), np.int64)
+        for k in range(K):
+            ids = np.flatnonzero(removed[k])
+            acts[k, :ids.size] = np.random.default_rng(k).permutation(ids)
+            acts[k, ids.size] = E  # the terminal id is ignored (utils.py:323)
+        for ia, al in enumerate(d["alphas"]):
+            alpha = torch.tensor(al, dtype=torch.float32)
+            rw = torch.stack(env.update(None, torch.from_numpy(acts), alpha)).cpu().numpy()
+            res = env.last_residual.cpu().numpy()
+            for k in range(K):
+                mr, mc, mv = O.copy_fill_coo(d["rows"], d["cols"], d["vals"], removed[k], n)
+                M = sp.csr_matrix((mv.astype(np.float64), (mr, mc)), shape=(n, n))
+                ref64 = O.residual_fro_fp64(M, Acsr) if side == "MA" else O.residual_fro_fp64(Acsr, M)
+                assert res[k] == pytest.approx(ref64, rel=1e-13, abs=1e-13)
+                golden = d["r_ma"][k] if side == "MA" else (d["r_mta"][k] if symmetric else None)
+                if golden is not None:
+                    assert res[k] == pytest.approx(golden, rel=0 if exact else 1e-6)
+                # reward formula + type promotion, bit-for-bit on our own residual
+                want = O.reward(res[k], len(mr), alpha, float(env.orig_residual), env.orig_flops, n)
+                assert rw[k] == pytest.approx(want, rel=1e-15, abs=1e-12)
+                if side == "MA" and exact:
+                    assert rw[k] == pytest.approx(d["reward"][k, ia], rel=1e-12, abs=1e-9)
+
+
+def test_calculate_residual_and_reward_api():
+    from gflownet_spai_amd import PreconditionerEnv
+    d = load("c1_removal.npz")
+    n = int(d["n"])
+    A = coo(d["rows"], d["cols"], d["vals"], n)
+    env = PreconditionerEnv(n, A, A)
+    k = 20
+    mr, mc, mv = O.copy_fill_coo(d["rows"], d["cols"], d["vals"], d["removed"][k], n)
+    M = coo(mr, mc, mv, n)
+    assert float(env.calculate_residual(M, A)) == d["r_ma"][k]
+    r = env.reward(M, 5, torch.tensor(0.5))
+    assert float(r) == pytest.approx(d["reward"][k, 0], rel=1e-12)
+    assert env.matrix_flops(M) == (len(mr) * n * 2, len(mr))
+
+
+@pytest.mark.parametrize("E,B,seed,stream", [(1216, 4, 0, 0), (1216, 3, 5, 9), (40, 2, 1, 0), (5000, 7, 2**40 + 3, 2**33 + 1)])
+def test_throughput_rollout_bit_exact_vs_oracle(E, B, seed, stream):
+    from gflownet_spai_amd import kernels
+    rng = np.random.default_rng(E + B)
+    logits = rng.standard_normal(E + 1).astype(np.float32)
+    logits[E] = 3.5
+    lg, lmax, z = kernels.logits_stats(torch.from_numpy(logits).to(DEV), B)
+    removed, counts, ws = kernels.rollout_select(lg, B, seed, stream, sample_base=3)
+    counts_h = counts.cpu()
+    actions, fwd = kernels.rollout_order(lg, B, lmax, z, counts, counts_h, ws)
+    r_o, a_o, f_o, c_o = O.throughput_rollout(logits, B, seed, stream, sample_base=3)
+    assert np.array_equal(counts_h.numpy(), c_o)
+    bits = removed.cpu().numpy().view(np.uint32)
+    got = ((bits[:, :, None] >> np.arange(32, dtype=np.uint32)) & 1).reshape(B, -1)[:, :E].astype(bool)
+    assert np.array_equal(got, r_o)
+    assert np.array_equal(actions.cpu().numpy(), a_o.T)
+    np.testing.assert_allclose(fwd.cpu().numpy(), f_o, rtol=1e-6)
+
+
+def test_throughput_sample_states_end_to_end():
+    from gflownet_spai_amd import GFlowNet, PreconditionerEnv, poisson_2d
+    A = poisson_2d(32)
+    n = 32 * 32
+    env = PreconditionerEnv(n, A, A, side="AM", fill="lsq", keep_m=True)
+    E = env.num_actions - 1
+    logits = torch.randn(E + 1, generator=torch.Generator().manual_seed(123))
+    logits[E] = 6.0
+    g = GFlowNet(FixedLogits(logits), None, env, mode="throughput", seed=42)
+    log = g.sample_states([A] * 4, return_log=True)
+    r_o, a_o, f_o, c_o = O.throughput_rollout(logits.numpy(), 4, 42, 0)
+    assert np.array_equal(log.actions.cpu().numpy(), a_o)
+    # LSQ fill vs the oracle (stacked QR, fp64) and ||AM-I|| from the stored fp32 M
+    r, c, v, _ = O.poisson2d(32)
+    idx, act, _ = O.lines_from_coo(r, c, v, n, "col")
+    a_idx, _, a_val = O.lines_from_coo(r, c, v.astype(np.float64), n, "col")
+    Acsc = sp.csc_matrix((v.astype(np.float64), (r, c)), shape=(n, n))
+    for b in range(4):
+        keep = (idx >= 0) & ~r_o[b][np.clip(act, 0, None)]
+        m_ref = O.lsq_fill(idx, keep, a_idx, a_val)
+        m_gpu = env.last_m[b].cpu().numpy().astype(np.float64)
+        assert np.linalg.norm(m_gpu - m_ref) / np.linalg.norm(m_ref) < 1e-6
+        res = O.residual_fro_fp64(Acsc, O.m_to_csc(idx, env.last_m[b].cpu().numpy(), n))
+        assert float(env.last_residual[b]) == pytest.approx(res, rel=1e-10)
+
+
+def test_lsq_fp64_3d_vs_oracle():
+    """64^3 is the C3 config; a 12^3 7-pt fp64 lattice checks the fp64 LSQ kernel exactly."""
+    from gflownet_spai_amd import GFlowNet, PreconditionerEnv, poisson_3d
+    g3 = 12
+    A = poisson_3d(g3)
+    n = g3 ** 3
+    env = PreconditionerEnv(n, A, A, side="AM", fill="lsq", keep_m=True)
+    E = env.num_actions - 1
+    logits = torch.randn(E + 1, generator=torch.Generator().manual_seed(7))
+    logits[E] = 7.0
+    g = GFlowNet(FixedLogits(logits), None, env, mode="throughput", seed=3)
+    g.sample_states([A] * 2, return_log=True)
+    r_o, *_ = O.throughput_rollout(logits.numpy(), 2, 3, 0)
+    r, c, v, _ = O.poisson3d(g3)
+    idx, act, _ = O.lines_from_coo(r, c, v, n, "col")
+    a_idx, _, a_val = O.lines_from_coo(r, c, v, n, "col")
+    Acsc = sp.csc_matrix((v, (r, c)), shape=(n, n))
+    for b in range(2):
+        keep = (idx >= 0) & ~r_o[b][np.clip(act, 0, None)]
+        m_ref = O.lsq_fill(idx, keep, a_idx, a_val)
+        m_gpu = env.last_m[b].cpu().numpy()
+        assert env.last_m.dtype == torch.float64
+        assert np.linalg.norm(m_gpu - m_ref) / np.linalg.norm(m_ref) < 1e-12
+        res = O.residual_fro_fp64(Acsc, O.m_to_csc(idx, m_gpu, n, np.float64))
+        assert float(env.last_residual[b]) == pytest.approx(res, rel=1e-10)
+
+
+def test_full_size_c4_residuals_vs_reference():
+    """1024^2 (C4): r0 and one 20%-removed candidate against the reference's own numbers."""
+    from gflownet_spai_amd import PreconditionerEnv, kernels, poisson_2d
+    meta = json.load(open(os.path.join(GOLDEN, "meta.json")))["cases"]["c4_residual"]
+    A = poisson_2d(1024)
+    n = 1024 * 1024
+    for side, key in (("MA", "r_ma"), ("AM", "r_mta")):
+        env = PreconditionerEnv(n, A, A, side=side)
+        assert float(env.orig_residual) == pytest.approx(meta["r0"], rel=1e-15)
+        st = meta["sets"][0]
+        removed = np.random.default_rng(1000).random(env.init_nnz) < 0.2
+        words = (env.init_nnz + 31) // 32
+        bits = np.zeros(words, np.uint32)
+        ids = np.flatnonzero(removed)
+        np.bitwise_or.at(bits, ids >> 5, (np.uint32(1) << (ids & 31).astype(np.uint32)))
+        rb = torch.from_numpy(bits.view(np.int32).reshape(1, words)).to(DEV)
+        counts = torch.tensor([int(removed.sum())], dtype=torch.int32, device=DEV)
+        rw = env.rewards_from_removed(rb, counts, torch.tensor(0.5))
+        assert float(env.last_residual[0]) == pytest.approx(st[key], rel=1e-15)
+        if side == "MA":
+            assert float(rw[0]) == pytest.approx(st["reward"][0], rel=1e-12)
+
+
+def test_edge_cases():
+    from gflownet_spai_amd import GFlowNet, PreconditionerEnv, kernels
+    d = load("c1_removal.npz")
+    n = int(d["n"])
+    A = coo(d["rows"], d["cols"], d["vals"], n)
+    env = PreconditionerEnv(n, A, A)
+    E = env.num_actions - 1
+    # immediate terminal (nothing removed) and every edge removed
+    env.update(None, torch.tensor([[E, -1], [E, -1]]), torch.tensor(0.5))
+    assert float(env.last_residual[0]) == d["r_ma"][0]
+    env.update(None, torch.arange(E + 1).view(1, -1), torch.tensor(0.5))
+    assert float(env.last_residual[0]) == d["r_ma"][1] == pytest.approx(16.0)  # ||-I||_F = sqrt(256)
+    # B = 1 (the reference crashes there, gflownet.py:121)
+    logits = torch.full((E + 1,), -5.0)
+    logits[E] = 20.0
+    g = GFlowNet(FixedLogits(logits), None, env, mode="throughput", seed=1)
+    log = g.sample_states([A], return_log=True)
+    assert tuple(log.actions.shape) == (1, 1) and int(log.actions[0, 0]) == E
+    # parity mode with B = 1 too
+    g2 = GFlowNet(FixedLogits(logits), None, env, mode="parity")
+    log2 = g2.sample_states([A], return_log=True)
+    assert int(log2.actions[-1, 0]) == E
+    # malformed input -> ValueError, widths beyond the compiled kernels -> NotImplementedError
+    lg, lmax, z = kernels.logits_stats(logits.to(DEV), 1)
+    with pytest.raises(ValueError):
+        kernels.parity_step(lg, 1, torch.ones(1, 3), lmax, torch.zeros(1, (E + 32) // 32, dtype=torch.int32,
+                                                                        device=DEV),
+                            torch.ones(1, dtype=torch.uint8, device=DEV), z.clone())
+    D = torch.ones(10, 10).to_sparse()
+    with pytest.raises(NotImplementedError):
+        PreconditionerEnv(10, D, D)

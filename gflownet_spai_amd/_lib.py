@@ -18,7 +18,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libspai_hip
 SPAI_OK, SPAI_ERR_INVALID, SPAI_ERR_HIP, SPAI_ERR_UNSUPPORTED = 0, 1, 2, 3
 FILL_COPY, FILL_LSQ = 0, 1
 DTYPE_F32, DTYPE_F64 = 0, 1
-ABI_VERSION = 1
+ABI_VERSION = 3
 
 _c_i32, _c_i64, _c_u64, _c_sz, _c_p = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_size_t, ctypes.c_void_p
 
@@ -32,14 +32,16 @@ SIGNATURES = {
     "spai_parity_step": (ctypes.c_int, [_c_p, _c_i64, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_i32, _c_p, _c_p,
                                         _c_p, _c_p, _c_p, _c_sz, _c_p]),
     "spai_rollout_workspace_bytes": (_c_sz, [_c_i32, _c_i32]),
-    "spai_rollout_select": (ctypes.c_int, [_c_p, _c_i64, _c_i32, _c_i32, _c_u64, _c_u64, _c_i32, _c_p, _c_i32,
+    "spai_rollout_select": (ctypes.c_int, [_c_p, _c_i64, _c_i32, _c_i32, _c_p, _c_u64, _c_u64, _c_i32, _c_p, _c_i32,
                                            _c_p, _c_p, _c_sz, _c_p]),
-    "spai_rollout_order": (ctypes.c_int, [_c_p, _c_i64, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_i64, _c_i32, _c_i64,
-                                          _c_p, _c_p, _c_p, _c_sz, _c_p]),
+    "spai_rollout_order": (ctypes.c_int, [_c_p, _c_i64, _c_i32, _c_i32, _c_p, _c_p, _c_i64, _c_p, _c_p, _c_p, _c_p,
+                                          _c_sz, _c_p]),
     "spai_actions_to_removed": (ctypes.c_int, [_c_p, _c_i64, _c_i64, _c_i32, _c_i32, _c_i32, _c_p, _c_i32, _c_p,
                                                _c_p]),
     "spai_fill_workspace_bytes": (_c_sz, [_c_i32, _c_i32]),
-    "spai_fill_residual": (ctypes.c_int, [_c_i32, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_i32, _c_p, _c_p,
+    "spai_rewards": (ctypes.c_int, [_c_p, _c_p, _c_i32, _c_i64, _c_i32, ctypes.c_double, ctypes.c_double, _c_p, _c_p,
+                                    _c_p, _c_p]),
+    "spai_fill_residual": (ctypes.c_int, [_c_i32, _c_i32, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_i32, _c_p, _c_p,
                                           _c_i32, _c_i32, _c_p, _c_i32, _c_p, _c_i32, _c_p, _c_p, _c_sz, _c_p]),
 }
 
@@ -97,8 +99,9 @@ _ws_cache: dict = {}
 
 
 def workspace(nbytes: int, device, tag: str) -> torch.Tensor:
-    """Caller-owned workspace (a byte tensor from torch's caching allocator), reused per tag."""
-    key = (tag, str(device))
+    """Caller-owned workspace (a byte tensor from torch's caching allocator), reused per
+    (tag, device, current stream) so concurrent streams never share one."""
+    key = (tag, str(device), torch.cuda.current_stream(device).cuda_stream)
     ws = _ws_cache.get(key)
     if ws is None or ws.numel() < nbytes:
         ws = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)

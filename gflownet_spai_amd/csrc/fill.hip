@@ -162,6 +162,90 @@ __global__ __launch_bounds__(kNT) void k_line(int32_t line_begin, int32_t line_e
   }
 }
 
+// Generic COPY-fill residual for lines of any width (e.g. the reference drivers' spilu
+// L@U candidate patterns, GFlowNet100.py:137-153): one workgroup per line accumulates the
+// line of M*A (or A*M) of one sample in an LDS open-addressing table of fp64 sums keyed by
+// the other index (the diagonal is seeded with -1), then sums the squares.
+__device__ __forceinline__ void hash_add(int* keys, double* vals, int tb, int key, double v) {
+  unsigned h = ((unsigned)key * 2654435761u) % (unsigned)tb;
+  while (true) {
+    const int prev = atomicCAS(&keys[h], -1, key);
+    if (prev == -1 || prev == key) {
+      atomicAdd(&vals[h], v);
+      return;
+    }
+    h = (h + 1 == (unsigned)tb) ? 0u : h + 1;
+  }
+}
+
+template <typename TA>
+__global__ __launch_bounds__(kNT) void k_line_hash(int32_t line_begin, int32_t line_end, int32_t wrt, int32_t wart,
+                                                   const int32_t* __restrict__ pat_idx,
+                                                   const int32_t* __restrict__ pat_act,
+                                                   const float* __restrict__ pat_val,
+                                                   const int32_t* __restrict__ a_idx, const TA* __restrict__ a_val,
+                                                   int32_t B, const uint32_t* __restrict__ removed, int32_t words,
+                                                   float* __restrict__ m_out, double* __restrict__ partials,
+                                                   int32_t tb) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  double* vals = reinterpret_cast<double*>(smem);
+  int* keys = reinterpret_cast<int*>(smem + (size_t)tb * sizeof(double));
+  __shared__ double sred[kNT / 64];
+  const int j = line_begin + blockIdx.x;
+  const int64_t nloc = line_end - line_begin;
+  const int nprod = wrt * wart;
+  const int64_t base = (int64_t)j * wrt;
+  for (int b = 0; b < B; ++b) {
+    const uint32_t* rb = removed + (int64_t)b * words;
+    for (int t = threadIdx.x; t < tb; t += kNT) {
+      keys[t] = -1;
+      vals[t] = 0.0;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) hash_add(keys, vals, tb, j, -1.0);
+    if (m_out != nullptr) {
+      for (int p = threadIdx.x; p < wrt; p += kNT) {
+        const int k = pat_idx[base + p], a = pat_act[base + p];
+        const bool keep = k >= 0 && !((rb[a >> 5] >> (a & 31)) & 1u);
+        m_out[((int64_t)b * nloc + (j - line_begin)) * wrt + p] = keep ? pat_val[base + p] : 0.0f;
+      }
+    }
+    for (int f = threadIdx.x; f < nprod; f += kNT) {
+      const int p = f / wart, s = f - p * wart;
+      const int k = pat_idx[base + p];
+      if (k < 0) continue;
+      const int a = pat_act[base + p];
+      if ((rb[a >> 5] >> (a & 31)) & 1u) continue;
+      const int64_t o = (int64_t)k * wart + s;
+      const int l = a_idx[o];
+      if (l < 0) continue;
+      hash_add(keys, vals, tb, l, (double)pat_val[base + p] * (double)a_val[o]);
+    }
+    __syncthreads();
+    double s2 = 0.0;
+    for (int t = threadIdx.x; t < tb; t += kNT)
+      if (keys[t] >= 0) s2 += vals[t] * vals[t];
+    s2 = block_sum<kNT>(s2, sred);
+    if (threadIdx.x == 0) partials[(int64_t)b * gridDim.x + blockIdx.x] = s2;
+    __syncthreads();
+  }
+}
+
+constexpr int kHashMaxEntries = 13000;  // 13000 x 12 B = 152 KiB of the 160 KiB LDS
+
+template <typename TA>
+hipError_t launch_hash(int32_t lb, int32_t le, int32_t wrt, int32_t wart, const int32_t* pi, const int32_t* pa,
+                       const float* pv, const int32_t* ai, const void* av, int32_t B, const uint32_t* rm,
+                       int32_t words, void* mo, double* partials, int32_t tb, hipStream_t s) {
+  const size_t lds = (size_t)tb * (sizeof(double) + sizeof(int));
+  hipError_t e = hipFuncSetAttribute((const void*)k_line_hash<TA>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)lds);
+  if (e != hipSuccess) return e;
+  k_line_hash<TA><<<le - lb, kNT, lds, s>>>(lb, le, wrt, wart, pi, pa, pv, ai, static_cast<const TA*>(av), B, rm,
+                                             words, static_cast<float*>(mo), partials, tb);
+  return hipGetLastError();
+}
+
 __global__ __launch_bounds__(kNT) void k_reduce(const double* __restrict__ partials, int32_t nparts,
                                                 double* __restrict__ out) {
   __shared__ double sred[kNT / 64];
@@ -170,6 +254,27 @@ __global__ __launch_bounds__(kNT) void k_reduce(const double* __restrict__ parti
   for (int i = threadIdx.x; i < nparts; i += kNT) s += partials[(int64_t)b * nparts + i];
   s = block_sum<kNT>(s, sred);
   if (threadIdx.x == 0) out[b] = s;
+}
+
+// Reward of preconditioner.py:55-66 + 137-165 for every sample, with the reference's
+// torch type promotion reproduced op for op: alpha is fp32, the residual ratio fp64, the
+// flop ratio a python float, (1 - alpha) * (1 - flop_ratio) is an fp32 product and the sum
+// is fp64.  Contraction is disabled so every op rounds as torch's separate kernels do.
+__global__ void k_rewards(const double* __restrict__ res2, const int32_t* __restrict__ removed_counts, int32_t B,
+                          int64_t nnz0, int32_t n, double r0, double f0, const float* __restrict__ alpha,
+                          double* __restrict__ residual, double* __restrict__ reward) {
+#pragma clang fp contract(off)
+  for (int b = threadIdx.x; b < B; b += blockDim.x) {
+    const double r = sqrt(res2[b]);
+    residual[b] = r;
+    const double rr = r0 != 0.0 ? r / r0 : INFINITY;
+    const double flops = (double)(nnz0 - removed_counts[b]) * 2.0 * (double)n;
+    const double cr = f0 != 0.0 ? flops / f0 : INFINITY;
+    const float a = *alpha;
+    const double t1 = (double)a * (1.0 - rr);
+    const float t2 = (1.0f - a) * (float)(1.0 - cr);
+    reward[b] = (t1 + (double)t2) * 1000.0;
+  }
 }
 
 template <int W, int WA, typename TA, typename TM, bool LSQ>
@@ -208,13 +313,13 @@ static const Variant kVariants[] = {
 using namespace spai;
 
 extern "C" size_t spai_fill_workspace_bytes(int32_t n_lines, int32_t B) {
-  const int64_t nparts = ((int64_t)std::max(n_lines, 1) + kNT - 1) / kNT;
+  const int64_t nparts = std::max(n_lines, 1);  // one partial per line (hash variant) or per block
   Carve c(nullptr);
   c.take<double>((size_t)nparts * std::max(B, 1));
   return c.off;
 }
 
-extern "C" int spai_fill_residual(int32_t fill_mode, int32_t line_begin, int32_t line_end, int32_t W,
+extern "C" int spai_fill_residual(int32_t fill_mode, int32_t n, int32_t line_begin, int32_t line_end, int32_t W,
                                   const int32_t* pat_idx, const int32_t* pat_act, const float* pat_val, int32_t WA,
                                   const int32_t* a_idx, const void* a_val, int32_t a_dtype, int32_t B,
                                   const uint32_t* removed, int32_t words, void* m_out, int32_t m_dtype,
@@ -223,17 +328,18 @@ extern "C" int spai_fill_residual(int32_t fill_mode, int32_t line_begin, int32_t
                  fill_mode);
   SPAI_CHECK_ARG(a_dtype == SPAI_DTYPE_F32 || a_dtype == SPAI_DTYPE_F64, "spai_fill_residual: bad a_dtype");
   SPAI_CHECK_ARG(m_dtype == SPAI_DTYPE_F32 || m_dtype == SPAI_DTYPE_F64, "spai_fill_residual: bad m_dtype");
-  SPAI_CHECK_ARG(line_begin >= 0 && line_end >= line_begin && W >= 1 && WA >= 1 && B >= 1 && words >= 0,
+  SPAI_CHECK_ARG(n >= 1 && line_begin >= 0 && line_end >= line_begin && line_end <= n && W >= 1 && WA >= 1 &&
+                     B >= 1 && words >= 0,
                  "spai_fill_residual: bad shape");
   SPAI_CHECK_ARG(res2_out && workspace, "spai_fill_residual: null output/workspace");
   hipStream_t s = (hipStream_t)stream;
-  const int32_t n = line_end - line_begin;
-  if (n == 0) {
+  const int32_t nl = line_end - line_begin;
+  if (nl == 0) {
     SPAI_CHECK_HIP(hipMemsetAsync(res2_out, 0, sizeof(double) * B, s));
     return SPAI_OK;
   }
   SPAI_CHECK_ARG(pat_idx && pat_act && pat_val && a_idx && a_val && removed, "spai_fill_residual: null input");
-  SPAI_CHECK_ARG(workspace_bytes >= spai_fill_workspace_bytes(n, B), "spai_fill_residual: workspace too small");
+  SPAI_CHECK_ARG(workspace_bytes >= spai_fill_workspace_bytes(nl, B), "spai_fill_residual: workspace too small");
   const int32_t want_m = fill_mode == SPAI_FILL_COPY ? SPAI_DTYPE_F32 : m_dtype;
   SPAI_CHECK_ARG(fill_mode != SPAI_FILL_COPY || m_dtype == SPAI_DTYPE_F32,
                  "spai_fill_residual: copy fill stores fp32 values (utils.py:350)");
@@ -245,15 +351,38 @@ extern "C" int spai_fill_residual(int32_t fill_mode, int32_t line_begin, int32_t
     }
   }
   if (!v) {
+    const int64_t bound = std::min<int64_t>((int64_t)W * WA + 1, (int64_t)n);
+    if (fill_mode == SPAI_FILL_COPY && bound < kHashMaxEntries) {
+      const int32_t tb = (int32_t)std::min<int64_t>(kHashMaxEntries, std::max<int64_t>(64, 2 * bound));
+      double* partials = static_cast<double*>(workspace);
+      hipError_t e = a_dtype == SPAI_DTYPE_F32
+                         ? launch_hash<float>(line_begin, line_end, W, WA, pat_idx, pat_act, pat_val, a_idx, a_val, B,
+                                              removed, words, m_out, partials, tb, s)
+                         : launch_hash<double>(line_begin, line_end, W, WA, pat_idx, pat_act, pat_val, a_idx, a_val,
+                                               B, removed, words, m_out, partials, tb, s);
+      SPAI_CHECK_HIP(e);
+      k_reduce<<<B, kNT, 0, s>>>(partials, nl, res2_out);
+      SPAI_CHECK_LAUNCH();
+      return SPAI_OK;
+    }
     set_error("spai_fill_residual: no compiled kernel for W=%d WA=%d a_dtype=%d m_dtype=%d mode=%d", W, WA, a_dtype,
               m_dtype, fill_mode);
     return SPAI_ERR_UNSUPPORTED;
   }
-  const int32_t nparts = (n + kNT - 1) / kNT;
+  const int32_t nparts = (nl + kNT - 1) / kNT;
   double* partials = static_cast<double*>(workspace);
   SPAI_CHECK_HIP(v->fn(line_begin, line_end, W, WA, pat_idx, pat_act, pat_val, a_idx, a_val, B, removed, words, m_out,
                        partials, nparts, s));
   k_reduce<<<B, kNT, 0, s>>>(partials, nparts, res2_out);
+  SPAI_CHECK_LAUNCH();
+  return SPAI_OK;
+}
+
+extern "C" int spai_rewards(const double* res2, const int32_t* removed_counts, int32_t B, int64_t nnz0, int32_t n,
+                            double r0, double f0, const float* alpha, double* residual, double* reward, void* stream) {
+  SPAI_CHECK_ARG(res2 && removed_counts && alpha && residual && reward && B >= 1 && n >= 1 && nnz0 >= 0,
+                 "spai_rewards: bad arguments");
+  k_rewards<<<1, 256, 0, (hipStream_t)stream>>>(res2, removed_counts, B, nnz0, n, r0, f0, alpha, residual, reward);
   SPAI_CHECK_LAUNCH();
   return SPAI_OK;
 }

@@ -1,5 +1,5 @@
-// Rollout kernels for gfx950: logits statistics, the reference-parity sampling step and
-// the one-pass Gumbel-top-k trajectory sampler with its ordered trajectory log.
+// Rollout kernels for gfx950: logits statistics, the reference-parity sampling step and the
+// actions -> removal-bitmap conversion (the one-pass sampler lives in trajectory.hip).
 //
 // Replaces the T-step Python loop of GFlowNet.sample_states (gflownet/gflownet.py:135-179)
 // and Log.log (gflownet/log.py:24-89).  Layout in HBM (per rollout of B samples, E edges):
@@ -10,8 +10,6 @@
 // Every kernel is HBM/L2-bound integer + transcendental work: coalesced 4-wide action
 // runs per lane, wave64 ballots/shuffles for the bitmap words and the block-local
 // compaction, no MFMA (there is no matrix product on this path).
-#include <hipcub/hipcub.hpp>
-
 #include "spai_device.h"
 #include "spai_status.h"
 
@@ -19,8 +17,6 @@ namespace spai {
 namespace {
 
 constexpr int kNT = 256;         // threads per block
-constexpr int kPer = 4;          // actions per thread (one Philox call)
-constexpr int kBlk = kNT * kPer; // actions per block
 constexpr int kStatChunk = 8192;
 constexpr int kParChunk = 4096;
 
@@ -166,235 +162,6 @@ __global__ __launch_bounds__(64) void k_parity_commit(const float* __restrict__ 
   }
 }
 
-// ------------------------------------------------------------------ throughput rollout
-struct RolloutWs {
-  int32_t nblk;
-  int32_t* block_counts;  // [B][nblk]
-  int32_t* block_offsets; // [B][nblk]
-  int32_t* seg_start;     // [B]
-  double* stot;           // [B]
-  uint64_t* loc_keys;     // [B][nblk*kBlk]  (reused as scan output after compaction)
-  int32_t* loc_acts;      // [B][nblk*kBlk]
-  uint64_t* keys_in;      // [B*E]           (reused as fp64 weights after the sort)
-  int32_t* acts_in;       // [B*E]           (reused as segment ids after the sort)
-  uint64_t* keys_out;     // [B*E]
-  int32_t* acts_out;      // [B*E]
-  void* temp;
-  size_t temp_bytes;
-  size_t total_bytes;
-};
-
-static hipError_t cub_temp_bytes(int64_t n, size_t* out) {
-  size_t sort_b = 0, scan_b = 0;
-  hipError_t e = hipcub::DeviceRadixSort::SortPairs(nullptr, sort_b, (const uint64_t*)nullptr, (uint64_t*)nullptr,
-                                                    (const int32_t*)nullptr, (int32_t*)nullptr, (int64_t)n, 0, 64,
-                                                    (hipStream_t)0);
-  if (e != hipSuccess) return e;
-  e = hipcub::DeviceScan::ExclusiveSumByKey(nullptr, scan_b, (const int32_t*)nullptr, (const double*)nullptr,
-                                            (double*)nullptr, (int64_t)n, hipcub::Equality(), (hipStream_t)0);
-  if (e != hipSuccess) return e;
-  *out = std::max(sort_b, scan_b);
-  return hipSuccess;
-}
-
-static hipError_t rollout_ws(void* base, int32_t E, int32_t B, RolloutWs* w) {
-  Carve c(base);
-  w->nblk = (E + kBlk - 1) / kBlk;
-  const int64_t nb = (int64_t)B * w->nblk;
-  const int64_t cap = (int64_t)B * E;
-  w->block_counts = c.take<int32_t>(nb);
-  w->block_offsets = c.take<int32_t>(nb);
-  w->seg_start = c.take<int32_t>(B);
-  w->stot = c.take<double>(B);
-  w->loc_keys = c.take<uint64_t>(nb * kBlk);
-  w->loc_acts = c.take<int32_t>(nb * kBlk);
-  w->keys_in = c.take<uint64_t>(cap);
-  w->acts_in = c.take<int32_t>(cap);
-  w->keys_out = c.take<uint64_t>(cap);
-  w->acts_out = c.take<int32_t>(cap);
-  hipError_t e = cub_temp_bytes(cap > 0 ? cap : 1, &w->temp_bytes);
-  if (e != hipSuccess) return e;
-  w->temp = c.take<char>(w->temp_bytes);
-  w->total_bytes = c.off;
-  return hipSuccess;
-}
-
-__global__ __launch_bounds__(kNT) void k_select(const float* __restrict__ logits, int64_t bstride, int32_t E,
-                                                int32_t nblk, uint32_t seed0, uint32_t seed1, uint32_t st0,
-                                                uint32_t st1, int32_t sample_base, uint32_t* __restrict__ removed,
-                                                int32_t words, int32_t* __restrict__ counts,
-                                                int32_t* __restrict__ block_counts,
-                                                uint64_t* __restrict__ loc_keys, int32_t* __restrict__ loc_acts) {
-  const int b = blockIdx.y, blk = blockIdx.x, tid = threadIdx.x;
-  const float* lg = logits + (int64_t)b * bstride;
-  const uint32_t bg = (uint32_t)(sample_base + b);
-  __shared__ float s_tk;
-  __shared__ int s_wc[kNT / 64];
-  if (tid == 0) {
-    const uint4 r = philox4x32_10((uint32_t)E >> 2, bg, st0, st1, seed0, seed1);
-    s_tk = gumbel_key(lg[E], pick_word(r, E & 3));
-  }
-  __syncthreads();
-  const float tk = s_tk;
-  const int a0 = blk * kBlk + tid * kPer;
-  uint32_t nib = 0;
-  float key[kPer];
-  if (a0 < E) {
-    const uint4 r = philox4x32_10((uint32_t)a0 >> 2, bg, st0, st1, seed0, seed1);
-#pragma unroll
-    for (int s = 0; s < kPer; ++s) {
-      key[s] = 0.0f;
-      if (a0 + s < E) {
-        key[s] = gumbel_key(lg[a0 + s], pick_word(r, s));
-        if (key[s] > tk) nib |= 1u << s;
-      }
-    }
-  }
-  // removal bitmap: 8 lanes x 4 bits = one 32-bit word
-  uint32_t x = nib << ((tid & 7) * kPer);
-  x |= __shfl_xor(x, 1, kWave);
-  x |= __shfl_xor(x, 2, kWave);
-  x |= __shfl_xor(x, 4, kWave);
-  if ((tid & 7) == 0) {
-    const int wi = (blk * kBlk + (tid & ~7) * kPer) >> 5;
-    if (wi < words) removed[(int64_t)b * words + wi] = x;
-  }
-  // block-local ordered compaction of the winners (key, action)
-  const int c = __popc(nib);
-  int incl = c;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int y = __shfl_up(incl, o, kWave);
-    if ((tid & 63) >= o) incl += y;
-  }
-  if ((tid & 63) == 63) s_wc[tid >> 6] = incl;
-  __syncthreads();
-  int wbase = 0, tot = 0;
-#pragma unroll
-  for (int w = 0; w < kNT / 64; ++w) {
-    if (w < (tid >> 6)) wbase += s_wc[w];
-    tot += s_wc[w];
-  }
-  int pos = wbase + incl - c;
-  const int64_t lbase = ((int64_t)b * nblk + blk) * kBlk;
-#pragma unroll
-  for (int s = 0; s < kPer; ++s) {
-    if ((nib >> s) & 1u) {
-      loc_keys[lbase + pos] = ((uint64_t)b << 32) | (uint64_t)(uint32_t)(~orderable(key[s]));
-      loc_acts[lbase + pos] = a0 + s;
-      ++pos;
-    }
-  }
-  if (tid == 0) {
-    block_counts[b * nblk + blk] = tot;
-    if (tot) atomicAdd(&counts[b], tot);
-  }
-}
-
-// Exclusive scan of the per-block winner counts of one sample (one 1024-thread block per sample).
-__global__ __launch_bounds__(1024) void k_scan_blocks(const int32_t* __restrict__ block_counts, int32_t nblk,
-                                                      int32_t* __restrict__ block_offsets) {
-  const int b = blockIdx.x, tid = threadIdx.x;
-  const int per = (nblk + 1023) / 1024;
-  const int beg = min(tid * per, nblk), end = min(beg + per, nblk);
-  const int32_t* bc = block_counts + (int64_t)b * nblk;
-  int32_t* bo = block_offsets + (int64_t)b * nblk;
-  int loc = 0;
-  for (int i = beg; i < end; ++i) loc += bc[i];
-  int incl = loc;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int y = __shfl_up(incl, o, kWave);
-    if ((tid & 63) >= o) incl += y;
-  }
-  __shared__ int s_wc[16];
-  if ((tid & 63) == 63) s_wc[tid >> 6] = incl;
-  __syncthreads();
-  int base = 0;
-  for (int w = 0; w < (tid >> 6); ++w) base += s_wc[w];
-  int run = base + incl - loc;
-  for (int i = beg; i < end; ++i) {
-    bo[i] = run;
-    run += bc[i];
-  }
-}
-
-__global__ void k_seg_start(const int32_t* __restrict__ counts, int32_t B, int32_t* __restrict__ seg_start,
-                            double* __restrict__ stot) {
-  if (threadIdx.x == 0 && blockIdx.x == 0) {
-    int run = 0;
-    for (int b = 0; b < B; ++b) {
-      seg_start[b] = run;
-      run += counts[b];
-      stot[b] = 0.0;
-    }
-  }
-}
-
-__global__ __launch_bounds__(kNT) void k_compact(int32_t nblk, const int32_t* __restrict__ block_counts,
-                                                 const int32_t* __restrict__ block_offsets,
-                                                 const int32_t* __restrict__ seg_start,
-                                                 const uint64_t* __restrict__ loc_keys,
-                                                 const int32_t* __restrict__ loc_acts, uint64_t* __restrict__ keys,
-                                                 int32_t* __restrict__ acts) {
-  const int b = blockIdx.y, blk = blockIdx.x;
-  const int n = block_counts[b * nblk + blk];
-  const int64_t dst = (int64_t)seg_start[b] + block_offsets[b * nblk + blk];
-  const int64_t src = ((int64_t)b * nblk + blk) * kBlk;
-  for (int i = threadIdx.x; i < n; i += kNT) {
-    keys[dst + i] = loc_keys[src + i];
-    acts[dst + i] = loc_acts[src + i];
-  }
-}
-
-__global__ __launch_bounds__(kNT) void k_weights(int64_t total, const uint64_t* __restrict__ keys,
-                                                 const int32_t* __restrict__ acts, const float* __restrict__ logits,
-                                                 int64_t bstride, const float* __restrict__ lmax,
-                                                 int32_t* __restrict__ segid, double* __restrict__ wv) {
-  const int64_t t = (int64_t)blockIdx.x * kNT + threadIdx.x;
-  if (t >= total) return;
-  const int b = (int)(keys[t] >> 32);
-  const int a = acts[t];
-  wv[t] = exp((double)logits[(int64_t)b * bstride + a] - (double)lmax[b]);
-  segid[t] = b;
-}
-
-__global__ __launch_bounds__(kNT) void k_log_write(int64_t total, const int32_t* __restrict__ segid,
-                                                   const int32_t* __restrict__ acts, const double* __restrict__ wv,
-                                                   const double* __restrict__ S, const double* __restrict__ z,
-                                                   const int32_t* __restrict__ seg_start,
-                                                   const int32_t* __restrict__ counts, int64_t t_cap,
-                                                   int64_t* __restrict__ actions, float* __restrict__ fwd,
-                                                   double* __restrict__ stot) {
-  const int64_t t = (int64_t)blockIdx.x * kNT + threadIdx.x;
-  if (t >= total) return;
-  const int b = segid[t];
-  const int64_t tl = t - seg_start[b];
-  const double w = wv[t], s = S[t];
-  actions[(int64_t)b * t_cap + tl] = acts[t];
-  fwd[(int64_t)b * t_cap + tl] = (float)(w / (z[b] - s));
-  if (tl == counts[b] - 1) stot[b] = s + w;
-}
-
-__global__ __launch_bounds__(kNT) void k_log_pad(int32_t T, int32_t E, const int32_t* __restrict__ counts,
-                                                 const double* __restrict__ stot, const double* __restrict__ z,
-                                                 const float* __restrict__ logits, int64_t bstride,
-                                                 const float* __restrict__ lmax, int64_t t_cap,
-                                                 int64_t* __restrict__ actions, float* __restrict__ fwd) {
-  const int b = blockIdx.y;
-  const int t = blockIdx.x * kNT + threadIdx.x;
-  const int k = counts[b];
-  if (t >= T || t < k) return;
-  if (t == k) {
-    const double wE = exp((double)logits[(int64_t)b * bstride + E] - (double)lmax[b]);
-    actions[(int64_t)b * t_cap + t] = E;
-    fwd[(int64_t)b * t_cap + t] = (float)(wE / (z[b] - stot[b]));
-  } else {
-    actions[(int64_t)b * t_cap + t] = -1;
-    fwd[(int64_t)b * t_cap + t] = 1.0f;
-  }
-}
-
 // ------------------------------------------------------------------ actions -> removal sets
 __global__ __launch_bounds__(kNT) void k_actions_to_bits(const int64_t* __restrict__ actions, int64_t sb,
                                                          int64_t st, int32_t T, int32_t E,
@@ -473,76 +240,6 @@ extern "C" int spai_parity_step(const float* logits, int64_t bstride, int32_t E1
   SPAI_CHECK_LAUNCH();
   k_parity_commit<<<B, 64, 0, s>>>(logits, bstride, E1, lmax, ps, pa, nchunk, chosen, words1, active, zrem,
                                    out_action, out_prob);
-  SPAI_CHECK_LAUNCH();
-  return SPAI_OK;
-}
-
-extern "C" size_t spai_rollout_workspace_bytes(int32_t E, int32_t B) {
-  if (E <= 0 || B <= 0) return 0;
-  RolloutWs w;
-  if (rollout_ws(nullptr, E, B, &w) != hipSuccess) return 0;
-  return w.total_bytes;
-}
-
-extern "C" int spai_rollout_select(const float* logits, int64_t bstride, int32_t E, int32_t B, uint64_t seed,
-                                   uint64_t stream_id, int32_t sample_base, uint32_t* removed, int32_t words,
-                                   int32_t* counts, void* workspace, size_t workspace_bytes, void* stream) {
-  SPAI_CHECK_ARG(logits && removed && counts && workspace, "spai_rollout_select: null pointer");
-  SPAI_CHECK_ARG(E > 0 && B > 0 && bstride >= 0 && sample_base >= 0, "spai_rollout_select: bad shape");
-  SPAI_CHECK_ARG(words == (E + 31) / 32, "spai_rollout_select: words must be ceil(E/32)");
-  RolloutWs w;
-  SPAI_CHECK_HIP(rollout_ws(workspace, E, B, &w));
-  SPAI_CHECK_ARG(workspace_bytes >= w.total_bytes, "spai_rollout_select: workspace too small (%zu < %zu)",
-                 workspace_bytes, w.total_bytes);
-  hipStream_t s = (hipStream_t)stream;
-  SPAI_CHECK_HIP(hipMemsetAsync(counts, 0, sizeof(int32_t) * B, s));
-  k_select<<<dim3(w.nblk, B), kNT, 0, s>>>(logits, bstride, E, w.nblk, (uint32_t)seed, (uint32_t)(seed >> 32),
-                                           (uint32_t)stream_id, (uint32_t)(stream_id >> 32), sample_base, removed,
-                                           words, counts, w.block_counts, w.loc_keys, w.loc_acts);
-  SPAI_CHECK_LAUNCH();
-  k_scan_blocks<<<B, 1024, 0, s>>>(w.block_counts, w.nblk, w.block_offsets);
-  SPAI_CHECK_LAUNCH();
-  k_seg_start<<<1, 64, 0, s>>>(counts, B, w.seg_start, w.stot);
-  SPAI_CHECK_LAUNCH();
-  k_compact<<<dim3(w.nblk, B), kNT, 0, s>>>(w.nblk, w.block_counts, w.block_offsets, w.seg_start, w.loc_keys,
-                                            w.loc_acts, w.keys_in, w.acts_in);
-  SPAI_CHECK_LAUNCH();
-  return SPAI_OK;
-}
-
-extern "C" int spai_rollout_order(const float* logits, int64_t bstride, int32_t E, int32_t B, const float* lmax,
-                                  const double* z, const int32_t* counts, int64_t total, int32_t T, int64_t t_cap,
-                                  int64_t* actions, float* fwd_probs, void* workspace, size_t workspace_bytes,
-                                  void* stream) {
-  SPAI_CHECK_ARG(logits && lmax && z && counts && actions && fwd_probs && workspace,
-                 "spai_rollout_order: null pointer");
-  SPAI_CHECK_ARG(E > 0 && B > 0 && total >= 0 && total <= (int64_t)B * E && T >= 1 && t_cap >= T && T <= E + 1,
-                 "spai_rollout_order: bad shape (E=%d B=%d total=%lld T=%d t_cap=%lld)", E, B, (long long)total, T,
-                 (long long)t_cap);
-  RolloutWs w;
-  SPAI_CHECK_HIP(rollout_ws(workspace, E, B, &w));
-  SPAI_CHECK_ARG(workspace_bytes >= w.total_bytes, "spai_rollout_order: workspace too small");
-  hipStream_t s = (hipStream_t)stream;
-  if (total > 0) {
-    int bbits = 0;
-    while ((1 << bbits) < B) ++bbits;
-    size_t tb = w.temp_bytes;
-    SPAI_CHECK_HIP(hipcub::DeviceRadixSort::SortPairs(w.temp, tb, w.keys_in, w.keys_out, w.acts_in, w.acts_out,
-                                                      total, 0, 32 + bbits, s));
-    int32_t* segid = w.acts_in;                                   // reuse
-    double* wv = reinterpret_cast<double*>(w.keys_in);            // reuse
-    double* S = reinterpret_cast<double*>(w.loc_keys);            // reuse
-    const int nb = (int)((total + kNT - 1) / kNT);
-    k_weights<<<nb, kNT, 0, s>>>(total, w.keys_out, w.acts_out, logits, bstride, lmax, segid, wv);
-    SPAI_CHECK_LAUNCH();
-    tb = w.temp_bytes;
-    SPAI_CHECK_HIP(hipcub::DeviceScan::ExclusiveSumByKey(w.temp, tb, segid, wv, S, total, hipcub::Equality(), s));
-    k_log_write<<<nb, kNT, 0, s>>>(total, segid, w.acts_out, wv, S, z, w.seg_start, counts, t_cap, actions,
-                                   fwd_probs, w.stot);
-    SPAI_CHECK_LAUNCH();
-  }
-  k_log_pad<<<dim3((T + kNT - 1) / kNT, B), kNT, 0, s>>>(T, E, counts, w.stot, z, logits, bstride, lmax, t_cap,
-                                                          actions, fwd_probs);
   SPAI_CHECK_LAUNCH();
   return SPAI_OK;
 }

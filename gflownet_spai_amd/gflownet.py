@@ -21,7 +21,7 @@ import torch
 from torch import Tensor, nn
 
 from . import kernels
-from .log import Log
+from .log import Log, trajectory_probs
 from .preconditioner import Data
 
 
@@ -39,6 +39,8 @@ class GFlowNet(nn.Module):
         self.seed = int(torch.initial_seed() if seed is None else seed) & (2**64 - 1)
         self.sample_base = sample_base
         self.rollouts = 0  # Philox stream id of the next throughput rollout
+        self._data_cache = {}
+        self._side = None  # HIP stream for the fill/reward, overlapped with the trajectory sort
 
     # ------------------------------------------------------------------ policy
     def policy_logits(self, data, batch_size: int):
@@ -81,9 +83,16 @@ class GFlowNet(nn.Module):
         for i, m in enumerate(s):
             if not m.is_sparse:
                 raise ValueError(f"Tensor at index {i} is not a sparse tensor.")
-            dev = self.env.device
-            out.append(Data(x=torch.ones((self.env.matrix_size * 2, 1), device=dev),
-                            edge_index=m._indices().to(dev), edge_attr=m._values().float().to(dev)))
+            key = (m._indices().data_ptr(), m._values().data_ptr(), m._nnz(), self.env.matrix_size)
+            hit = self._data_cache.get(key)
+            if hit is None:  # states are never modified by a rollout: build each graph once
+                dev = self.env.device
+                d = Data(x=torch.ones((self.env.matrix_size * 2, 1), device=dev),
+                         edge_index=m._indices().to(dev), edge_attr=m._values().float().to(dev))
+                hit = self._data_cache[key] = (m, d)  # holding m pins its storage (key stays unique)
+                if len(self._data_cache) > 8:
+                    self._data_cache.pop(next(iter(self._data_cache)))
+            out.append(hit[1])
         return out
 
     # ------------------------------------------------------------------ sampler
@@ -100,14 +109,29 @@ class GFlowNet(nn.Module):
         if self.mode == "parity":
             actions_bt, fwd_bt = self._parity_rollout(lg, B, lmax, z)
             removed, counts = kernels.actions_to_removed(actions_bt, E)
+            rewards = env.rewards_from_removed(removed, counts, alpha)
+            log._set_rollout(logits, actions_bt, fwd_bt)
         else:
-            removed, counts, ws = kernels.rollout_select(lg, B, self.seed, self.rollouts, self.sample_base)
+            removed, counts, ws = kernels.rollout_select(lg, B, lmax, self.seed, self.rollouts, self.sample_base)
             self.rollouts += 1
-            counts_h = counts.cpu()
-            actions_bt, fwd_bt = kernels.rollout_order(lg, B, lmax, z, counts, counts_h, ws)
-        log._set_rollout(logits, actions_bt, fwd_bt)
+            # the fill + ||.||_F reward needs only the removal bitmaps: run it on a second
+            # HIP stream while the main stream sorts the trajectories
+            main = torch.cuda.current_stream(lg.device)
+            if self._side is None or self._side.device != lg.device:
+                self._side = torch.cuda.Stream(lg.device)
+            side = self._side
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                rewards = env.rewards_from_removed(removed, counts, alpha)
+            for t in (removed, counts, alpha):
+                if torch.is_tensor(t) and t.is_cuda:
+                    t.record_stream(side)
+            actions_full, fwd_full, t_dev = kernels.rollout_order(lg, B, lmax, counts, ws)
+            main.wait_stream(side)
+            for t in (rewards, env.last_residual) + ((env.last_m,) if env.last_m is not None else ()):
+                t.record_stream(main)
+            log._set_rollout(logits, actions_full, fwd_full, t_dev)
         log.removed, log.counts = removed, counts
-        rewards = env.rewards_from_removed(removed, counts, alpha)
         log.rewards = rewards.detach().to(torch.float32)
         return log if return_log else None
 
@@ -126,4 +150,6 @@ class GFlowNet(nn.Module):
             probs.append(p)
             if not bool(active.any()):
                 break
-        return torch.stack(acts, 1), torch.stack(probs, 1)
+        actions_bt = torch.stack(acts, 1)
+        # logged probabilities from the remaining mass (no running-sum cancellation)
+        return actions_bt, trajectory_probs(lg, actions_bt)

@@ -73,7 +73,7 @@ def parity_step(lg: torch.Tensor, B: int, noise: torch.Tensor, lmax, chosen, act
     return out_a, out_p
 
 
-def rollout_select(lg: torch.Tensor, B: int, seed: int, stream_id: int, sample_base: int = 0):
+def rollout_select(lg: torch.Tensor, B: int, lmax: torch.Tensor, seed: int, stream_id: int, sample_base: int = 0):
     """Phase 1 of the throughput rollout: removal bitmaps [B, ceil(E/32)] and counts [B]."""
     _lib.require_device(lg)
     E = lg.shape[-1] - 1
@@ -85,26 +85,29 @@ def rollout_select(lg: torch.Tensor, B: int, seed: int, stream_id: int, sample_b
         raise RuntimeError("spai_rollout_workspace_bytes failed: " + _l().spai_last_error().decode())
     ws = _lib.workspace(nb, lg.device, "rollout")
     with _timed("rollout_select"):
-        st = _l().spai_rollout_select(_lib.ptr(lg), 0 if lg.dim() == 1 else E + 1, E, B, seed & (2**64 - 1),
+        st = _l().spai_rollout_select(_lib.ptr(lg), 0 if lg.dim() == 1 else E + 1, E, B, _lib.ptr(lmax),
+                                      seed & (2**64 - 1),
                                         stream_id & (2**64 - 1), sample_base, _lib.ptr(removed), words,
                                         _lib.ptr(counts), _lib.ptr(ws), ws.numel(), _lib.stream_ptr(lg.device))
     _lib.check(st, "spai_rollout_select")
     return removed, counts, ws
 
 
-def rollout_order(lg, B, lmax, z, counts, counts_host, ws):
-    """Phase 2: ordered trajectories. Returns actions [B, T] int64, fwd_probs [B, T] fp32."""
+def rollout_order(lg, B, lmax, counts, ws):
+    """Phase 2: ordered trajectories, no host round trip.
+
+    Returns actions [B, E+1] int64 and fwd_probs [B, E+1] fp32 (only the first T columns
+    are written) and T as a 1-element int32 device tensor."""
     E = lg.shape[-1] - 1
-    total = int(counts_host.sum())
-    T = int(counts_host.max()) + 1
-    actions = torch.empty(B, T, dtype=torch.int64, device=lg.device)
-    fwd = torch.empty(B, T, dtype=torch.float32, device=lg.device)
+    actions = torch.empty(B, E + 1, dtype=torch.int64, device=lg.device)
+    fwd = torch.empty(B, E + 1, dtype=torch.float32, device=lg.device)
+    t_dev = torch.empty(1, dtype=torch.int32, device=lg.device)
     with _timed("rollout_order"):
         st = _l().spai_rollout_order(_lib.ptr(lg), 0 if lg.dim() == 1 else E + 1, E, B, _lib.ptr(lmax),
-                                       _lib.ptr(z), _lib.ptr(counts), total, T, T, _lib.ptr(actions), _lib.ptr(fwd),
-                                       _lib.ptr(ws), ws.numel(), _lib.stream_ptr(lg.device))
+                                     _lib.ptr(counts), E + 1, _lib.ptr(actions), _lib.ptr(fwd), _lib.ptr(t_dev),
+                                     _lib.ptr(ws), ws.numel(), _lib.stream_ptr(lg.device))
     _lib.check(st, "spai_rollout_order")
-    return actions, fwd
+    return actions, fwd, t_dev
 
 
 def actions_to_removed(actions_bt: torch.Tensor, E: int):
@@ -139,10 +142,21 @@ def fill_residual(pattern: Lines, a_lines: Lines, removed: torch.Tensor, lsq: bo
     nb = _l().spai_fill_workspace_bytes(max(n_loc, 1), B)
     ws = _lib.workspace(nb, removed.device, "fill")
     with _timed("fill_residual"):
-        st = _l().spai_fill_residual(mode, line_begin, line_end, pattern.width, _lib.ptr(pattern.idx),
+        st = _l().spai_fill_residual(mode, pattern.n, line_begin, line_end, pattern.width, _lib.ptr(pattern.idx),
                                        _lib.ptr(pattern.act), _lib.ptr(pattern.val), a_lines.width,
                                        _lib.ptr(a_lines.idx), _lib.ptr(a_lines.val), _DT[a_lines.val.dtype], B,
                                        _lib.ptr(removed), words, _lib.ptr(m), _DT[m_dtype], _lib.ptr(res2),
                                        _lib.ptr(ws), ws.numel(), _lib.stream_ptr(removed.device))
     _lib.check(st, "spai_fill_residual")
     return res2, m
+
+
+def rewards(res2: torch.Tensor, counts: torch.Tensor, nnz0: int, n: int, r0: float, f0: int, alpha: torch.Tensor):
+    """(residual [B] fp64, reward [B] fp64) with the reference's reward formula and type promotion."""
+    B = res2.numel()
+    a = alpha.detach().to(device=res2.device, dtype=torch.float32).reshape(1)
+    residual = torch.empty(B, dtype=torch.float64, device=res2.device)
+    reward = torch.empty(B, dtype=torch.float64, device=res2.device)
+    _lib.check(_l().spai_rewards(_lib.ptr(res2), _lib.ptr(counts), B, nnz0, n, float(r0), float(f0), _lib.ptr(a),
+                                 _lib.ptr(residual), _lib.ptr(reward), _lib.stream_ptr(res2.device)), "spai_rewards")
+    return residual, reward

@@ -17,17 +17,26 @@ from torch import Tensor
 
 
 def trajectory_probs(logits: Tensor, actions_bt: Tensor) -> Tensor:
-    """Differentiable [B, T] probabilities of the logged actions (-1 -> 1.0), fp64 internally."""
+    """Differentiable [B, T] probabilities of the logged actions (-1 -> 1.0), fp64 inside.
+
+    p_t = w_{a_t} / (untouched mass + sum_{s>=t} w_{a_s}), w = exp(l - max l): the masked
+    softmax of step t (policy.py:65-73) written with the remaining mass, so it stays
+    accurate however much mass the trajectory removes."""
     l = logits.reshape(-1) if logits.dim() == 1 or logits.shape[0] == 1 else logits
     l64 = l.double()
     w = torch.exp(l64 - l64.detach().max(dim=-1, keepdim=True).values)
-    Z = w.sum(-1, keepdim=True)
+    B, T = actions_bt.shape
+    W = w.expand(B, -1) if w.dim() == 1 else w
     valid = actions_bt >= 0
     idx = actions_bt.clamp(min=0)
-    wa = (w.expand(actions_bt.shape[0], -1) if w.dim() == 1 or w.shape[0] == 1 else w).gather(1, idx)
-    wa = torch.where(valid, wa, torch.zeros((), dtype=wa.dtype, device=wa.device))
-    before = torch.cumsum(wa, 1) - wa
-    p = wa / (Z.view(-1, 1) - before)
+    zero = torch.zeros((), dtype=W.dtype, device=W.device)
+    wa = torch.where(valid, W.gather(1, idx), zero)
+    chosen = torch.zeros(W.shape, dtype=torch.bool, device=W.device)
+    rows = torch.arange(B, device=W.device).view(-1, 1).expand(B, T)
+    chosen[rows[valid], actions_bt[valid]] = True
+    untouched = torch.where(chosen, zero, W).sum(1, keepdim=True)
+    suffix = torch.flip(torch.cumsum(torch.flip(wa, [1]), 1), [1])
+    p = wa / (untouched + suffix)
     return torch.where(valid, p, torch.ones((), dtype=p.dtype, device=p.device)).float()
 
 
@@ -35,7 +44,8 @@ class Log:
     def __init__(self, s0, backward_policy, total_flow, env):
         self._fwd_probs = []
         self._back_probs = None
-        self._actions = []
+        self._act_list = []
+        self._act_tb = None  # [T, B] once known
         self.rewards = torch.zeros(len(s0))
         self.backward_policy = backward_policy
         self.total_flow = total_flow
@@ -43,6 +53,7 @@ class Log:
         self.num_samples = len(s0)
         # set by the MI355X sampler
         self._logits = None
+        self._full = None  # (actions [B, cap] i64, fwd [B, cap] f32, T int32 device scalar)
         self._actions_bt = None
         self.removed = None
         self.counts = None
@@ -56,16 +67,36 @@ class Log:
         self._fwd_probs.append(fwd)
         la = -torch.ones(self.num_samples, dtype=torch.long, device=actions.device)
         la[active] = actions.view(-1)[active]
-        self._actions.append(la)
+        self._act_list.append(la)
 
-    def _set_rollout(self, logits: Tensor, actions_bt: Tensor, fwd_bt: Tensor):
+    def _set_rollout(self, logits: Tensor, actions_bt: Tensor, fwd_bt: Tensor, t_dev: Tensor | None = None):
+        """actions_bt / fwd_bt: [B, T] or, with t_dev, [B, cap] buffers of which the first
+        T = int(t_dev) columns are the trajectory (T is read lazily: no sync in the rollout)."""
         self._logits = logits
-        self._actions_bt = actions_bt
-        self._actions = actions_bt.t()
-        self._fwd_probs = fwd_bt
+        if t_dev is None:
+            self._actions_bt, self._fwd_probs, self._act_tb = actions_bt, fwd_bt, actions_bt.t()
+        else:
+            self._full = (actions_bt, fwd_bt, t_dev)
+
+    def _materialize(self):
+        if self._full is not None:
+            a, f, t = self._full
+            T = int(t)
+            self._actions_bt, self._fwd_probs = a[:, :T], f[:, :T]
+            self._act_tb = self._actions_bt.t()
+            self._full = None
+
+    @property
+    def _actions(self):
+        """[T, B] after a rollout (gflownet.py:181 leaves log._actions as that tensor)."""
+        self._materialize()
+        if self._act_tb is None and self._act_list:
+            self._act_tb = torch.stack(self._act_list, dim=0)
+        return self._act_tb if self._act_tb is not None else self._act_list
 
     @property
     def fwd_probs(self) -> Tensor:
+        self._materialize()
         if isinstance(self._fwd_probs, list):
             self._fwd_probs = torch.stack(self._fwd_probs, dim=0).t()
         if self._logits is not None and self._logits.requires_grad and torch.is_grad_enabled():
@@ -74,8 +105,6 @@ class Log:
 
     @property
     def actions(self) -> Tensor:
-        if isinstance(self._actions, list):
-            self._actions = torch.stack(self._actions, dim=0)
         return self._actions
 
     @property

@@ -104,9 +104,11 @@ class PreconditionerEnv(Env):
             dist.all_reduce(res2, group=group)
         if self.keep_m:
             self.last_m = m
-        self.last_residual = torch.sqrt(res2)
-        nnz = self.init_nnz - counts.to(torch.int64)
-        return self._performance(self.last_residual, nnz, alpha).to(torch.float64) * 1000
+        if not torch.is_tensor(alpha):
+            alpha = torch.tensor(float(alpha), dtype=torch.float32)
+        self.last_residual, reward = kernels.rewards(res2, counts, self.init_nnz, self.matrix_size, self._r0,
+                                                     self.orig_flops, alpha)
+        return reward
 
     def _performance(self, residual: Tensor, nnz: Tensor, alpha) -> Tensor:
         """preconditioner.py:137-165 with the reference's type promotion: alpha 0-d fp32,

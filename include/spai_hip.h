@@ -85,21 +85,24 @@ int spai_parity_step(const float* logits, int64_t bstride, int32_t E1, int32_t B
  *
  * Phase 1 (spai_rollout_select): writes removed[B][words] (words = ceil(E/32)),
  * counts[B] (= k_b, the number removed) and stages the winners in the workspace.
- * Phase 2 (spai_rollout_order): total = sum_b counts[b] (read by the caller), T = max
- * k_b + 1.  Sorts each sample's winners by key descending (ties: action ascending),
- * then writes the trajectory log in [B][t_cap] layout (t_cap >= T):
- *   actions[b][t] = t-th removed action, actions[b][k_b] = E, -1 after;
- *   fwd_probs[b][t] = w_{a_t} / (Z_b - sum_{s<t} w_{a_s}), 1.0 after the terminal;
- * (log.py:67-87 semantics: the Log's actions [T,B] is the transpose).  lmax/z come
- * from spai_logits_stats.  One workspace serves both phases of one rollout. */
+ * Phase 2 (spai_rollout_order): sorts each sample's winners by key descending (ties:
+ * action ascending; MSD bucketing + LDS bitonic sort, no host round trip) and writes the
+ * trajectory log in [B][t_cap] layout (t_cap >= E + 1, only the first T columns are
+ * written, T = max_b k_b + 1 is stored to *t_out):
+ *   actions[b][t] = t-th removed action, actions[b][k_b] = E, -1 up to T;
+ *   fwd_probs[b][t] = w_{a_t} / (W_rest + sum_{s>=t} w_{a_s}), w = exp(l - lmax), W_rest =
+ *   mass of the actions never removed (terminal included) = the masked-softmax probability
+ *   of step t (policy.py:65-73, log.py:70), 1.0 after the terminal;
+ * (log.py:67-87 semantics: the Log's actions [T,B] is the transpose).  lmax comes from
+ * spai_logits_stats.  One workspace serves both phases of one rollout. */
 size_t spai_rollout_workspace_bytes(int32_t E, int32_t B);
-int spai_rollout_select(const float* logits, int64_t bstride, int32_t E, int32_t B, uint64_t seed,
-                        uint64_t stream_id, int32_t sample_base, uint32_t* removed, int32_t words,
-                        int32_t* counts, void* workspace, size_t workspace_bytes, void* stream);
+int spai_rollout_select(const float* logits, int64_t bstride, int32_t E, int32_t B, const float* lmax,
+                        uint64_t seed, uint64_t stream_id, int32_t sample_base, uint32_t* removed,
+                        int32_t words, int32_t* counts, void* workspace, size_t workspace_bytes,
+                        void* stream);
 int spai_rollout_order(const float* logits, int64_t bstride, int32_t E, int32_t B, const float* lmax,
-                       const double* z, const int32_t* counts, int64_t total, int32_t T, int64_t t_cap,
-                       int64_t* actions, float* fwd_probs, void* workspace, size_t workspace_bytes,
-                       void* stream);
+                       const int32_t* counts, int64_t t_cap, int64_t* actions, float* fwd_probs,
+                       int32_t* t_out, void* workspace, size_t workspace_bytes, void* stream);
 
 /* ---------------------------------------------------------------- actions -> removal sets
  * removed[b] = { a : 0 <= a < E, a in actions[b, :] } (preconditioner.py:37-43 +
@@ -120,14 +123,25 @@ int spai_actions_to_removed(const int64_t* actions, int64_t stride_b, int64_t st
  * the lines (e.g. the ranks of a column-sharded job) gives the full square norm.
  * M is evaluated from its STORED precision (m_dtype).  m_out (may be NULL) receives
  * [B][line_end - line_begin][W] values in m_dtype (0 where not kept).
- * a_idx/a_val: [n_lines][WA] lines of the original matrix A in the same orientation.
- * Shapes outside the compiled widths (W, WA <= 7) return SPAI_ERR_UNSUPPORTED. */
+ * a_idx/a_val: [n][WA] lines of the original matrix A (n x n) in the same orientation.
+ * Widths W, WA <= 7 run the register kernel (one thread per line, all samples); wider
+ * COPY lines run the LDS hash kernel (one workgroup per line and sample, bounded by
+ * min(W*WA + 1, n) < 13000 distinct entries per line); anything else returns
+ * SPAI_ERR_UNSUPPORTED. */
 size_t spai_fill_workspace_bytes(int32_t n_lines, int32_t B);
-int spai_fill_residual(int32_t fill_mode, int32_t line_begin, int32_t line_end, int32_t W,
+int spai_fill_residual(int32_t fill_mode, int32_t n, int32_t line_begin, int32_t line_end, int32_t W,
                        const int32_t* pat_idx, const int32_t* pat_act, const float* pat_val, int32_t WA,
                        const int32_t* a_idx, const void* a_val, int32_t a_dtype, int32_t B,
                        const uint32_t* removed, int32_t words, void* m_out, int32_t m_dtype,
                        double* res2_out, void* workspace, size_t workspace_bytes, void* stream);
+
+/* ---------------------------------------------------------------- rewards
+ * residual[b] = sqrt(res2[b]) and reward[b] = 1000 * (alpha (1 - r/r0) + (1 - alpha)(1 - f/f0))
+ * with f = 2 n (nnz0 - removed_counts[b]) (preconditioner.py:55-66, 68-77, 137-165; alpha is
+ * the device fp32 scalar the rollout passes, not the never-set self.alpha of :163).  The
+ * fp32/fp64 mix of the reference's torch type promotion is reproduced op for op. */
+int spai_rewards(const double* res2, const int32_t* removed_counts, int32_t B, int64_t nnz0, int32_t n,
+                 double r0, double f0, const float* alpha, double* residual, double* reward, void* stream);
 
 #ifdef __cplusplus
 }

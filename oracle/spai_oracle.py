@@ -220,14 +220,15 @@ def throughput_rollout(logits, B, seed, stream, sample_base=0):
 
     Returns (removed [B,E] bool, actions [T,B] int64, fwd_probs [B,T] fp32, counts [B]).
     Order: key descending, ties by action id ascending; trajectory = winners then E.
-    fwd_probs[t] = w_{a_t} / (Z - sum_{s<t} w_{a_s}) with w = exp(l - lmax) in fp64
-    (the probability the sequential reference assigns to that step, log.py:70).
+    fwd_probs[t] = w_{a_t} / (W_rest + sum_{s>=t} w_{a_s}), w = exp(l - lmax) in fp64 and
+    W_rest the mass of the actions never removed (terminal included): the masked-softmax
+    probability the sequential reference assigns to that step (policy.py:65-73, log.py:70),
+    formed from the remaining mass directly (no Z - prefix cancellation).
     """
     logits = np.asarray(logits, np.float32)
     E = logits.size - 1
     lmax = np.float64(logits.max())
     w = np.exp(logits.astype(np.float64) - lmax)
-    Z = w.sum()
     removed = np.zeros((B, E), np.bool_)
     orders, probs = [], []
     for b in range(B):
@@ -236,8 +237,9 @@ def throughput_rollout(logits, B, seed, stream, sample_base=0):
         removed[b, win] = True
         o = win[np.lexsort((win, -key[win]))]
         ww = w[o]
-        pref = np.concatenate([[0.0], np.cumsum(ww)])
-        p = np.concatenate([ww / (Z - pref[:-1]), [w[E] / (Z - pref[-1])]])
+        rest = w[E] + w[:E][~removed[b]].sum()
+        suffix = np.cumsum(ww[::-1])[::-1]
+        p = np.concatenate([ww / (rest + suffix), [w[E] / rest]])
         orders.append(np.concatenate([o, [E]]))
         probs.append(p)
     counts = np.array([len(o) - 1 for o in orders])

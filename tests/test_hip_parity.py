@@ -147,9 +147,12 @@ def test_throughput_rollout_bit_exact_vs_oracle(E, B, seed, stream):
     logits = rng.standard_normal(E + 1).astype(np.float32)
     logits[E] = 3.5
     lg, lmax, z = kernels.logits_stats(torch.from_numpy(logits).to(DEV), B)
-    removed, counts, ws = kernels.rollout_select(lg, B, seed, stream, sample_base=3)
+    removed, counts, ws = kernels.rollout_select(lg, B, lmax, seed, stream, sample_base=3)
+    actions, fwd, t_dev = kernels.rollout_order(lg, B, lmax, counts, ws)
     counts_h = counts.cpu()
-    actions, fwd = kernels.rollout_order(lg, B, lmax, z, counts, counts_h, ws)
+    T = int(t_dev)
+    assert T == int(counts_h.max()) + 1
+    actions, fwd = actions[:, :T], fwd[:, :T]
     r_o, a_o, f_o, c_o = O.throughput_rollout(logits, B, seed, stream, sample_base=3)
     assert np.array_equal(counts_h.numpy(), c_o)
     bits = removed.cpu().numpy().view(np.uint32)
@@ -157,6 +160,24 @@ def test_throughput_rollout_bit_exact_vs_oracle(E, B, seed, stream):
     assert np.array_equal(got, r_o)
     assert np.array_equal(actions.cpu().numpy(), a_o.T)
     np.testing.assert_allclose(fwd.cpu().numpy(), f_o, rtol=1e-6)
+
+
+def test_throughput_rollout_clustered_keys_overflow_path():
+    """Keys clustered in a tiny part of the key range (one huge logit) overfill the MSD
+    buckets; the exact rank-counting fallback must still give the oracle's order."""
+    from gflownet_spai_amd import kernels
+    E, B = 20000, 2
+    logits = np.zeros(E + 1, np.float32)
+    logits[7] = 1e30
+    lg, lmax, z = kernels.logits_stats(torch.from_numpy(logits).to(DEV), B)
+    removed, counts, ws = kernels.rollout_select(lg, B, lmax, 99, 1)
+    actions, fwd, t_dev = kernels.rollout_order(lg, B, lmax, counts, ws)
+    T = int(t_dev)
+    r_o, a_o, f_o, c_o = O.throughput_rollout(logits, B, 99, 1)
+    assert c_o.min() > 4096  # several buckets beyond the 2048-element LDS capacity
+    assert np.array_equal(counts.cpu().numpy(), c_o)
+    assert np.array_equal(actions[:, :T].cpu().numpy(), a_o.T)
+    np.testing.assert_allclose(fwd[:, :T].cpu().numpy(), f_o, rtol=1e-6)
 
 
 def test_throughput_sample_states_end_to_end():
@@ -264,5 +285,7 @@ def test_edge_cases():
                                                                         device=DEV),
                             torch.ones(1, dtype=torch.uint8, device=DEV), z.clone())
     D = torch.ones(10, 10).to_sparse()
-    with pytest.raises(NotImplementedError):
-        PreconditionerEnv(10, D, D)
+    dense_env = PreconditionerEnv(10, D, D)  # wide lines -> LDS hash kernel (copy fill)
+    assert float(dense_env.orig_residual) == pytest.approx(np.sqrt(90 * 100 + 10 * 81), rel=1e-15)
+    with pytest.raises(NotImplementedError):  # no LSQ kernel for 10-wide lines
+        PreconditionerEnv(10, D, D, side="AM", fill="lsq").update(None, torch.tensor([[0, 100]]), 0.5)

@@ -8,11 +8,13 @@
 // Pipeline (all stream-ordered, no host synchronisation; B samples per launch):
 //   k_select        Philox4x32-10 + deterministic fp32 keys for 4 actions per lane; removal
 //                   bitmap words via wave shuffles; block-local ordered staging of the
-//                   winners (orderable key, action, logit); per-block count/min/max.
+//                   winners (orderable key, action); per-block count/min/max and the mass
+//                   of the untouched actions.
 //   k_sample_stats  per-sample count, key range and bucket count (no global atomics).
-//   k_part_hist     MSD bucketing: per (sample, part) LDS histogram over the key range.
-//   k_bucket_scan   per-sample bucket offsets and per-part scatter offsets (deterministic).
-//   k_scatter       scatter winners into their buckets (LDS cursors).
+//   k_part<0>       MSD bucketing: per (sample, part) LDS histogram, buckets linear in the
+//                   key value over [min, max] of the sample's winners.
+//   k_bucket_count  per-bucket part offsets and totals; k_bucket_scan: bucket starts.
+//   k_part<1>       scatter winners into their buckets (LDS cursors).
 //   k_bucket_sort   bitonic sort of each bucket in LDS by (key desc, action asc), fp64
 //                   weights w = exp(l - lmax) and in-bucket inclusive SUFFIX sums.
 //   k_wscan         per-sample suffix scan of the bucket weight sums (fixed order).
@@ -33,13 +35,14 @@ namespace {
 constexpr int kNT = 256;
 constexpr int kPer = 4;
 constexpr int kBlk = kNT * kPer;   // actions per select block
-constexpr int kParts = 32;         // histogram/scatter parts per sample
-constexpr int kPT = 1024;          // threads of the part kernels
+constexpr int kParts = 64;         // histogram/scatter parts per sample
+constexpr int kPT = 1024;          // threads of the part kernels (2 blocks per CU with a 64 KiB LDS histogram)
 constexpr int kMaxBuckets = 16384; // per sample
-constexpr int kPerBucket = 160;    // target mean bucket occupancy
+constexpr int kPerBucket = 96;     // target mean bucket occupancy
 constexpr int kCap = 2048;         // LDS bitonic capacity per bucket
 constexpr int kSortNT = 256;
-constexpr int kSortGrid = 1024;    // bucket-sort blocks per sample (grid-stride over buckets)
+constexpr int kSortGrid = 512;     // bucket-sort blocks per sample (grid-stride over buckets)
+constexpr int kRankMax = kSortNT;  // buckets up to this size are ranked by counting, larger ones bitonic-sorted
 
 struct TrajWs {
   int32_t nblk;
@@ -47,17 +50,15 @@ struct TrajWs {
   uint32_t *block_min, *block_max;
   double* block_wrest;
   double* wrest;
-  uint32_t *lo, *hi;
+  double *klo, *kscale;
   int32_t *nbk, *seg, *tdev;
   uint32_t* st_ord;
   int32_t* st_act;
-  float* st_logit;
   int32_t* part_hist;
   int32_t* bucket_start;
+  int32_t* bucket_tot;
   double *bucket_wsum, *bucket_wsuf;
-  uint32_t* bk_ord;
-  int32_t* bk_act;
-  float* bk_logit;
+  uint64_t* bk_key;  // (~orderable(key) << 32) | action: ascending == trajectory order
   int32_t* out_act;
   double *out_w, *out_suf;
   size_t total_bytes;
@@ -72,21 +73,19 @@ static void traj_ws(void* base, int32_t E, int32_t B, TrajWs* w) {
   w->block_max = c.take<uint32_t>(nb);
   w->block_wrest = c.take<double>(nb);
   w->wrest = c.take<double>(B);
-  w->lo = c.take<uint32_t>(B);
-  w->hi = c.take<uint32_t>(B);
+  w->klo = c.take<double>(B);
+  w->kscale = c.take<double>(B);
   w->nbk = c.take<int32_t>(B);
   w->seg = c.take<int32_t>(B);
   w->tdev = c.take<int32_t>(1);
   w->st_ord = c.take<uint32_t>(stage);
   w->st_act = c.take<int32_t>(stage);
-  w->st_logit = c.take<float>(stage);
   w->part_hist = c.take<int32_t>((size_t)B * kParts * kMaxBuckets);
   w->bucket_start = c.take<int32_t>((size_t)B * (kMaxBuckets + 1));
+  w->bucket_tot = c.take<int32_t>((size_t)B * kMaxBuckets);
   w->bucket_wsum = c.take<double>((size_t)B * kMaxBuckets);
   w->bucket_wsuf = c.take<double>((size_t)B * kMaxBuckets);
-  w->bk_ord = c.take<uint32_t>(cap);
-  w->bk_act = c.take<int32_t>(cap);
-  w->bk_logit = c.take<float>(cap);
+  w->bk_key = c.take<uint64_t>(cap);
   w->out_act = c.take<int32_t>(cap);
   w->out_w = c.take<double>(cap);
   w->out_suf = c.take<double>(cap);
@@ -156,10 +155,16 @@ __device__ __forceinline__ double block_excl_scan_d(double v, double* lds, doubl
   return base + (incl - v);
 }
 
-// Bucket of an orderable key: bucket 0 holds the LARGEST keys.  Monotone in o.
-__device__ __forceinline__ int bucket_of(uint32_t o, uint32_t lo, double scale, int nbk) {
-  int k = (int)((double)(o - lo) * scale);
-  k = min(k, nbk - 1);
+__device__ __forceinline__ float from_orderable(uint32_t o) {
+  return __uint_as_float((o & 0x80000000u) ? (o & 0x7FFFFFFFu) : ~o);
+}
+
+// Bucket of a key: linear in the key VALUE over [kmin, kmax] (the orderable bits are
+// log-like per exponent and badly skewed when the range crosses zero); bucket 0 holds
+// the LARGEST keys.  Monotone in the key, which is all the ordering needs.
+__device__ __forceinline__ int bucket_of(uint32_t o, double klo, double scale, int nbk) {
+  int k = (int)(((double)from_orderable(o) - klo) * scale);
+  k = max(0, min(k, nbk - 1));
   return nbk - 1 - k;
 }
 
@@ -171,7 +176,7 @@ __global__ __launch_bounds__(kNT) void k_select(const float* __restrict__ logits
                                                 int32_t* __restrict__ block_counts,
                                                 uint32_t* __restrict__ block_min, uint32_t* __restrict__ block_max,
                                                 double* __restrict__ block_wrest, uint32_t* __restrict__ st_ord,
-                                                int32_t* __restrict__ st_act, float* __restrict__ st_logit) {
+                                                int32_t* __restrict__ st_act) {
   const int b = blockIdx.y, blk = blockIdx.x, tid = threadIdx.x;
   const float* lg = logits + (int64_t)b * bstride;
   const uint32_t bg = (uint32_t)(sample_base + b);
@@ -206,7 +211,7 @@ __global__ __launch_bounds__(kNT) void k_select(const float* __restrict__ logits
           mn = min(mn, ord[s]);
           mx = max(mx, ord[s]);
         } else {
-          wr += exp((double)lv[s] - lm);
+          wr += (double)expf((float)((double)lv[s] - lm));
         }
       }
     }
@@ -243,7 +248,6 @@ __global__ __launch_bounds__(kNT) void k_select(const float* __restrict__ logits
     if ((nib >> s) & 1u) {
       st_ord[lbase + pos] = ord[s];
       st_act[lbase + pos] = a0 + s;
-      st_logit[lbase + pos] = lv[s];
       ++pos;
     }
   }
@@ -270,8 +274,8 @@ __global__ __launch_bounds__(1024) void k_sample_stats(int32_t nblk, int32_t E, 
                                                        const uint32_t* __restrict__ block_min,
                                                        const uint32_t* __restrict__ block_max,
                                                        const double* __restrict__ block_wrest,
-                                                       int32_t* __restrict__ counts, uint32_t* __restrict__ lo,
-                                                       uint32_t* __restrict__ hi, int32_t* __restrict__ nbk,
+                                                       int32_t* __restrict__ counts, double* __restrict__ klo,
+                                                       double* __restrict__ kscale, int32_t* __restrict__ nbk,
                                                        double* __restrict__ wrest) {
   const int b = blockIdx.x;
   __shared__ int si[16];
@@ -310,74 +314,84 @@ __global__ __launch_bounds__(1024) void k_sample_stats(int32_t nblk, int32_t E, 
     int k = 1;
     while (k < kMaxBuckets && (int64_t)k * kPerBucket < tot) k <<= 1;
     counts[b] = tot;
-    lo[b] = tot ? mn : 0u;
-    hi[b] = tot ? mx : 0u;
+    const double vlo = tot ? (double)from_orderable(mn) : 0.0, vhi = tot ? (double)from_orderable(mx) : 0.0;
+    klo[b] = vlo;
+    kscale[b] = vhi > vlo ? (double)k / (vhi - vlo) : 0.0;
     nbk[b] = k;
   }
 }
 
-// Maps a part's flat winner index to (select block, offset) through an LDS prefix.
-__device__ __forceinline__ int find_block(const int* pre, int n, int f) {
-  int lo = 0, hi = n;  // pre[lo] <= f < pre[hi]
-  while (hi - lo > 1) {
-    const int mid = (lo + hi) >> 1;
-    if (pre[mid] <= f) lo = mid;
-    else hi = mid;
-  }
-  return lo;
-}
-
-// Shared body of k_part_hist (SCATTER = false) and k_scatter (SCATTER = true).
+// Shared body of the MSD histogram (SCATTER = false) and scatter (SCATTER = true) passes.
+// Part p of sample b owns a contiguous range of select blocks; each wave walks whole select
+// blocks (their winners are contiguous in the staging area) 4 elements per lane at a time,
+// so loads are coalesced and independent.  Histograms/cursors live in LDS; the scatter
+// writes one 8-byte sort key per winner.
 template <bool SCATTER>
 __global__ __launch_bounds__(kPT) void k_part(int32_t nblk, const int32_t* __restrict__ block_counts,
-                                              const uint32_t* __restrict__ lo_, const uint32_t* __restrict__ hi_,
+                                              const double* __restrict__ klo_, const double* __restrict__ kscale_,
                                               const int32_t* __restrict__ nbk_, const int32_t* __restrict__ seg_,
+                                              const int32_t* __restrict__ bucket_start,
                                               const uint32_t* __restrict__ st_ord, const int32_t* __restrict__ st_act,
-                                              const float* __restrict__ st_logit, int32_t* __restrict__ part_hist,
-                                              uint32_t* __restrict__ bk_ord, int32_t* __restrict__ bk_act,
-                                              float* __restrict__ bk_logit) {
+                                              int32_t* __restrict__ part_hist, uint64_t* __restrict__ bk_key) {
   const int p = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
   __shared__ int cnt[kMaxBuckets];
-  __shared__ int pre[kPT + 1];
-  __shared__ int sw[kPT / 64];
   const int nbk = nbk_[b];
-  const uint32_t lo = lo_[b];
-  const double scale = (double)nbk / ((double)(hi_[b] - lo) + 1.0);
+  const double klo = klo_[b], scale = kscale_[b];
   int32_t* ph = part_hist + ((int64_t)b * kParts + p) * kMaxBuckets;
-  for (int k = tid; k < nbk; k += kPT) cnt[k] = SCATTER ? ph[k] : 0;
+  const int32_t* bs = bucket_start + (int64_t)b * (kMaxBuckets + 1);
+  for (int k = tid; k < nbk; k += kPT) cnt[k] = SCATTER ? ph[k] + bs[k] : 0;
+  __syncthreads();
   const int bb = (int)((int64_t)p * nblk / kParts), be = (int)((int64_t)(p + 1) * nblk / kParts);
   const int64_t seg = SCATTER ? (int64_t)seg_[b] : 0;
-  for (int c0 = bb; c0 < be; c0 += kPT) {
-    const int nb = min(kPT, be - c0);
-    const int v = tid < nb ? block_counts[b * nblk + c0 + tid] : 0;
-    int total;
-    const int ex = block_excl_scan<kPT>(v, sw, &total);
-    pre[tid] = ex;
-    if (tid == 0) pre[nb] = total;
-    __syncthreads();
-    for (int f = tid; f < total; f += kPT) {
-      const int i = find_block(pre, nb, f);
-      const int64_t src = ((int64_t)b * nblk + c0 + i) * kBlk + (f - pre[i]);
-      const uint32_t o = st_ord[src];
-      const int k = bucket_of(o, lo, scale, nbk);
-      const int slot = atomicAdd(&cnt[k], 1);
-      if constexpr (SCATTER) {
-        const int64_t dst = seg + slot;
-        bk_ord[dst] = o;
-        bk_act[dst] = st_act[src];
-        bk_logit[dst] = st_logit[src];
+  for (int blk = bb + wave; blk < be; blk += kPT / 64) {
+    const int n = block_counts[b * nblk + blk];
+    const int64_t src0 = ((int64_t)b * nblk + blk) * kBlk;
+    for (int i0 = 0; i0 < n; i0 += 256) {
+      uint32_t o[4];
+      int a[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int i = i0 + u * 64 + lane;
+        o[u] = i < n ? st_ord[src0 + i] : 0u;
+        if constexpr (SCATTER) a[u] = i < n ? st_act[src0 + i] : 0;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (i0 + u * 64 + lane < n) {
+          const int slot = atomicAdd(&cnt[bucket_of(o[u], klo, scale, nbk)], 1);
+          if constexpr (SCATTER) bk_key[seg + slot] = ((uint64_t)(~o[u]) << 32) | (uint32_t)a[u];
+        }
       }
     }
-    __syncthreads();
   }
   if constexpr (!SCATTER) {
+    __syncthreads();
     for (int k = tid; k < nbk; k += kPT) ph[k] = cnt[k];
   }
 }
 
-// Per-sample: bucket totals -> exclusive bucket starts; part counts -> absolute scatter offsets.
+// Per bucket k (one thread each): exclusive prefix of the part counts (in place) and the
+// bucket total.  Coalesced across k.
+__global__ __launch_bounds__(256) void k_bucket_count(const int32_t* __restrict__ nbk_, int32_t* __restrict__ part_hist,
+                                                      int32_t* __restrict__ bucket_tot) {
+  const int b = blockIdx.y, k = blockIdx.x * 256 + threadIdx.x;
+  if (k >= nbk_[b]) return;
+  int32_t* ph = part_hist + (int64_t)b * kParts * kMaxBuckets + k;
+  int run = 0;
+#pragma unroll 8
+  for (int p = 0; p < kParts; ++p) {
+    const int c = ph[(int64_t)p * kMaxBuckets];
+    ph[(int64_t)p * kMaxBuckets] = run;
+    run += c;
+  }
+  bucket_tot[(int64_t)b * kMaxBuckets + k] = run;
+}
+
+// Per sample: exclusive scan of the bucket totals -> bucket starts; segment offsets and T.
 __global__ __launch_bounds__(1024) void k_bucket_scan(int32_t B, const int32_t* __restrict__ counts,
-                                                      const int32_t* __restrict__ nbk_, int32_t* __restrict__ part_hist,
+                                                      const int32_t* __restrict__ nbk_,
+                                                      const int32_t* __restrict__ bucket_tot,
                                                       int32_t* __restrict__ bucket_start, int32_t* __restrict__ seg,
                                                       int32_t* __restrict__ tdev, int32_t* __restrict__ t_out) {
   const int b = blockIdx.x, tid = threadIdx.x;
@@ -385,26 +399,15 @@ __global__ __launch_bounds__(1024) void k_bucket_scan(int32_t B, const int32_t* 
   const int nbk = nbk_[b];
   const int per = (nbk + 1023) / 1024;  // <= 16
   const int kb = min(tid * per, nbk), ke = min(kb + per, nbk);
-  int32_t* ph = part_hist + (int64_t)b * kParts * kMaxBuckets;
-  int tot[16];
+  const int32_t* bt = bucket_tot + (int64_t)b * kMaxBuckets;
   int loc = 0;
-  for (int k = kb, i = 0; k < ke; ++k, ++i) {
-    int run = 0;
-    for (int p = 0; p < kParts; ++p) {
-      const int c = ph[p * kMaxBuckets + k];
-      ph[p * kMaxBuckets + k] = run;
-      run += c;
-    }
-    tot[i] = run;
-    loc += run;
-  }
+  for (int k = kb; k < ke; ++k) loc += bt[k];
   int total;
   int base = block_excl_scan<1024>(loc, sw, &total);
   int32_t* bs = bucket_start + (int64_t)b * (kMaxBuckets + 1);
-  for (int k = kb, i = 0; k < ke; ++k, ++i) {
+  for (int k = kb; k < ke; ++k) {
     bs[k] = base;
-    for (int p = 0; p < kParts; ++p) ph[p * kMaxBuckets + k] += base;
-    base += tot[i];
+    base += bt[k];
   }
   if (tid == 0) {
     bs[nbk] = total;
@@ -421,91 +424,104 @@ __global__ __launch_bounds__(1024) void k_bucket_scan(int32_t B, const int32_t* 
   }
 }
 
-// Sort one bucket per iteration in LDS; emit sorted actions, fp64 weights, in-bucket prefixes.
+// Sort one bucket per iteration in LDS (rank by counting up to kRankMax elements, bitonic up
+// to kCap, exact tiled rank counting beyond), then emit sorted actions, fp64 weights
+// w = exp(l - lmax) (logit gathered by action) and in-bucket inclusive suffix sums.
 __global__ __launch_bounds__(kSortNT) void k_bucket_sort(const int32_t* __restrict__ nbk_,
                                                           const int32_t* __restrict__ seg_,
                                                           const int32_t* __restrict__ bucket_start,
-                                                          const uint32_t* __restrict__ bk_ord,
-                                                          const int32_t* __restrict__ bk_act,
-                                                          const float* __restrict__ bk_logit,
+                                                          const uint64_t* __restrict__ bk_key,
+                                                          const float* __restrict__ logits, int64_t bstride,
                                                           const float* __restrict__ lmax_, int32_t* __restrict__ out_act,
                                                           double* __restrict__ out_w, double* __restrict__ out_suf,
                                                           double* __restrict__ bucket_wsum) {
   const int b = blockIdx.y, tid = threadIdx.x;
   __shared__ uint64_t key[kCap];
-  __shared__ float lgv[kCap];
   __shared__ double sd[kSortNT / 64];
   const int nbk = nbk_[b];
   const int64_t seg = seg_[b];
   const double lmax = (double)lmax_[b];
+  const float* lg = logits + (int64_t)b * bstride;
   const int32_t* bs = bucket_start + (int64_t)b * (kMaxBuckets + 1);
   for (int k = blockIdx.x; k < nbk; k += gridDim.x) {
     const int s = bs[k], n = bs[k + 1] - s;
     const int64_t base = seg + s;
     double wsum = 0.0;
     if (n > 0 && n <= kCap) {
-      int np2 = 1;
-      while (np2 < n) np2 <<= 1;
-      for (int i = tid; i < np2; i += kSortNT) {
-        if (i < n) {
-          key[i] = ((uint64_t)(~bk_ord[base + i]) << 32) | (uint32_t)bk_act[base + i];
-          lgv[i] = bk_logit[base + i];
-        } else {
-          key[i] = ~0ull;
-          lgv[i] = 0.0f;
-        }
-      }
-      __syncthreads();
-      for (int size = 2; size <= np2; size <<= 1) {
-        for (int stride = size >> 1; stride > 0; stride >>= 1) {
-          for (int i = tid; i < (np2 >> 1); i += kSortNT) {
-            const int j = 2 * i - (i & (stride - 1));
-            const int q = j + stride;
-            const bool asc = (j & size) == 0;
-            const uint64_t kj = key[j], kq = key[q];
-            if ((kj > kq) == asc) {
-              key[j] = kq;
-              key[q] = kj;
-              const float t = lgv[j];
-              lgv[j] = lgv[q];
-              lgv[q] = t;
+      if (n <= kRankMax) {
+        const uint64_t mine = tid < n ? bk_key[base + tid] : ~0ull;
+        key[tid] = mine;
+        __syncthreads();
+        int rank = 0;
+        for (int j = 0; j < n; ++j) rank += key[j] < mine;  // broadcast LDS reads
+        __syncthreads();
+        if (tid < n) key[rank] = mine;
+        __syncthreads();
+      } else {
+        int np2 = 1;
+        while (np2 < n) np2 <<= 1;
+        for (int i = tid; i < np2; i += kSortNT) key[i] = i < n ? bk_key[base + i] : ~0ull;
+        __syncthreads();
+        for (int size = 2; size <= np2; size <<= 1) {
+          for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            for (int i = tid; i < (np2 >> 1); i += kSortNT) {
+              const int j = 2 * i - (i & (stride - 1));
+              const int q = j + stride;
+              const bool asc = (j & size) == 0;
+              const uint64_t kj = key[j], kq = key[q];
+              if ((kj > kq) == asc) {
+                key[j] = kq;
+                key[q] = kj;
+              }
             }
+            __syncthreads();
           }
-          __syncthreads();
         }
       }
       // inclusive suffix sums: thread t owns the t-th chunk counted from the END of the
       // bucket (contiguous, fixed order -> deterministic, all terms positive)
       const int per = (n + kSortNT - 1) / kSortNT;
       const int hi_ = n - min(tid * per, n), lo_ = max(hi_ - per, 0);  // chunk = [lo_, hi_)
+      double wv[kCap / kSortNT];
       double loc = 0.0;
-      for (int i = hi_ - 1; i >= lo_; --i) loc += exp((double)lgv[i] - lmax);
+      for (int i = hi_ - 1, u = 0; i >= lo_; --i, ++u) {
+        wv[u] = exp((double)lg[(uint32_t)key[i]] - lmax);
+        loc += wv[u];
+      }
       double run = block_excl_scan_d<kSortNT>(loc, sd, &wsum);  // mass of all later elements
-      for (int i = hi_ - 1; i >= lo_; --i) {
-        const double w = exp((double)lgv[i] - lmax);
-        run += w;
+      for (int i = hi_ - 1, u = 0; i >= lo_; --i, ++u) {
+        run += wv[u];
         out_act[base + i] = (int32_t)(uint32_t)key[i];
-        out_w[base + i] = w;
+        out_w[base + i] = wv[u];
         out_suf[base + i] = run;
       }
       __syncthreads();
     } else if (n > kCap) {
-      // exact fallback: rank by counting (keys are unique: actions differ)
-      for (int i = tid; i < n; i += kSortNT) {
-        const uint64_t ki = ((uint64_t)(~bk_ord[base + i]) << 32) | (uint32_t)bk_act[base + i];
+      // exact fallback: rank by counting with the j-loop tiled through LDS; only reached by
+      // pathologically clustered keys
+      for (int i0 = 0; i0 < n; i0 += kSortNT) {
+        const int i = i0 + tid;
+        const uint64_t ki = i < n ? bk_key[base + i] : ~0ull;
         int rank = 0;
-        for (int j = 0; j < n; ++j) {
-          const uint64_t kj = ((uint64_t)(~bk_ord[base + j]) << 32) | (uint32_t)bk_act[base + j];
-          rank += kj < ki;
+        for (int j0 = 0; j0 < n; j0 += kCap) {
+          const int m = min(kCap, n - j0);
+          __syncthreads();
+          for (int j = tid; j < m; j += kSortNT) key[j] = bk_key[base + j0 + j];
+          __syncthreads();
+          if (i < n)
+            for (int j = 0; j < m; ++j) rank += key[j] < ki;
         }
-        out_act[base + rank] = bk_act[base + i];
-        out_w[base + rank] = exp((double)bk_logit[base + i] - lmax);
+        if (i < n) {
+          const int a = (int32_t)(uint32_t)ki;
+          out_act[base + rank] = a;
+          out_w[base + rank] = exp((double)lg[a] - lmax);
+        }
       }
       __syncthreads();
       double carry = 0.0;  // suffix sums from the end, chunk by chunk
       for (int c1 = n; c1 > 0; c1 -= kSortNT) {
         const int i = c1 - 1 - tid;  // thread 0 takes the last element of the chunk
-        const double w = i >= 0 && i < c1 ? out_w[base + i] : 0.0;
+        const double w = i >= 0 ? out_w[base + i] : 0.0;
         double tot;
         const double ex = block_excl_scan_d<kSortNT>(w, sd, &tot);
         if (i >= 0) out_suf[base + i] = carry + ex + w;
@@ -538,8 +554,8 @@ __global__ __launch_bounds__(1024) void k_wscan(const int32_t* __restrict__ nbk_
   }
 }
 
-__global__ __launch_bounds__(kNT) void k_final(const int32_t* __restrict__ counts, const int32_t* __restrict__ nbk_,
-                                               const int32_t* __restrict__ seg_,
+// One bucket per iteration: fwd_probs = w / (W_rest + later buckets + in-bucket suffix).
+__global__ __launch_bounds__(kNT) void k_final(const int32_t* __restrict__ nbk_, const int32_t* __restrict__ seg_,
                                                const int32_t* __restrict__ bucket_start,
                                                const double* __restrict__ bucket_wsuf,
                                                const int32_t* __restrict__ out_act, const double* __restrict__ out_w,
@@ -547,21 +563,21 @@ __global__ __launch_bounds__(kNT) void k_final(const int32_t* __restrict__ count
                                                int64_t t_cap, int64_t* __restrict__ actions,
                                                float* __restrict__ fwd) {
   const int b = blockIdx.y;
-  const int n = counts[b], nbk = nbk_[b];
+  const int nbk = nbk_[b];
   const int64_t seg = seg_[b];
   const int32_t* bs = bucket_start + (int64_t)b * (kMaxBuckets + 1);
   const double* wp = bucket_wsuf + (int64_t)b * kMaxBuckets;
   const double rest = wrest[b];
-  for (int t = blockIdx.x * kNT + threadIdx.x; t < n; t += gridDim.x * kNT) {
-    int lo = 0, hi = nbk;  // bs[lo] <= t < bs[hi]
-    while (hi - lo > 1) {
-      const int mid = (lo + hi) >> 1;
-      if (bs[mid] <= t) lo = mid;
-      else hi = mid;
+  int64_t* act_b = actions + (int64_t)b * t_cap;
+  float* fwd_b = fwd + (int64_t)b * t_cap;
+  for (int k = blockIdx.x; k < nbk; k += gridDim.x) {
+    const int s = bs[k], e = bs[k + 1];
+    const double later = rest + wp[k];
+    for (int t = s + threadIdx.x; t < e; t += kNT) {
+      const int64_t i = seg + t;
+      act_b[t] = out_act[i];
+      fwd_b[t] = (float)(out_w[i] / (later + out_suf[i]));
     }
-    const int64_t i = seg + t;
-    actions[(int64_t)b * t_cap + t] = out_act[i];
-    fwd[(int64_t)b * t_cap + t] = (float)(out_w[i] / (rest + (wp[lo] + out_suf[i])));
   }
 }
 
@@ -611,10 +627,10 @@ extern "C" int spai_rollout_select(const float* logits, int64_t bstride, int32_t
   k_select<<<dim3(w.nblk, B), kNT, 0, s>>>(logits, bstride, E, w.nblk, (uint32_t)seed, (uint32_t)(seed >> 32),
                                            (uint32_t)stream_id, (uint32_t)(stream_id >> 32), sample_base, removed,
                                            words, lmax, w.block_counts, w.block_min, w.block_max, w.block_wrest,
-                                           w.st_ord, w.st_act, w.st_logit);
+                                           w.st_ord, w.st_act);
   SPAI_CHECK_LAUNCH();
   k_sample_stats<<<B, 1024, 0, s>>>(w.nblk, E, logits, bstride, lmax, w.block_counts, w.block_min, w.block_max,
-                                    w.block_wrest, counts, w.lo, w.hi, w.nbk, w.wrest);
+                                    w.block_wrest, counts, w.klo, w.kscale, w.nbk, w.wrest);
   SPAI_CHECK_LAUNCH();
   return SPAI_OK;
 }
@@ -630,21 +646,23 @@ extern "C" int spai_rollout_order(const float* logits, int64_t bstride, int32_t 
   traj_ws(workspace, E, B, &w);
   SPAI_CHECK_ARG(workspace_bytes >= w.total_bytes, "spai_rollout_order: workspace too small");
   hipStream_t s = (hipStream_t)stream;
-  k_part<false><<<dim3(kParts, B), kPT, 0, s>>>(w.nblk, w.block_counts, w.lo, w.hi, w.nbk, w.seg, w.st_ord, w.st_act,
-                                                w.st_logit, w.part_hist, nullptr, nullptr, nullptr);
+  k_part<false><<<dim3(kParts, B), kPT, 0, s>>>(w.nblk, w.block_counts, w.klo, w.kscale, w.nbk, w.seg,
+                                                w.bucket_start, w.st_ord, w.st_act, w.part_hist, nullptr);
   SPAI_CHECK_LAUNCH();
-  k_bucket_scan<<<B, 1024, 0, s>>>(B, counts, w.nbk, w.part_hist, w.bucket_start, w.seg, w.tdev, t_out);
+  k_bucket_count<<<dim3(kMaxBuckets / 256, B), 256, 0, s>>>(w.nbk, w.part_hist, w.bucket_tot);
   SPAI_CHECK_LAUNCH();
-  k_part<true><<<dim3(kParts, B), kPT, 0, s>>>(w.nblk, w.block_counts, w.lo, w.hi, w.nbk, w.seg, w.st_ord, w.st_act,
-                                               w.st_logit, w.part_hist, w.bk_ord, w.bk_act, w.bk_logit);
+  k_bucket_scan<<<B, 1024, 0, s>>>(B, counts, w.nbk, w.bucket_tot, w.bucket_start, w.seg, w.tdev, t_out);
   SPAI_CHECK_LAUNCH();
-  k_bucket_sort<<<dim3(kSortGrid, B), kSortNT, 0, s>>>(w.nbk, w.seg, w.bucket_start, w.bk_ord, w.bk_act, w.bk_logit,
+  k_part<true><<<dim3(kParts, B), kPT, 0, s>>>(w.nblk, w.block_counts, w.klo, w.kscale, w.nbk, w.seg,
+                                               w.bucket_start, w.st_ord, w.st_act, w.part_hist, w.bk_key);
+  SPAI_CHECK_LAUNCH();
+  k_bucket_sort<<<dim3(kSortGrid, B), kSortNT, 0, s>>>(w.nbk, w.seg, w.bucket_start, w.bk_key, logits, bstride,
                                                        lmax, w.out_act, w.out_w, w.out_suf, w.bucket_wsum);
   SPAI_CHECK_LAUNCH();
   k_wscan<<<B, 1024, 0, s>>>(w.nbk, w.bucket_wsum, w.bucket_wsuf);
   SPAI_CHECK_LAUNCH();
-  k_final<<<dim3(1024, B), kNT, 0, s>>>(counts, w.nbk, w.seg, w.bucket_start, w.bucket_wsuf, w.out_act, w.out_w,
-                                        w.out_suf, w.wrest, t_cap, actions, fwd_probs);
+  k_final<<<dim3(kSortGrid, B), kNT, 0, s>>>(w.nbk, w.seg, w.bucket_start, w.bucket_wsuf, w.out_act, w.out_w,
+                                             w.out_suf, w.wrest, t_cap, actions, fwd_probs);
   SPAI_CHECK_LAUNCH();
   k_pad<<<dim3(64, B), kNT, 0, s>>>(E, counts, w.tdev, w.wrest, logits, bstride, lmax, t_cap, actions, fwd_probs);
   SPAI_CHECK_LAUNCH();

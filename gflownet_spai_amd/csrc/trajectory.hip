@@ -15,8 +15,9 @@
 //                   key value over [min, max] of the sample's winners.
 //   k_bucket_count  per-bucket part offsets and totals; k_bucket_scan: bucket starts.
 //   k_part<1>       scatter winners into their buckets (LDS cursors).
-//   k_bucket_sort   bitonic sort of each bucket in LDS by (key desc, action asc), fp64
-//                   weights w = exp(l - lmax) and in-bucket inclusive SUFFIX sums.
+//   k_sort_small    one wave per bucket of <= 256 winners: rank by counting in LDS by
+//                   (key desc, action asc); fp64 weights w = exp(l - lmax) and in-bucket
+//                   inclusive SUFFIX sums.  k_sort_large: bitonic in LDS for larger buckets.
 //   k_wscan         per-sample suffix scan of the bucket weight sums (fixed order).
 //   k_final         fwd_probs = w_t / (W_rest + sum_{s>=t} w_s), actions, [B][t_cap] layout.
 // The step probability is formed from the mass still available at step t (the untouched
@@ -42,7 +43,9 @@ constexpr int kPerBucket = 96;     // target mean bucket occupancy
 constexpr int kCap = 2048;         // LDS bitonic capacity per bucket
 constexpr int kSortNT = 256;
 constexpr int kSortGrid = 512;     // bucket-sort blocks per sample (grid-stride over buckets)
-constexpr int kRankMax = kSortNT;  // buckets up to this size are ranked by counting, larger ones bitonic-sorted
+constexpr int kWaveMax = 256;      // buckets up to this size: one wave ranks them by counting (4 per lane)
+constexpr int kSmallNT = 256;      // 4 waves per block in the small-bucket kernels
+constexpr int kSmallGrid = 2048;   // small-bucket blocks per sample (grid-stride, 4 waves each)
 
 struct TrajWs {
   int32_t nblk;
@@ -211,7 +214,7 @@ __global__ __launch_bounds__(kNT) void k_select(const float* __restrict__ logits
           mn = min(mn, ord[s]);
           mx = max(mx, ord[s]);
         } else {
-          wr += (double)expf((float)((double)lv[s] - lm));
+          wr += (double)__expf(lv[s] - (float)lm);
         }
       }
     }
@@ -424,10 +427,104 @@ __global__ __launch_bounds__(1024) void k_bucket_scan(int32_t B, const int32_t* 
   }
 }
 
-// Sort one bucket per iteration in LDS (rank by counting up to kRankMax elements, bitonic up
-// to kCap, exact tiled rank counting beyond), then emit sorted actions, fp64 weights
-// w = exp(l - lmax) (logit gathered by action) and in-bucket inclusive suffix sums.
-__global__ __launch_bounds__(kSortNT) void k_bucket_sort(const int32_t* __restrict__ nbk_,
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Exclusive scan over the 64 lanes in lane order (fixed order -> deterministic).
+__device__ __forceinline__ double wave_excl_scan_d(double v, double* total) {
+  double incl = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const double y = __shfl_up(incl, o, kWave);
+    if ((threadIdx.x & 63) >= o) incl += y;
+  }
+  *total = __shfl(incl, 63, kWave);
+  const double ex = __shfl_up(incl, 1, kWave);
+  return (threadIdx.x & 63) ? ex : 0.0;
+}
+
+// Buckets of <= kWaveMax winners (the common case): one wave per bucket, no block barriers.
+// Rank by counting against the bucket's keys in the wave's LDS slice (broadcast reads), then
+// gather the logits, fp64 weights and suffix sums over contiguous per-lane chunks.
+__global__ __launch_bounds__(kSmallNT) void k_sort_small(const int32_t* __restrict__ nbk_,
+                                                         const int32_t* __restrict__ seg_,
+                                                         const int32_t* __restrict__ bucket_start,
+                                                         const uint64_t* __restrict__ bk_key,
+                                                         const float* __restrict__ logits, int64_t bstride,
+                                                         const float* __restrict__ lmax_,
+                                                         int32_t* __restrict__ out_act, double* __restrict__ out_w,
+                                                         double* __restrict__ out_suf,
+                                                         double* __restrict__ bucket_wsum) {
+  const int b = blockIdx.y, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  __shared__ uint64_t kin[kSmallNT / 64][kWaveMax];
+  __shared__ uint64_t kso[kSmallNT / 64][kWaveMax];
+  uint64_t* ki = kin[wave];
+  uint64_t* ks = kso[wave];
+  const int nbk = nbk_[b];
+  const int64_t seg = seg_[b];
+  const double lmax = (double)lmax_[b];
+  const float* lg = logits + (int64_t)b * bstride;
+  const int32_t* bs = bucket_start + (int64_t)b * (kMaxBuckets + 1);
+  const int wstride = gridDim.x * (kSmallNT / 64);
+  for (int k = blockIdx.x * (kSmallNT / 64) + wave; k < nbk; k += wstride) {
+    const int s = bs[k], n = bs[k + 1] - s;
+    if (n > kWaveMax) continue;  // k_sort_large
+    double wsum = 0.0;
+    if (n > 0) {
+      const int64_t base = seg + s;
+      uint64_t mine[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int e = u * 64 + lane;
+        mine[u] = e < n ? bk_key[base + e] : ~0ull;
+        ki[e] = mine[u];
+      }
+      wave_sync();
+      int rank[4] = {0, 0, 0, 0};
+      for (int j = 0; j < n; ++j) {
+        const uint64_t kj = ki[j];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) rank[u] += kj < mine[u];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (u * 64 + lane < n) ks[rank[u]] = mine[u];
+      wave_sync();
+      const int c = (n + 63) >> 6;                               // chunk length (<= 4)
+      const int hi = n - min(lane * c, n), lo = max(hi - c, 0);  // lane 0 owns the tail
+      double wv[4];
+      double loc = 0.0;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int i = hi - 1 - u;
+        wv[u] = (i >= lo) ? exp((double)lg[(uint32_t)ks[i]] - lmax) : 0.0;
+        loc += wv[u];
+      }
+      double run = wave_excl_scan_d(loc, &wsum);  // mass of all later elements
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int i = hi - 1 - u;
+        if (i >= lo) {
+          run += wv[u];
+          out_act[base + i] = (int32_t)(uint32_t)ks[i];
+          out_w[base + i] = wv[u];
+          out_suf[base + i] = run;
+        }
+      }
+      wave_sync();  // LDS slices are reused by the next bucket
+    }
+    if (lane == 0) bucket_wsum[(int64_t)b * kMaxBuckets + k] = wsum;
+  }
+}
+
+// Buckets of more than kWaveMax winners: up to kCap keys are split in LDS into value
+// sub-buckets of ~32 and ranked inside them; beyond kCap an exact tiled rank count; then
+// sorted actions, fp64 weights w = exp(l - lmax) (logit gathered by action) and in-bucket
+// inclusive suffix sums.
+__global__ __launch_bounds__(kSortNT) void k_sort_large(const int32_t* __restrict__ nbk_,
                                                           const int32_t* __restrict__ seg_,
                                                           const int32_t* __restrict__ bucket_start,
                                                           const uint64_t* __restrict__ bk_key,
@@ -435,8 +532,12 @@ __global__ __launch_bounds__(kSortNT) void k_bucket_sort(const int32_t* __restri
                                                           const float* __restrict__ lmax_, int32_t* __restrict__ out_act,
                                                           double* __restrict__ out_w, double* __restrict__ out_suf,
                                                           double* __restrict__ bucket_wsum) {
+  constexpr int kMaxSub = 64;
   const int b = blockIdx.y, tid = threadIdx.x;
   __shared__ uint64_t key[kCap];
+  __shared__ uint64_t kmid[kCap];
+  __shared__ int scnt[kMaxSub], sst[kMaxSub], scur[kMaxSub];
+  __shared__ float sfl[8];
   __shared__ double sd[kSortNT / 64];
   const int nbk = nbk_[b];
   const int64_t seg = seg_[b];
@@ -447,37 +548,78 @@ __global__ __launch_bounds__(kSortNT) void k_bucket_sort(const int32_t* __restri
     const int s = bs[k], n = bs[k + 1] - s;
     const int64_t base = seg + s;
     double wsum = 0.0;
-    if (n > 0 && n <= kCap) {
-      if (n <= kRankMax) {
-        const uint64_t mine = tid < n ? bk_key[base + tid] : ~0ull;
-        key[tid] = mine;
-        __syncthreads();
-        int rank = 0;
-        for (int j = 0; j < n; ++j) rank += key[j] < mine;  // broadcast LDS reads
-        __syncthreads();
-        if (tid < n) key[rank] = mine;
-        __syncthreads();
-      } else {
-        int np2 = 1;
-        while (np2 < n) np2 <<= 1;
-        for (int i = tid; i < np2; i += kSortNT) key[i] = i < n ? bk_key[base + i] : ~0ull;
-        __syncthreads();
-        for (int size = 2; size <= np2; size <<= 1) {
-          for (int stride = size >> 1; stride > 0; stride >>= 1) {
-            for (int i = tid; i < (np2 >> 1); i += kSortNT) {
-              const int j = 2 * i - (i & (stride - 1));
-              const int q = j + stride;
-              const bool asc = (j & size) == 0;
-              const uint64_t kj = key[j], kq = key[q];
-              if ((kj > kq) == asc) {
-                key[j] = kq;
-                key[q] = kj;
-              }
-            }
-            __syncthreads();
-          }
+    if (n <= kWaveMax) continue;  // k_sort_small (block-uniform branch)
+    if (n <= kCap) {
+      // sub-bucket by value inside the bucket (linear over its own [min, max]), then rank
+      // each key against its sub-bucket only: ~6 barriers instead of a bitonic network
+      constexpr int kPerT = kCap / kSortNT;  // keys per thread (8)
+      uint64_t mine[kPerT];
+      float v[kPerT];
+      float vmn = INFINITY, vmx = -INFINITY;
+#pragma unroll
+      for (int u = 0; u < kPerT; ++u) {
+        const int i = u * kSortNT + tid;
+        mine[u] = i < n ? bk_key[base + i] : ~0ull;
+        v[u] = i < n ? from_orderable(~(uint32_t)(mine[u] >> 32)) : 0.0f;
+        if (i < n) {
+          vmn = fminf(vmn, v[u]);
+          vmx = fmaxf(vmx, v[u]);
         }
       }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        vmn = fminf(vmn, __shfl_xor(vmn, o, kWave));
+        vmx = fmaxf(vmx, __shfl_xor(vmx, o, kWave));
+      }
+      if ((tid & 63) == 0) {
+        sfl[tid >> 6] = vmn;
+        sfl[4 + (tid >> 6)] = vmx;
+      }
+      const int nsub = min(kMaxSub, (n + 31) / 32);
+      for (int i = tid; i < nsub; i += kSortNT) scnt[i] = 0;
+      __syncthreads();
+      vmn = fminf(fminf(sfl[0], sfl[1]), fminf(sfl[2], sfl[3]));
+      vmx = fmaxf(fmaxf(sfl[4], sfl[5]), fmaxf(sfl[6], sfl[7]));
+      const double sc = vmx > vmn ? (double)nsub / ((double)vmx - (double)vmn) : 0.0;
+      int sb[kPerT];
+#pragma unroll
+      for (int u = 0; u < kPerT; ++u) {
+        sb[u] = 0;
+        if (u * kSortNT + tid < n) {
+          // reversed: sub-bucket 0 holds the largest values (trajectory order)
+          sb[u] = nsub - 1 - min(nsub - 1, (int)(((double)v[u] - (double)vmn) * sc));
+          atomicAdd(&scnt[sb[u]], 1);
+        }
+      }
+      __syncthreads();
+      if (tid < 64) {  // exclusive scan of <= 64 sub-bucket counts by one wave
+        const int c = tid < nsub ? scnt[tid] : 0;
+        const int inc = wave_incl_scan(c);
+        if (tid < nsub) {
+          sst[tid] = inc - c;
+          scur[tid] = inc - c;
+        }
+      }
+      __syncthreads();
+      int pos[kPerT];
+#pragma unroll
+      for (int u = 0; u < kPerT; ++u) {
+        if (u * kSortNT + tid < n) {
+          pos[u] = atomicAdd(&scur[sb[u]], 1);
+          kmid[pos[u]] = mine[u];
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int u = 0; u < kPerT; ++u) {
+        if (u * kSortNT + tid < n) {
+          const int a = sst[sb[u]], e = a + scnt[sb[u]];
+          int r = a;
+          for (int j = a; j < e; ++j) r += kmid[j] < mine[u];
+          key[r] = mine[u];
+        }
+      }
+      __syncthreads();
       // inclusive suffix sums: thread t owns the t-th chunk counted from the END of the
       // bucket (contiguous, fixed order -> deterministic, all terms positive)
       const int per = (n + kSortNT - 1) / kSortNT;
@@ -554,15 +696,16 @@ __global__ __launch_bounds__(1024) void k_wscan(const int32_t* __restrict__ nbk_
   }
 }
 
-// One bucket per iteration: fwd_probs = w / (W_rest + later buckets + in-bucket suffix).
-__global__ __launch_bounds__(kNT) void k_final(const int32_t* __restrict__ nbk_, const int32_t* __restrict__ seg_,
-                                               const int32_t* __restrict__ bucket_start,
-                                               const double* __restrict__ bucket_wsuf,
-                                               const int32_t* __restrict__ out_act, const double* __restrict__ out_w,
-                                               const double* __restrict__ out_suf, const double* __restrict__ wrest,
-                                               int64_t t_cap, int64_t* __restrict__ actions,
-                                               float* __restrict__ fwd) {
-  const int b = blockIdx.y;
+// One wave per bucket: fwd_probs = w / (W_rest + later buckets + in-bucket suffix).
+__global__ __launch_bounds__(kSmallNT) void k_final(const int32_t* __restrict__ nbk_, const int32_t* __restrict__ seg_,
+                                                    const int32_t* __restrict__ bucket_start,
+                                                    const double* __restrict__ bucket_wsuf,
+                                                    const int32_t* __restrict__ out_act,
+                                                    const double* __restrict__ out_w,
+                                                    const double* __restrict__ out_suf,
+                                                    const double* __restrict__ wrest, int64_t t_cap,
+                                                    int64_t* __restrict__ actions, float* __restrict__ fwd) {
+  const int b = blockIdx.y, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int nbk = nbk_[b];
   const int64_t seg = seg_[b];
   const int32_t* bs = bucket_start + (int64_t)b * (kMaxBuckets + 1);
@@ -570,10 +713,11 @@ __global__ __launch_bounds__(kNT) void k_final(const int32_t* __restrict__ nbk_,
   const double rest = wrest[b];
   int64_t* act_b = actions + (int64_t)b * t_cap;
   float* fwd_b = fwd + (int64_t)b * t_cap;
-  for (int k = blockIdx.x; k < nbk; k += gridDim.x) {
+  const int wstride = gridDim.x * (kSmallNT / 64);
+  for (int k = blockIdx.x * (kSmallNT / 64) + wave; k < nbk; k += wstride) {
     const int s = bs[k], e = bs[k + 1];
     const double later = rest + wp[k];
-    for (int t = s + threadIdx.x; t < e; t += kNT) {
+    for (int t = s + lane; t < e; t += 64) {
       const int64_t i = seg + t;
       act_b[t] = out_act[i];
       fwd_b[t] = (float)(out_w[i] / (later + out_suf[i]));
@@ -656,12 +800,15 @@ extern "C" int spai_rollout_order(const float* logits, int64_t bstride, int32_t 
   k_part<true><<<dim3(kParts, B), kPT, 0, s>>>(w.nblk, w.block_counts, w.klo, w.kscale, w.nbk, w.seg,
                                                w.bucket_start, w.st_ord, w.st_act, w.part_hist, w.bk_key);
   SPAI_CHECK_LAUNCH();
-  k_bucket_sort<<<dim3(kSortGrid, B), kSortNT, 0, s>>>(w.nbk, w.seg, w.bucket_start, w.bk_key, logits, bstride,
-                                                       lmax, w.out_act, w.out_w, w.out_suf, w.bucket_wsum);
+  k_sort_small<<<dim3(kSmallGrid, B), kSmallNT, 0, s>>>(w.nbk, w.seg, w.bucket_start, w.bk_key, logits, bstride,
+                                                        lmax, w.out_act, w.out_w, w.out_suf, w.bucket_wsum);
+  SPAI_CHECK_LAUNCH();
+  k_sort_large<<<dim3(kSortGrid, B), kSortNT, 0, s>>>(w.nbk, w.seg, w.bucket_start, w.bk_key, logits, bstride,
+                                                      lmax, w.out_act, w.out_w, w.out_suf, w.bucket_wsum);
   SPAI_CHECK_LAUNCH();
   k_wscan<<<B, 1024, 0, s>>>(w.nbk, w.bucket_wsum, w.bucket_wsuf);
   SPAI_CHECK_LAUNCH();
-  k_final<<<dim3(kSortGrid, B), kNT, 0, s>>>(w.nbk, w.seg, w.bucket_start, w.bucket_wsuf, w.out_act, w.out_w,
+  k_final<<<dim3(kSmallGrid, B), kSmallNT, 0, s>>>(w.nbk, w.seg, w.bucket_start, w.bucket_wsuf, w.out_act, w.out_w,
                                              w.out_suf, w.wrest, t_cap, actions, fwd_probs);
   SPAI_CHECK_LAUNCH();
   k_pad<<<dim3(64, B), kNT, 0, s>>>(E, counts, w.tdev, w.wrest, logits, bstride, lmax, t_cap, actions, fwd_probs);

@@ -180,6 +180,27 @@ def test_throughput_rollout_clustered_keys_overflow_path():
     np.testing.assert_allclose(fwd[:, :T].cpu().numpy(), f_o, rtol=1e-6)
 
 
+def test_full_size_c4_rollout_vs_oracle():
+    """BASELINE's 1024^2 action space (E = 5,238,784) with the bench's logits: the removed set,
+    the whole ordered trajectory and its probabilities of sample 0 vs the oracle."""
+    from gflownet_spai_amd import kernels
+    import bench
+    E, B = 5238784, 2
+    logits = torch.randn(E + 1, generator=torch.Generator().manual_seed(123))
+    logits[E] = bench.terminal_logit(logits[:E].numpy(), 0.2)
+    lg, lmax, z = kernels.logits_stats(logits.to(DEV), B)
+    removed, counts, ws = kernels.rollout_select(lg, B, lmax, 1234, 0)
+    actions, fwd, t_dev = kernels.rollout_order(lg, B, lmax, counts, ws)
+    r_o, a_o, f_o, c_o = O.throughput_rollout(logits.numpy(), 1, 1234, 0)
+    k = int(c_o[0])
+    assert int(counts[0]) == k and int(t_dev) == int(counts.max()) + 1
+    bits = removed[0].cpu().numpy().view(np.uint32)
+    got = ((bits[:, None] >> np.arange(32, dtype=np.uint32)) & 1).reshape(-1)[:E].astype(bool)
+    assert np.array_equal(got, r_o[0])
+    assert np.array_equal(actions[0, :k + 1].cpu().numpy(), a_o[:k + 1, 0])
+    np.testing.assert_allclose(fwd[0, :k + 1].cpu().numpy(), f_o[0, :k + 1], rtol=1e-6)
+
+
 def test_throughput_sample_states_end_to_end():
     from gflownet_spai_amd import GFlowNet, PreconditionerEnv, poisson_2d
     A = poisson_2d(32)

@@ -310,3 +310,26 @@ def test_edge_cases():
     assert float(dense_env.orig_residual) == pytest.approx(np.sqrt(90 * 100 + 10 * 81), rel=1e-15)
     with pytest.raises(NotImplementedError):  # no LSQ kernel for 10-wide lines
         PreconditionerEnv(10, D, D, side="AM", fill="lsq").update(None, torch.tensor([[0, 100]]), 0.5)
+
+
+def test_line_shards_sum_to_full_residual():
+    """Column-sharded evaluation (the multi-GPU strong-scaling layout): the per-shard
+    partials of ||AM - I||_F^2 sum to the unsharded value and the M blocks concatenate."""
+    from gflownet_spai_amd import PreconditionerEnv, kernels, poisson_2d
+    from gflownet_spai_amd.distributed import shard_lines
+    A = poisson_2d(64)
+    n = 64 * 64
+    env = PreconditionerEnv(n, A, A, side="AM", fill="lsq")
+    E = env.init_nnz
+    rng = np.random.default_rng(3)
+    acts = torch.from_numpy(np.where(rng.random((4, E)) < 0.25, np.arange(E), -1))
+    removed, counts = kernels.actions_to_removed(acts.to(DEV), E)
+    full, m_full = kernels.fill_residual(env.pattern, env.a_lines, removed, True, store_m=True)
+    parts, blocks = [], []
+    for r in range(3):
+        b, e = shard_lines(n, r, 3)
+        res2, m = kernels.fill_residual(env.pattern, env.a_lines, removed, True, b, e, store_m=True)
+        parts.append(res2)
+        blocks.append(m)
+    np.testing.assert_allclose(sum(parts).cpu().numpy(), full.cpu().numpy(), rtol=1e-12)
+    assert torch.equal(torch.cat(blocks, 1), m_full)

@@ -114,6 +114,8 @@ def main():
     ap.add_argument("--batch", type=int, default=8)
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-overlap", action="store_true",
+                    help="run the fill/reward after the trajectory sort on one stream (isolated kernel timing)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -136,7 +138,8 @@ def main():
     logits = torch.randn(E + 1, generator=g)
     logits[E] = terminal_logit(logits[:E].numpy(), 0.2)
     B = args.batch
-    model = GFlowNet(SyntheticLogits(logits.to(dev)), None, env, mode="throughput", seed=1234, sample_base=rank * B)
+    model = GFlowNet(SyntheticLogits(logits.to(dev)), None, env, mode="throughput", seed=1234, sample_base=rank * B,
+                     overlap=not args.no_overlap)
     s0 = [A] * B
 
     def step():

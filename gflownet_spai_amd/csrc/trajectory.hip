@@ -5,105 +5,106 @@
 // of the Gumbel keys key_a = l_a - ln(-ln u_a); the removed set is {a < E : key_a > key_E}
 // and the trajectory lists it by key descending (ties: action ascending), then E.
 //
-// Pipeline (all stream-ordered, no host synchronisation; B samples per launch):
-//   k_select        Philox4x32-10 + deterministic fp32 keys for 4 actions per lane; removal
-//                   bitmap words via wave shuffles; block-local ordered staging of the
-//                   winners (orderable key, action); per-block count/min/max and the mass
-//                   of the untouched actions.
-//   k_sample_stats  per-sample count, key range and bucket count (no global atomics).
-//   k_part<0>       MSD bucketing: per (sample, part) LDS histogram, buckets linear in the
-//                   key value over [min, max] of the sample's winners.
-//   k_bucket_count  per-bucket part offsets and totals; k_bucket_scan: bucket starts.
-//   k_part<1>       scatter winners into their buckets (LDS cursors).
-//   k_sort_small    one wave per bucket of <= 256 winners: rank by counting in LDS by
-//                   (key desc, action asc); fp64 weights w = exp(l - lmax) and in-bucket
-//                   inclusive SUFFIX sums.  k_sort_large: bitonic in LDS for larger buckets.
-//   k_wscan         per-sample suffix scan of the bucket weight sums (fixed order).
-//   k_final         fwd_probs = w_t / (W_rest + sum_{s>=t} w_s), actions, [B][t_cap] layout.
-// The step probability is formed from the mass still available at step t (the untouched
-// actions W_rest, summed directly in k_select, plus the suffix of the trajectory), so no
-// "Z - prefix" cancellation occurs however much of the mass the removed edges carry.
-//   k_pad           terminal step and -1 / 1.0 padding up to T = max_b k_b + 1.
-// Buckets hold ~160 winners on average (k_sample_stats picks the count), far below the
-// 2048-element LDS capacity; an over-full bucket (pathologically clustered keys) falls
-// back to an exact rank-counting sort in global memory inside the same kernel.
+// Ordering ~1e6 winners per sample is a SAMPLE SORT whose only global data movement is
+// one coalesced staging write and one gather of contiguous runs:
+//   k_presample  keys of a pseudo-random stratified subset of <= 65536 actions per sample
+//                (1.2 % of the Philox work at C4); winners kept in subset order.
+//   k_splitters  one block per sample sorts up to 8192 sampled winner keys in LDS (LSD
+//                radix, 1 bit per pass) and picks nb = est/4096 bucket splitters: buckets
+//                of ~4096 winners whatever the key distribution.
+//   k_select     16384 actions per block: Philox4x32-10 + deterministic fp32 keys, removal
+//                bitmap words, mass of the untouched actions, and the tile's winners
+//                grouped by bucket in LDS and written as one contiguous 8-byte stream
+//                (never a scattered global write); per-(bucket, tile) counts and offsets.
+//   k_bscan      per sample: bucket starts, winner count, untouched mass, T.
+//   k_sort2      one block per bucket: gathers the bucket's runs (one per tile) into LDS,
+//                value-linear sub-buckets + rank counting, then fp64 weights
+//                w = exp(l - lmax) and in-bucket suffix sums; writes the actions in place.
+//                Buckets above the LDS capacity take an exact in-block radix path.
+//   k_wscan      per sample suffix over the bucket weight sums (fixed order).
+//   k_final      fwd_probs = w / (W_rest + later buckets + in-bucket suffix).
+//   k_pad        terminal step, -1 / 1.0 padding up to T = max_b k_b + 1.
+// The step probability is formed from the mass still available at step t (untouched
+// actions + trajectory suffix), so no "Z - prefix" cancellation occurs.  Every sum is taken
+// in a fixed order: results are bit-reproducible run to run.
 #include "spai_device.h"
 #include "spai_status.h"
 
 namespace spai {
 namespace {
 
-constexpr int kNT = 256;
-constexpr int kPer = 4;
-constexpr int kBlk = kNT * kPer;   // actions per select block
-constexpr int kParts = 64;         // histogram/scatter parts per sample
-constexpr int kPT = 1024;          // threads of the part kernels (2 blocks per CU with a 64 KiB LDS histogram)
-constexpr int kMaxBuckets = 16384; // per sample
-constexpr int kPerBucket = 96;     // target mean bucket occupancy
-constexpr int kCap = 2048;         // LDS bitonic capacity per bucket
-constexpr int kSortNT = 256;
-constexpr int kSortGrid = 512;     // bucket-sort blocks per sample (grid-stride over buckets)
-constexpr int kWaveMax = 256;      // buckets up to this size: one wave ranks them by counting (4 per lane)
-constexpr int kSmallNT = 256;      // 4 waves per block in the small-bucket kernels
-constexpr int kSmallGrid = 2048;   // small-bucket blocks per sample (grid-stride, 4 waves each)
+constexpr int kSelNT = 1024;               // threads of a select block
+constexpr int kSelRounds = 4;              // rounds of 4 consecutive actions per thread
+constexpr int kTile = kSelNT * 4 * kSelRounds;  // 16384 actions per select tile
+constexpr int kTileBits = 14;              // log2(kTile)
+constexpr int kSampM = 65536;              // subset size (power of two, capped by E)
+constexpr int kSampNT = 256;
+constexpr int kSampCap = 32768;            // sampled winners behind the splitters
+constexpr int kTarget = 4096;              // winners per bucket (target)
+constexpr int kMaxB = 2048;                // buckets per sample (11 bits in the LDS record)
+constexpr int kCap2 = 8192;               // LDS capacity of k_sort2 (records per bucket)
+constexpr int kMaxSub = 4096;              // value sub-buckets per bucket in k_sort2
+constexpr int kSortNT = 1024;
+constexpr int kMaxTiles = 2048;            // E <= 33.5M actions
+constexpr int kFinNT = 256;
+constexpr int kMaxSamples = 1024;          // B per rollout call
+constexpr int kBins = 4096;                // splitter histogram / bucket lookup table bins
 
 struct TrajWs {
-  int32_t nblk;
-  int32_t *block_counts;
-  uint32_t *block_min, *block_max;
-  double* block_wrest;
-  double* wrest;
-  double *klo, *kscale;
-  int32_t *nbk, *seg, *tdev;
-  uint32_t* st_ord;
-  int32_t* st_act;
-  int32_t* part_hist;
-  int32_t* bucket_start;
-  int32_t* bucket_tot;
-  double *bucket_wsum, *bucket_wsuf;
-  uint64_t* bk_key;  // (~orderable(key) << 32) | action: ascending == trajectory order
-  int32_t* out_act;
-  double *out_w, *out_suf;
+  int32_t ntiles, M;
+  int32_t* ctl;           // zeroed per rollout: btot [B][kMaxB] | reserved [B] | tdev
+  int32_t* btot;          // [B][kMaxB] winners per bucket (atomic sums over tiles)
+  int32_t* tdev;
+  int32_t* samp_cnt;      // [B][M / kSampNT] winners per presample block
+  uint32_t* samp;         // [B][M] winner keys (orderable), block-compacted
+  int32_t* nb;            // [B] buckets
+  uint32_t* spl;          // [B][kMaxB] ascending orderable splitters
+  uint16_t* lut;          // [B][kBins] bucket lookup table
+  uint32_t* lut_base;     // [B][2] (min key, shift) of the table
+  uint64_t* staging;      // [B][ntiles][kTile] (~ord << 32 | action), grouped by bucket per tile
+  float* stlog;           // [B][ntiles][kTile] logit of each staged record
+  int32_t* tcount;        // [B][kMaxB][ntiles]
+  int32_t* tloc;          // [B][kMaxB][ntiles]
+  double* tile_wrest;     // [B][ntiles]
+  int32_t* bstart;        // [B][kMaxB + 1]
+  double* wrest;          // [B]
+  double* bwsum;          // [B][kMaxB]
+  double* bwsuf;          // [B][kMaxB]
+  float* out_w;           // [B][E]
+  float* out_suf;         // [B][E] in-bucket suffix sums (one rounding of an fp64 sum of positives)
+  uint64_t* scratch;      // [B][E] oversized-bucket radix scratch
   size_t total_bytes;
 };
 
 static void traj_ws(void* base, int32_t E, int32_t B, TrajWs* w) {
   Carve c(base);
-  w->nblk = (E + kBlk - 1) / kBlk;
-  const size_t nb = (size_t)B * w->nblk, stage = nb * kBlk, cap = (size_t)B * E;
-  w->block_counts = c.take<int32_t>(nb);
-  w->block_min = c.take<uint32_t>(nb);
-  w->block_max = c.take<uint32_t>(nb);
-  w->block_wrest = c.take<double>(nb);
+  w->ntiles = (E + kTile - 1) / kTile;
+  int M = 1;
+  while (M * 2 <= E && M * 2 <= kSampM) M *= 2;
+  w->M = M;
+  const int nsb = (M + kSampNT - 1) / kSampNT;
+  w->ctl = c.take<int32_t>((size_t)B * kMaxB + B + 1);
+  w->btot = w->ctl;
+  w->tdev = w->ctl + (size_t)B * kMaxB + B;
+  w->samp_cnt = c.take<int32_t>((size_t)B * nsb);
+  w->samp = c.take<uint32_t>((size_t)B * M);
+  w->nb = c.take<int32_t>(B);
+  w->spl = c.take<uint32_t>((size_t)B * kMaxB);
+  w->lut = c.take<uint16_t>((size_t)B * kBins);
+  w->lut_base = c.take<uint32_t>((size_t)B * 2);
+  w->staging = c.take<uint64_t>((size_t)B * w->ntiles * kTile);
+  w->stlog = c.take<float>((size_t)B * w->ntiles * kTile);
+  w->tcount = c.take<int32_t>((size_t)B * kMaxB * w->ntiles);
+  w->tloc = c.take<int32_t>((size_t)B * kMaxB * w->ntiles);
+  w->tile_wrest = c.take<double>((size_t)B * w->ntiles);
+  w->bstart = c.take<int32_t>((size_t)B * (kMaxB + 1));
   w->wrest = c.take<double>(B);
-  w->klo = c.take<double>(B);
-  w->kscale = c.take<double>(B);
-  w->nbk = c.take<int32_t>(B);
-  w->seg = c.take<int32_t>(B);
-  w->tdev = c.take<int32_t>(1);
-  w->st_ord = c.take<uint32_t>(stage);
-  w->st_act = c.take<int32_t>(stage);
-  w->part_hist = c.take<int32_t>((size_t)B * kParts * kMaxBuckets);
-  w->bucket_start = c.take<int32_t>((size_t)B * (kMaxBuckets + 1));
-  w->bucket_tot = c.take<int32_t>((size_t)B * kMaxBuckets);
-  w->bucket_wsum = c.take<double>((size_t)B * kMaxBuckets);
-  w->bucket_wsuf = c.take<double>((size_t)B * kMaxBuckets);
-  w->bk_key = c.take<uint64_t>(cap);
-  w->out_act = c.take<int32_t>(cap);
-  w->out_w = c.take<double>(cap);
-  w->out_suf = c.take<double>(cap);
+  w->bwsum = c.take<double>((size_t)B * kMaxB);
+  w->bwsuf = c.take<double>((size_t)B * kMaxB);
+  w->out_w = c.take<float>((size_t)B * E);
+  w->out_suf = c.take<float>((size_t)B * E);
+  w->scratch = c.take<uint64_t>((size_t)B * E);
   w->total_bytes = c.off;
-}
-
-__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o, kWave));
-  return v;
-}
-__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o, kWave));
-  return v;
 }
 
 // Inclusive wave scan (int).
@@ -116,10 +117,9 @@ __device__ __forceinline__ int wave_incl_scan(int v) {
   return v;
 }
 
-// Block-wide exclusive scan of one int per thread (NT <= 1024); returns the exclusive
-// prefix, *total receives the block total.  Uses lds[NT/64].
+// Block-wide exclusive scan of one int per thread (NT <= 1024); *total = block total.
 template <int NT>
-__device__ __forceinline__ int block_excl_scan(int v, int* lds, int* total) {
+__device__ __forceinline__ int block_excl_scan(int v, int* lds /* NT/64 */, int* total) {
   const int incl = wave_incl_scan(v);
   __syncthreads();
   if ((threadIdx.x & 63) == 63) lds[threadIdx.x >> 6] = incl;
@@ -158,534 +158,806 @@ __device__ __forceinline__ double block_excl_scan_d(double v, double* lds, doubl
   return base + (incl - v);
 }
 
-__device__ __forceinline__ float from_orderable(uint32_t o) {
-  return __uint_as_float((o & 0x80000000u) ? (o & 0x7FFFFFFFu) : ~o);
+__device__ __forceinline__ uint32_t wave_and_u32(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v &= (uint32_t)__shfl_xor((int)v, o, kWave);
+  return v;
+}
+__device__ __forceinline__ uint32_t wave_or_u32(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v |= (uint32_t)__shfl_xor((int)v, o, kWave);
+  return v;
 }
 
-// Bucket of a key: linear in the key VALUE over [kmin, kmax] (the orderable bits are
-// log-like per exponent and badly skewed when the range crosses zero); bucket 0 holds
-// the LARGEST keys.  Monotone in the key, which is all the ordering needs.
-__device__ __forceinline__ int bucket_of(uint32_t o, double klo, double scale, int nbk) {
-  int k = (int)(((double)from_orderable(o) - klo) * scale);
-  k = max(0, min(k, nbk - 1));
-  return nbk - 1 - k;
+__device__ __forceinline__ float terminal_key(const float* lg, int32_t E, uint32_t bg, uint32_t st0, uint32_t st1,
+                                              uint32_t seed0, uint32_t seed1) {
+  const uint4 r = philox4x32_10((uint32_t)E >> 2, bg, st0, st1, seed0, seed1);
+  return gumbel_key(lg[E], pick_word(r, E & 3));
+}
+
+// Stratified pseudo-random subset: subset index i -> stratum (i * odd) mod M -> one action
+// of that stratum chosen by an integer hash; independent of the noise and of the logits.
+__device__ __forceinline__ int32_t subset_action(int i, int M, int32_t E) {
+  const uint32_t s = ((uint32_t)i * 0x9E3779B1u) & (uint32_t)(M - 1);
+  const int64_t lo = (int64_t)s * E / M, hi = (int64_t)(s + 1) * E / M;
+  uint32_t h = (uint32_t)i * 0x85EBCA6Bu;
+  h ^= h >> 13;
+  h *= 0xC2B2AE35u;
+  h ^= h >> 16;
+  return (int32_t)(lo + (int64_t)(h % (uint32_t)(hi - lo)));
+}
+
+// Block-wide exclusive scan of one uint64 per thread (packed 16-bit fields never overflow).
+template <int NT>
+__device__ __forceinline__ uint64_t block_excl_scan_u64(uint64_t c, uint64_t* lds /* NT/64 */, uint64_t* total) {
+  uint64_t incl = c;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint64_t y = __shfl_up(incl, o, kWave);
+    if ((threadIdx.x & 63) >= o) incl += y;
+  }
+  __syncthreads();
+  if ((threadIdx.x & 63) == 63) lds[threadIdx.x >> 6] = incl;
+  __syncthreads();
+  uint64_t base = 0, t = 0;
+#pragma unroll
+  for (int w = 0; w < NT / 64; ++w) {
+    const uint64_t x = lds[w];
+    base += (w < (int)(threadIdx.x >> 6)) ? x : 0ull;
+    t += x;
+  }
+  *total = t;
+  return base + incl - c;
+}
+
+// ------------------------------------------------------------------ k_presample
+__global__ __launch_bounds__(kSampNT) void k_presample(const float* __restrict__ logits, int64_t bstride, int32_t E,
+                                                       int32_t M, uint32_t seed0, uint32_t seed1, uint32_t st0,
+                                                       uint32_t st1, int32_t sample_base,
+                                                       uint32_t* __restrict__ samp, int32_t* __restrict__ samp_cnt) {
+  const int b = blockIdx.y, tid = threadIdx.x;
+  const float* lg = logits + (int64_t)b * bstride;
+  const uint32_t bg = (uint32_t)(sample_base + b);
+  __shared__ float s_tk;
+  __shared__ int s_wc[kSampNT / 64];
+  if (tid == 0) s_tk = terminal_key(lg, E, bg, st0, st1, seed0, seed1);
+  __syncthreads();
+  const int i = blockIdx.x * kSampNT + tid;
+  int win = 0;
+  uint32_t o = 0;
+  if (i < M) {
+    const int32_t a = subset_action(i, M, E);
+    const uint4 r = philox4x32_10((uint32_t)a >> 2, bg, st0, st1, seed0, seed1);
+    const float key = gumbel_key(lg[a], pick_word(r, a & 3));
+    if (key > s_tk) {
+      win = 1;
+      o = orderable(key);
+    }
+  }
+  int tot;
+  const int pos = block_excl_scan<kSampNT>(win, s_wc, &tot);
+  const int nsb = gridDim.x;
+  if (win) samp[(int64_t)b * M + blockIdx.x * kSampNT + pos] = o;
+  if (tid == 0) samp_cnt[b * nsb + blockIdx.x] = tot;
+}
+
+// ------------------------------------------------------------------ k_splitters
+// Splitters at equal-count quantiles of the sampled winner keys (up to kSampCap, in subset
+// order) from a 4096-bin value-linear histogram over [min, max] of the sample (orderable
+// space), interpolating inside a bin: monotone in j, no sort, four block barriers.
+__global__ __launch_bounds__(kSortNT) void k_splitters(int32_t E, int32_t M, int32_t nsb,
+                                                       const uint32_t* __restrict__ samp,
+                                                       const int32_t* __restrict__ samp_cnt,
+                                                       int32_t* __restrict__ nb_out, uint32_t* __restrict__ spl,
+                                                       uint16_t* __restrict__ lut, uint32_t* __restrict__ lut_base) {
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  __shared__ int hist[kBins + 1];
+  __shared__ int sblk[1024 + 1];
+  __shared__ int s_wc[kSortNT / 64];
+  __shared__ uint32_t s_mn[kSortNT / 64], s_mx[kSortNT / 64];
+  const int c = tid < nsb ? samp_cnt[b * nsb + tid] : 0;
+  int total;
+  const int ex = block_excl_scan<kSortNT>(c, s_wc, &total);
+  if (tid < nsb) sblk[tid] = ex;
+  if (tid == 0) sblk[nsb] = total;
+  for (int i = tid; i <= kBins; i += kSortNT) hist[i] = 0;
+  __syncthreads();
+  const int ns = min(total, kSampCap);
+  const uint32_t* sb = samp + (int64_t)b * M;
+  // pass 1: key range of the first ns sampled winners (wave per presample block)
+  uint32_t mn = 0xFFFFFFFFu, mx = 0u;
+  for (int k = wave; k < nsb && sblk[k] < ns; k += kSortNT / 64) {
+    const int cnt = min(sblk[k + 1], ns) - sblk[k];
+    for (int i = lane; i < cnt; i += 64) {
+      const uint32_t v = sb[k * kSampNT + i];
+      mn = min(mn, v);
+      mx = max(mx, v);
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    mn = min(mn, (uint32_t)__shfl_xor((int)mn, o, kWave));
+    mx = max(mx, (uint32_t)__shfl_xor((int)mx, o, kWave));
+  }
+  if (lane == 0) {
+    s_mn[wave] = mn;
+    s_mx[wave] = mx;
+  }
+  __syncthreads();
+  mn = 0xFFFFFFFFu;
+  mx = 0u;
+#pragma unroll
+  for (int w = 0; w < kSortNT / 64; ++w) {
+    mn = min(mn, s_mn[w]);
+    mx = max(mx, s_mx[w]);
+  }
+  const uint32_t range = ns > 0 ? mx - mn : 0u;
+  const int shift = range >= (uint32_t)kBins ? 32 - __clz((int)(range >> 12)) : 0;  // (range >> shift) < kBins
+  // pass 2: histogram
+  for (int k = wave; k < nsb && sblk[k] < ns; k += kSortNT / 64) {
+    const int cnt = min(sblk[k + 1], ns) - sblk[k];
+    for (int i = lane; i < cnt; i += 64) atomicAdd(&hist[(sb[k * kSampNT + i] - mn) >> shift], 1);
+  }
+  __syncthreads();
+  // exclusive scan of the bins (4 per thread), in place
+  {
+    int cv[4], loc = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      cv[q] = hist[tid * 4 + q];
+      loc += cv[q];
+    }
+    int t2;
+    int run = block_excl_scan<kSortNT>(loc, s_wc, &t2);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      hist[tid * 4 + q] = run;
+      run += cv[q];
+    }
+    if (tid == 0) hist[kBins] = t2;
+  }
+  __syncthreads();
+  // bucket count from the winner estimate: >= 16 sampled winners per bucket
+  const double est = (double)total * (double)E / (double)M;
+  int nb = (int)ceil(est / (double)kTarget);
+  nb = max(1, min(nb, min(kMaxB, max(1, ns / 16))));
+  __shared__ uint32_t s_spl[kMaxB];
+  for (int j = tid + 1; j < nb; j += kSortNT) {
+    const int64_t rj = (int64_t)j * ns / nb;  // target rank
+    int lo = 0, hi = kBins - 1;               // last bin with start <= rj
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (hist[mid] <= rj) lo = mid;
+      else hi = mid - 1;
+    }
+    const int cnt = hist[lo + 1] - hist[lo];
+    const double frac = cnt > 0 ? (double)(rj - hist[lo]) / (double)cnt : 0.0;
+    const uint64_t v = (uint64_t)mn + ((uint64_t)lo << shift) + (uint64_t)(frac * (double)(1ull << shift));
+    const uint32_t sv = (uint32_t)min(v, (uint64_t)mx);
+    spl[(int64_t)b * kMaxB + j - 1] = sv;
+    s_spl[j - 1] = sv;
+  }
+  __syncthreads();
+  // lookup table over the same bins: lut[bin] = #(splitters < start of bin); a key's bucket
+  // count is then lut[bin] plus the few splitters inside its bin (k_select)
+  for (int bin = tid; bin < kBins; bin += kSortNT) {
+    const uint64_t start = (uint64_t)mn + ((uint64_t)bin << shift);
+    int lo = 0, hi = nb - 1;  // lower_bound over s_spl[0 .. nb-2]
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if ((uint64_t)s_spl[mid] < start) lo = mid + 1;
+      else hi = mid;
+    }
+    lut[(int64_t)b * kBins + bin] = (uint16_t)lo;
+  }
+  if (tid == 0) {
+    nb_out[b] = nb;
+    lut_base[2 * b] = mn;
+    lut_base[2 * b + 1] = (uint32_t)shift;
+  }
 }
 
 // ------------------------------------------------------------------ k_select
-__global__ __launch_bounds__(kNT) void k_select(const float* __restrict__ logits, int64_t bstride, int32_t E,
-                                                int32_t nblk, uint32_t seed0, uint32_t seed1, uint32_t st0,
-                                                uint32_t st1, int32_t sample_base, uint32_t* __restrict__ removed,
-                                                int32_t words, const float* __restrict__ lmax,
-                                                int32_t* __restrict__ block_counts,
-                                                uint32_t* __restrict__ block_min, uint32_t* __restrict__ block_max,
-                                                double* __restrict__ block_wrest, uint32_t* __restrict__ st_ord,
-                                                int32_t* __restrict__ st_act) {
-  const int b = blockIdx.y, blk = blockIdx.x, tid = threadIdx.x;
+// LDS record per winner: (orderable key << 32) | (bucket << 14) | action within the tile.
+__global__ __launch_bounds__(kSelNT) void k_select(const float* __restrict__ logits, int64_t bstride, int32_t E,
+                                                   int32_t ntiles, uint32_t seed0, uint32_t seed1, uint32_t st0,
+                                                   uint32_t st1, int32_t sample_base, uint32_t* __restrict__ removed,
+                                                   int32_t words, const float* __restrict__ lmax,
+                                                   const int32_t* __restrict__ nb_, const uint32_t* __restrict__ spl_,
+                                                   const uint16_t* __restrict__ lut_, const uint32_t* __restrict__ lut_base,
+                                                   uint64_t* __restrict__ staging, float* __restrict__ stlog,
+                                                   int32_t* __restrict__ tcount,
+                                                   int32_t* __restrict__ tloc, int32_t* __restrict__ btot,
+                                                   double* __restrict__ tile_wrest) {
+  constexpr int kWaveSpan = kTile / (kSelNT / 64);  // actions (and LDS slots) per wave: 1024
+  __shared__ uint64_t u[kTile];                     // per-wave regions of winner records
+  __shared__ uint32_t s_spl[kMaxB];
+  __shared__ int s_hist[kMaxB];
+  __shared__ uint16_t s_lut[kBins];
+  __shared__ int s_wc[kSelNT / 64];
+  __shared__ double s_wr[kSelNT / 64];
+  __shared__ float s_tk;
+  const int b = blockIdx.y, tile = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const float* lg = logits + (int64_t)b * bstride;
   const uint32_t bg = (uint32_t)(sample_base + b);
-  const double lm = (double)lmax[b];
-  __shared__ float s_tk;
-  __shared__ int s_wc[kNT / 64];
-  __shared__ uint32_t s_mn[kNT / 64], s_mx[kNT / 64];
-  __shared__ double s_wr[kNT / 64];
-  if (tid == 0) {
-    const uint4 r = philox4x32_10((uint32_t)E >> 2, bg, st0, st1, seed0, seed1);
-    s_tk = gumbel_key(lg[E], pick_word(r, E & 3));
+  const int nb = nb_[b];
+  for (int k = tid; k < nb; k += kSelNT) {
+    s_hist[k] = 0;
+    if (k < nb - 1) s_spl[k] = spl_[(int64_t)b * kMaxB + k];
   }
+  for (int i = tid; i < kBins; i += kSelNT) s_lut[i] = lut_[(int64_t)b * kBins + i];
+  const uint32_t lmn = lut_base[2 * b];
+  const int lsh = (int)lut_base[2 * b + 1];
+  if (tid == 0) s_tk = terminal_key(lg, E, bg, st0, st1, seed0, seed1);
   __syncthreads();
   const float tk = s_tk;
-  const int a0 = blk * kBlk + tid * kPer;
-  uint32_t nib = 0, ord[kPer];
-  float lv[kPer];
-  uint32_t mn = 0xFFFFFFFFu, mx = 0u;
-  double wr = 0.0;  // mass of the actions this lane leaves untouched
-  if (a0 < E) {
-    const uint4 r = philox4x32_10((uint32_t)a0 >> 2, bg, st0, st1, seed0, seed1);
+  const float lm = lmax[b];
+  const int tbase = tile * kTile;
+  uint64_t* uw = u + wave * kWaveSpan;
+  int wc = 0;       // records of this wave so far (wave-uniform)
+  double wr = 0.0;  // mass of the actions this thread leaves untouched
+#pragma unroll 1
+  for (int r = 0; r < kSelRounds; ++r) {
+    const int al = r * (kSelNT * 4) + tid * 4;  // action within the tile
+    const int a0 = tbase + al;
+    uint32_t nib = 0, ord[4];
+    if (a0 < E) {
+      const uint4 rr = philox4x32_10((uint32_t)a0 >> 2, bg, st0, st1, seed0, seed1);
 #pragma unroll
-    for (int s = 0; s < kPer; ++s) {
-      ord[s] = 0;
-      lv[s] = 0.0f;
-      if (a0 + s < E) {
-        lv[s] = lg[a0 + s];
-        const float key = gumbel_key(lv[s], pick_word(r, s));
-        if (key > tk) {
-          nib |= 1u << s;
-          ord[s] = orderable(key);
-          mn = min(mn, ord[s]);
-          mx = max(mx, ord[s]);
-        } else {
-          wr += (double)__expf(lv[s] - (float)lm);
+      for (int s = 0; s < 4; ++s) {
+        ord[s] = 0;
+        if (a0 + s < E) {
+          const float lv = lg[a0 + s];
+          const float key = gumbel_key(lv, pick_word(rr, s));
+          if (key > tk) {
+            nib |= 1u << s;
+            ord[s] = orderable(key);
+          } else {
+            wr += (double)__expf(lv - lm);
+          }
         }
       }
     }
-  }
-  uint32_t x = nib << ((tid & 7) * kPer);
-  x |= __shfl_xor(x, 1, kWave);
-  x |= __shfl_xor(x, 2, kWave);
-  x |= __shfl_xor(x, 4, kWave);
-  if ((tid & 7) == 0) {
-    const int wi = (blk * kBlk + (tid & ~7) * kPer) >> 5;
-    if (wi < words) removed[(int64_t)b * words + wi] = x;
-  }
-  const int c = __popc(nib);
-  const int incl = wave_incl_scan(c);
-  mn = wave_min_u32(mn);
-  mx = wave_max_u32(mx);
-  wr = wave_sum(wr);
-  if ((tid & 63) == 63) s_wc[tid >> 6] = incl;
-  if ((tid & 63) == 0) {
-    s_mn[tid >> 6] = mn;
-    s_mx[tid >> 6] = mx;
-    s_wr[tid >> 6] = wr;
-  }
-  __syncthreads();
-  int pos = incl - c, tot = 0;
-#pragma unroll
-  for (int w = 0; w < kNT / 64; ++w) {
-    pos += (w < (tid >> 6)) ? s_wc[w] : 0;
-    tot += s_wc[w];
-  }
-  const int64_t lbase = ((int64_t)b * nblk + blk) * kBlk;
-#pragma unroll
-  for (int s = 0; s < kPer; ++s) {
-    if ((nib >> s) & 1u) {
-      st_ord[lbase + pos] = ord[s];
-      st_act[lbase + pos] = a0 + s;
-      ++pos;
+    uint32_t x = nib << ((tid & 7) * 4);
+    x |= __shfl_xor(x, 1, kWave);
+    x |= __shfl_xor(x, 2, kWave);
+    x |= __shfl_xor(x, 4, kWave);
+    if ((tid & 7) == 0 && a0 < E) {
+      const int wi = a0 >> 5;
+      if (wi < words) removed[(int64_t)b * words + wi] = x;
     }
+    const int c = __popc(nib);
+    const int incl = wave_incl_scan(c);
+    int pos = wc + incl - c;
+    wc += __shfl(incl, 63, kWave);
+    // bucket = nb - 1 - #(splitters <= key): table count at the key's bin, then the few
+    // splitters inside that bin; the four lookups of a thread are independent
+    int cnt[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const uint32_t o = ord[s];
+      const uint32_t bin = o < lmn ? 0u : min((uint32_t)(kBins - 1), (o - lmn) >> lsh);
+      cnt[s] = s_lut[bin];
+    }
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+      if (cnt[s] < nb - 1 && s_spl[cnt[s]] <= ord[s]) ++cnt[s];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      if ((nib >> s) & 1u) {
+        while (cnt[s] < nb - 1 && s_spl[cnt[s]] <= ord[s]) ++cnt[s];
+        const int bk = nb - 1 - cnt[s];
+        atomicAdd(&s_hist[bk], 1);
+        uw[pos++] = ((uint64_t)ord[s] << 32) | ((uint32_t)bk << kTileBits) | (uint32_t)(al + s);
+      }
+    }
+  }
+  // fixed-order untouched mass of the tile
+  wr = wave_sum(wr);
+  if (lane == 0) s_wr[wave] = wr;
+  __syncthreads();
+  // bucket offsets inside the tile (exclusive scan, 2 buckets per thread)
+  const int k0 = 2 * tid, k1 = 2 * tid + 1;
+  const int h0 = k0 < nb ? s_hist[k0] : 0, h1 = k1 < nb ? s_hist[k1] : 0;
+  int tot;
+  const int ex = block_excl_scan<kSelNT>(h0 + h1, s_wc, &tot);
+  const int64_t trow = (int64_t)b * kMaxB * ntiles + tile;
+  if (k0 < nb) {
+    s_hist[k0] = ex;
+    tcount[trow + (int64_t)k0 * ntiles] = h0;
+    tloc[trow + (int64_t)k0 * ntiles] = ex;
+    if (h0) atomicAdd(&btot[(int64_t)b * kMaxB + k0], h0);
+  }
+  if (k1 < nb) {
+    s_hist[k1] = ex + h0;
+    tcount[trow + (int64_t)k1 * ntiles] = h1;
+    tloc[trow + (int64_t)k1 * ntiles] = ex + h0;
+    if (h1) atomicAdd(&btot[(int64_t)b * kMaxB + k1], h1);
   }
   if (tid == 0) {
-    uint32_t bmn = s_mn[0], bmx = s_mx[0];
-    double bwr = s_wr[0];
+    double t = 0.0;
 #pragma unroll
-    for (int w = 1; w < kNT / 64; ++w) {
-      bmn = min(bmn, s_mn[w]);
-      bmx = max(bmx, s_mx[w]);
-      bwr += s_wr[w];
+    for (int w = 0; w < kSelNT / 64; ++w) t += s_wr[w];
+    tile_wrest[(int64_t)b * ntiles + tile] = t;
+  }
+  __syncthreads();
+  // group: each wave places its own records (4 per lane per step, loads in flight together)
+  uint64_t* st = staging + ((int64_t)b * ntiles + tile) * kTile;
+  float* sl = stlog + ((int64_t)b * ntiles + tile) * kTile;
+#pragma unroll 1
+  for (int j0 = lane; j0 < wc; j0 += 256) {
+    uint64_t e[4];
+    float lv[4];
+    int p[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int j = j0 + 64 * q;
+      e[q] = j < wc ? uw[j] : 0ull;
+      lv[q] = j < wc ? lg[tbase + (int)((uint32_t)e[q] & (kTile - 1))] : 0.0f;
     }
-    block_counts[b * nblk + blk] = tot;
-    block_min[b * nblk + blk] = bmn;
-    block_max[b * nblk + blk] = bmx;
-    block_wrest[b * nblk + blk] = bwr;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      p[q] = j0 + 64 * q < wc ? atomicAdd(&s_hist[(int)((uint32_t)e[q] >> kTileBits)], 1) : 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (j0 + 64 * q < wc) {
+        const uint32_t lo = (uint32_t)e[q];
+        st[p[q]] = ((uint64_t)(~(uint32_t)(e[q] >> 32)) << 32) | (uint32_t)(tbase + (int)(lo & (kTile - 1)));
+        sl[p[q]] = lv[q];  // the tile's logits are cache-hot: the weight travels with the record
+      }
+    }
   }
 }
 
-// ------------------------------------------------------------------ k_sample_stats
-__global__ __launch_bounds__(1024) void k_sample_stats(int32_t nblk, int32_t E, const float* __restrict__ logits,
-                                                       int64_t bstride, const float* __restrict__ lmax,
-                                                       const int32_t* __restrict__ block_counts,
-                                                       const uint32_t* __restrict__ block_min,
-                                                       const uint32_t* __restrict__ block_max,
-                                                       const double* __restrict__ block_wrest,
-                                                       int32_t* __restrict__ counts, double* __restrict__ klo,
-                                                       double* __restrict__ kscale, int32_t* __restrict__ nbk,
-                                                       double* __restrict__ wrest) {
-  const int b = blockIdx.x;
-  __shared__ int si[16];
-  __shared__ uint32_t smn[16], smx[16];
-  __shared__ double sw[16];
-  int c = 0;
-  uint32_t mn = 0xFFFFFFFFu, mx = 0u;
+// ------------------------------------------------------------------ k_bscan
+__global__ __launch_bounds__(1024) void k_bscan(int32_t E, int32_t ntiles, const float* __restrict__ logits,
+                                                int64_t bstride, const float* __restrict__ lmax,
+                                                const int32_t* __restrict__ nb_, const int32_t* __restrict__ btot,
+                                                const double* __restrict__ tile_wrest, int32_t* __restrict__ bstart,
+                                                int32_t* __restrict__ counts, double* __restrict__ wrest,
+                                                int32_t* __restrict__ tdev) {
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  __shared__ int s_wc[16];
+  __shared__ double s_wr[16];
+  const int nb = nb_[b];
   double wr = 0.0;
-  for (int i = threadIdx.x; i < nblk; i += 1024) {
-    c += block_counts[b * nblk + i];
-    mn = min(mn, block_min[b * nblk + i]);
-    mx = max(mx, block_max[b * nblk + i]);
-    wr += block_wrest[b * nblk + i];
-  }
-  c = wave_sum(c);
-  mn = wave_min_u32(mn);
-  mx = wave_max_u32(mx);
+  for (int t = tid; t < ntiles; t += 1024) wr += tile_wrest[(int64_t)b * ntiles + t];
   wr = wave_sum(wr);
-  if ((threadIdx.x & 63) == 0) {
-    si[threadIdx.x >> 6] = c;
-    smn[threadIdx.x >> 6] = mn;
-    smx[threadIdx.x >> 6] = mx;
-    sw[threadIdx.x >> 6] = wr;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    int tot = 0;
-    wr = exp((double)logits[(int64_t)b * bstride + E] - (double)lmax[b]);  // the terminal id stays available
-    for (int w = 0; w < 16; ++w) {
-      tot += si[w];
-      mn = min(mn, smn[w]);
-      mx = max(mx, smx[w]);
-      wr += sw[w];
-    }
-    wrest[b] = wr;
-    int k = 1;
-    while (k < kMaxBuckets && (int64_t)k * kPerBucket < tot) k <<= 1;
-    counts[b] = tot;
-    const double vlo = tot ? (double)from_orderable(mn) : 0.0, vhi = tot ? (double)from_orderable(mx) : 0.0;
-    klo[b] = vlo;
-    kscale[b] = vhi > vlo ? (double)k / (vhi - vlo) : 0.0;
-    nbk[b] = k;
-  }
-}
-
-// Shared body of the MSD histogram (SCATTER = false) and scatter (SCATTER = true) passes.
-// Part p of sample b owns a contiguous range of select blocks; each wave walks whole select
-// blocks (their winners are contiguous in the staging area) 4 elements per lane at a time,
-// so loads are coalesced and independent.  Histograms/cursors live in LDS; the scatter
-// writes one 8-byte sort key per winner.
-template <bool SCATTER>
-__global__ __launch_bounds__(kPT) void k_part(int32_t nblk, const int32_t* __restrict__ block_counts,
-                                              const double* __restrict__ klo_, const double* __restrict__ kscale_,
-                                              const int32_t* __restrict__ nbk_, const int32_t* __restrict__ seg_,
-                                              const int32_t* __restrict__ bucket_start,
-                                              const uint32_t* __restrict__ st_ord, const int32_t* __restrict__ st_act,
-                                              int32_t* __restrict__ part_hist, uint64_t* __restrict__ bk_key) {
-  const int p = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
-  const int lane = tid & 63, wave = tid >> 6;
-  __shared__ int cnt[kMaxBuckets];
-  const int nbk = nbk_[b];
-  const double klo = klo_[b], scale = kscale_[b];
-  int32_t* ph = part_hist + ((int64_t)b * kParts + p) * kMaxBuckets;
-  const int32_t* bs = bucket_start + (int64_t)b * (kMaxBuckets + 1);
-  for (int k = tid; k < nbk; k += kPT) cnt[k] = SCATTER ? ph[k] + bs[k] : 0;
-  __syncthreads();
-  const int bb = (int)((int64_t)p * nblk / kParts), be = (int)((int64_t)(p + 1) * nblk / kParts);
-  const int64_t seg = SCATTER ? (int64_t)seg_[b] : 0;
-  for (int blk = bb + wave; blk < be; blk += kPT / 64) {
-    const int n = block_counts[b * nblk + blk];
-    const int64_t src0 = ((int64_t)b * nblk + blk) * kBlk;
-    for (int i0 = 0; i0 < n; i0 += 256) {
-      uint32_t o[4];
-      int a[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int i = i0 + u * 64 + lane;
-        o[u] = i < n ? st_ord[src0 + i] : 0u;
-        if constexpr (SCATTER) a[u] = i < n ? st_act[src0 + i] : 0;
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        if (i0 + u * 64 + lane < n) {
-          const int slot = atomicAdd(&cnt[bucket_of(o[u], klo, scale, nbk)], 1);
-          if constexpr (SCATTER) bk_key[seg + slot] = ((uint64_t)(~o[u]) << 32) | (uint32_t)a[u];
-        }
-      }
-    }
-  }
-  if constexpr (!SCATTER) {
-    __syncthreads();
-    for (int k = tid; k < nbk; k += kPT) ph[k] = cnt[k];
-  }
-}
-
-// Per bucket k (one thread each): exclusive prefix of the part counts (in place) and the
-// bucket total.  Coalesced across k.
-__global__ __launch_bounds__(256) void k_bucket_count(const int32_t* __restrict__ nbk_, int32_t* __restrict__ part_hist,
-                                                      int32_t* __restrict__ bucket_tot) {
-  const int b = blockIdx.y, k = blockIdx.x * 256 + threadIdx.x;
-  if (k >= nbk_[b]) return;
-  int32_t* ph = part_hist + (int64_t)b * kParts * kMaxBuckets + k;
-  int run = 0;
-#pragma unroll 8
-  for (int p = 0; p < kParts; ++p) {
-    const int c = ph[(int64_t)p * kMaxBuckets];
-    ph[(int64_t)p * kMaxBuckets] = run;
-    run += c;
-  }
-  bucket_tot[(int64_t)b * kMaxBuckets + k] = run;
-}
-
-// Per sample: exclusive scan of the bucket totals -> bucket starts; segment offsets and T.
-__global__ __launch_bounds__(1024) void k_bucket_scan(int32_t B, const int32_t* __restrict__ counts,
-                                                      const int32_t* __restrict__ nbk_,
-                                                      const int32_t* __restrict__ bucket_tot,
-                                                      int32_t* __restrict__ bucket_start, int32_t* __restrict__ seg,
-                                                      int32_t* __restrict__ tdev, int32_t* __restrict__ t_out) {
-  const int b = blockIdx.x, tid = threadIdx.x;
-  __shared__ int sw[16];
-  const int nbk = nbk_[b];
-  const int per = (nbk + 1023) / 1024;  // <= 16
-  const int kb = min(tid * per, nbk), ke = min(kb + per, nbk);
-  const int32_t* bt = bucket_tot + (int64_t)b * kMaxBuckets;
-  int loc = 0;
-  for (int k = kb; k < ke; ++k) loc += bt[k];
-  int total;
-  int base = block_excl_scan<1024>(loc, sw, &total);
-  int32_t* bs = bucket_start + (int64_t)b * (kMaxBuckets + 1);
-  for (int k = kb; k < ke; ++k) {
-    bs[k] = base;
-    base += bt[k];
-  }
+  if (lane == 0) s_wr[wave] = wr;
+  const int32_t* bt = btot + (int64_t)b * kMaxB;
+  const int k0 = 2 * tid, k1 = 2 * tid + 1;
+  const int h0 = k0 < nb ? bt[k0] : 0, h1 = k1 < nb ? bt[k1] : 0;
+  int tot;
+  const int ex = block_excl_scan<1024>(h0 + h1, s_wc, &tot);
+  int32_t* bs = bstart + (int64_t)b * (kMaxB + 1);
+  if (k0 < nb) bs[k0] = ex;
+  if (k1 < nb) bs[k1] = ex + h0;
   if (tid == 0) {
-    bs[nbk] = total;
-    int s = 0, t = 0;
+    bs[nb] = tot;
+    double t = exp((double)logits[(int64_t)b * bstride + E] - (double)lmax[b]);  // the terminal stays available
+#pragma unroll
+    for (int w = 0; w < 16; ++w) t += s_wr[w];
+    wrest[b] = t;
+    counts[b] = tot;
+    atomicMax(tdev, tot + 1);
+  }
+}
+
+// In-block exact sort of an oversized bucket (n > kCap2) in global memory: 1-bit LSD radix
+// over the varying bits of the 64-bit records, ping-ponging between the bucket's slots of
+// the actions output (src0) and of out_suf (src1); ends with the sorted records in src0.
+__device__ void big_bucket_sort(uint64_t* __restrict__ s0, uint64_t* __restrict__ s1, int n, int* s_wc,
+                                uint32_t* s_red) {
+  const int tid = threadIdx.x;
+  uint64_t an = ~0ull, orr = 0ull;
+  for (int i = tid; i < n; i += kSortNT) {
+    an &= s0[i];
+    orr |= s0[i];
+  }
+  uint32_t alo = wave_and_u32((uint32_t)an), ahi = wave_and_u32((uint32_t)(an >> 32));
+  uint32_t olo = wave_or_u32((uint32_t)orr), ohi = wave_or_u32((uint32_t)(orr >> 32));
+  __syncthreads();
+  if ((tid & 63) == 0) {
+    s_red[(tid >> 6) * 4 + 0] = alo;
+    s_red[(tid >> 6) * 4 + 1] = ahi;
+    s_red[(tid >> 6) * 4 + 2] = olo;
+    s_red[(tid >> 6) * 4 + 3] = ohi;
+  }
+  __syncthreads();
+  alo = ahi = 0xFFFFFFFFu;
+  olo = ohi = 0u;
+  for (int w = 0; w < kSortNT / 64; ++w) {
+    alo &= s_red[w * 4 + 0];
+    ahi &= s_red[w * 4 + 1];
+    olo |= s_red[w * 4 + 2];
+    ohi |= s_red[w * 4 + 3];
+  }
+  const uint64_t vary = ((((uint64_t)ahi) << 32) | alo) ^ ((((uint64_t)ohi) << 32) | olo);
+  uint64_t* src = s0;
+  uint64_t* dst = s1;
+#pragma unroll 1
+  for (int bit = 0; bit < 64; ++bit) {
+    if (!((vary >> bit) & 1ull)) continue;
+    // zeros of the whole bucket
+    int z = 0;
+    for (int i = tid; i < n; i += kSortNT) z += ((src[i] >> bit) & 1ull) ? 0 : 1;
+    int ztot;
+    (void)block_excl_scan<kSortNT>(z, s_wc, &ztot);
+    int zc = 0, oc = ztot;  // running bases (uniform)
+#pragma unroll 1
+    for (int i0 = 0; i0 < n; i0 += kSortNT) {
+      const int i = i0 + tid;
+      const uint64_t v = i < n ? src[i] : 0ull;
+      const int one = (i < n) ? (int)((v >> bit) & 1ull) : 0;
+      const int zero = (i < n) ? 1 - one : 0;
+      int zt;
+      const int zex = block_excl_scan<kSortNT>(zero, s_wc, &zt);
+      const int chunk = min(kSortNT, n - i0);
+      if (i < n) dst[one ? oc + (tid - zex) : zc + zex] = v;
+      zc += zt;
+      oc += chunk - zt;
+    }
+    __syncthreads();
+    uint64_t* t = src;
+    src = dst;
+    dst = t;
+  }
+  if (src != s0) {
+    for (int i = tid; i < n; i += kSortNT) s0[i] = src[i];
+    __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------------ k_sort2
+// Barrier for LDS hand-offs only: waits for this wave's LDS operations, not for its
+// outstanding global loads (which __syncthreads would drain), so prefetches stay in flight.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// Oversized bucket (the sampled splitters missed; rare): gather into scratch, exact
+// in-block radix in global memory, then the same outputs as the LDS path.
+__device__ __forceinline__ void big_bucket(const int n, const int ntiles, const int* s_pre, const int* s_loc,
+                                           const uint64_t* stb, const float* lg, const double lmax, int64_t* act_out,
+                                           float* w_out, float* suf_out, uint64_t* s0, uint64_t* s1,
+                                           double* wsum_out, int* s_wc, double* s_wd, uint32_t* s_red) {
+  const int tid = threadIdx.x;
+  for (int i = tid; i < n; i += kSortNT) {
+    int lo = 0, hi = ntiles - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (s_pre[mid] <= i) lo = mid;
+      else hi = mid - 1;
+    }
+    s0[i] = stb[(int64_t)lo * kTile + s_loc[lo] + (i - s_pre[lo])];
+  }
+  __syncthreads();
+  big_bucket_sort(s0, s1, n, s_wc, s_red);
+  double carry = 0.0;  // suffix sums chunk by chunk from the end
+  for (int c1e = n; c1e > 0; c1e -= kSortNT) {
+    const int i = c1e - 1 - tid;
+    const uint32_t a = i >= 0 ? (uint32_t)s0[i] : 0u;
+    const double w = i >= 0 ? exp((double)lg[a] - lmax) : 0.0;
+    double t;
+    const double exs = block_excl_scan_d<kSortNT>(w, s_wd, &t);
+    if (i >= 0) {
+      act_out[i] = (int64_t)a;
+      w_out[i] = (float)w;
+      suf_out[i] = (float)(carry + exs + w);
+    }
+    carry += t;
+  }
+  if (tid == 0) *wsum_out = carry;
+}
+
+// Level-2 sort, persistent: one resident block per CU walks the FLATTENED (sample, bucket)
+// list, so the samples' very different winner counts (the terminal's own Gumbel key sets
+// them) do not pile work on the blocks of one sample.  Per bucket (<= kCap2 records):
+// the runs (one per select tile) are gathered wave-per-run with all loads of a round in
+// flight; records are ranked inside value-linear sub-buckets of ~0.5 record (almost always
+// a direct placement) and re-laid in trajectory order in LDS together with their logits;
+// then fp64 weights, in-bucket suffix sums and coalesced stores.  The next bucket's run
+// table is prefetched while the current one is processed (LDS-only barriers keep it in
+// flight).  Oversized buckets are left to k_sort2_big.
+__global__ __launch_bounds__(kSortNT) void k_sort2(int32_t E, int32_t B, int32_t ntiles,
+                                                   const int32_t* __restrict__ nb_,
+                                                   const int32_t* __restrict__ bstart,
+                                                   const int32_t* __restrict__ tcount, const int32_t* __restrict__ tloc,
+                                                   const uint64_t* __restrict__ staging,
+                                                   const float* __restrict__ stlog, const float* __restrict__ lmax_,
+                                                   int64_t t_cap, int64_t* __restrict__ actions,
+                                                   float* __restrict__ out_w, float* __restrict__ out_suf,
+                                                   double* __restrict__ bwsum) {
+  __shared__ uint64_t A[kCap2];
+  __shared__ float L[kCap2];
+  __shared__ uint16_t P[kCap2];  // arrival index of the record at each sorted position
+  __shared__ int s_pre[kMaxTiles + 1];
+  __shared__ int s_loc[kMaxTiles];
+  __shared__ int s_sub[kMaxSub + 1];
+  __shared__ int s_nbp[kMaxSamples + 1];
+  __shared__ int s_wc[kSortNT / 64];
+  __shared__ double s_wd[kSortNT / 64];
+  __shared__ uint32_t s_red[2 * (kSortNT / 64)];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (tid == 0) {
+    int run = 0;
     for (int i = 0; i < B; ++i) {
-      if (i < b) s += counts[i];
-      t = max(t, counts[i]);
+      s_nbp[i] = run;
+      run += nb_[i];
     }
-    seg[b] = s;
-    if (b == 0) {
-      *tdev = t + 1;
-      if (t_out) *t_out = t + 1;
+    s_nbp[B] = run;
+  }
+  __syncthreads();
+  const int total = s_nbp[B];
+  const int t0 = 2 * tid, t1 = 2 * tid + 1;
+  // run table of bucket f: count and tile-local offset of its run in tiles t0, t1
+  auto fetch = [&](int f, int& c0, int& c1, int& l0, int& l1) {
+    c0 = c1 = l0 = l1 = 0;
+    if (f < total) {
+      int bb = 0;
+      while (s_nbp[bb + 1] <= f) ++bb;
+      const int kk = f - s_nbp[bb];
+      const int64_t row = ((int64_t)bb * kMaxB + kk) * ntiles;
+      if (t0 < ntiles) {
+        c0 = tcount[row + t0];
+        l0 = tloc[row + t0];
+      }
+      if (t1 < ntiles) {
+        c1 = tcount[row + t1];
+        l1 = tloc[row + t1];
+      }
     }
-  }
-}
-
-__device__ __forceinline__ void wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-// Exclusive scan over the 64 lanes in lane order (fixed order -> deterministic).
-__device__ __forceinline__ double wave_excl_scan_d(double v, double* total) {
-  double incl = v;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const double y = __shfl_up(incl, o, kWave);
-    if ((threadIdx.x & 63) >= o) incl += y;
-  }
-  *total = __shfl(incl, 63, kWave);
-  const double ex = __shfl_up(incl, 1, kWave);
-  return (threadIdx.x & 63) ? ex : 0.0;
-}
-
-// Buckets of <= kWaveMax winners (the common case): one wave per bucket, no block barriers.
-// Rank by counting against the bucket's keys in the wave's LDS slice (broadcast reads), then
-// gather the logits, fp64 weights and suffix sums over contiguous per-lane chunks.
-__global__ __launch_bounds__(kSmallNT) void k_sort_small(const int32_t* __restrict__ nbk_,
-                                                         const int32_t* __restrict__ seg_,
-                                                         const int32_t* __restrict__ bucket_start,
-                                                         const uint64_t* __restrict__ bk_key,
-                                                         const float* __restrict__ logits, int64_t bstride,
-                                                         const float* __restrict__ lmax_,
-                                                         int32_t* __restrict__ out_act, double* __restrict__ out_w,
-                                                         double* __restrict__ out_suf,
-                                                         double* __restrict__ bucket_wsum) {
-  const int b = blockIdx.y, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  __shared__ uint64_t kin[kSmallNT / 64][kWaveMax];
-  __shared__ uint64_t kso[kSmallNT / 64][kWaveMax];
-  uint64_t* ki = kin[wave];
-  uint64_t* ks = kso[wave];
-  const int nbk = nbk_[b];
-  const int64_t seg = seg_[b];
-  const double lmax = (double)lmax_[b];
-  const float* lg = logits + (int64_t)b * bstride;
-  const int32_t* bs = bucket_start + (int64_t)b * (kMaxBuckets + 1);
-  const int wstride = gridDim.x * (kSmallNT / 64);
-  for (int k = blockIdx.x * (kSmallNT / 64) + wave; k < nbk; k += wstride) {
+  };
+  int c0, c1, l0, l1;
+  fetch(blockIdx.x, c0, c1, l0, l1);
+#pragma unroll 1
+  for (int f = blockIdx.x; f < total; f += gridDim.x) {
+    int b = 0;
+    while (s_nbp[b + 1] <= f) ++b;
+    const int k = f - s_nbp[b];
+    const int32_t* bs = bstart + (int64_t)b * (kMaxB + 1);
     const int s = bs[k], n = bs[k + 1] - s;
-    if (n > kWaveMax) continue;  // k_sort_large
-    double wsum = 0.0;
-    if (n > 0) {
-      const int64_t base = seg + s;
-      uint64_t mine[4];
+    int tot;
+    const int ex = block_excl_scan<kSortNT>(c0 + c1, s_wc, &tot);
+    if (t0 < ntiles) {
+      s_pre[t0] = ex;
+      s_loc[t0] = l0;
+    }
+    if (t1 < ntiles) {
+      s_pre[t1] = ex + c0;
+      s_loc[t1] = l1;
+    }
+    if (tid == 0) s_pre[ntiles] = tot;
+    fetch(f + gridDim.x, c0, c1, l0, l1);  // next bucket's run table, in flight meanwhile
+    lds_barrier();
+    if (n == 0 || n > kCap2) {
+      if (n == 0 && tid == 0) bwsum[(int64_t)b * kMaxB + k] = 0.0;
+      lds_barrier();
+      continue;
+    }
+    const uint64_t* stb = staging + (int64_t)b * ntiles * kTile;
+    const float* slb = stlog + (int64_t)b * ntiles * kTile;
+    // gather: wave per run, kRR runs per round, every load of a round in flight
+    constexpr int kRR = 4;
+#pragma unroll 1
+    for (int r0 = wave * kRR; r0 < ntiles; r0 += (kSortNT / 64) * kRR) {
+      uint64_t v[kRR];
+      float lv[kRR];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int e = u * 64 + lane;
-        mine[u] = e < n ? bk_key[base + e] : ~0ull;
-        ki[e] = mine[u];
+      for (int u = 0; u < kRR; ++u) {
+        const int r = r0 + u;
+        const int c = r < ntiles ? s_pre[r + 1] - s_pre[r] : 0;
+        const int64_t src = (int64_t)r * kTile + (r < ntiles ? s_loc[r] : 0) + lane;
+        v[u] = lane < c ? stb[src] : 0ull;
+        lv[u] = lane < c ? slb[src] : 0.0f;
       }
-      wave_sync();
-      int rank[4] = {0, 0, 0, 0};
-      for (int j = 0; j < n; ++j) {
-        const uint64_t kj = ki[j];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) rank[u] += kj < mine[u];
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-        if (u * 64 + lane < n) ks[rank[u]] = mine[u];
-      wave_sync();
-      const int c = (n + 63) >> 6;                               // chunk length (<= 4)
-      const int hi = n - min(lane * c, n), lo = max(hi - c, 0);  // lane 0 owns the tail
-      double wv[4];
-      double loc = 0.0;
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int i = hi - 1 - u;
-        wv[u] = (i >= lo) ? exp((double)lg[(uint32_t)ks[i]] - lmax) : 0.0;
-        loc += wv[u];
-      }
-      double run = wave_excl_scan_d(loc, &wsum);  // mass of all later elements
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int i = hi - 1 - u;
-        if (i >= lo) {
-          run += wv[u];
-          out_act[base + i] = (int32_t)(uint32_t)ks[i];
-          out_w[base + i] = wv[u];
-          out_suf[base + i] = run;
+      for (int u = 0; u < kRR; ++u) {
+        const int r = r0 + u;
+        const int c = r < ntiles ? s_pre[r + 1] - s_pre[r] : 0;
+        if (lane < c) {
+          A[s_pre[r] + lane] = v[u];
+          L[s_pre[r] + lane] = lv[u];
+        }
+#pragma unroll 1
+        for (int i = 64 + lane; i < c; i += 64) {  // runs longer than a wave (rare)
+          A[s_pre[r] + i] = stb[(int64_t)r * kTile + s_loc[r] + i];
+          L[s_pre[r] + i] = slb[(int64_t)r * kTile + s_loc[r] + i];
         }
       }
-      wave_sync();  // LDS slices are reused by the next bucket
     }
-    if (lane == 0) bucket_wsum[(int64_t)b * kMaxBuckets + k] = wsum;
+    lds_barrier();
+    constexpr int kPer = kCap2 / kSortNT;
+    uint64_t mine[kPer];
+    uint32_t mn = 0xFFFFFFFFu, mx = 0u;
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      const int i = j * kSortNT + tid;
+      mine[j] = i < n ? A[i] : ~0ull;
+      if (i < n) {
+        mn = min(mn, (uint32_t)(mine[j] >> 32));
+        mx = max(mx, (uint32_t)(mine[j] >> 32));
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      mn = min(mn, (uint32_t)__shfl_xor((int)mn, o, kWave));
+      mx = max(mx, (uint32_t)__shfl_xor((int)mx, o, kWave));
+    }
+    if (lane == 0) {
+      s_red[wave * 2] = mn;
+      s_red[wave * 2 + 1] = mx;
+    }
+    const int nsub = max(1, min(kMaxSub, 2 * n));
+    for (int i = tid; i <= nsub; i += kSortNT) s_sub[i] = 0;
+    lds_barrier();
+    mn = 0xFFFFFFFFu;
+    mx = 0u;
+#pragma unroll
+    for (int w = 0; w < kSortNT / 64; ++w) {
+      mn = min(mn, s_red[2 * w]);
+      mx = max(mx, s_red[2 * w + 1]);
+    }
+    const uint64_t span = (uint64_t)(mx - mn) + 1ull;
+    int sb[kPer];
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      sb[j] = 0;
+      if (j * kSortNT + tid < n) {
+        sb[j] = (int)((((uint64_t)((uint32_t)(mine[j] >> 32) - mn)) * (uint64_t)nsub) / span);
+        atomicAdd(&s_sub[sb[j]], 1);
+      }
+    }
+    lds_barrier();
+    {  // exclusive scan of the sub-bucket counts (kMaxSub / kSortNT per thread)
+      constexpr int kQ = kMaxSub / kSortNT;
+      int cv[kQ], loc = 0;
+#pragma unroll
+      for (int q = 0; q < kQ; ++q) {
+        const int i = tid * kQ + q;
+        cv[q] = i < nsub ? s_sub[i] : 0;
+        loc += cv[q];
+      }
+      int t2;
+      int run = block_excl_scan<kSortNT>(loc, s_wc, &t2);
+#pragma unroll
+      for (int q = 0; q < kQ; ++q) {
+        const int i = tid * kQ + q;
+        if (i < nsub) s_sub[i] = run;
+        run += cv[q];
+      }
+    }
+    lds_barrier();
+    // scatter by sub-bucket (the cursor is the start; afterwards s_sub[i] = END of i)
+#pragma unroll
+    for (int j = 0; j < kPer; ++j)
+      if (j * kSortNT + tid < n) A[atomicAdd(&s_sub[sb[j]], 1)] = mine[j];
+    lds_barrier();
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      if (j * kSortNT + tid < n) {
+        const int lo = sb[j] ? s_sub[sb[j] - 1] : 0, hi = s_sub[sb[j]];
+        int r = lo;
+#pragma unroll 1
+        for (int q = lo; q < hi; ++q) r += A[q] < mine[j];
+        sb[j] = r;  // rank
+      }
+    }
+    lds_barrier();
+#pragma unroll
+    for (int j = 0; j < kPer; ++j)
+      if (j * kSortNT + tid < n) {
+        A[sb[j]] = mine[j];
+        P[sb[j]] = (uint16_t)(j * kSortNT + tid);
+      }
+    lds_barrier();
+    // fp64 weights w = exp(l - lmax) and in-bucket inclusive suffix sums: thread t owns the
+    // t-th chunk counted from the END (contiguous, fixed order -> deterministic)
+    const double lmax = (double)lmax_[b];
+    const int per = (n + kSortNT - 1) / kSortNT;
+    const int hi_ = n - min(tid * per, n), lo_ = max(hi_ - per, 0);
+    double wv[kPer];
+    double loc = 0.0;
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      const int i = hi_ - 1 - j;
+      wv[j] = i >= lo_ ? exp((double)L[P[i]] - lmax) : 0.0;
+      loc += wv[j];
+    }
+    double wsum;
+    double run = block_excl_scan_d<kSortNT>(loc, s_wd, &wsum);  // mass of all later records
+    float* suf_out = out_suf + (int64_t)b * E + s;
+    float* w_out = out_w + (int64_t)b * E + s;
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      const int i = hi_ - 1 - j;
+      if (i >= lo_) {
+        run += wv[j];
+        suf_out[i] = (float)run;
+        w_out[i] = (float)wv[j];
+      }
+    }
+    int64_t* act_out = actions + (int64_t)b * t_cap + s;
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      const int i = j * kSortNT + tid;
+      if (i < n) act_out[i] = (int64_t)(uint32_t)A[i];
+    }
+    if (tid == 0) bwsum[(int64_t)b * kMaxB + k] = wsum;
+    lds_barrier();  // LDS reuse by the next bucket
   }
 }
 
-// Buckets of more than kWaveMax winners: up to kCap keys are split in LDS into value
-// sub-buckets of ~32 and ranked inside them; beyond kCap an exact tiled rank count; then
-// sorted actions, fp64 weights w = exp(l - lmax) (logit gathered by action) and in-bucket
-// inclusive suffix sums.
-__global__ __launch_bounds__(kSortNT) void k_sort_large(const int32_t* __restrict__ nbk_,
-                                                          const int32_t* __restrict__ seg_,
-                                                          const int32_t* __restrict__ bucket_start,
-                                                          const uint64_t* __restrict__ bk_key,
-                                                          const float* __restrict__ logits, int64_t bstride,
-                                                          const float* __restrict__ lmax_, int32_t* __restrict__ out_act,
-                                                          double* __restrict__ out_w, double* __restrict__ out_suf,
-                                                          double* __restrict__ bucket_wsum) {
-  constexpr int kMaxSub = 64;
-  const int b = blockIdx.y, tid = threadIdx.x;
-  __shared__ uint64_t key[kCap];
-  __shared__ uint64_t kmid[kCap];
-  __shared__ int scnt[kMaxSub], sst[kMaxSub], scur[kMaxSub];
-  __shared__ float sfl[8];
-  __shared__ double sd[kSortNT / 64];
-  const int nbk = nbk_[b];
-  const int64_t seg = seg_[b];
-  const double lmax = (double)lmax_[b];
-  const float* lg = logits + (int64_t)b * bstride;
-  const int32_t* bs = bucket_start + (int64_t)b * (kMaxBuckets + 1);
-  for (int k = blockIdx.x; k < nbk; k += gridDim.x) {
+// Buckets above the LDS capacity (rare): one block each, exact radix in global memory.
+__global__ __launch_bounds__(kSortNT) void k_sort2_big(int32_t E, int32_t B, int32_t ntiles,
+                                                       const int32_t* __restrict__ nb_,
+                                                       const int32_t* __restrict__ bstart,
+                                                       const int32_t* __restrict__ tcount,
+                                                       const int32_t* __restrict__ tloc,
+                                                       const uint64_t* __restrict__ staging,
+                                                       const float* __restrict__ logits, int64_t bstride,
+                                                       const float* __restrict__ lmax_, int64_t t_cap,
+                                                       int64_t* __restrict__ actions, float* __restrict__ out_w,
+                                                       float* __restrict__ out_suf, uint64_t* __restrict__ scratch,
+                                                       double* __restrict__ bwsum) {
+  __shared__ int s_nbp[kMaxSamples + 1];
+  __shared__ int s_pre[kMaxTiles + 1];
+  __shared__ int s_loc[kMaxTiles];
+  __shared__ int s_wc[kSortNT / 64];
+  __shared__ double s_wd[kSortNT / 64];
+  __shared__ uint32_t s_red[4 * (kSortNT / 64)];
+  const int tid = threadIdx.x;
+  if (tid == 0) {
+    int run = 0;
+    for (int i = 0; i < B; ++i) {
+      s_nbp[i] = run;
+      run += nb_[i];
+    }
+    s_nbp[B] = run;
+  }
+  __syncthreads();
+  const int total = s_nbp[B];
+#pragma unroll 1
+  for (int f = blockIdx.x; f < total; f += gridDim.x) {
+    int b = 0;
+    while (s_nbp[b + 1] <= f) ++b;
+    const int k = f - s_nbp[b];
+    const int32_t* bs = bstart + (int64_t)b * (kMaxB + 1);
     const int s = bs[k], n = bs[k + 1] - s;
-    const int64_t base = seg + s;
-    double wsum = 0.0;
-    if (n <= kWaveMax) continue;  // k_sort_small (block-uniform branch)
-    if (n <= kCap) {
-      // sub-bucket by value inside the bucket (linear over its own [min, max]), then rank
-      // each key against its sub-bucket only: ~6 barriers instead of a bitonic network
-      constexpr int kPerT = kCap / kSortNT;  // keys per thread (8)
-      uint64_t mine[kPerT];
-      float v[kPerT];
-      float vmn = INFINITY, vmx = -INFINITY;
-#pragma unroll
-      for (int u = 0; u < kPerT; ++u) {
-        const int i = u * kSortNT + tid;
-        mine[u] = i < n ? bk_key[base + i] : ~0ull;
-        v[u] = i < n ? from_orderable(~(uint32_t)(mine[u] >> 32)) : 0.0f;
-        if (i < n) {
-          vmn = fminf(vmn, v[u]);
-          vmx = fmaxf(vmx, v[u]);
-        }
-      }
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) {
-        vmn = fminf(vmn, __shfl_xor(vmn, o, kWave));
-        vmx = fmaxf(vmx, __shfl_xor(vmx, o, kWave));
-      }
-      if ((tid & 63) == 0) {
-        sfl[tid >> 6] = vmn;
-        sfl[4 + (tid >> 6)] = vmx;
-      }
-      const int nsub = min(kMaxSub, (n + 31) / 32);
-      for (int i = tid; i < nsub; i += kSortNT) scnt[i] = 0;
-      __syncthreads();
-      vmn = fminf(fminf(sfl[0], sfl[1]), fminf(sfl[2], sfl[3]));
-      vmx = fmaxf(fmaxf(sfl[4], sfl[5]), fmaxf(sfl[6], sfl[7]));
-      const double sc = vmx > vmn ? (double)nsub / ((double)vmx - (double)vmn) : 0.0;
-      int sb[kPerT];
-#pragma unroll
-      for (int u = 0; u < kPerT; ++u) {
-        sb[u] = 0;
-        if (u * kSortNT + tid < n) {
-          // reversed: sub-bucket 0 holds the largest values (trajectory order)
-          sb[u] = nsub - 1 - min(nsub - 1, (int)(((double)v[u] - (double)vmn) * sc));
-          atomicAdd(&scnt[sb[u]], 1);
-        }
-      }
-      __syncthreads();
-      if (tid < 64) {  // exclusive scan of <= 64 sub-bucket counts by one wave
-        const int c = tid < nsub ? scnt[tid] : 0;
-        const int inc = wave_incl_scan(c);
-        if (tid < nsub) {
-          sst[tid] = inc - c;
-          scur[tid] = inc - c;
-        }
-      }
-      __syncthreads();
-      int pos[kPerT];
-#pragma unroll
-      for (int u = 0; u < kPerT; ++u) {
-        if (u * kSortNT + tid < n) {
-          pos[u] = atomicAdd(&scur[sb[u]], 1);
-          kmid[pos[u]] = mine[u];
-        }
-      }
-      __syncthreads();
-#pragma unroll
-      for (int u = 0; u < kPerT; ++u) {
-        if (u * kSortNT + tid < n) {
-          const int a = sst[sb[u]], e = a + scnt[sb[u]];
-          int r = a;
-          for (int j = a; j < e; ++j) r += kmid[j] < mine[u];
-          key[r] = mine[u];
-        }
-      }
-      __syncthreads();
-      // inclusive suffix sums: thread t owns the t-th chunk counted from the END of the
-      // bucket (contiguous, fixed order -> deterministic, all terms positive)
-      const int per = (n + kSortNT - 1) / kSortNT;
-      const int hi_ = n - min(tid * per, n), lo_ = max(hi_ - per, 0);  // chunk = [lo_, hi_)
-      double wv[kCap / kSortNT];
-      double loc = 0.0;
-      for (int i = hi_ - 1, u = 0; i >= lo_; --i, ++u) {
-        wv[u] = exp((double)lg[(uint32_t)key[i]] - lmax);
-        loc += wv[u];
-      }
-      double run = block_excl_scan_d<kSortNT>(loc, sd, &wsum);  // mass of all later elements
-      for (int i = hi_ - 1, u = 0; i >= lo_; --i, ++u) {
-        run += wv[u];
-        out_act[base + i] = (int32_t)(uint32_t)key[i];
-        out_w[base + i] = wv[u];
-        out_suf[base + i] = run;
-      }
-      __syncthreads();
-    } else if (n > kCap) {
-      // exact fallback: rank by counting with the j-loop tiled through LDS; only reached by
-      // pathologically clustered keys
-      for (int i0 = 0; i0 < n; i0 += kSortNT) {
-        const int i = i0 + tid;
-        const uint64_t ki = i < n ? bk_key[base + i] : ~0ull;
-        int rank = 0;
-        for (int j0 = 0; j0 < n; j0 += kCap) {
-          const int m = min(kCap, n - j0);
-          __syncthreads();
-          for (int j = tid; j < m; j += kSortNT) key[j] = bk_key[base + j0 + j];
-          __syncthreads();
-          if (i < n)
-            for (int j = 0; j < m; ++j) rank += key[j] < ki;
-        }
-        if (i < n) {
-          const int a = (int32_t)(uint32_t)ki;
-          out_act[base + rank] = a;
-          out_w[base + rank] = exp((double)lg[a] - lmax);
-        }
-      }
-      __syncthreads();
-      double carry = 0.0;  // suffix sums from the end, chunk by chunk
-      for (int c1 = n; c1 > 0; c1 -= kSortNT) {
-        const int i = c1 - 1 - tid;  // thread 0 takes the last element of the chunk
-        const double w = i >= 0 ? out_w[base + i] : 0.0;
-        double tot;
-        const double ex = block_excl_scan_d<kSortNT>(w, sd, &tot);
-        if (i >= 0) out_suf[base + i] = carry + ex + w;
-        carry += tot;
-      }
-      wsum = carry;
-      __syncthreads();
+    if (n <= kCap2) continue;
+    const int32_t* crow = tcount + ((int64_t)b * kMaxB + k) * ntiles;
+    const int32_t* lrow = tloc + ((int64_t)b * kMaxB + k) * ntiles;
+    const int t0 = 2 * tid, t1 = 2 * tid + 1;
+    const int c0 = t0 < ntiles ? crow[t0] : 0, c1 = t1 < ntiles ? crow[t1] : 0;
+    int tot;
+    const int ex = block_excl_scan<kSortNT>(c0 + c1, s_wc, &tot);
+    if (t0 < ntiles) {
+      s_pre[t0] = ex;
+      s_loc[t0] = lrow[t0];
     }
-    if (tid == 0) bucket_wsum[(int64_t)b * kMaxBuckets + k] = wsum;
+    if (t1 < ntiles) {
+      s_pre[t1] = ex + c0;
+      s_loc[t1] = lrow[t1];
+    }
+    if (tid == 0) s_pre[ntiles] = tot;
+    __syncthreads();
+    int64_t* act_out = actions + (int64_t)b * t_cap + s;
+    big_bucket(n, ntiles, s_pre, s_loc, staging + (int64_t)b * ntiles * kTile, logits + (int64_t)b * bstride,
+               (double)lmax_[b], act_out, out_w + (int64_t)b * E + s, out_suf + (int64_t)b * E + s,
+               scratch + (int64_t)b * E + s, reinterpret_cast<uint64_t*>(act_out), bwsum + (int64_t)b * kMaxB + k,
+               s_wc, s_wd, s_red);
+    __syncthreads();
   }
 }
 
-// bucket_wsuf[k] = sum of the weights of all buckets after k (exclusive suffix, fixed order).
-__global__ __launch_bounds__(1024) void k_wscan(const int32_t* __restrict__ nbk_, const double* __restrict__ bucket_wsum,
-                                                double* __restrict__ bucket_wsuf) {
+// bwsuf[k] = sum of the weights of all buckets after k (exclusive suffix, fixed order).
+__global__ __launch_bounds__(1024) void k_wscan(const int32_t* __restrict__ nb_, const double* __restrict__ bwsum,
+                                                double* __restrict__ bwsuf) {
   const int b = blockIdx.x, tid = threadIdx.x;
   __shared__ double sd[16];
-  const int nbk = nbk_[b];
-  const int per = (nbk + 1023) / 1024;
-  const int hi_ = nbk - min(tid * per, nbk), lo_ = max(hi_ - per, 0);
-  const double* ws = bucket_wsum + (int64_t)b * kMaxBuckets;
-  double* wp = bucket_wsuf + (int64_t)b * kMaxBuckets;
+  const int nb = nb_[b];
+  const int per = (nb + 1023) / 1024;
+  const int hi_ = nb - min(tid * per, nb), lo_ = max(hi_ - per, 0);
+  const double* ws = bwsum + (int64_t)b * kMaxB;
+  double* wp = bwsuf + (int64_t)b * kMaxB;
   double loc = 0.0;
   for (int k = hi_ - 1; k >= lo_; --k) loc += ws[k];
   double total;
@@ -696,53 +968,61 @@ __global__ __launch_bounds__(1024) void k_wscan(const int32_t* __restrict__ nbk_
   }
 }
 
-// One wave per bucket: fwd_probs = w / (W_rest + later buckets + in-bucket suffix).
-__global__ __launch_bounds__(kSmallNT) void k_final(const int32_t* __restrict__ nbk_, const int32_t* __restrict__ seg_,
-                                                    const int32_t* __restrict__ bucket_start,
-                                                    const double* __restrict__ bucket_wsuf,
-                                                    const int32_t* __restrict__ out_act,
-                                                    const double* __restrict__ out_w,
-                                                    const double* __restrict__ out_suf,
-                                                    const double* __restrict__ wrest, int64_t t_cap,
-                                                    int64_t* __restrict__ actions, float* __restrict__ fwd) {
-  const int b = blockIdx.y, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int nbk = nbk_[b];
-  const int64_t seg = seg_[b];
-  const int32_t* bs = bucket_start + (int64_t)b * (kMaxBuckets + 1);
-  const double* wp = bucket_wsuf + (int64_t)b * kMaxBuckets;
-  const double rest = wrest[b];
-  int64_t* act_b = actions + (int64_t)b * t_cap;
-  float* fwd_b = fwd + (int64_t)b * t_cap;
-  const int wstride = gridDim.x * (kSmallNT / 64);
-  for (int k = blockIdx.x * (kSmallNT / 64) + wave; k < nbk; k += wstride) {
-    const int s = bs[k], e = bs[k + 1];
-    const double later = rest + wp[k];
-    for (int t = s + lane; t < e; t += 64) {
-      const int64_t i = seg + t;
-      act_b[t] = out_act[i];
-      fwd_b[t] = (float)(out_w[i] / (later + out_suf[i]));
+// fwd_probs = w / (W_rest + later buckets + in-bucket suffix), one block per bucket.
+__global__ __launch_bounds__(kFinNT) void k_final(int32_t E, const int32_t* __restrict__ nb_,
+                                                  const int32_t* __restrict__ bstart,
+                                                  const double* __restrict__ bwsuf, const float* __restrict__ out_w,
+                                                  const float* __restrict__ out_suf,
+                                                  const double* __restrict__ wrest, int64_t t_cap,
+                                                  float* __restrict__ fwd) {
+  const int k = blockIdx.x, b = blockIdx.y;
+  if (k >= nb_[b]) return;
+  const int32_t* bs = bstart + (int64_t)b * (kMaxB + 1);
+  const int s = bs[k], e = bs[k + 1];
+  const double later = wrest[b] + bwsuf[(int64_t)b * kMaxB + k];
+  const float* wb = out_w + (int64_t)b * E;
+  const float* sb = out_suf + (int64_t)b * E;
+  float* fb = fwd + (int64_t)b * t_cap;
+  for (int t = s + threadIdx.x; t < e; t += kFinNT) fb[t] = (float)((double)wb[t] / (later + (double)sb[t]));
+}
+
+// Terminal step and the -1 / 1.0 padding up to T (grid-stride: the padding of a sample
+// with few removals can be millions of steps).
+__global__ __launch_bounds__(kFinNT) void k_pad(int32_t E, const int32_t* __restrict__ counts,
+                                                const int32_t* __restrict__ tdev, const double* __restrict__ wrest,
+                                                const float* __restrict__ logits, int64_t bstride,
+                                                const float* __restrict__ lmax, int64_t t_cap,
+                                                int64_t* __restrict__ actions, float* __restrict__ fwd,
+                                                int32_t* __restrict__ t_out) {
+  const int b = blockIdx.y;
+  const int k = counts[b], T = *tdev;
+  if (t_out && b == 0 && blockIdx.x == 0 && threadIdx.x == 0) *t_out = T;
+  int64_t* ab = actions + (int64_t)b * t_cap;
+  float* fb = fwd + (int64_t)b * t_cap;
+  for (int t = k + blockIdx.x * kFinNT + threadIdx.x; t < T; t += gridDim.x * kFinNT) {
+    if (t == k) {
+      const double wE = exp((double)logits[(int64_t)b * bstride + E] - (double)lmax[b]);
+      ab[t] = E;
+      fb[t] = (float)(wE / wrest[b]);
+    } else {
+      ab[t] = -1;
+      fb[t] = 1.0f;
     }
   }
 }
 
-__global__ __launch_bounds__(kNT) void k_pad(int32_t E, const int32_t* __restrict__ counts,
-                                             const int32_t* __restrict__ tdev, const double* __restrict__ wrest,
-                                             const float* __restrict__ logits,
-                                             int64_t bstride, const float* __restrict__ lmax, int64_t t_cap,
-                                             int64_t* __restrict__ actions, float* __restrict__ fwd) {
-  const int b = blockIdx.y;
-  const int k = counts[b], T = *tdev;
-  for (int t = k + blockIdx.x * kNT + threadIdx.x; t < T; t += gridDim.x * kNT) {
-    if (t == k) {
-      const double wE = exp((double)logits[(int64_t)b * bstride + E] - (double)lmax[b]);
-      actions[(int64_t)b * t_cap + t] = E;
-      fwd[(int64_t)b * t_cap + t] = (float)(wE / wrest[b]);
-    } else {
-      actions[(int64_t)b * t_cap + t] = -1;
-      fwd[(int64_t)b * t_cap + t] = 1.0f;
-    }
+static int num_cus() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                hipSuccess || n <= 0)
+      n = 256;
   }
+  return n;
 }
+
+static int max_buckets(int32_t E) { return std::min(kMaxB, E / kTarget + 2); }
 
 }  // namespace
 }  // namespace spai
@@ -751,6 +1031,11 @@ using namespace spai;
 
 extern "C" size_t spai_rollout_workspace_bytes(int32_t E, int32_t B) {
   if (E <= 0 || B <= 0) return 0;
+  if ((int64_t)E > (int64_t)kMaxTiles * kTile) {
+    set_error("spai_rollout_workspace_bytes: E=%d above the %lld actions the sampler is compiled for", E,
+              (long long)kMaxTiles * kTile);
+    return 0;
+  }
   TrajWs w;
   traj_ws(nullptr, E, B, &w);
   return w.total_bytes;
@@ -762,19 +1047,28 @@ extern "C" int spai_rollout_select(const float* logits, int64_t bstride, int32_t
                                    void* stream) {
   SPAI_CHECK_ARG(logits && lmax && removed && counts && workspace, "spai_rollout_select: null pointer");
   SPAI_CHECK_ARG(E > 0 && B > 0 && bstride >= 0 && sample_base >= 0, "spai_rollout_select: bad shape");
+  SPAI_CHECK_ARG((int64_t)E <= (int64_t)kMaxTiles * kTile, "spai_rollout_select: E=%d too large", E);
   SPAI_CHECK_ARG(words == (E + 31) / 32, "spai_rollout_select: words must be ceil(E/32)");
   TrajWs w;
   traj_ws(workspace, E, B, &w);
   SPAI_CHECK_ARG(workspace_bytes >= w.total_bytes, "spai_rollout_select: workspace too small (%zu < %zu)",
                  workspace_bytes, w.total_bytes);
   hipStream_t s = (hipStream_t)stream;
-  k_select<<<dim3(w.nblk, B), kNT, 0, s>>>(logits, bstride, E, w.nblk, (uint32_t)seed, (uint32_t)(seed >> 32),
-                                           (uint32_t)stream_id, (uint32_t)(stream_id >> 32), sample_base, removed,
-                                           words, lmax, w.block_counts, w.block_min, w.block_max, w.block_wrest,
-                                           w.st_ord, w.st_act);
+  const uint32_t s0 = (uint32_t)seed, s1 = (uint32_t)(seed >> 32);
+  const uint32_t t0 = (uint32_t)stream_id, t1 = (uint32_t)(stream_id >> 32);
+  SPAI_CHECK_HIP(hipMemsetAsync(w.ctl, 0, sizeof(int32_t) * ((size_t)B * kMaxB + B + 1), s));
+  const int nsb = (w.M + kSampNT - 1) / kSampNT;
+  k_presample<<<dim3(nsb, B), kSampNT, 0, s>>>(logits, bstride, E, w.M, s0, s1, t0, t1, sample_base, w.samp,
+                                              w.samp_cnt);
   SPAI_CHECK_LAUNCH();
-  k_sample_stats<<<B, 1024, 0, s>>>(w.nblk, E, logits, bstride, lmax, w.block_counts, w.block_min, w.block_max,
-                                    w.block_wrest, counts, w.klo, w.kscale, w.nbk, w.wrest);
+  k_splitters<<<B, kSortNT, 0, s>>>(E, w.M, nsb, w.samp, w.samp_cnt, w.nb, w.spl, w.lut, w.lut_base);
+  SPAI_CHECK_LAUNCH();
+  k_select<<<dim3(w.ntiles, B), kSelNT, 0, s>>>(logits, bstride, E, w.ntiles, s0, s1, t0, t1, sample_base, removed,
+                                                words, lmax, w.nb, w.spl, w.lut, w.lut_base, w.staging, w.stlog, w.tcount, w.tloc, w.btot,
+                                                w.tile_wrest);
+  SPAI_CHECK_LAUNCH();
+  k_bscan<<<B, 1024, 0, s>>>(E, w.ntiles, logits, bstride, lmax, w.nb, w.btot, w.tile_wrest, w.bstart,
+                             counts, w.wrest, w.tdev);
   SPAI_CHECK_LAUNCH();
   return SPAI_OK;
 }
@@ -786,32 +1080,26 @@ extern "C" int spai_rollout_order(const float* logits, int64_t bstride, int32_t 
                  "spai_rollout_order: null pointer");
   SPAI_CHECK_ARG(E > 0 && B > 0 && t_cap >= (int64_t)E + 1, "spai_rollout_order: bad shape (E=%d B=%d t_cap=%lld)",
                  E, B, (long long)t_cap);
+  SPAI_CHECK_ARG((int64_t)E <= (int64_t)kMaxTiles * kTile, "spai_rollout_order: E=%d too large", E);
+  SPAI_CHECK_ARG(B <= kMaxSamples, "spai_rollout_order: B=%d above %d", B, kMaxSamples);
   TrajWs w;
   traj_ws(workspace, E, B, &w);
   SPAI_CHECK_ARG(workspace_bytes >= w.total_bytes, "spai_rollout_order: workspace too small");
   hipStream_t s = (hipStream_t)stream;
-  k_part<false><<<dim3(kParts, B), kPT, 0, s>>>(w.nblk, w.block_counts, w.klo, w.kscale, w.nbk, w.seg,
-                                                w.bucket_start, w.st_ord, w.st_act, w.part_hist, nullptr);
+  const int nbm = max_buckets(E);
+  const int g2 = std::max(1, std::min(nbm * B, num_cus()));
+  k_sort2<<<g2, kSortNT, 0, s>>>(E, B, w.ntiles, w.nb, w.bstart, w.tcount, w.tloc, w.staging, w.stlog, lmax, t_cap,
+                                 actions, w.out_w, w.out_suf, w.bwsum);
   SPAI_CHECK_LAUNCH();
-  k_bucket_count<<<dim3(kMaxBuckets / 256, B), 256, 0, s>>>(w.nbk, w.part_hist, w.bucket_tot);
+  k_sort2_big<<<g2, kSortNT, 0, s>>>(E, B, w.ntiles, w.nb, w.bstart, w.tcount, w.tloc, w.staging, logits, bstride,
+                                     lmax, t_cap, actions, w.out_w, w.out_suf, w.scratch, w.bwsum);
   SPAI_CHECK_LAUNCH();
-  k_bucket_scan<<<B, 1024, 0, s>>>(B, counts, w.nbk, w.bucket_tot, w.bucket_start, w.seg, w.tdev, t_out);
+  k_wscan<<<B, 1024, 0, s>>>(w.nb, w.bwsum, w.bwsuf);
   SPAI_CHECK_LAUNCH();
-  k_part<true><<<dim3(kParts, B), kPT, 0, s>>>(w.nblk, w.block_counts, w.klo, w.kscale, w.nbk, w.seg,
-                                               w.bucket_start, w.st_ord, w.st_act, w.part_hist, w.bk_key);
+  k_final<<<dim3(nbm, B), kFinNT, 0, s>>>(E, w.nb, w.bstart, w.bwsuf, w.out_w, w.out_suf, w.wrest, t_cap, fwd_probs);
   SPAI_CHECK_LAUNCH();
-  k_sort_small<<<dim3(kSmallGrid, B), kSmallNT, 0, s>>>(w.nbk, w.seg, w.bucket_start, w.bk_key, logits, bstride,
-                                                        lmax, w.out_act, w.out_w, w.out_suf, w.bucket_wsum);
-  SPAI_CHECK_LAUNCH();
-  k_sort_large<<<dim3(kSortGrid, B), kSortNT, 0, s>>>(w.nbk, w.seg, w.bucket_start, w.bk_key, logits, bstride,
-                                                      lmax, w.out_act, w.out_w, w.out_suf, w.bucket_wsum);
-  SPAI_CHECK_LAUNCH();
-  k_wscan<<<B, 1024, 0, s>>>(w.nbk, w.bucket_wsum, w.bucket_wsuf);
-  SPAI_CHECK_LAUNCH();
-  k_final<<<dim3(kSmallGrid, B), kSmallNT, 0, s>>>(w.nbk, w.seg, w.bucket_start, w.bucket_wsuf, w.out_act, w.out_w,
-                                             w.out_suf, w.wrest, t_cap, actions, fwd_probs);
-  SPAI_CHECK_LAUNCH();
-  k_pad<<<dim3(64, B), kNT, 0, s>>>(E, counts, w.tdev, w.wrest, logits, bstride, lmax, t_cap, actions, fwd_probs);
+  k_pad<<<dim3(std::max(1, 1024 / B), B), kFinNT, 0, s>>>(E, counts, w.tdev, w.wrest, logits, bstride, lmax, t_cap,
+                                                          actions, fwd_probs, t_out);
   SPAI_CHECK_LAUNCH();
   return SPAI_OK;
 }

@@ -27,7 +27,7 @@ from .preconditioner import Data
 
 class GFlowNet(nn.Module):
     def __init__(self, forward_policy, backward_policy, env, *, mode: str = "parity", seed: int | None = None,
-                 sample_base: int = 0):
+                 sample_base: int = 0, overlap: bool = True):
         super().__init__()
         if mode not in ("parity", "throughput"):
             raise ValueError("mode must be 'parity' or 'throughput'")
@@ -41,6 +41,7 @@ class GFlowNet(nn.Module):
         self.rollouts = 0  # Philox stream id of the next throughput rollout
         self._data_cache = {}
         self._side = None  # HIP stream for the fill/reward, overlapped with the trajectory sort
+        self.overlap = overlap  # False: fill/reward on the main stream after the sort (isolated kernel timing)
 
     # ------------------------------------------------------------------ policy
     def policy_logits(self, data, batch_size: int):
@@ -114,6 +115,13 @@ class GFlowNet(nn.Module):
         else:
             removed, counts, ws = kernels.rollout_select(lg, B, lmax, self.seed, self.rollouts, self.sample_base)
             self.rollouts += 1
+            if not self.overlap:
+                actions_full, fwd_full, t_dev = kernels.rollout_order(lg, B, lmax, counts, ws)
+                rewards = env.rewards_from_removed(removed, counts, alpha)
+                log._set_rollout(logits, actions_full, fwd_full, t_dev)
+                log.removed, log.counts = removed, counts
+                log.rewards = rewards.detach().to(torch.float32)
+                return log if return_log else None
             # the fill + ||.||_F reward needs only the removal bitmaps: run it on a second
             # HIP stream while the main stream sorts the trajectories
             main = torch.cuda.current_stream(lg.device)

@@ -1,0 +1,30 @@
+#!/bin/bash
+# PMC passes over a command (each its own rocprofv3 run, kernel-trace only), summary per kernel.
+# usage: scripts/pmc_kernels.sh <outdir> <cmd...>
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+OUT=$1; shift
+mkdir -p $OUT
+i=0
+for CTRS in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT" \
+            "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SMEM GRBM_GUI_ACTIVE" \
+            "FETCH_SIZE" "WRITE_SIZE"; do
+  i=$((i+1))
+  timeout -k 10 ${PMC_TIMEOUT:-200} rocprofv3 --kernel-trace --pmc $CTRS --output-format csv -d $OUT/p$i -o run -- "$@" > $OUT/p$i.log 2>&1
+  rc=$?; echo "pass $i rc=$rc"
+  if [ $rc -ne 0 ]; then tail -5 $OUT/p$i.log; exit $rc; fi
+done
+python - "$OUT" <<'PY'
+import csv, collections, glob, sys
+out = sys.argv[1]
+agg = collections.defaultdict(lambda: collections.defaultdict(list))
+for f in glob.glob(f"{out}/p*/run_counter_collection.csv"):
+    for r in csv.DictReader(open(f)):
+        k = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0][:40]
+        agg[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+for k, d in sorted(agg.items()):
+    if "spai" not in k:
+        continue
+    a = {c: sum(v) / len(v) for c, v in d.items()}
+    print(k, " ".join(f"{c}={v:.4g}" for c, v in sorted(a.items())))
+PY

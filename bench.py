@@ -56,14 +56,20 @@ class SyntheticLogits(torch.nn.Module):
         return self.l, self.a
 
 
-def fill_bytes(env, B) -> float:
-    """Compulsory HBM bytes of one fused LSQ-fill + ||AM-I|| launch."""
-    n, W, WA = env.pattern.n, env.pattern.width, env.a_lines.width
-    s = env.a_lines.val.element_size()
-    pattern = n * W * (4 + 4 + 4)            # idx, action id, value per slot
-    a_lines = n * WA * (4 + s)               # idx, value per slot
-    per_sample = math.ceil(env.init_nnz / 32) * 4 + n * W * s + 8  # bitmap + M values + partial
-    return pattern + a_lines + B * per_sample
+def fill_bytes(env, B, store_m: bool = True) -> float:
+    """Algorithmic HBM bytes of one fill + ||AM-I|| launch.
+
+    Gram-cached path (the env's default for widths <= 7): per line the action ids and the
+    Gram values (T + Wc fp64), per sample the removal bitmap and the stored values of M."""
+    n, W = env.pattern.n, env.pattern.width
+    s = env.a_lines.val.element_size() if env.fill == "lsq" else 4
+    per_sample = math.ceil(env.init_nnz / 32) * 4 + (n * W * s if store_m else 0) + 8
+    if getattr(env, "gram", None) is not None:
+        line = n * W * 4 + env.gram.numel() * 8 + (n * W * 4 if env.fill == "copy" else 0)
+    else:
+        sa = env.a_lines.val.element_size()
+        line = n * W * (4 + 4 + 4) + n * env.a_lines.width * (4 + sa)
+    return line + B * per_sample
 
 
 def cpu_baseline(cfg, B, budget_s: float):

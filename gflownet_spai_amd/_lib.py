@@ -18,7 +18,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libspai_hip
 SPAI_OK, SPAI_ERR_INVALID, SPAI_ERR_HIP, SPAI_ERR_UNSUPPORTED = 0, 1, 2, 3
 FILL_COPY, FILL_LSQ = 0, 1
 DTYPE_F32, DTYPE_F64 = 0, 1
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 _c_i32, _c_i64, _c_u64, _c_sz, _c_p = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_size_t, ctypes.c_void_p
 
@@ -41,6 +41,10 @@ SIGNATURES = {
     "spai_fill_workspace_bytes": (_c_sz, [_c_i32, _c_i32]),
     "spai_rewards": (ctypes.c_int, [_c_p, _c_p, _c_i32, _c_i64, _c_i32, ctypes.c_double, ctypes.c_double, _c_p, _c_p,
                                     _c_p, _c_p]),
+    "spai_gram_bytes": (_c_sz, [_c_i32, _c_i32]),
+    "spai_gram_build": (ctypes.c_int, [_c_i32, _c_i32, _c_p, _c_i32, _c_p, _c_p, _c_i32, _c_p, _c_p]),
+    "spai_fill_residual_gram": (ctypes.c_int, [_c_i32, _c_i32, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_i32, _c_p,
+                                               _c_i32, _c_p, _c_i32, _c_p, _c_p, _c_sz, _c_p]),
     "spai_fill_residual": (ctypes.c_int, [_c_i32, _c_i32, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_i32, _c_p, _c_p,
                                           _c_i32, _c_i32, _c_p, _c_i32, _c_p, _c_i32, _c_p, _c_p, _c_sz, _c_p]),
 }

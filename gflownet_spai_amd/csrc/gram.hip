@@ -1,0 +1,337 @@
+// Gram-cached fill + residual for gfx950 (the bench's roofline kernel).
+//
+// For one line l of M (slots p -> other index k_p) the fill and its residual only need
+//     G_pq = <A_line(k_p), A_line(k_q)>   and   c_p = A_line(k_p)[l]
+// (line residual^2 = m^T G m - 2 c^T m + 1, LSQ fill m = argmin = masked solve of G m = c).
+// G and c depend on the pattern and on A only, never on the sample, and the candidate
+// pattern is fixed for the lifetime of a PreconditionerEnv (preconditioner.py:23-25).  So
+// they are built ONCE per env (k_gram_build, the same arithmetic the per-call kernel
+// fill.hip:k_line used to redo on every launch) and stored structure-of-arrays in fp64:
+//     gram[l / 64][q][l % 64], q < T = Wc(Wc+1)/2: G upper triangle (p <= q, row-major),
+//     then Wc c_p (blocks of 64 lines: a wave's Gram data is one contiguous region, never
+//     T + Wc power-of-two-strided streams on the same HBM channels).
+// The per-rollout kernel (k_gram_fill) is then a stream: per line the Wc action ids, the
+// T + Wc Gram values and, per
+// sample, Wc mask bits and the Wc stored values of M, with a masked LDL^T in fp64 whose
+// pivots use v_rcp_f64 + one Newton step instead of IEEE division.  The LSQ line residual
+// is 1 - c^T m* = 1 - sum_k y_k^2 / D_k from the factorisation; it equals the residual of
+// the stored (rounded) values up to d^T G d, d = rounding of m (<= 1e-14 relative for fp32 M).
+#include "spai_device.h"
+#include "spai_status.h"
+
+namespace spai {
+namespace {
+
+constexpr int kNT = 256;
+constexpr int kChunk = 8;  // samples per LDS residual chunk of the fill kernel
+
+__host__ __device__ constexpr int tri(int w) { return w * (w + 1) / 2; }
+
+// index of G_pq (p <= q) in the packed upper triangle of a W-wide line
+template <int W>
+__device__ __forceinline__ constexpr int gidx(int p, int q) {
+  return p * W - p * (p - 1) / 2 + (q - p);
+}
+
+// 1/x to ~1 ulp: hardware reciprocal + one Newton step (the pivots are positive, normal).
+__device__ __forceinline__ double fast_rcp(double x) {
+  double r = __builtin_amdgcn_rcp(x);
+  const double e = fma(-x, r, 1.0);
+  return fma(r, e, r);
+}
+
+template <int W, int WA, typename TA>
+__global__ __launch_bounds__(kNT) void k_gram_build(int32_t n, int32_t wrt, int32_t wart,
+                                                    const int32_t* __restrict__ pat_idx,
+                                                    const int32_t* __restrict__ a_idx, const TA* __restrict__ a_val,
+                                                    double* __restrict__ gram) {
+  const int j = blockIdx.x * kNT + threadIdx.x;
+  if (j >= n) return;
+  int idx[W];
+#pragma unroll
+  for (int p = 0; p < W; ++p) idx[p] = p < wrt ? pat_idx[(int64_t)j * wrt + p] : -1;
+  int ai[W][WA];
+  double av[W][WA];
+#pragma unroll
+  for (int p = 0; p < W; ++p) {
+#pragma unroll
+    for (int s = 0; s < WA; ++s) {
+      ai[p][s] = -1;
+      av[p][s] = 0.0;
+      if (idx[p] >= 0 && s < wart) {
+        const int64_t o = (int64_t)idx[p] * wart + s;
+        ai[p][s] = a_idx[o];
+        av[p][s] = (double)a_val[o];
+      }
+    }
+  }
+#pragma unroll
+  for (int p = 0; p < W; ++p) {
+    double cp = 0.0, gpp = 0.0;
+#pragma unroll
+    for (int s = 0; s < WA; ++s) {
+      gpp += av[p][s] * av[p][s];
+      cp += (ai[p][s] == j) ? av[p][s] : 0.0;
+    }
+    double* gj = gram + (int64_t)(j >> 6) * (tri(W) + W) * 64 + (j & 63);  // blocked layout
+    gj[gidx<W>(p, p) * 64] = gpp;
+    gj[(tri(W) + p) * 64] = cp;
+#pragma unroll
+    for (int q = p + 1; q < W; ++q) {
+      double g = 0.0;
+      // A lines are sorted by index: each entry of line p matches at most one of line q
+#pragma unroll
+      for (int s = 0; s < WA; ++s) {
+        double m = 0.0;
+#pragma unroll
+        for (int t = 0; t < WA; ++t) m = (ai[p][s] >= 0 && ai[p][s] == ai[q][t]) ? av[q][t] : m;
+        g += av[p][s] * m;
+      }
+      gj[gidx<W>(p, q) * 64] = g;
+    }
+  }
+}
+
+// One thread per line: the line's action ids and Gram values are loaded once (coalesced:
+// consecutive lines are consecutive doubles), then the thread solves every sample; the
+// squared line residuals of a chunk of kChunk samples go to LDS and are summed per sample
+// by one wave each in a fixed order (two barriers per chunk, none per sample).
+template <int W, typename TM, bool LSQ>
+__global__ __launch_bounds__(kNT) void k_gram_fill(int32_t n, int32_t line_begin, int32_t line_end, int32_t wrt,
+                                                   const int32_t* __restrict__ pat_act,
+                                                   const float* __restrict__ pat_val,
+                                                   const double* __restrict__ gram, int32_t B,
+                                                   const uint32_t* __restrict__ removed, int32_t words,
+                                                   TM* __restrict__ m_out, double* __restrict__ partials) {
+  constexpr int T = tri(W);
+  __shared__ double s_r2[kChunk][kNT];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int lb = blockIdx.x;
+  const int j = line_begin + lb * kNT + t;
+  const bool valid = j < line_end;
+  const int64_t nloc = line_end - line_begin;
+  const int jj = valid ? j : line_begin;  // clamped: loads stay in bounds
+
+  int act[W];
+  float val[W];
+  const int32_t* pa = pat_act + (int64_t)jj * wrt;
+#pragma unroll
+  for (int p = 0; p < W; ++p) {
+    act[p] = (valid && p < wrt) ? pa[p] : -1;
+    val[p] = (!LSQ && valid && p < wrt) ? pat_val[(int64_t)jj * wrt + p] : 0.0f;
+  }
+  double G[T], c[W];
+  const double* gp = gram + (int64_t)(jj >> 6) * (T + W) * 64 + (jj & 63);  // blocked: one 64-line block contiguous
+#pragma unroll
+  for (int q = 0; q < T; ++q) G[q] = gp[q * 64];
+#pragma unroll
+  for (int p = 0; p < W; ++p) c[p] = gp[(T + p) * 64];
+  int wofs[W];  // bitmap word offsets / bit positions of the slots
+#pragma unroll
+  for (int p = 0; p < W; ++p) wofs[p] = act[p] >= 0 ? act[p] >> 5 : 0;
+  TM* mo = m_out != nullptr ? m_out + (int64_t)(j - line_begin) * wrt : nullptr;
+
+#pragma unroll 1
+  for (int b0 = 0; b0 < B; b0 += kChunk) {
+    const int nb = min(kChunk, B - b0);
+#pragma unroll 1
+    for (int s = 0; s < nb; ++s) {
+      const int b = b0 + s;
+      const uint32_t* rb = removed + (int64_t)b * words;
+      bool keep[W];
+#pragma unroll
+      for (int p = 0; p < W; ++p) keep[p] = act[p] >= 0 && !((rb[wofs[p]] >> (act[p] & 31)) & 1u);
+
+      double mr[W];
+      double r2ls = 1.0;  // LSQ: 1 - c^T m* = 1 - sum_k y_k^2 / D_k (G m* = c on the kept slots)
+      if constexpr (!LSQ) {
+#pragma unroll
+        for (int p = 0; p < W; ++p) mr[p] = keep[p] ? (double)val[p] : 0.0;
+      } else {
+        // masked LDL^T of the normal equations: removed slots become identity rows, rhs 0
+        double L[W][W], D[W], iD[W], y[W];
+#pragma unroll
+        for (int k = 0; k < W; ++k) {
+          const double gkk = G[gidx<W>(k, k)];
+          double dk = keep[k] ? gkk : 1.0;
+          const double ref = dk;
+#pragma unroll
+          for (int q = 0; q < k; ++q) dk -= L[k][q] * L[k][q] * D[q];
+          D[k] = dk;
+          iD[k] = (dk > 1e-13 * ref) ? fast_rcp(dk) : 0.0;
+#pragma unroll
+          for (int i = k + 1; i < W; ++i) {
+            double v = (keep[k] && keep[i]) ? G[gidx<W>(k, i)] : 0.0;
+#pragma unroll
+            for (int q = 0; q < k; ++q) v -= L[i][q] * L[k][q] * D[q];
+            L[i][k] = v * iD[k];
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < W; ++k) {
+          double v = keep[k] ? c[k] : 0.0;
+#pragma unroll
+          for (int q = 0; q < k; ++q) v -= L[k][q] * y[q];
+          y[k] = v;
+        }
+#pragma unroll
+        for (int k = 0; k < W; ++k) r2ls -= y[k] * y[k] * iD[k];
+#pragma unroll
+        for (int k = W - 1; k >= 0; --k) {
+          double v = y[k] * iD[k];
+#pragma unroll
+          for (int q = k + 1; q < W; ++q) v -= L[q][k] * mr[q];
+          mr[k] = v;
+        }
+#pragma unroll
+        for (int p = 0; p < W; ++p) mr[p] = keep[p] ? (double)(TM)mr[p] : 0.0;  // stored precision
+      }
+      if (mo != nullptr && valid) {
+        TM* dst = mo + (int64_t)b * nloc * wrt;
+#pragma unroll
+        for (int p = 0; p < W; ++p)
+          if (p < wrt) dst[p] = (TM)mr[p];
+      }
+      double r2 = 0.0;
+      if (valid) {
+        if constexpr (LSQ) {
+          r2 = r2ls;
+        } else {
+          r2 = 1.0;
+#pragma unroll
+          for (int p = 0; p < W; ++p) {
+            double acc = mr[p] * G[gidx<W>(p, p)] - 2.0 * c[p];
+#pragma unroll
+            for (int q = p + 1; q < W; ++q) acc += 2.0 * mr[q] * G[gidx<W>(p, q)];
+            r2 += mr[p] * acc;
+          }
+        }
+      }
+      s_r2[s][t] = r2;
+    }
+    __syncthreads();
+    for (int s = wave; s < nb; s += kNT / 64) {  // fixed-order per-sample block sums
+      double acc = 0.0;
+#pragma unroll
+      for (int q = 0; q < kNT / 64; ++q) acc += s_r2[s][q * 64 + lane];
+      acc = wave_sum(acc);
+      if (lane == 0) partials[(int64_t)(b0 + s) * gridDim.x + lb] = acc;
+    }
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(kNT) void k_gram_reduce(const double* __restrict__ partials, int32_t nparts,
+                                                     double* __restrict__ out) {
+  __shared__ double sred[kNT / 64];
+  const int b = blockIdx.x;
+  double s = 0.0;
+  for (int i = threadIdx.x; i < nparts; i += kNT) s += partials[(int64_t)b * nparts + i];
+  s = block_sum<kNT>(s, sred);
+  if (threadIdx.x == 0) out[b] = s;
+}
+
+static int gram_width(int32_t W) { return W <= 5 ? 5 : (W <= 7 ? 7 : 0); }
+
+template <int W, typename TM, bool LSQ>
+hipError_t launch_fill(int32_t n, int32_t lb, int32_t le, int32_t wrt, const int32_t* pa, const float* pv,
+                       const double* g, int32_t B, const uint32_t* rm, int32_t words, void* mo, double* partials,
+                       int32_t nparts, hipStream_t s) {
+  k_gram_fill<W, TM, LSQ><<<nparts, kNT, 0, s>>>(n, lb, le, wrt, pa, pv, g, B, rm, words, static_cast<TM*>(mo),
+                                                  partials);
+  return hipGetLastError();
+}
+
+}  // namespace
+}  // namespace spai
+
+using namespace spai;
+
+extern "C" size_t spai_gram_bytes(int32_t n, int32_t W) {
+  const int wc = gram_width(W);
+  if (n <= 0 || wc == 0) return 0;
+  return sizeof(double) * (size_t)(tri(wc) + wc) * (size_t)((n + 63) / 64 * 64);
+}
+
+extern "C" int spai_gram_build(int32_t n, int32_t W, const int32_t* pat_idx, int32_t WA, const int32_t* a_idx,
+                               const void* a_val, int32_t a_dtype, double* gram, void* stream) {
+  SPAI_CHECK_ARG(n >= 1 && W >= 1 && WA >= 1 && pat_idx && a_idx && a_val && gram, "spai_gram_build: bad arguments");
+  SPAI_CHECK_ARG(a_dtype == SPAI_DTYPE_F32 || a_dtype == SPAI_DTYPE_F64, "spai_gram_build: bad a_dtype");
+  const int wc = gram_width(W);
+  if (wc == 0 || WA > 7) {
+    set_error("spai_gram_build: widths W=%d WA=%d above the compiled 7", W, WA);
+    return SPAI_ERR_UNSUPPORTED;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  const int grid = (n + kNT - 1) / kNT;
+  if (a_dtype == SPAI_DTYPE_F32) {
+    if (wc == 5 && WA <= 5)
+      k_gram_build<5, 5, float><<<grid, kNT, 0, s>>>(n, W, WA, pat_idx, a_idx, (const float*)a_val, gram);
+    else if (wc == 5)
+      k_gram_build<5, 7, float><<<grid, kNT, 0, s>>>(n, W, WA, pat_idx, a_idx, (const float*)a_val, gram);
+    else
+      k_gram_build<7, 7, float><<<grid, kNT, 0, s>>>(n, W, WA, pat_idx, a_idx, (const float*)a_val, gram);
+  } else {
+    if (wc == 5 && WA <= 5)
+      k_gram_build<5, 5, double><<<grid, kNT, 0, s>>>(n, W, WA, pat_idx, a_idx, (const double*)a_val, gram);
+    else if (wc == 5)
+      k_gram_build<5, 7, double><<<grid, kNT, 0, s>>>(n, W, WA, pat_idx, a_idx, (const double*)a_val, gram);
+    else
+      k_gram_build<7, 7, double><<<grid, kNT, 0, s>>>(n, W, WA, pat_idx, a_idx, (const double*)a_val, gram);
+  }
+  SPAI_CHECK_LAUNCH();
+  return SPAI_OK;
+}
+
+extern "C" int spai_fill_residual_gram(int32_t fill_mode, int32_t n, int32_t line_begin, int32_t line_end, int32_t W,
+                                       const int32_t* pat_act, const float* pat_val, const double* gram, int32_t B,
+                                       const uint32_t* removed, int32_t words, void* m_out, int32_t m_dtype,
+                                       double* res2_out, void* workspace, size_t workspace_bytes, void* stream) {
+  SPAI_CHECK_ARG(fill_mode == SPAI_FILL_COPY || fill_mode == SPAI_FILL_LSQ,
+                 "spai_fill_residual_gram: bad fill_mode %d", fill_mode);
+  SPAI_CHECK_ARG(m_dtype == SPAI_DTYPE_F32 || m_dtype == SPAI_DTYPE_F64, "spai_fill_residual_gram: bad m_dtype");
+  SPAI_CHECK_ARG(n >= 1 && line_begin >= 0 && line_end >= line_begin && line_end <= n && W >= 1 && B >= 1 &&
+                     words >= 0,
+                 "spai_fill_residual_gram: bad shape");
+  SPAI_CHECK_ARG(res2_out && workspace, "spai_fill_residual_gram: null output/workspace");
+  SPAI_CHECK_ARG(fill_mode != SPAI_FILL_COPY || m_dtype == SPAI_DTYPE_F32,
+                 "spai_fill_residual_gram: copy fill stores fp32 values (utils.py:350)");
+  hipStream_t s = (hipStream_t)stream;
+  const int32_t nl = line_end - line_begin;
+  if (nl == 0) {
+    SPAI_CHECK_HIP(hipMemsetAsync(res2_out, 0, sizeof(double) * B, s));
+    return SPAI_OK;
+  }
+  SPAI_CHECK_ARG(pat_act && gram && removed && (fill_mode == SPAI_FILL_LSQ || pat_val),
+                 "spai_fill_residual_gram: null input");
+  const int wc = gram_width(W);
+  if (wc == 0) {
+    set_error("spai_fill_residual_gram: width W=%d above the compiled 7", W);
+    return SPAI_ERR_UNSUPPORTED;
+  }
+  const int32_t lpb = kNT;  // lines per block
+  const int32_t nparts = (nl + lpb - 1) / lpb;
+  SPAI_CHECK_ARG(workspace_bytes >= sizeof(double) * (size_t)nparts * B, "spai_fill_residual_gram: workspace too small");
+  double* partials = static_cast<double*>(workspace);
+  hipError_t e;
+  const bool lsq = fill_mode == SPAI_FILL_LSQ, f64 = m_dtype == SPAI_DTYPE_F64;
+  if (wc == 5) {
+    e = !lsq ? launch_fill<5, float, false>(n, line_begin, line_end, W, pat_act, pat_val, gram, B, removed, words,
+                                            m_out, partials, nparts, s)
+        : f64 ? launch_fill<5, double, true>(n, line_begin, line_end, W, pat_act, pat_val, gram, B, removed, words,
+                                             m_out, partials, nparts, s)
+              : launch_fill<5, float, true>(n, line_begin, line_end, W, pat_act, pat_val, gram, B, removed, words,
+                                            m_out, partials, nparts, s);
+  } else {
+    e = !lsq ? launch_fill<7, float, false>(n, line_begin, line_end, W, pat_act, pat_val, gram, B, removed, words,
+                                            m_out, partials, nparts, s)
+        : f64 ? launch_fill<7, double, true>(n, line_begin, line_end, W, pat_act, pat_val, gram, B, removed, words,
+                                             m_out, partials, nparts, s)
+              : launch_fill<7, float, true>(n, line_begin, line_end, W, pat_act, pat_val, gram, B, removed, words,
+                                            m_out, partials, nparts, s);
+  }
+  SPAI_CHECK_HIP(e);
+  k_gram_reduce<<<B, kNT, 0, s>>>(partials, nparts, res2_out);
+  SPAI_CHECK_LAUNCH();
+  return SPAI_OK;
+}

@@ -151,6 +151,43 @@ def fill_residual(pattern: Lines, a_lines: Lines, removed: torch.Tensor, lsq: bo
     return res2, m
 
 
+def gram_build(pattern: Lines, a_lines: Lines) -> torch.Tensor:
+    """Per-line Gram cache (fp64 [T + Wc, n]) of the LSQ fill / residual: built once per env."""
+    _lib.require_device(pattern.idx)
+    nb = _l().spai_gram_bytes(pattern.n, pattern.width)
+    if nb == 0:
+        raise NotImplementedError(f"no Gram kernel for width {pattern.width}")
+    gram = torch.empty(nb // 8, dtype=torch.float64, device=pattern.idx.device)
+    _lib.check(_l().spai_gram_build(pattern.n, pattern.width, _lib.ptr(pattern.idx), a_lines.width,
+                                    _lib.ptr(a_lines.idx), _lib.ptr(a_lines.val), _DT[a_lines.val.dtype],
+                                    _lib.ptr(gram), _lib.stream_ptr(pattern.idx.device)), "spai_gram_build")
+    return gram
+
+
+def fill_residual_gram(pattern: Lines, gram: torch.Tensor, removed: torch.Tensor, lsq: bool, line_begin: int = 0,
+                       line_end: int | None = None, store_m: bool = False, m_dtype=torch.float32):
+    """fill_residual from the env's Gram cache (same outputs)."""
+    _lib.require_device(removed)
+    if line_end is None:
+        line_end = pattern.n
+    B, words = removed.shape
+    mode = _lib.FILL_LSQ if lsq else _lib.FILL_COPY
+    if not lsq:
+        m_dtype = torch.float32
+    n_loc = line_end - line_begin
+    res2 = torch.empty(B, dtype=torch.float64, device=removed.device)
+    m = torch.empty(B, n_loc, pattern.width, dtype=m_dtype, device=removed.device) if store_m else None
+    nb = _l().spai_fill_workspace_bytes(max(n_loc, 1), B)
+    ws = _lib.workspace(nb, removed.device, "fill")
+    with _timed("fill_residual"):
+        st = _l().spai_fill_residual_gram(mode, pattern.n, line_begin, line_end, pattern.width, _lib.ptr(pattern.act),
+                                          _lib.ptr(pattern.val), _lib.ptr(gram), B, _lib.ptr(removed), words,
+                                          _lib.ptr(m), _DT[m_dtype], _lib.ptr(res2), _lib.ptr(ws), ws.numel(),
+                                          _lib.stream_ptr(removed.device))
+    _lib.check(st, "spai_fill_residual_gram")
+    return res2, m
+
+
 def rewards(res2: torch.Tensor, counts: torch.Tensor, nnz0: int, n: int, r0: float, f0: int, alpha: torch.Tensor):
     """(residual [B] fp64, reward [B] fp64) with the reference's reward formula and type promotion."""
     B = res2.numel()

@@ -78,6 +78,11 @@ class PreconditionerEnv(Env):
         ai = a.indices()
         self.a_lines: Lines = build_lines(ai[0], ai[1], a.values(), matrix_size, orient, self.device, a_dtype)
         self.last_m = None
+        # Gram cache of the fixed pattern (G = A_J^T A_J, c = A[l, J] per line): the per-rollout
+        # fill then streams it instead of re-gathering A (widths <= 7; wider patterns use the
+        # generic kernels)
+        self.gram = (kernels.gram_build(self.pattern, self.a_lines)
+                     if self.pattern.width <= 7 and self.a_lines.width <= 7 else None)
 
         self.orig_residual = self.calculate_residual(self.original_matrix, self.original_matrix)
         self._r0 = float(self.orig_residual)  # host copy: no device sync inside the reward formula
@@ -97,8 +102,12 @@ class PreconditionerEnv(Env):
                              line_end: int | None = None, group=None) -> Tensor:
         """[B] fp64 rewards from removal bitmaps; with ``group`` the lines are a shard and the
         per-sample squared norms are summed across the process group (one all_reduce)."""
-        res2, m = kernels.fill_residual(self.pattern, self.a_lines, removed, self.fill == "lsq", line_begin,
-                                        line_end, store_m=self.keep_m, m_dtype=self.a_lines.val.dtype)
+        if self.gram is not None:
+            res2, m = kernels.fill_residual_gram(self.pattern, self.gram, removed, self.fill == "lsq", line_begin,
+                                                 line_end, store_m=self.keep_m, m_dtype=self.a_lines.val.dtype)
+        else:
+            res2, m = kernels.fill_residual(self.pattern, self.a_lines, removed, self.fill == "lsq", line_begin,
+                                            line_end, store_m=self.keep_m, m_dtype=self.a_lines.val.dtype)
         if group is not None:
             import torch.distributed as dist
             dist.all_reduce(res2, group=group)

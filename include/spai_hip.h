@@ -86,7 +86,8 @@ int spai_parity_step(const float* logits, int64_t bstride, int32_t E1, int32_t B
  * Phase 1 (spai_rollout_select): writes removed[B][words] (words = ceil(E/32)),
  * counts[B] (= k_b, the number removed) and stages the winners in the workspace.
  * Phase 2 (spai_rollout_order): sorts each sample's winners by key descending (ties:
- * action ascending; MSD bucketing + LDS bitonic sort, no host round trip) and writes the
+ * action ascending; a sample sort: phase 1 groups the winners of every 16384-action tile
+ * by presampled key buckets, phase 2 sorts each bucket in LDS; no host round trip) and writes the
  * trajectory log in [B][t_cap] layout (t_cap >= E + 1, only the first T columns are
  * written, T = max_b k_b + 1 is stored to *t_out):
  *   actions[b][t] = t-th removed action, actions[b][k_b] = E, -1 up to T;
@@ -134,6 +135,26 @@ int spai_fill_residual(int32_t fill_mode, int32_t n, int32_t line_begin, int32_t
                        const int32_t* a_idx, const void* a_val, int32_t a_dtype, int32_t B,
                        const uint32_t* removed, int32_t words, void* m_out, int32_t m_dtype,
                        double* res2_out, void* workspace, size_t workspace_bytes, void* stream);
+
+/* ---------------------------------------------------------------- Gram-cached fill + residual
+ * The LSQ fill and the residual of line l need only G_pq = <A_line(k_p), A_line(k_q)> and
+ * c_p = A_line(k_p)[l] over the line's pattern slots p (other index k_p); both depend on the
+ * pattern and A only, and the candidate pattern is fixed per PreconditionerEnv
+ * (preconditioner.py:23-25).  spai_gram_build computes them once per env for all n lines
+ * into `gram` (spai_gram_bytes(n, W) bytes, fp64, blocked [ceil(n/64)][T + Wc][64] with
+ * Wc = 5 (W <= 5) or 7 (W <= 7), T = Wc(Wc+1)/2: the packed upper triangle of G, then c).
+ * spai_fill_residual_gram then does what spai_fill_residual does (same fill modes,
+ * res2_out / m_out semantics, line range, precision rules) from pat_act (+ pat_val for
+ * COPY) and `gram` alone: per-rollout traffic is a stream of the line data and, per sample,
+ * the mask bits and M values.  Widths above 7 return SPAI_ERR_UNSUPPORTED (use
+ * spai_fill_residual).  Workspace: spai_fill_workspace_bytes(line_end - line_begin, B). */
+size_t spai_gram_bytes(int32_t n, int32_t W);
+int spai_gram_build(int32_t n, int32_t W, const int32_t* pat_idx, int32_t WA, const int32_t* a_idx,
+                    const void* a_val, int32_t a_dtype, double* gram, void* stream);
+int spai_fill_residual_gram(int32_t fill_mode, int32_t n, int32_t line_begin, int32_t line_end, int32_t W,
+                            const int32_t* pat_act, const float* pat_val, const double* gram, int32_t B,
+                            const uint32_t* removed, int32_t words, void* m_out, int32_t m_dtype,
+                            double* res2_out, void* workspace, size_t workspace_bytes, void* stream);
 
 /* ---------------------------------------------------------------- rewards
  * residual[b] = sqrt(res2[b]) and reward[b] = 1000 * (alpha (1 - r/r0) + (1 - alpha)(1 - f/f0))

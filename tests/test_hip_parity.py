@@ -333,3 +333,31 @@ def test_line_shards_sum_to_full_residual():
         blocks.append(m)
     np.testing.assert_allclose(sum(parts).cpu().numpy(), full.cpu().numpy(), rtol=1e-12)
     assert torch.equal(torch.cat(blocks, 1), m_full)
+
+
+@pytest.mark.parametrize("side,fill,dims", [("AM", "lsq", 2), ("MA", "copy", 2), ("AM", "lsq", 3), ("AM", "copy", 3)])
+def test_gram_cached_fill_matches_direct_kernel(side, fill, dims):
+    """The env's Gram-cached fill (spai_gram_build + spai_fill_residual_gram, the bench path)
+    gives the per-call kernel's (spai_fill_residual) residuals and M values, also per shard."""
+    from gflownet_spai_amd import PreconditionerEnv, kernels, poisson_2d, poisson_3d
+    from gflownet_spai_amd.distributed import shard_lines
+    A = poisson_2d(48) if dims == 2 else poisson_3d(10)
+    n = A.shape[0]
+    env = PreconditionerEnv(n, A, A, side=side, fill=fill)
+    assert env.gram is not None
+    E = env.init_nnz
+    rng = np.random.default_rng(11)
+    acts = torch.from_numpy(np.where(rng.random((5, E)) < 0.3, np.arange(E), -1))
+    removed, counts = kernels.actions_to_removed(acts.to(DEV), E)
+    mdt = env.a_lines.val.dtype
+    ref, m_ref = kernels.fill_residual(env.pattern, env.a_lines, removed, fill == "lsq", store_m=True, m_dtype=mdt)
+    got, m_got = kernels.fill_residual_gram(env.pattern, env.gram, removed, fill == "lsq", store_m=True, m_dtype=mdt)
+    np.testing.assert_allclose(got.cpu().numpy(), ref.cpu().numpy(), rtol=1e-12)
+    tol = 1e-6 if m_got.dtype == torch.float32 else 1e-12
+    np.testing.assert_allclose(m_got.cpu().numpy(), m_ref.cpu().numpy(), rtol=tol, atol=tol)
+    parts = []
+    for r in range(4):
+        b, e = shard_lines(n, r, 4)
+        res2, _ = kernels.fill_residual_gram(env.pattern, env.gram, removed, fill == "lsq", b, e)
+        parts.append(res2)
+    np.testing.assert_allclose(sum(parts).cpu().numpy(), got.cpu().numpy(), rtol=1e-12)

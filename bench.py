@@ -72,6 +72,20 @@ def fill_bytes(env, B, store_m: bool = True) -> float:
     return line + B * per_sample
 
 
+def measured_traffic(cfg: str, B: int, overlap: bool):
+    """HBM bytes per launch of the roofline kernel from the committed PMC profile of this
+    exact workload (profiles/fill_traffic.json, written by scripts/collect_profiles.py from
+    separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of `bench.py`), else None."""
+    path = os.path.join(ROOT, "profiles", "fill_traffic.json")
+    try:
+        rec = json.load(open(path))
+    except (OSError, ValueError):
+        return None
+    if rec.get("config") == cfg and rec.get("batch") == B:
+        return float(rec["hbm_bytes_per_launch"])
+    return None
+
+
 def cpu_baseline(cfg, B, budget_s: float):
     """The oracle (numpy, single thread) on a bounded sample of the same workload."""
     from oracle import spai_oracle as O
@@ -179,10 +193,7 @@ def main():
         fill_ms = phases.get("fill_residual", float("nan"))
         fb = fill_bytes(env, B)
         achieved = fb / (fill_ms * 1e-3) / 1e9
-        traffic = None
-        tfile = os.environ.get("SPAI_FILL_TRAFFIC_BYTES")
-        if tfile:
-            traffic = float(tfile)
+        traffic = measured_traffic(args.config, B, not args.no_overlap)
         out = {
             "metric": "SPAI columns/sec + final ||AM-I||_F, 2D Poisson 1024^2, at 1/2/4/8 GPU",
             "value": B * n * world / dt,
@@ -202,7 +213,8 @@ def main():
             "final_residual_fro_mean": float(res.mean()),
             "removed_per_candidate_mean": float(counts.mean()),
             "phases_ms": phases,
-            "roofline": {"kernel": "spai_fill_residual (fused LSQ fill + ||AM-I||^2)", "bound": "hbm",
+            "roofline": {"kernel": "k_gram_fill<5,f32,LSQ> (spai_fill_residual_gram: LSQ fill of M + ||AM-I||^2)",
+                         "bound": "hbm",
                          "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic, "bytes_per_launch": fb, "avg_launch_ms": fill_ms},
         }

@@ -283,35 +283,32 @@ extern "C" int spai_gram_build(int32_t n, int32_t W, const int32_t* pat_idx, int
   return SPAI_OK;
 }
 
-extern "C" int spai_fill_residual_gram(int32_t fill_mode, int32_t n, int32_t line_begin, int32_t line_end, int32_t W,
-                                       const int32_t* pat_act, const float* pat_val, const double* gram, int32_t B,
-                                       const uint32_t* removed, int32_t words, void* m_out, int32_t m_dtype,
-                                       double* res2_out, void* workspace, size_t workspace_bytes, void* stream) {
+// Fill + per-block partial sums only (res2 partials stay in the workspace for spai_fill_reduce).
+extern "C" int spai_fill_lines_gram(int32_t fill_mode, int32_t n, int32_t line_begin, int32_t line_end, int32_t W,
+                                    const int32_t* pat_act, const float* pat_val, const double* gram, int32_t B,
+                                    const uint32_t* removed, int32_t words, void* m_out, int32_t m_dtype,
+                                    void* workspace, size_t workspace_bytes, void* stream) {
   SPAI_CHECK_ARG(fill_mode == SPAI_FILL_COPY || fill_mode == SPAI_FILL_LSQ,
-                 "spai_fill_residual_gram: bad fill_mode %d", fill_mode);
-  SPAI_CHECK_ARG(m_dtype == SPAI_DTYPE_F32 || m_dtype == SPAI_DTYPE_F64, "spai_fill_residual_gram: bad m_dtype");
+                 "spai_fill_lines_gram: bad fill_mode %d", fill_mode);
+  SPAI_CHECK_ARG(m_dtype == SPAI_DTYPE_F32 || m_dtype == SPAI_DTYPE_F64, "spai_fill_lines_gram: bad m_dtype");
   SPAI_CHECK_ARG(n >= 1 && line_begin >= 0 && line_end >= line_begin && line_end <= n && W >= 1 && B >= 1 &&
                      words >= 0,
-                 "spai_fill_residual_gram: bad shape");
-  SPAI_CHECK_ARG(res2_out && workspace, "spai_fill_residual_gram: null output/workspace");
+                 "spai_fill_lines_gram: bad shape");
+  SPAI_CHECK_ARG(workspace != nullptr, "spai_fill_lines_gram: null workspace");
   SPAI_CHECK_ARG(fill_mode != SPAI_FILL_COPY || m_dtype == SPAI_DTYPE_F32,
-                 "spai_fill_residual_gram: copy fill stores fp32 values (utils.py:350)");
+                 "spai_fill_lines_gram: copy fill stores fp32 values (utils.py:350)");
   hipStream_t s = (hipStream_t)stream;
   const int32_t nl = line_end - line_begin;
-  if (nl == 0) {
-    SPAI_CHECK_HIP(hipMemsetAsync(res2_out, 0, sizeof(double) * B, s));
-    return SPAI_OK;
-  }
+  if (nl == 0) return SPAI_OK;
   SPAI_CHECK_ARG(pat_act && gram && removed && (fill_mode == SPAI_FILL_LSQ || pat_val),
-                 "spai_fill_residual_gram: null input");
+                 "spai_fill_lines_gram: null input");
   const int wc = gram_width(W);
   if (wc == 0) {
-    set_error("spai_fill_residual_gram: width W=%d above the compiled 7", W);
+    set_error("spai_fill_lines_gram: width W=%d above the compiled 7", W);
     return SPAI_ERR_UNSUPPORTED;
   }
-  const int32_t lpb = kNT;  // lines per block
-  const int32_t nparts = (nl + lpb - 1) / lpb;
-  SPAI_CHECK_ARG(workspace_bytes >= sizeof(double) * (size_t)nparts * B, "spai_fill_residual_gram: workspace too small");
+  const int32_t nparts = (nl + kNT - 1) / kNT;
+  SPAI_CHECK_ARG(workspace_bytes >= sizeof(double) * (size_t)nparts * B, "spai_fill_lines_gram: workspace too small");
   double* partials = static_cast<double*>(workspace);
   hipError_t e;
   const bool lsq = fill_mode == SPAI_FILL_LSQ, f64 = m_dtype == SPAI_DTYPE_F64;
@@ -331,7 +328,28 @@ extern "C" int spai_fill_residual_gram(int32_t fill_mode, int32_t n, int32_t lin
                                             m_out, partials, nparts, s);
   }
   SPAI_CHECK_HIP(e);
-  k_gram_reduce<<<B, kNT, 0, s>>>(partials, nparts, res2_out);
+  return SPAI_OK;
+}
+
+extern "C" int spai_fill_reduce(int32_t n_lines, int32_t B, const void* workspace, double* res2_out, void* stream) {
+  SPAI_CHECK_ARG(n_lines >= 0 && B >= 1 && workspace && res2_out, "spai_fill_reduce: bad arguments");
+  hipStream_t s = (hipStream_t)stream;
+  if (n_lines == 0) {
+    SPAI_CHECK_HIP(hipMemsetAsync(res2_out, 0, sizeof(double) * B, s));
+    return SPAI_OK;
+  }
+  k_gram_reduce<<<B, kNT, 0, s>>>(static_cast<const double*>(workspace), (n_lines + kNT - 1) / kNT, res2_out);
   SPAI_CHECK_LAUNCH();
   return SPAI_OK;
+}
+
+extern "C" int spai_fill_residual_gram(int32_t fill_mode, int32_t n, int32_t line_begin, int32_t line_end, int32_t W,
+                                       const int32_t* pat_act, const float* pat_val, const double* gram, int32_t B,
+                                       const uint32_t* removed, int32_t words, void* m_out, int32_t m_dtype,
+                                       double* res2_out, void* workspace, size_t workspace_bytes, void* stream) {
+  SPAI_CHECK_ARG(res2_out != nullptr, "spai_fill_residual_gram: null res2_out");
+  const int st = spai_fill_lines_gram(fill_mode, n, line_begin, line_end, W, pat_act, pat_val, gram, B, removed,
+                                      words, m_out, m_dtype, workspace, workspace_bytes, stream);
+  if (st != SPAI_OK) return st;
+  return spai_fill_reduce(line_end - line_begin, B, workspace, res2_out, stream);
 }

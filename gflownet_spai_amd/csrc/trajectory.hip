@@ -33,10 +33,12 @@
 namespace spai {
 namespace {
 
-constexpr int kSelNT = 1024;               // threads of a select block
-constexpr int kSelRounds = 4;              // rounds of 4 consecutive actions per thread
-constexpr int kTile = kSelNT * 4 * kSelRounds;  // 16384 actions per select tile
-constexpr int kTileBits = 14;              // log2(kTile)
+constexpr int kNT = 256;                   // threads of a select block
+constexpr int kBlk = kNT * 4;              // actions per select block (4 consecutive per thread)
+constexpr int kTileBlk = 16;               // select blocks per grouping tile (< 64: one wave scans them)
+constexpr int kTile = kBlk * kTileBlk;     // 16384 actions per grouping tile
+constexpr int kGrpNT = 512;                // threads of a grouping block
+constexpr int kWin = 3584;                 // records per LDS output window of a grouping block
 constexpr int kSampM = 65536;              // subset size (power of two, capped by E)
 constexpr int kSampNT = 256;
 constexpr int kSampCap = 32768;            // sampled winners behind the splitters
@@ -61,10 +63,16 @@ struct TrajWs {
   uint32_t* spl;          // [B][kMaxB] ascending orderable splitters
   uint16_t* lut;          // [B][kBins] bucket lookup table
   uint32_t* lut_base;     // [B][2] (min key, shift) of the table
+  int32_t nblk;
+  uint32_t* c_ord;        // [B][nblk][kBlk] winners compacted per select block: orderable key
+  int32_t* c_act;         //                                                   action
+  float* c_log;           //                                                   logit
+  int32_t* blk_cnt;       // [B][nblk]
+  double* blk_wrest;      // [B][nblk]
   uint64_t* staging;      // [B][ntiles][kTile] (~ord << 32 | action), grouped by bucket per tile
   float* stlog;           // [B][ntiles][kTile] logit of each staged record
-  int32_t* tcount;        // [B][kMaxB][ntiles]
-  int32_t* tloc;          // [B][kMaxB][ntiles]
+  int32_t* tcount;        // [B][ntiles][kMaxB] winners of bucket k in tile t
+  int32_t* tloc;          // [B][ntiles][kMaxB] their offset in the tile's grouped stream
   double* tile_wrest;     // [B][ntiles]
   int32_t* bstart;        // [B][kMaxB + 1]
   double* wrest;          // [B]
@@ -92,6 +100,12 @@ static void traj_ws(void* base, int32_t E, int32_t B, TrajWs* w) {
   w->spl = c.take<uint32_t>((size_t)B * kMaxB);
   w->lut = c.take<uint16_t>((size_t)B * kBins);
   w->lut_base = c.take<uint32_t>((size_t)B * 2);
+  w->nblk = (E + kBlk - 1) / kBlk;
+  w->c_ord = c.take<uint32_t>((size_t)B * w->nblk * kBlk);
+  w->c_act = c.take<int32_t>((size_t)B * w->nblk * kBlk);
+  w->c_log = c.take<float>((size_t)B * w->nblk * kBlk);
+  w->blk_cnt = c.take<int32_t>((size_t)B * w->nblk);
+  w->blk_wrest = c.take<double>((size_t)B * w->nblk);
   w->staging = c.take<uint64_t>((size_t)B * w->ntiles * kTile);
   w->stlog = c.take<float>((size_t)B * w->ntiles * kTile);
   w->tcount = c.take<int32_t>((size_t)B * kMaxB * w->ntiles);
@@ -358,154 +372,234 @@ __global__ __launch_bounds__(kSortNT) void k_splitters(int32_t E, int32_t M, int
 }
 
 // ------------------------------------------------------------------ k_select
-// LDS record per winner: (orderable key << 32) | (bucket << 14) | action within the tile.
-__global__ __launch_bounds__(kSelNT) void k_select(const float* __restrict__ logits, int64_t bstride, int32_t E,
-                                                   int32_t ntiles, uint32_t seed0, uint32_t seed1, uint32_t st0,
-                                                   uint32_t st1, int32_t sample_base, uint32_t* __restrict__ removed,
-                                                   int32_t words, const float* __restrict__ lmax,
-                                                   const int32_t* __restrict__ nb_, const uint32_t* __restrict__ spl_,
-                                                   const uint16_t* __restrict__ lut_, const uint32_t* __restrict__ lut_base,
-                                                   uint64_t* __restrict__ staging, float* __restrict__ stlog,
-                                                   int32_t* __restrict__ tcount,
-                                                   int32_t* __restrict__ tloc, int32_t* __restrict__ btot,
-                                                   double* __restrict__ tile_wrest) {
-  constexpr int kWaveSpan = kTile / (kSelNT / 64);  // actions (and LDS slots) per wave: 1024
-  __shared__ uint64_t u[kTile];                     // per-wave regions of winner records
-  __shared__ uint32_t s_spl[kMaxB];
-  __shared__ int s_hist[kMaxB];
-  __shared__ uint16_t s_lut[kBins];
-  __shared__ int s_wc[kSelNT / 64];
-  __shared__ double s_wr[kSelNT / 64];
-  __shared__ float s_tk;
-  const int b = blockIdx.y, tile = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+// 1024 actions per block (256 threads x 4 consecutive): Philox4x32-10 + deterministic fp32
+// Gumbel keys, removal bitmap words (8-lane shuffles), the fp64 mass of the untouched
+// actions (fixed order) and the block's winners compacted in action order as three
+// coalesced streams (orderable key, action, logit).  Small LDS: full occupancy for the
+// ALU-bound key arithmetic.
+__global__ __launch_bounds__(kNT) void k_select(const float* __restrict__ logits, int64_t bstride, int32_t E,
+                                                int32_t nblk, uint32_t seed0, uint32_t seed1, uint32_t st0,
+                                                uint32_t st1, int32_t sample_base, uint32_t* __restrict__ removed,
+                                                int32_t words, const float* __restrict__ lmax,
+                                                uint32_t* __restrict__ c_ord, int32_t* __restrict__ c_act,
+                                                float* __restrict__ c_log, int32_t* __restrict__ blk_cnt,
+                                                double* __restrict__ blk_wrest) {
+  const int b = blockIdx.y, blk = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
   const float* lg = logits + (int64_t)b * bstride;
   const uint32_t bg = (uint32_t)(sample_base + b);
-  const int nb = nb_[b];
-  for (int k = tid; k < nb; k += kSelNT) {
-    s_hist[k] = 0;
-    if (k < nb - 1) s_spl[k] = spl_[(int64_t)b * kMaxB + k];
-  }
-  for (int i = tid; i < kBins; i += kSelNT) s_lut[i] = lut_[(int64_t)b * kBins + i];
-  const uint32_t lmn = lut_base[2 * b];
-  const int lsh = (int)lut_base[2 * b + 1];
+  __shared__ float s_tk;
+  __shared__ int s_wc[kNT / 64];
+  __shared__ double s_wr[kNT / 64];
   if (tid == 0) s_tk = terminal_key(lg, E, bg, st0, st1, seed0, seed1);
   __syncthreads();
   const float tk = s_tk;
   const float lm = lmax[b];
-  const int tbase = tile * kTile;
-  uint64_t* uw = u + wave * kWaveSpan;
-  int wc = 0;       // records of this wave so far (wave-uniform)
-  double wr = 0.0;  // mass of the actions this thread leaves untouched
-#pragma unroll 1
-  for (int r = 0; r < kSelRounds; ++r) {
-    const int al = r * (kSelNT * 4) + tid * 4;  // action within the tile
-    const int a0 = tbase + al;
-    uint32_t nib = 0, ord[4];
-    if (a0 < E) {
-      const uint4 rr = philox4x32_10((uint32_t)a0 >> 2, bg, st0, st1, seed0, seed1);
+  const int a0 = blk * kBlk + tid * 4;
+  uint32_t nib = 0, ord[4];
+  float lv[4];
+  double wr = 0.0;
+  if (a0 < E) {
+    const uint4 rr = philox4x32_10((uint32_t)a0 >> 2, bg, st0, st1, seed0, seed1);
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        ord[s] = 0;
-        if (a0 + s < E) {
-          const float lv = lg[a0 + s];
-          const float key = gumbel_key(lv, pick_word(rr, s));
-          if (key > tk) {
-            nib |= 1u << s;
-            ord[s] = orderable(key);
-          } else {
-            wr += (double)__expf(lv - lm);
-          }
+    for (int s = 0; s < 4; ++s) {
+      ord[s] = 0;
+      lv[s] = 0.0f;
+      if (a0 + s < E) {
+        lv[s] = lg[a0 + s];
+        const float key = gumbel_key(lv[s], pick_word(rr, s));
+        if (key > tk) {
+          nib |= 1u << s;
+          ord[s] = orderable(key);
+        } else {
+          wr += (double)__expf(lv[s] - lm);
         }
       }
     }
-    uint32_t x = nib << ((tid & 7) * 4);
-    x |= __shfl_xor(x, 1, kWave);
-    x |= __shfl_xor(x, 2, kWave);
-    x |= __shfl_xor(x, 4, kWave);
-    if ((tid & 7) == 0 && a0 < E) {
-      const int wi = a0 >> 5;
-      if (wi < words) removed[(int64_t)b * words + wi] = x;
-    }
-    const int c = __popc(nib);
-    const int incl = wave_incl_scan(c);
-    int pos = wc + incl - c;
-    wc += __shfl(incl, 63, kWave);
-    // bucket = nb - 1 - #(splitters <= key): table count at the key's bin, then the few
-    // splitters inside that bin; the four lookups of a thread are independent
-    int cnt[4];
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const uint32_t o = ord[s];
-      const uint32_t bin = o < lmn ? 0u : min((uint32_t)(kBins - 1), (o - lmn) >> lsh);
-      cnt[s] = s_lut[bin];
-    }
-#pragma unroll
-    for (int s = 0; s < 4; ++s)
-      if (cnt[s] < nb - 1 && s_spl[cnt[s]] <= ord[s]) ++cnt[s];
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      if ((nib >> s) & 1u) {
-        while (cnt[s] < nb - 1 && s_spl[cnt[s]] <= ord[s]) ++cnt[s];
-        const int bk = nb - 1 - cnt[s];
-        atomicAdd(&s_hist[bk], 1);
-        uw[pos++] = ((uint64_t)ord[s] << 32) | ((uint32_t)bk << kTileBits) | (uint32_t)(al + s);
-      }
-    }
   }
-  // fixed-order untouched mass of the tile
+  uint32_t x = nib << ((tid & 7) * 4);
+  x |= __shfl_xor(x, 1, kWave);
+  x |= __shfl_xor(x, 2, kWave);
+  x |= __shfl_xor(x, 4, kWave);
+  if ((tid & 7) == 0 && a0 < E) {
+    const int wi = a0 >> 5;
+    if (wi < words) removed[(int64_t)b * words + wi] = x;
+  }
   wr = wave_sum(wr);
-  if (lane == 0) s_wr[wave] = wr;
-  __syncthreads();
-  // bucket offsets inside the tile (exclusive scan, 2 buckets per thread)
-  const int k0 = 2 * tid, k1 = 2 * tid + 1;
-  const int h0 = k0 < nb ? s_hist[k0] : 0, h1 = k1 < nb ? s_hist[k1] : 0;
+  if (lane == 0) s_wr[tid >> 6] = wr;
   int tot;
-  const int ex = block_excl_scan<kSelNT>(h0 + h1, s_wc, &tot);
-  const int64_t trow = (int64_t)b * kMaxB * ntiles + tile;
-  if (k0 < nb) {
-    s_hist[k0] = ex;
-    tcount[trow + (int64_t)k0 * ntiles] = h0;
-    tloc[trow + (int64_t)k0 * ntiles] = ex;
-    if (h0) atomicAdd(&btot[(int64_t)b * kMaxB + k0], h0);
-  }
-  if (k1 < nb) {
-    s_hist[k1] = ex + h0;
-    tcount[trow + (int64_t)k1 * ntiles] = h1;
-    tloc[trow + (int64_t)k1 * ntiles] = ex + h0;
-    if (h1) atomicAdd(&btot[(int64_t)b * kMaxB + k1], h1);
+  int pos = block_excl_scan<kNT>(__popc(nib), s_wc, &tot);
+  const int64_t base = ((int64_t)b * nblk + blk) * kBlk;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    if ((nib >> s) & 1u) {
+      c_ord[base + pos] = ord[s];
+      c_act[base + pos] = a0 + s;
+      c_log[base + pos] = lv[s];
+      ++pos;
+    }
   }
   if (tid == 0) {
     double t = 0.0;
 #pragma unroll
-    for (int w = 0; w < kSelNT / 64; ++w) t += s_wr[w];
-    tile_wrest[(int64_t)b * ntiles + tile] = t;
+    for (int w = 0; w < kNT / 64; ++w) t += s_wr[w];
+    blk_wrest[(int64_t)b * nblk + blk] = t;
+    blk_cnt[(int64_t)b * nblk + blk] = tot;
+  }
+}
+
+// ------------------------------------------------------------------ k_group
+// One 16384-action tile (kTileBlk select blocks) per block: bucket of every winner from the
+// splitter lookup table, LDS histogram, per-(bucket, tile) counts and offsets, and the
+// winners re-written grouped by bucket as one contiguous 8 B + 4 B stream per tile (the
+// records are read twice; the second read hits L2).
+__device__ __forceinline__ int bucket_lut(uint32_t o, const uint16_t* s_lut, const uint32_t* s_spl, uint32_t lmn,
+                                          int lsh, int nb) {
+  const uint32_t bin = o < lmn ? 0u : min((uint32_t)(kBins - 1), (o - lmn) >> lsh);
+  int c = s_lut[bin];
+  while (c < nb - 1 && s_spl[c] <= o) ++c;
+  return nb - 1 - c;
+}
+
+__global__ __launch_bounds__(kGrpNT) void k_group(int32_t nblk, int32_t ntiles, const uint32_t* __restrict__ c_ord,
+                                                  const int32_t* __restrict__ c_act, const float* __restrict__ c_log,
+                                                  const int32_t* __restrict__ blk_cnt,
+                                                  const double* __restrict__ blk_wrest,
+                                                  const int32_t* __restrict__ nb_, const uint32_t* __restrict__ spl_,
+                                                  const uint16_t* __restrict__ lut_,
+                                                  const uint32_t* __restrict__ lut_base,
+                                                  uint64_t* __restrict__ staging, float* __restrict__ stlog,
+                                                  int32_t* __restrict__ tcount, int32_t* __restrict__ tloc,
+                                                  int32_t* __restrict__ btot, double* __restrict__ tile_wrest) {
+  constexpr int kWB = kTileBlk / (kGrpNT / 64);  // select blocks per wave (2)
+  constexpr int kR = 8;                          // records per lane in flight
+  __shared__ uint64_t w_rec[kWin];  // one window of the grouped output (whole cache lines out)
+  __shared__ float w_log[kWin];
+  __shared__ __attribute__((aligned(16))) uint32_t s_spl[kMaxB];
+  __shared__ int s_off[kMaxB + 1];  // histogram, then tile-local bucket offsets
+  __shared__ int s_cur[kMaxB];
+  __shared__ __attribute__((aligned(16))) uint16_t s_lut[kBins];
+  __shared__ int s_bpre[kTileBlk + 1];
+  __shared__ int s_wc[kGrpNT / 64];
+  const int b = blockIdx.y, tile = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nb = nb_[b];
+  // prologue: every load in one round (16 B per lane for the table and the splitters)
+  static_assert(kBins * 2 == kGrpNT * 16 && kMaxB * 4 == kGrpNT * 16, "prologue vector widths");
+  static_assert(kTileBlk < 64, "the block prefix (kTileBlk + 1 entries) is one wave's scan");
+  reinterpret_cast<uint4*>(s_lut)[tid] = reinterpret_cast<const uint4*>(lut_ + (int64_t)b * kBins)[tid];
+  if (tid * 4 < nb - 1)
+    reinterpret_cast<uint4*>(s_spl)[tid] = reinterpret_cast<const uint4*>(spl_ + (int64_t)b * kMaxB)[tid];
+  for (int k = tid; k < nb; k += kGrpNT) s_off[k] = 0;
+  const uint32_t lmn = lut_base[2 * b];
+  const int lsh = (int)lut_base[2 * b + 1];
+  const int blk0 = tile * kTileBlk, nbt = min(kTileBlk, nblk - blk0);
+  if (tid < 64) {  // one lane per select block: parallel loads, wave scan (fixed order)
+    const int c = tid < nbt ? blk_cnt[(int64_t)b * nblk + blk0 + tid] : 0;
+    double wr = tid < nbt ? blk_wrest[(int64_t)b * nblk + blk0 + tid] : 0.0;
+    const int incl = wave_incl_scan(c);
+    if (tid <= nbt) s_bpre[tid] = incl - c;
+    wr = wave_sum(wr);
+    if (tid == 0) tile_wrest[(int64_t)b * ntiles + tile] = wr;
   }
   __syncthreads();
-  // group: each wave places its own records (4 per lane per step, loads in flight together)
+  const int64_t cbase = ((int64_t)b * nblk + blk0) * kBlk;
+  // this wave's records: select blocks wave*kWB .. +kWB, flattened
+  const int wb0 = min(wave * kWB, nbt), wb1 = min(wb0 + kWB, nbt);
+  const int wn = s_bpre[wb1] - s_bpre[wb0];
+  auto src = [&](int j) {  // j-th record of this wave -> index in the compacted streams
+    int bi = wb0;
+#pragma unroll
+    for (int q = 1; q < kWB; ++q) bi += (wb0 + q < wb1 && j >= s_bpre[wb0 + q] - s_bpre[wb0]) ? 1 : 0;
+    return cbase + (int64_t)bi * kBlk + (j - (s_bpre[bi] - s_bpre[wb0]));
+  };
+  for (int j0 = lane; j0 < wn; j0 += 64 * kR) {
+    uint32_t o[kR];
+#pragma unroll
+    for (int q = 0; q < kR; ++q) o[q] = j0 + 64 * q < wn ? c_ord[src(j0 + 64 * q)] : 0u;
+#pragma unroll
+    for (int q = 0; q < kR; ++q)
+      if (j0 + 64 * q < wn) atomicAdd(&s_off[bucket_lut(o[q], s_lut, s_spl, lmn, lsh, nb)], 1);
+  }
+  __syncthreads();
+  // bucket offsets inside the tile (exclusive scan, kMaxB / kGrpNT buckets per thread)
+  constexpr int kQ = kMaxB / kGrpNT;
+  int hv[kQ], loc = 0;
+#pragma unroll
+  for (int q = 0; q < kQ; ++q) {
+    const int k = tid * kQ + q;
+    hv[q] = k < nb ? s_off[k] : 0;
+    loc += hv[q];
+  }
+  int tot;
+  int run = block_excl_scan<kGrpNT>(loc, s_wc, &tot);
+  const int64_t trow = ((int64_t)b * ntiles + tile) * kMaxB;  // tile-major: one contiguous row per tile
+#pragma unroll
+  for (int q = 0; q < kQ; ++q) {
+    const int k = tid * kQ + q;
+    if (k < nb) {
+      s_off[k] = run;
+      tcount[trow + k] = hv[q];
+      tloc[trow + k] = run;
+      if (hv[q]) atomicAdd(&btot[(int64_t)b * kMaxB + k], hv[q]);
+    }
+    run += hv[q];
+  }
+  if (tid == 0) s_off[nb] = tot;
+  __syncthreads();
   uint64_t* st = staging + ((int64_t)b * ntiles + tile) * kTile;
   float* sl = stlog + ((int64_t)b * ntiles + tile) * kTile;
+  // windows of consecutive buckets whose records fit the LDS stage; a (tile, bucket) run
+  // longer than the stage is scattered directly (rare)
 #pragma unroll 1
-  for (int j0 = lane; j0 < wc; j0 += 256) {
-    uint64_t e[4];
-    float lv[4];
-    int p[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int j = j0 + 64 * q;
-      e[q] = j < wc ? uw[j] : 0ull;
-      lv[q] = j < wc ? lg[tbase + (int)((uint32_t)e[q] & (kTile - 1))] : 0.0f;
+  for (int kw = 0; kw < nb;) {
+    const int base = s_off[kw];
+    int lo = kw + 1, hi = nb;  // largest kw' with s_off[kw'] - base <= kWin
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (s_off[mid] - base <= kWin) lo = mid;
+      else hi = mid - 1;
     }
+    const int kw2 = lo;
+    const bool direct = s_off[kw2] - base > kWin;  // single oversized bucket
+    for (int k = kw + tid; k < kw2; k += kGrpNT) s_cur[k] = s_off[k] - (direct ? 0 : base);
+    __syncthreads();
+    for (int j0 = lane; j0 < wn; j0 += 64 * kR) {
+      uint32_t o[kR];
+      int a[kR];
+      float lv[kR];
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
-      p[q] = j0 + 64 * q < wc ? atomicAdd(&s_hist[(int)((uint32_t)e[q] >> kTileBits)], 1) : 0;
+      for (int q = 0; q < kR; ++q) {
+        const bool in = j0 + 64 * q < wn;
+        const int64_t si = in ? src(j0 + 64 * q) : cbase;
+        o[q] = in ? c_ord[si] : 0u;
+        a[q] = in ? c_act[si] : 0;
+        lv[q] = in ? c_log[si] : 0.0f;
+      }
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      if (j0 + 64 * q < wc) {
-        const uint32_t lo = (uint32_t)e[q];
-        st[p[q]] = ((uint64_t)(~(uint32_t)(e[q] >> 32)) << 32) | (uint32_t)(tbase + (int)(lo & (kTile - 1)));
-        sl[p[q]] = lv[q];  // the tile's logits are cache-hot: the weight travels with the record
+      for (int q = 0; q < kR; ++q) {
+        const int bk = j0 + 64 * q < wn ? bucket_lut(o[q], s_lut, s_spl, lmn, lsh, nb) : -1;
+        if (bk >= kw && bk < kw2) {
+          const int p = atomicAdd(&s_cur[bk], 1);
+          const uint64_t rec = ((uint64_t)(~o[q]) << 32) | (uint32_t)a[q];
+          if (direct) {
+            st[p] = rec;
+            sl[p] = lv[q];
+          } else {
+            w_rec[p] = rec;
+            w_log[p] = lv[q];
+          }
+        }
       }
     }
+    __syncthreads();
+    if (!direct) {
+      const int cnt = s_off[kw2] - base;
+      for (int e = tid; e < cnt; e += kGrpNT) {
+        st[base + e] = w_rec[e];
+        sl[base + e] = w_log[e];
+      }
+      __syncthreads();
+    }
+    kw = kw2;
   }
 }
 
@@ -677,13 +771,12 @@ __global__ __launch_bounds__(kSortNT) void k_sort2(int32_t E, int32_t B, int32_t
   __shared__ double s_wd[kSortNT / 64];
   __shared__ uint32_t s_red[2 * (kSortNT / 64)];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  if (tid == 0) {
-    int run = 0;
-    for (int i = 0; i < B; ++i) {
-      s_nbp[i] = run;
-      run += nb_[i];
-    }
-    s_nbp[B] = run;
+  {  // prefix of the bucket counts over the samples (parallel loads)
+    const int v = tid < B ? nb_[tid] : 0;
+    int tot;
+    const int ex = block_excl_scan<kSortNT>(v, s_wc, &tot);
+    if (tid < B) s_nbp[tid] = ex;
+    if (tid == 0) s_nbp[B] = tot;
   }
   __syncthreads();
   const int total = s_nbp[B];
@@ -695,14 +788,14 @@ __global__ __launch_bounds__(kSortNT) void k_sort2(int32_t E, int32_t B, int32_t
       int bb = 0;
       while (s_nbp[bb + 1] <= f) ++bb;
       const int kk = f - s_nbp[bb];
-      const int64_t row = ((int64_t)bb * kMaxB + kk) * ntiles;
+      const int64_t row = (int64_t)bb * ntiles * kMaxB + kk;  // [b][tile][bucket]
       if (t0 < ntiles) {
-        c0 = tcount[row + t0];
-        l0 = tloc[row + t0];
+        c0 = tcount[row + (int64_t)t0 * kMaxB];
+        l0 = tloc[row + (int64_t)t0 * kMaxB];
       }
       if (t1 < ntiles) {
-        c1 = tcount[row + t1];
-        l1 = tloc[row + t1];
+        c1 = tcount[row + (int64_t)t1 * kMaxB];
+        l1 = tloc[row + (int64_t)t1 * kMaxB];
       }
     }
   };
@@ -905,13 +998,12 @@ __global__ __launch_bounds__(kSortNT) void k_sort2_big(int32_t E, int32_t B, int
   __shared__ double s_wd[kSortNT / 64];
   __shared__ uint32_t s_red[4 * (kSortNT / 64)];
   const int tid = threadIdx.x;
-  if (tid == 0) {
-    int run = 0;
-    for (int i = 0; i < B; ++i) {
-      s_nbp[i] = run;
-      run += nb_[i];
-    }
-    s_nbp[B] = run;
+  {  // prefix of the bucket counts over the samples (parallel loads)
+    const int v = tid < B ? nb_[tid] : 0;
+    int tot;
+    const int ex = block_excl_scan<kSortNT>(v, s_wc, &tot);
+    if (tid < B) s_nbp[tid] = ex;
+    if (tid == 0) s_nbp[B] = tot;
   }
   __syncthreads();
   const int total = s_nbp[B];
@@ -923,19 +1015,19 @@ __global__ __launch_bounds__(kSortNT) void k_sort2_big(int32_t E, int32_t B, int
     const int32_t* bs = bstart + (int64_t)b * (kMaxB + 1);
     const int s = bs[k], n = bs[k + 1] - s;
     if (n <= kCap2) continue;
-    const int32_t* crow = tcount + ((int64_t)b * kMaxB + k) * ntiles;
-    const int32_t* lrow = tloc + ((int64_t)b * kMaxB + k) * ntiles;
+    const int32_t* crow = tcount + (int64_t)b * ntiles * kMaxB + k;  // [b][tile][bucket]
+    const int32_t* lrow = tloc + (int64_t)b * ntiles * kMaxB + k;
     const int t0 = 2 * tid, t1 = 2 * tid + 1;
-    const int c0 = t0 < ntiles ? crow[t0] : 0, c1 = t1 < ntiles ? crow[t1] : 0;
+    const int c0 = t0 < ntiles ? crow[(int64_t)t0 * kMaxB] : 0, c1 = t1 < ntiles ? crow[(int64_t)t1 * kMaxB] : 0;
     int tot;
     const int ex = block_excl_scan<kSortNT>(c0 + c1, s_wc, &tot);
     if (t0 < ntiles) {
       s_pre[t0] = ex;
-      s_loc[t0] = lrow[t0];
+      s_loc[t0] = lrow[(int64_t)t0 * kMaxB];
     }
     if (t1 < ntiles) {
       s_pre[t1] = ex + c0;
-      s_loc[t1] = lrow[t1];
+      s_loc[t1] = lrow[(int64_t)t1 * kMaxB];
     }
     if (tid == 0) s_pre[ntiles] = tot;
     __syncthreads();
@@ -1063,9 +1155,12 @@ extern "C" int spai_rollout_select(const float* logits, int64_t bstride, int32_t
   SPAI_CHECK_LAUNCH();
   k_splitters<<<B, kSortNT, 0, s>>>(E, w.M, nsb, w.samp, w.samp_cnt, w.nb, w.spl, w.lut, w.lut_base);
   SPAI_CHECK_LAUNCH();
-  k_select<<<dim3(w.ntiles, B), kSelNT, 0, s>>>(logits, bstride, E, w.ntiles, s0, s1, t0, t1, sample_base, removed,
-                                                words, lmax, w.nb, w.spl, w.lut, w.lut_base, w.staging, w.stlog, w.tcount, w.tloc, w.btot,
-                                                w.tile_wrest);
+  k_select<<<dim3(w.nblk, B), kNT, 0, s>>>(logits, bstride, E, w.nblk, s0, s1, t0, t1, sample_base, removed, words,
+                                           lmax, w.c_ord, w.c_act, w.c_log, w.blk_cnt, w.blk_wrest);
+  SPAI_CHECK_LAUNCH();
+  k_group<<<dim3(w.ntiles, B), kGrpNT, 0, s>>>(w.nblk, w.ntiles, w.c_ord, w.c_act, w.c_log, w.blk_cnt, w.blk_wrest,
+                                               w.nb, w.spl, w.lut, w.lut_base, w.staging, w.stlog, w.tcount, w.tloc,
+                                               w.btot, w.tile_wrest);
   SPAI_CHECK_LAUNCH();
   k_bscan<<<B, 1024, 0, s>>>(E, w.ntiles, logits, bstride, lmax, w.nb, w.btot, w.tile_wrest, w.bstart,
                              counts, w.wrest, w.tdev);

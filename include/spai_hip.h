@@ -155,6 +155,14 @@ int spai_fill_residual_gram(int32_t fill_mode, int32_t n, int32_t line_begin, in
                             const int32_t* pat_act, const float* pat_val, const double* gram, int32_t B,
                             const uint32_t* removed, int32_t words, void* m_out, int32_t m_dtype,
                             double* res2_out, void* workspace, size_t workspace_bytes, void* stream);
+/* The two halves of spai_fill_residual_gram: the fill kernel leaves per-block fp64 partial
+ * sums in the workspace; spai_fill_reduce (n_lines = line_end - line_begin of that call)
+ * sums them per sample in a fixed order into res2_out. */
+int spai_fill_lines_gram(int32_t fill_mode, int32_t n, int32_t line_begin, int32_t line_end, int32_t W,
+                         const int32_t* pat_act, const float* pat_val, const double* gram, int32_t B,
+                         const uint32_t* removed, int32_t words, void* m_out, int32_t m_dtype,
+                         void* workspace, size_t workspace_bytes, void* stream);
+int spai_fill_reduce(int32_t n_lines, int32_t B, const void* workspace, double* res2_out, void* stream);
 
 /* ---------------------------------------------------------------- rewards
  * residual[b] = sqrt(res2[b]) and reward[b] = 1000 * (alpha (1 - r/r0) + (1 - alpha)(1 - f/f0))

@@ -1,0 +1,70 @@
+"""Summarise a rocprofv3 --kernel-trace --stats run and the separate PMC passes of the same
+bench command into profiles/: kernel_stats_<tag>.md/.csv, pmc_<tag>.json and
+fill_traffic.json (HBM bytes per launch of the roofline kernel, read back by bench.py).
+
+HBM traffic per launch = (2 * FETCH_SIZE + WRITE_SIZE) * 1024: MI355X_MICROARCH.md §HBM
+(FETCH_SIZE reports half of the bytes of coalesced reads on gfx950; calibrated here against
+the fill kernel's known read bytes).
+usage: python scripts/collect_profiles.py <tag> <prof_dir> <pmc_dir> [--config c4 --batch 8 --out profiles]
+"""
+import argparse
+import csv
+import json
+import os
+import shutil
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOF_KERNEL = "k_gram_fill<5, float, true>"
+
+
+def short(name):
+    return name.replace("(anonymous namespace)::", "").split("(")[0][:80]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("tag")
+    ap.add_argument("prof")
+    ap.add_argument("pmc")
+    ap.add_argument("--config", default="c4")
+    ap.add_argument("--batch", type=int, default=8)
+    ap.add_argument("--out", default=os.path.join(ROOT, "profiles"))
+    ap.add_argument("--cmd", default="python bench.py --steps 10 --warmup 2 --no-cpu-baseline")
+    args = ap.parse_args()
+    os.makedirs(args.out, exist_ok=True)
+    stats = os.path.join(args.prof, "run_kernel_stats.csv")
+    rows = list(csv.DictReader(open(stats)))
+    lines = ["| kernel | calls | avg us | total ms | % |", "|---|---|---|---|---|"]
+    summary = {"tag": args.tag, "command": args.cmd, "kernels": {}}
+    for r in rows:
+        k = short(r["Name"])
+        summary["kernels"].setdefault(k, {})["avg_us"] = float(r["AverageNs"]) / 1e3
+        summary["kernels"][k]["calls"] = int(r["Calls"])
+        if len(lines) < 32:
+            lines.append(f"| {k} | {r['Calls']} | {float(r['AverageNs']) / 1e3:.1f} | "
+                         f"{float(r['TotalDurationNs']) / 1e6:.3f} | {float(r['Percentage']):.2f} |")
+    with open(os.path.join(args.out, f"kernel_stats_{args.tag}.md"), "w") as f:
+        f.write(f"# rocprofv3 --kernel-trace --stats ({args.tag})\n\nCommand on one MI355X: "
+                f"`rocprofv3 --kernel-trace --stats --output-format csv -- {args.cmd}`\n\n" + "\n".join(lines) + "\n")
+    shutil.copy(stats, os.path.join(args.out, f"kernel_stats_{args.tag}.csv"))
+    pmc = json.load(open(os.path.join(args.pmc, "summary.json")))
+    for k, e in pmc.items():
+        kk = k.replace("spai::", "")
+        match = [n for n in summary["kernels"] if n.replace("spai::", "").replace("void ", "").startswith(kk.replace("void ", ""))]
+        dst = summary["kernels"].setdefault(match[0] if match else k, {})
+        dst.update(e)
+    with open(os.path.join(args.out, f"pmc_{args.tag}.json"), "w") as f:
+        json.dump(summary, f, indent=1)
+    roof = [(k, v) for k, v in summary["kernels"].items() if ROOF_KERNEL in k and "hbm_bytes_per_launch" in v]
+    if roof:
+        k, v = roof[0]
+        rec = {"config": args.config, "batch": args.batch, "kernel": k, "avg_us": v.get("avg_us"),
+               "hbm_bytes_per_launch": v["hbm_bytes_per_launch"], "FETCH_SIZE_KB": v["pmc"].get("FETCH_SIZE"),
+               "WRITE_SIZE_KB": v["pmc"].get("WRITE_SIZE"), "source": f"profiles/pmc_{args.tag}.json",
+               "command": args.cmd}
+        json.dump(rec, open(os.path.join(args.out, "fill_traffic.json"), "w"), indent=1)
+        print(json.dumps(rec))
+
+
+if __name__ == "__main__":
+    main()

@@ -37,6 +37,7 @@ constexpr int kNT = 256;                   // threads of a select block
 constexpr int kBlk = kNT * 4;              // actions per select block (4 consecutive per thread)
 constexpr int kTileBlk = 16;               // select blocks per grouping tile (< 64: one wave scans them)
 constexpr int kTile = kBlk * kTileBlk;     // 16384 actions per grouping tile
+static_assert(kTile <= 65535, "run offsets and counts are packed in 16 bits (k_group, k_runs)");
 constexpr int kGrpNT = 512;                // threads of a grouping block
 constexpr int kWin = 3584;                 // records per LDS output window of a grouping block
 constexpr int kSampM = 65536;              // subset size (power of two, capped by E)
@@ -71,8 +72,8 @@ struct TrajWs {
   double* blk_wrest;      // [B][nblk]
   uint64_t* staging;      // [B][ntiles][kTile] (~ord << 32 | action), grouped by bucket per tile
   float* stlog;           // [B][ntiles][kTile] logit of each staged record
-  int32_t* tcount;        // [B][ntiles][kMaxB] winners of bucket k in tile t
-  int32_t* tloc;          // [B][ntiles][kMaxB] their offset in the tile's grouped stream
+  uint32_t* trun;         // [B][ntiles][kMaxB] run of bucket k in tile t: offset << 16 | count
+  uint32_t* runs;         // [B][kMaxB][ntiles] the same, bucket-major (k_runs)
   double* tile_wrest;     // [B][ntiles]
   int32_t* bstart;        // [B][kMaxB + 1]
   double* wrest;          // [B]
@@ -108,8 +109,8 @@ static void traj_ws(void* base, int32_t E, int32_t B, TrajWs* w) {
   w->blk_wrest = c.take<double>((size_t)B * w->nblk);
   w->staging = c.take<uint64_t>((size_t)B * w->ntiles * kTile);
   w->stlog = c.take<float>((size_t)B * w->ntiles * kTile);
-  w->tcount = c.take<int32_t>((size_t)B * kMaxB * w->ntiles);
-  w->tloc = c.take<int32_t>((size_t)B * kMaxB * w->ntiles);
+  w->trun = c.take<uint32_t>((size_t)B * kMaxB * w->ntiles);
+  w->runs = c.take<uint32_t>((size_t)B * kMaxB * w->ntiles);
   w->tile_wrest = c.take<double>((size_t)B * w->ntiles);
   w->bstart = c.take<int32_t>((size_t)B * (kMaxB + 1));
   w->wrest = c.take<double>(B);
@@ -131,13 +132,24 @@ __device__ __forceinline__ int wave_incl_scan(int v) {
   return v;
 }
 
+// Barrier for LDS hand-offs only: waits for this wave's LDS operations, not for its
+// outstanding global loads (which __syncthreads would drain), so prefetches stay in flight.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+template <bool kLdsOnly>
+__device__ __forceinline__ void scan_barrier() {
+  if constexpr (kLdsOnly) lds_barrier();
+  else __syncthreads();
+}
+
 // Block-wide exclusive scan of one int per thread (NT <= 1024); *total = block total.
-template <int NT>
+// kLdsOnly: LDS-only barriers (outstanding global loads of the caller stay in flight).
+template <int NT, bool kLdsOnly = false>
 __device__ __forceinline__ int block_excl_scan(int v, int* lds /* NT/64 */, int* total) {
   const int incl = wave_incl_scan(v);
-  __syncthreads();
+  scan_barrier<kLdsOnly>();
   if ((threadIdx.x & 63) == 63) lds[threadIdx.x >> 6] = incl;
-  __syncthreads();
+  scan_barrier<kLdsOnly>();
   int base = 0, tot = 0;
 #pragma unroll
   for (int w = 0; w < NT / 64; ++w) {
@@ -150,7 +162,7 @@ __device__ __forceinline__ int block_excl_scan(int v, int* lds /* NT/64 */, int*
 }
 
 // Same for doubles (fixed summation order => deterministic).
-template <int NT>
+template <int NT, bool kLdsOnly = false>
 __device__ __forceinline__ double block_excl_scan_d(double v, double* lds, double* total) {
   double incl = v;
 #pragma unroll
@@ -158,9 +170,9 @@ __device__ __forceinline__ double block_excl_scan_d(double v, double* lds, doubl
     const double y = __shfl_up(incl, o, kWave);
     if ((threadIdx.x & 63) >= o) incl += y;
   }
-  __syncthreads();
+  scan_barrier<kLdsOnly>();
   if ((threadIdx.x & 63) == 63) lds[threadIdx.x >> 6] = incl;
-  __syncthreads();
+  scan_barrier<kLdsOnly>();
   double base = 0.0, tot = 0.0;
 #pragma unroll
   for (int w = 0; w < NT / 64; ++w) {
@@ -377,6 +389,16 @@ __global__ __launch_bounds__(kSortNT) void k_splitters(int32_t E, int32_t M, int
 // actions (fixed order) and the block's winners compacted in action order as three
 // coalesced streams (orderable key, action, logit).  Small LDS: full occupancy for the
 // ALU-bound key arithmetic.
+// w = exp(l - lmax) in fp32 to within ~1 ulp of the correctly rounded value: l - lmax is
+// exact in fp64, split into a float head and a tiny tail, exp(hi + lo) = exp(hi) (1 + lo).
+// (An fp64 exp costs ~30 us per rollout wherever it is placed.)
+__device__ __forceinline__ float winner_weight(float l, float lm) {
+  const double d = (double)l - (double)lm;
+  const float hi = (float)d, lo = (float)(d - (double)hi);
+  const float e = expf(hi);
+  return fmaf(e, lo, e);
+}
+
 __global__ __launch_bounds__(kNT) void k_select(const float* __restrict__ logits, int64_t bstride, int32_t E,
                                                 int32_t nblk, uint32_t seed0, uint32_t seed1, uint32_t st0,
                                                 uint32_t st1, int32_t sample_base, uint32_t* __restrict__ removed,
@@ -468,7 +490,7 @@ __global__ __launch_bounds__(kGrpNT) void k_group(int32_t nblk, int32_t ntiles, 
                                                   const uint16_t* __restrict__ lut_,
                                                   const uint32_t* __restrict__ lut_base,
                                                   uint64_t* __restrict__ staging, float* __restrict__ stlog,
-                                                  int32_t* __restrict__ tcount, int32_t* __restrict__ tloc,
+                                                  uint32_t* __restrict__ trun,
                                                   int32_t* __restrict__ btot, double* __restrict__ tile_wrest) {
   constexpr int kWB = kTileBlk / (kGrpNT / 64);  // select blocks per wave (2)
   constexpr int kR = 8;                          // records per lane in flight
@@ -537,8 +559,7 @@ __global__ __launch_bounds__(kGrpNT) void k_group(int32_t nblk, int32_t ntiles, 
     const int k = tid * kQ + q;
     if (k < nb) {
       s_off[k] = run;
-      tcount[trow + k] = hv[q];
-      tloc[trow + k] = run;
+      trun[trow + k] = ((uint32_t)run << 16) | (uint32_t)hv[q];
       if (hv[q]) atomicAdd(&btot[(int64_t)b * kMaxB + k], hv[q]);
     }
     run += hv[q];
@@ -702,10 +723,59 @@ __device__ void big_bucket_sort(uint64_t* __restrict__ s0, uint64_t* __restrict_
   }
 }
 
+// ------------------------------------------------------------------ k_runs
+// Run table transposed to bucket-major, so the level-2 sort reads one bucket's runs as a
+// contiguous row: block (tile chunk of 64, bucket chunk of 64, sample) through LDS.
+constexpr int kRunT = 64;
+__global__ __launch_bounds__(256) void k_runs(int32_t ntiles, const int32_t* __restrict__ nb_,
+                                              const uint32_t* __restrict__ trun, uint32_t* __restrict__ runs) {
+  __shared__ uint32_t t[kRunT][kRunT + 1];
+  const int b = blockIdx.z, t0 = blockIdx.x * kRunT, k0 = blockIdx.y * kRunT;
+  const int nb = nb_[b];
+  if (k0 >= nb) return;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const uint32_t* src = trun + (int64_t)b * ntiles * kMaxB;
+  for (int r = ty; r < kRunT; r += 4)
+    t[r][tx] = (t0 + r < ntiles && k0 + tx < nb) ? src[(int64_t)(t0 + r) * kMaxB + k0 + tx] : 0u;
+  __syncthreads();
+  uint32_t* dst = runs + (int64_t)b * kMaxB * ntiles;
+  for (int r = ty; r < kRunT; r += 4)
+    if (k0 + r < nb && t0 + tx < ntiles) dst[(int64_t)(k0 + r) * ntiles + t0 + tx] = t[tx][r];
+}
+
 // ------------------------------------------------------------------ k_sort2
-// Barrier for LDS hand-offs only: waits for this wave's LDS operations, not for its
-// outstanding global loads (which __syncthreads would drain), so prefetches stay in flight.
-__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+#ifdef SPAI_PROF  // phase timing of k_sort2 (variant builds only: make EXTRA=-DSPAI_PROF)
+__device__ unsigned long long g_sort2_prof[16];
+__device__ __forceinline__ uint64_t prof_stamp() {
+  uint64_t t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+#define PROF_INIT uint64_t pf_t = prof_stamp(), pf_acc[12] = {};
+#define PROF(i)                          \
+  if (tid == 0) {                        \
+    const uint64_t pf_n = prof_stamp();   \
+    pf_acc[i] += pf_n - pf_t;            \
+    pf_t = pf_n;                         \
+  }
+#define PROF_END \
+  if (tid == 0)  \
+    for (int q = 0; q < 12; ++q) atomicAdd(&g_sort2_prof[q], (unsigned long long)pf_acc[q]);
+extern "C" int spai_debug_sort2_prof(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sort2_prof), sizeof(g_sort2_prof)) != hipSuccess) return 2;
+  if (reset) {
+    static const unsigned long long z[16] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_sort2_prof), z, sizeof(z)) != hipSuccess) return 2;
+  }
+  return 0;
+}
+#else
+#define PROF_INIT
+#define PROF(i)
+#define PROF_END
+#endif
 
 // Oversized bucket (the sampled splitters missed; rare): gather into scratch, exact
 // in-block radix in global memory, then the same outputs as the LDS path.
@@ -745,27 +815,27 @@ __device__ __forceinline__ void big_bucket(const int n, const int ntiles, const 
 // Level-2 sort, persistent: one resident block per CU walks the FLATTENED (sample, bucket)
 // list, so the samples' very different winner counts (the terminal's own Gumbel key sets
 // them) do not pile work on the blocks of one sample.  Per bucket (<= kCap2 records):
-// the runs (one per select tile) are gathered wave-per-run with all loads of a round in
-// flight; records are ranked inside value-linear sub-buckets of ~0.5 record (almost always
-// a direct placement) and re-laid in trajectory order in LDS together with their logits;
-// then fp64 weights, in-bucket suffix sums and coalesced stores.  The next bucket's run
+// the runs (one per select tile) are mapped into an LDS gather table and every record is
+// loaded into registers in one round trip; records are ranked inside value-linear
+// sub-buckets of ~0.5 record (almost always a direct placement) and re-laid in trajectory
+// order in LDS together with their weights; then fp64 in-bucket suffix sums and coalesced
+// stores.  The next bucket's run
 // table is prefetched while the current one is processed (LDS-only barriers keep it in
 // flight).  Oversized buckets are left to k_sort2_big.
 __global__ __launch_bounds__(kSortNT) void k_sort2(int32_t E, int32_t B, int32_t ntiles,
                                                    const int32_t* __restrict__ nb_,
                                                    const int32_t* __restrict__ bstart,
-                                                   const int32_t* __restrict__ tcount, const int32_t* __restrict__ tloc,
+                                                   const uint32_t* __restrict__ runs,
                                                    const uint64_t* __restrict__ staging,
                                                    const float* __restrict__ stlog, const float* __restrict__ lmax_,
                                                    int64_t t_cap, int64_t* __restrict__ actions,
                                                    float* __restrict__ out_w, float* __restrict__ out_suf,
                                                    double* __restrict__ bwsum) {
-  __shared__ uint64_t A[kCap2];
-  __shared__ float L[kCap2];
-  __shared__ uint16_t P[kCap2];  // arrival index of the record at each sorted position
-  __shared__ int s_pre[kMaxTiles + 1];
-  __shared__ int s_loc[kMaxTiles];
+  __shared__ uint64_t A[kCap2];  // low half: gather map; high half: actions awaiting store
+  __shared__ float L[kCap2];     // weights in trajectory order
+  __shared__ float S[kCap2];     // suffix sums awaiting store
   __shared__ int s_sub[kMaxSub + 1];
+  __shared__ float s_lm[kMaxSamples];
   __shared__ int s_nbp[kMaxSamples + 1];
   __shared__ int s_wc[kSortNT / 64];
   __shared__ double s_wd[kSortNT / 64];
@@ -775,96 +845,118 @@ __global__ __launch_bounds__(kSortNT) void k_sort2(int32_t E, int32_t B, int32_t
     const int v = tid < B ? nb_[tid] : 0;
     int tot;
     const int ex = block_excl_scan<kSortNT>(v, s_wc, &tot);
+    if (tid < B) s_lm[tid] = lmax_[tid];
     if (tid < B) s_nbp[tid] = ex;
     if (tid == 0) s_nbp[B] = tot;
   }
   __syncthreads();
   const int total = s_nbp[B];
   const int t0 = 2 * tid, t1 = 2 * tid + 1;
-  // run table of bucket f: count and tile-local offset of its run in tiles t0, t1
-  auto fetch = [&](int f, int& c0, int& c1, int& l0, int& l1) {
-    c0 = c1 = l0 = l1 = 0;
+  // bucket f: sample, bucket index, start/size, and the count and tile-local offset of its
+  // runs in tiles t0, t1
+  auto fetch = [&](int f, int& bb, int& kk, int& s0, int& s1, uint32_t& r0, uint32_t& r1) {
+    r0 = r1 = 0u;
+    bb = kk = s0 = s1 = 0;
     if (f < total) {
-      int bb = 0;
       while (s_nbp[bb + 1] <= f) ++bb;
-      const int kk = f - s_nbp[bb];
-      const int64_t row = (int64_t)bb * ntiles * kMaxB + kk;  // [b][tile][bucket]
-      if (t0 < ntiles) {
-        c0 = tcount[row + (int64_t)t0 * kMaxB];
-        l0 = tloc[row + (int64_t)t0 * kMaxB];
-      }
-      if (t1 < ntiles) {
-        c1 = tcount[row + (int64_t)t1 * kMaxB];
-        l1 = tloc[row + (int64_t)t1 * kMaxB];
-      }
+      kk = f - s_nbp[bb];
+      const int32_t* bs = bstart + (int64_t)bb * (kMaxB + 1);
+      s0 = bs[kk];
+      s1 = bs[kk + 1];
+      const uint32_t* rr = runs + ((int64_t)bb * kMaxB + kk) * ntiles;  // [b][bucket][tile]
+      if (t0 < ntiles) r0 = rr[t0];
+      if (t1 < ntiles) r1 = rr[t1];
     }
   };
-  int c0, c1, l0, l1;
-  fetch(blockIdx.x, c0, c1, l0, l1);
+  int nxb, nxk, nxs0, nxs1;
+  uint32_t r0, r1;  // packed runs (offset << 16 | count) of the next bucket in tiles t0, t1
+  int* dlt = reinterpret_cast<int*>(A);
+  uint32_t* a_out = reinterpret_cast<uint32_t*>(A) + kCap2;
+  // Outputs of a bucket are stored during the NEXT bucket, right after its gather has
+  // landed: stores issued at the end of a bucket would sit ahead of the next bucket's loads
+  // in the (in-order) vmcnt, and every wait on those loads would wait for them.
+  int pv_n = 0;
+  int64_t* pv_act = nullptr;
+  float *pv_w = nullptr, *pv_suf = nullptr;
+  double* pv_bw = nullptr;
+  double pv_wsum = 0.0;
+  auto flush = [&]() {
+#pragma unroll
+    for (int j = 0; j < kCap2 / kSortNT; ++j) {
+      const int i = j * kSortNT + tid;
+      if (i < pv_n) {
+        pv_act[i] = (int64_t)a_out[i];
+        pv_w[i] = L[i];
+        pv_suf[i] = S[i];
+      }
+    }
+    if (tid == 0 && pv_n) *pv_bw = pv_wsum;
+    pv_n = 0;
+  };
+  // gather map of a bucket (in A, free until the scatter): record i sits at staging offset
+  // dlt[i] + i; each thread writes the entries of its two runs
+  auto build_map = [&]() {
+    const int c0 = (int)(r0 & 0xFFFFu), l0 = (int)(r0 >> 16), c1 = (int)(r1 & 0xFFFFu), l1 = (int)(r1 >> 16);
+    int tot;
+    const int ex = block_excl_scan<kSortNT, true>(c0 + c1, s_wc, &tot);
+    if (tot <= kCap2) {
+      const int d0 = t0 * kTile + l0 - ex, d1 = t1 * kTile + l1 - ex - c0;
+#pragma unroll 1
+      for (int i = 0; i < c0; ++i) dlt[ex + i] = d0;
+#pragma unroll 1
+      for (int i = 0; i < c1; ++i) dlt[ex + c0 + i] = d1;
+    }
+  };
+  fetch(blockIdx.x, nxb, nxk, nxs0, nxs1, r0, r1);
+  // retire the first fetch here: the loop header then has no load pending on either path,
+  // so the map build below never waits behind the previous bucket's stores
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+  PROF_INIT
 #pragma unroll 1
   for (int f = blockIdx.x; f < total; f += gridDim.x) {
-    int b = 0;
-    while (s_nbp[b + 1] <= f) ++b;
-    const int k = f - s_nbp[b];
-    const int32_t* bs = bstart + (int64_t)b * (kMaxB + 1);
-    const int s = bs[k], n = bs[k + 1] - s;
-    int tot;
-    const int ex = block_excl_scan<kSortNT>(c0 + c1, s_wc, &tot);
-    if (t0 < ntiles) {
-      s_pre[t0] = ex;
-      s_loc[t0] = l0;
-    }
-    if (t1 < ntiles) {
-      s_pre[t1] = ex + c0;
-      s_loc[t1] = l1;
-    }
-    if (tid == 0) s_pre[ntiles] = tot;
-    fetch(f + gridDim.x, c0, c1, l0, l1);  // next bucket's run table, in flight meanwhile
+    const int b = nxb, k = nxk, s = nxs0, n = nxs1 - nxs0;
+    build_map();
+    // the next bucket's run table is in flight during the gather (whose wait retires it)
+    fetch(f + gridDim.x, nxb, nxk, nxs0, nxs1, r0, r1);
     lds_barrier();
+    PROF(0)
     if (n == 0 || n > kCap2) {
       if (n == 0 && tid == 0) bwsum[(int64_t)b * kMaxB + k] = 0.0;
-      lds_barrier();
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): retire the fetch (see above)
       continue;
     }
     const uint64_t* stb = staging + (int64_t)b * ntiles * kTile;
     const float* slb = stlog + (int64_t)b * ntiles * kTile;
-    // gather: wave per run, kRR runs per round, every load of a round in flight
-    constexpr int kRR = 4;
-#pragma unroll 1
-    for (int r0 = wave * kRR; r0 < ntiles; r0 += (kSortNT / 64) * kRR) {
-      uint64_t v[kRR];
-      float lv[kRR];
-#pragma unroll
-      for (int u = 0; u < kRR; ++u) {
-        const int r = r0 + u;
-        const int c = r < ntiles ? s_pre[r + 1] - s_pre[r] : 0;
-        const int64_t src = (int64_t)r * kTile + (r < ntiles ? s_loc[r] : 0) + lane;
-        v[u] = lane < c ? stb[src] : 0ull;
-        lv[u] = lane < c ? slb[src] : 0.0f;
-      }
-#pragma unroll
-      for (int u = 0; u < kRR; ++u) {
-        const int r = r0 + u;
-        const int c = r < ntiles ? s_pre[r + 1] - s_pre[r] : 0;
-        if (lane < c) {
-          A[s_pre[r] + lane] = v[u];
-          L[s_pre[r] + lane] = lv[u];
-        }
-#pragma unroll 1
-        for (int i = 64 + lane; i < c; i += 64) {  // runs longer than a wave (rare)
-          A[s_pre[r] + i] = stb[(int64_t)r * kTile + s_loc[r] + i];
-          L[s_pre[r] + i] = slb[(int64_t)r * kTile + s_loc[r] + i];
-        }
-      }
-    }
-    lds_barrier();
     constexpr int kPer = kCap2 / kSortNT;
+    // flat gather: every record of the bucket in flight at once (one round trip)
+    int dv[kPer];
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      const int i = j * kSortNT + tid;
+      dv[j] = i < n ? dlt[i] + i : 0;
+    }
     uint64_t mine[kPer];
+    float lw[kPer];
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      const bool in = j * kSortNT + tid < n;
+      mine[j] = in ? stb[dv[j]] : ~0ull;
+      lw[j] = in ? slb[dv[j]] : 0.0f;
+    }
+    PROF(1)
+    // every load of this bucket (and the next bucket's run table) retired on all paths, so
+    // the loop header does not wait behind this bucket's stores
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+    flush();  // the previous bucket's outputs (drain during this bucket's LDS phases)
+    {
+      const float lm = s_lm[b];
+#pragma unroll
+      for (int j = 0; j < kPer; ++j) lw[j] = winner_weight(lw[j], lm);  // logit -> weight
+    }
     uint32_t mn = 0xFFFFFFFFu, mx = 0u;
 #pragma unroll
     for (int j = 0; j < kPer; ++j) {
       const int i = j * kSortNT + tid;
-      mine[j] = i < n ? A[i] : ~0ull;
       if (i < n) {
         mn = min(mn, (uint32_t)(mine[j] >> 32));
         mx = max(mx, (uint32_t)(mine[j] >> 32));
@@ -882,6 +974,7 @@ __global__ __launch_bounds__(kSortNT) void k_sort2(int32_t E, int32_t B, int32_t
     const int nsub = max(1, min(kMaxSub, 2 * n));
     for (int i = tid; i <= nsub; i += kSortNT) s_sub[i] = 0;
     lds_barrier();
+    PROF(2)
     mn = 0xFFFFFFFFu;
     mx = 0u;
 #pragma unroll
@@ -900,6 +993,7 @@ __global__ __launch_bounds__(kSortNT) void k_sort2(int32_t E, int32_t B, int32_t
       }
     }
     lds_barrier();
+    PROF(3)
     {  // exclusive scan of the sub-bucket counts (kMaxSub / kSortNT per thread)
       constexpr int kQ = kMaxSub / kSortNT;
       int cv[kQ], loc = 0;
@@ -910,7 +1004,7 @@ __global__ __launch_bounds__(kSortNT) void k_sort2(int32_t E, int32_t B, int32_t
         loc += cv[q];
       }
       int t2;
-      int run = block_excl_scan<kSortNT>(loc, s_wc, &t2);
+      int run = block_excl_scan<kSortNT, true>(loc, s_wc, &t2);
 #pragma unroll
       for (int q = 0; q < kQ; ++q) {
         const int i = tid * kQ + q;
@@ -919,11 +1013,13 @@ __global__ __launch_bounds__(kSortNT) void k_sort2(int32_t E, int32_t B, int32_t
       }
     }
     lds_barrier();
+    PROF(4)
     // scatter by sub-bucket (the cursor is the start; afterwards s_sub[i] = END of i)
 #pragma unroll
     for (int j = 0; j < kPer; ++j)
       if (j * kSortNT + tid < n) A[atomicAdd(&s_sub[sb[j]], 1)] = mine[j];
     lds_barrier();
+    PROF(5)
 #pragma unroll
     for (int j = 0; j < kPer; ++j) {
       if (j * kSortNT + tid < n) {
@@ -935,56 +1031,66 @@ __global__ __launch_bounds__(kSortNT) void k_sort2(int32_t E, int32_t B, int32_t
       }
     }
     lds_barrier();
+    PROF(6)
 #pragma unroll
     for (int j = 0; j < kPer; ++j)
       if (j * kSortNT + tid < n) {
         A[sb[j]] = mine[j];
-        P[sb[j]] = (uint16_t)(j * kSortNT + tid);
+        L[sb[j]] = lw[j];
       }
     lds_barrier();
-    // fp64 weights w = exp(l - lmax) and in-bucket inclusive suffix sums: thread t owns the
-    // t-th chunk counted from the END (contiguous, fixed order -> deterministic)
-    const double lmax = (double)lmax_[b];
+    PROF(7)
+    // weights (computed by k_group) and fp64 in-bucket inclusive suffix sums: thread t owns
+    // the t-th chunk counted from the END (contiguous, fixed order -> deterministic)
     const int per = (n + kSortNT - 1) / kSortNT;
     const int hi_ = n - min(tid * per, n), lo_ = max(hi_ - per, 0);
-    double wv[kPer];
     double loc = 0.0;
 #pragma unroll
     for (int j = 0; j < kPer; ++j) {
       const int i = hi_ - 1 - j;
-      wv[j] = i >= lo_ ? exp((double)L[P[i]] - lmax) : 0.0;
-      loc += wv[j];
+      loc += i >= lo_ ? (double)L[i] : 0.0;
+    }
+    uint32_t av[kPer];
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      const int i = j * kSortNT + tid;
+      av[j] = i < n ? (uint32_t)A[i] : 0u;
     }
     double wsum;
-    double run = block_excl_scan_d<kSortNT>(loc, s_wd, &wsum);  // mass of all later records
-    float* suf_out = out_suf + (int64_t)b * E + s;
-    float* w_out = out_w + (int64_t)b * E + s;
+    double run = block_excl_scan_d<kSortNT, true>(loc, s_wd, &wsum);  // mass of all later records
+    PROF(8)
+    // (every read of A above is behind the scan's barriers)
 #pragma unroll
     for (int j = 0; j < kPer; ++j) {
       const int i = hi_ - 1 - j;
       if (i >= lo_) {
-        run += wv[j];
-        suf_out[i] = (float)run;
-        w_out[i] = (float)wv[j];
+        run += (double)L[i];
+        S[i] = (float)run;
       }
     }
-    int64_t* act_out = actions + (int64_t)b * t_cap + s;
 #pragma unroll
     for (int j = 0; j < kPer; ++j) {
       const int i = j * kSortNT + tid;
-      if (i < n) act_out[i] = (int64_t)(uint32_t)A[i];
+      if (i < n) a_out[i] = av[j];
     }
-    if (tid == 0) bwsum[(int64_t)b * kMaxB + k] = wsum;
+    pv_n = n;
+    pv_act = actions + (int64_t)b * t_cap + s;
+    pv_w = out_w + (int64_t)b * E + s;
+    pv_suf = out_suf + (int64_t)b * E + s;
+    pv_bw = bwsum + (int64_t)b * kMaxB + k;
+    pv_wsum = wsum;
     lds_barrier();  // LDS reuse by the next bucket
+    PROF(9)
   }
+  flush();
+  PROF_END
 }
 
 // Buckets above the LDS capacity (rare): one block each, exact radix in global memory.
 __global__ __launch_bounds__(kSortNT) void k_sort2_big(int32_t E, int32_t B, int32_t ntiles,
                                                        const int32_t* __restrict__ nb_,
                                                        const int32_t* __restrict__ bstart,
-                                                       const int32_t* __restrict__ tcount,
-                                                       const int32_t* __restrict__ tloc,
+                                                       const uint32_t* __restrict__ runs,
                                                        const uint64_t* __restrict__ staging,
                                                        const float* __restrict__ logits, int64_t bstride,
                                                        const float* __restrict__ lmax_, int64_t t_cap,
@@ -1015,19 +1121,19 @@ __global__ __launch_bounds__(kSortNT) void k_sort2_big(int32_t E, int32_t B, int
     const int32_t* bs = bstart + (int64_t)b * (kMaxB + 1);
     const int s = bs[k], n = bs[k + 1] - s;
     if (n <= kCap2) continue;
-    const int32_t* crow = tcount + (int64_t)b * ntiles * kMaxB + k;  // [b][tile][bucket]
-    const int32_t* lrow = tloc + (int64_t)b * ntiles * kMaxB + k;
+    const uint32_t* rr = runs + ((int64_t)b * kMaxB + k) * ntiles;  // [b][bucket][tile]
     const int t0 = 2 * tid, t1 = 2 * tid + 1;
-    const int c0 = t0 < ntiles ? crow[(int64_t)t0 * kMaxB] : 0, c1 = t1 < ntiles ? crow[(int64_t)t1 * kMaxB] : 0;
+    const uint32_t r0 = t0 < ntiles ? rr[t0] : 0u, r1 = t1 < ntiles ? rr[t1] : 0u;
+    const int c0 = (int)(r0 & 0xFFFFu);
     int tot;
-    const int ex = block_excl_scan<kSortNT>(c0 + c1, s_wc, &tot);
+    const int ex = block_excl_scan<kSortNT>(c0 + (int)(r1 & 0xFFFFu), s_wc, &tot);
     if (t0 < ntiles) {
       s_pre[t0] = ex;
-      s_loc[t0] = lrow[(int64_t)t0 * kMaxB];
+      s_loc[t0] = (int)(r0 >> 16);
     }
     if (t1 < ntiles) {
       s_pre[t1] = ex + c0;
-      s_loc[t1] = lrow[(int64_t)t1 * kMaxB];
+      s_loc[t1] = (int)(r1 >> 16);
     }
     if (tid == 0) s_pre[ntiles] = tot;
     __syncthreads();
@@ -1159,7 +1265,7 @@ extern "C" int spai_rollout_select(const float* logits, int64_t bstride, int32_t
                                            lmax, w.c_ord, w.c_act, w.c_log, w.blk_cnt, w.blk_wrest);
   SPAI_CHECK_LAUNCH();
   k_group<<<dim3(w.ntiles, B), kGrpNT, 0, s>>>(w.nblk, w.ntiles, w.c_ord, w.c_act, w.c_log, w.blk_cnt, w.blk_wrest,
-                                               w.nb, w.spl, w.lut, w.lut_base, w.staging, w.stlog, w.tcount, w.tloc,
+                                               w.nb, w.spl, w.lut, w.lut_base, w.staging, w.stlog, w.trun,
                                                w.btot, w.tile_wrest);
   SPAI_CHECK_LAUNCH();
   k_bscan<<<B, 1024, 0, s>>>(E, w.ntiles, logits, bstride, lmax, w.nb, w.btot, w.tile_wrest, w.bstart,
@@ -1183,10 +1289,11 @@ extern "C" int spai_rollout_order(const float* logits, int64_t bstride, int32_t 
   hipStream_t s = (hipStream_t)stream;
   const int nbm = max_buckets(E);
   const int g2 = std::max(1, std::min(nbm * B, num_cus()));
-  k_sort2<<<g2, kSortNT, 0, s>>>(E, B, w.ntiles, w.nb, w.bstart, w.tcount, w.tloc, w.staging, w.stlog, lmax, t_cap,
+  k_runs<<<dim3((w.ntiles + kRunT - 1) / kRunT, kMaxB / kRunT, B), 256, 0, s>>>(w.ntiles, w.nb, w.trun, w.runs);
+  k_sort2<<<g2, kSortNT, 0, s>>>(E, B, w.ntiles, w.nb, w.bstart, w.runs, w.staging, w.stlog, lmax, t_cap,
                                  actions, w.out_w, w.out_suf, w.bwsum);
   SPAI_CHECK_LAUNCH();
-  k_sort2_big<<<g2, kSortNT, 0, s>>>(E, B, w.ntiles, w.nb, w.bstart, w.tcount, w.tloc, w.staging, logits, bstride,
+  k_sort2_big<<<g2, kSortNT, 0, s>>>(E, B, w.ntiles, w.nb, w.bstart, w.runs, w.staging, logits, bstride,
                                      lmax, t_cap, actions, w.out_w, w.out_suf, w.scratch, w.bwsum);
   SPAI_CHECK_LAUNCH();
   k_wscan<<<B, 1024, 0, s>>>(w.nb, w.bwsum, w.bwsuf);

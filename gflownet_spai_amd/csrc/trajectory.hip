@@ -9,18 +9,19 @@
 // one coalesced staging write and one gather of contiguous runs:
 //   k_presample  keys of a pseudo-random stratified subset of <= 65536 actions per sample
 //                (1.2 % of the Philox work at C4); winners kept in subset order.
-//   k_splitters  one block per sample sorts up to 8192 sampled winner keys in LDS (LSD
-//                radix, 1 bit per pass) and picks nb = est/4096 bucket splitters: buckets
-//                of ~4096 winners whatever the key distribution.
-//   k_select     16384 actions per block: Philox4x32-10 + deterministic fp32 keys, removal
-//                bitmap words, mass of the untouched actions, and the tile's winners
-//                grouped by bucket in LDS and written as one contiguous 8-byte stream
-//                (never a scattered global write); per-(bucket, tile) counts and offsets.
+//   k_splitters  per sample: value-linear histogram quantiles of the sampled winner keys
+//                -> nb ~ est/4096 bucket splitters and a 4096-bin bucket lookup table.
+//   k_tile       one 16384-action tile of one sample per block: Philox4x32-10 +
+//                deterministic fp32 keys (in registers), removal bitmap words, the fp64
+//                mass of the untouched actions, bucket histogram with in-bucket ranks, and
+//                the tile's winners written grouped by bucket through LDS windows as one
+//                contiguous 8 B record stream + 4 B logit stream; per-(bucket, tile) runs.
 //   k_bscan      per sample: bucket starts, winner count, untouched mass, T.
-//   k_sort2      one block per bucket: gathers the bucket's runs (one per tile) into LDS,
-//                value-linear sub-buckets + rank counting, then fp64 weights
-//                w = exp(l - lmax) and in-bucket suffix sums; writes the actions in place.
-//                Buckets above the LDS capacity take an exact in-block radix path.
+//   k_runs       run table transposed bucket-major (one contiguous row per bucket).
+//   k_sort2      persistent; per bucket: one-round-trip gather of its runs (one per tile)
+//                into registers, value-linear sub-buckets + rank counting in LDS, fp32
+//                weights w = exp(l - lmax), fp64 in-bucket suffix sums.  Outputs stored
+//                during the next bucket.  Buckets above the LDS capacity: k_sort2_big.
 //   k_wscan      per sample suffix over the bucket weight sums (fixed order).
 //   k_final      fwd_probs = w / (W_rest + later buckets + in-bucket suffix).
 //   k_pad        terminal step, -1 / 1.0 padding up to T = max_b k_b + 1.
@@ -33,13 +34,10 @@
 namespace spai {
 namespace {
 
-constexpr int kNT = 256;                   // threads of a select block
-constexpr int kBlk = kNT * 4;              // actions per select block (4 consecutive per thread)
-constexpr int kTileBlk = 16;               // select blocks per grouping tile (< 64: one wave scans them)
-constexpr int kTile = kBlk * kTileBlk;     // 16384 actions per grouping tile
-static_assert(kTile <= 65535, "run offsets and counts are packed in 16 bits (k_group, k_runs)");
-constexpr int kGrpNT = 512;                // threads of a grouping block
-constexpr int kWin = 3584;                 // records per LDS output window of a grouping block
+constexpr int kTile = 16384;               // actions per tile (k_tile block; a run per bucket)
+static_assert(kTile <= 65535, "run offsets and counts are packed in 16 bits (k_tile, k_runs)");
+constexpr int kGrpNT = 512;                // threads of a k_tile block
+constexpr int kWin = 3584;                 // records per LDS output window of k_tile
 constexpr int kSampM = 65536;              // subset size (power of two, capped by E)
 constexpr int kSampNT = 256;
 constexpr int kSampCap = 32768;            // sampled winners behind the splitters
@@ -64,12 +62,6 @@ struct TrajWs {
   uint32_t* spl;          // [B][kMaxB] ascending orderable splitters
   uint16_t* lut;          // [B][kBins] bucket lookup table
   uint32_t* lut_base;     // [B][2] (min key, shift) of the table
-  int32_t nblk;
-  uint32_t* c_ord;        // [B][nblk][kBlk] winners compacted per select block: orderable key
-  int32_t* c_act;         //                                                   action
-  float* c_log;           //                                                   logit
-  int32_t* blk_cnt;       // [B][nblk]
-  double* blk_wrest;      // [B][nblk]
   uint64_t* staging;      // [B][ntiles][kTile] (~ord << 32 | action), grouped by bucket per tile
   float* stlog;           // [B][ntiles][kTile] logit of each staged record
   uint32_t* trun;         // [B][ntiles][kMaxB] run of bucket k in tile t: offset << 16 | count
@@ -101,12 +93,6 @@ static void traj_ws(void* base, int32_t E, int32_t B, TrajWs* w) {
   w->spl = c.take<uint32_t>((size_t)B * kMaxB);
   w->lut = c.take<uint16_t>((size_t)B * kBins);
   w->lut_base = c.take<uint32_t>((size_t)B * 2);
-  w->nblk = (E + kBlk - 1) / kBlk;
-  w->c_ord = c.take<uint32_t>((size_t)B * w->nblk * kBlk);
-  w->c_act = c.take<int32_t>((size_t)B * w->nblk * kBlk);
-  w->c_log = c.take<float>((size_t)B * w->nblk * kBlk);
-  w->blk_cnt = c.take<int32_t>((size_t)B * w->nblk);
-  w->blk_wrest = c.take<double>((size_t)B * w->nblk);
   w->staging = c.take<uint64_t>((size_t)B * w->ntiles * kTile);
   w->stlog = c.take<float>((size_t)B * w->ntiles * kTile);
   w->trun = c.take<uint32_t>((size_t)B * kMaxB * w->ntiles);
@@ -365,7 +351,7 @@ __global__ __launch_bounds__(kSortNT) void k_splitters(int32_t E, int32_t M, int
   }
   __syncthreads();
   // lookup table over the same bins: lut[bin] = #(splitters < start of bin); a key's bucket
-  // count is then lut[bin] plus the few splitters inside its bin (k_select)
+  // count is then lut[bin] plus the few splitters inside its bin (bucket_lut)
   for (int bin = tid; bin < kBins; bin += kSortNT) {
     const uint64_t start = (uint64_t)mn + ((uint64_t)bin << shift);
     int lo = 0, hi = nb - 1;  // lower_bound over s_spl[0 .. nb-2]
@@ -383,12 +369,6 @@ __global__ __launch_bounds__(kSortNT) void k_splitters(int32_t E, int32_t M, int
   }
 }
 
-// ------------------------------------------------------------------ k_select
-// 1024 actions per block (256 threads x 4 consecutive): Philox4x32-10 + deterministic fp32
-// Gumbel keys, removal bitmap words (8-lane shuffles), the fp64 mass of the untouched
-// actions (fixed order) and the block's winners compacted in action order as three
-// coalesced streams (orderable key, action, logit).  Small LDS: full occupancy for the
-// ALU-bound key arithmetic.
 // w = exp(l - lmax) in fp32 to within ~1 ulp of the correctly rounded value: l - lmax is
 // exact in fp64, split into a float head and a tiny tail, exp(hi + lo) = exp(hi) (1 + lo).
 // (An fp64 exp costs ~30 us per rollout wherever it is placed.)
@@ -399,81 +379,41 @@ __device__ __forceinline__ float winner_weight(float l, float lm) {
   return fmaf(e, lo, e);
 }
 
-__global__ __launch_bounds__(kNT) void k_select(const float* __restrict__ logits, int64_t bstride, int32_t E,
-                                                int32_t nblk, uint32_t seed0, uint32_t seed1, uint32_t st0,
-                                                uint32_t st1, int32_t sample_base, uint32_t* __restrict__ removed,
-                                                int32_t words, const float* __restrict__ lmax,
-                                                uint32_t* __restrict__ c_ord, int32_t* __restrict__ c_act,
-                                                float* __restrict__ c_log, int32_t* __restrict__ blk_cnt,
-                                                double* __restrict__ blk_wrest) {
-  const int b = blockIdx.y, blk = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
-  const float* lg = logits + (int64_t)b * bstride;
-  const uint32_t bg = (uint32_t)(sample_base + b);
-  __shared__ float s_tk;
-  __shared__ int s_wc[kNT / 64];
-  __shared__ double s_wr[kNT / 64];
-  if (tid == 0) s_tk = terminal_key(lg, E, bg, st0, st1, seed0, seed1);
-  __syncthreads();
-  const float tk = s_tk;
-  const float lm = lmax[b];
-  const int a0 = blk * kBlk + tid * 4;
-  uint32_t nib = 0, ord[4];
-  float lv[4];
-  double wr = 0.0;
-  if (a0 < E) {
-    const uint4 rr = philox4x32_10((uint32_t)a0 >> 2, bg, st0, st1, seed0, seed1);
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      ord[s] = 0;
-      lv[s] = 0.0f;
-      if (a0 + s < E) {
-        lv[s] = lg[a0 + s];
-        const float key = gumbel_key(lv[s], pick_word(rr, s));
-        if (key > tk) {
-          nib |= 1u << s;
-          ord[s] = orderable(key);
-        } else {
-          wr += (double)__expf(lv[s] - lm);
-        }
-      }
-    }
-  }
-  uint32_t x = nib << ((tid & 7) * 4);
-  x |= __shfl_xor(x, 1, kWave);
-  x |= __shfl_xor(x, 2, kWave);
-  x |= __shfl_xor(x, 4, kWave);
-  if ((tid & 7) == 0 && a0 < E) {
-    const int wi = a0 >> 5;
-    if (wi < words) removed[(int64_t)b * words + wi] = x;
-  }
-  wr = wave_sum(wr);
-  if (lane == 0) s_wr[tid >> 6] = wr;
-  int tot;
-  int pos = block_excl_scan<kNT>(__popc(nib), s_wc, &tot);
-  const int64_t base = ((int64_t)b * nblk + blk) * kBlk;
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    if ((nib >> s) & 1u) {
-      c_ord[base + pos] = ord[s];
-      c_act[base + pos] = a0 + s;
-      c_log[base + pos] = lv[s];
-      ++pos;
-    }
-  }
-  if (tid == 0) {
-    double t = 0.0;
-#pragma unroll
-    for (int w = 0; w < kNT / 64; ++w) t += s_wr[w];
-    blk_wrest[(int64_t)b * nblk + blk] = t;
-    blk_cnt[(int64_t)b * nblk + blk] = tot;
-  }
+#ifdef SPAI_PROF  // phase timing (variant builds only: make EXTRA=-DSPAI_PROF); slots 16*kernel + phase
+__device__ unsigned long long g_prof[64];
+__device__ __forceinline__ uint64_t prof_stamp() {
+  uint64_t t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
 }
+#define PROF_INIT uint64_t pf_t = prof_stamp(), pf_acc[16] = {};
+#define PROF(i)                          \
+  if (threadIdx.x == 0) {                \
+    const uint64_t pf_n = prof_stamp();   \
+    pf_acc[i] += pf_n - pf_t;            \
+    pf_t = pf_n;                         \
+  }
+#define PROF_END(base)     \
+  if (threadIdx.x == 0)    \
+    for (int q = 0; q < 16; ++q) atomicAdd(&g_prof[(base) + q], (unsigned long long)pf_acc[q]);
+extern "C" int spai_debug_prof(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_prof), sizeof(g_prof)) != hipSuccess) return 2;
+  if (reset) {
+    static const unsigned long long z[64] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, sizeof(z)) != hipSuccess) return 2;
+  }
+  return 0;
+}
+#else
+#define PROF_INIT
+#define PROF(i)
+#define PROF_END(base)
+#endif
 
-// ------------------------------------------------------------------ k_group
-// One 16384-action tile (kTileBlk select blocks) per block: bucket of every winner from the
-// splitter lookup table, LDS histogram, per-(bucket, tile) counts and offsets, and the
-// winners re-written grouped by bucket as one contiguous 8 B + 4 B stream per tile (the
-// records are read twice; the second read hits L2).
+// Bucket of a winner's orderable key: value-linear lookup table, then the splitters
+// (usually 0-1 steps); buckets are numbered in trajectory order (descending key).
 __device__ __forceinline__ int bucket_lut(uint32_t o, const uint16_t* s_lut, const uint32_t* s_spl, uint32_t lmn,
                                           int lsh, int nb) {
   const uint32_t bin = o < lmn ? 0u : min((uint32_t)(kBins - 1), (o - lmn) >> lsh);
@@ -482,66 +422,117 @@ __device__ __forceinline__ int bucket_lut(uint32_t o, const uint16_t* s_lut, con
   return nb - 1 - c;
 }
 
-__global__ __launch_bounds__(kGrpNT) void k_group(int32_t nblk, int32_t ntiles, const uint32_t* __restrict__ c_ord,
-                                                  const int32_t* __restrict__ c_act, const float* __restrict__ c_log,
-                                                  const int32_t* __restrict__ blk_cnt,
-                                                  const double* __restrict__ blk_wrest,
-                                                  const int32_t* __restrict__ nb_, const uint32_t* __restrict__ spl_,
-                                                  const uint16_t* __restrict__ lut_,
-                                                  const uint32_t* __restrict__ lut_base,
-                                                  uint64_t* __restrict__ staging, float* __restrict__ stlog,
-                                                  uint32_t* __restrict__ trun,
-                                                  int32_t* __restrict__ btot, double* __restrict__ tile_wrest) {
-  constexpr int kWB = kTileBlk / (kGrpNT / 64);  // select blocks per wave (2)
-  constexpr int kR = 8;                          // records per lane in flight
-  __shared__ uint64_t w_rec[kWin];  // one window of the grouped output (whole cache lines out)
-  __shared__ float w_log[kWin];
+// ------------------------------------------------------------------ k_tile
+// Selection and grouping fused, one 16384-action tile of one sample per block: Gumbel keys
+// of the tile (32 actions per thread, kept in registers), the removed bitmap, the rest mass
+// of the tile's non-winners, then the grouping steps on the register-resident winners:
+// bucket histogram, per-(bucket, tile) runs, and the winners re-written grouped by bucket
+// through LDS windows (whole cache lines out).  The splitter tables load while the keys are
+// computed, so the only exposed global trip is the logits read.
+constexpr int kTileG = kTile / (kGrpNT * 4);  // Philox groups (of 4 actions) per thread: 8
+__global__ __launch_bounds__(kGrpNT) __attribute__((amdgpu_waves_per_eu(4)))
+void k_tile(const float* __restrict__ logits, int64_t bstride, int32_t E,
+                                                 int32_t ntiles, uint32_t seed0, uint32_t seed1, uint32_t st0,
+                                                 uint32_t st1, int32_t sample_base, uint32_t* __restrict__ removed,
+                                                 int32_t words, const float* __restrict__ lmax,
+                                                 const int32_t* __restrict__ nb_, const uint32_t* __restrict__ spl_,
+                                                 const uint16_t* __restrict__ lut_,
+                                                 const uint32_t* __restrict__ lut_base,
+                                                 uint64_t* __restrict__ staging, float* __restrict__ stlog,
+                                                 uint32_t* __restrict__ trun, int32_t* __restrict__ btot,
+                                                 double* __restrict__ tile_wrest) {
+  __shared__ uint64_t w_rec[kWin];  // one window of the grouped output
   __shared__ __attribute__((aligned(16))) uint32_t s_spl[kMaxB];
   __shared__ int s_off[kMaxB + 1];  // histogram, then tile-local bucket offsets
-  __shared__ int s_cur[kMaxB];
   __shared__ __attribute__((aligned(16))) uint16_t s_lut[kBins];
-  __shared__ int s_bpre[kTileBlk + 1];
   __shared__ int s_wc[kGrpNT / 64];
+  __shared__ double s_wr[kGrpNT / 64];
+  __shared__ float s_tk;
   const int b = blockIdx.y, tile = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  PROF_INIT
+  const float* lg = logits + (int64_t)b * bstride;
+  const uint32_t bg = (uint32_t)(sample_base + b);
   const int nb = nb_[b];
-  // prologue: every load in one round (16 B per lane for the table and the splitters)
+  // splitter tables (consumed only after the keys; their latency hides behind the Philox work)
   static_assert(kBins * 2 == kGrpNT * 16 && kMaxB * 4 == kGrpNT * 16, "prologue vector widths");
-  static_assert(kTileBlk < 64, "the block prefix (kTileBlk + 1 entries) is one wave's scan");
   reinterpret_cast<uint4*>(s_lut)[tid] = reinterpret_cast<const uint4*>(lut_ + (int64_t)b * kBins)[tid];
   if (tid * 4 < nb - 1)
     reinterpret_cast<uint4*>(s_spl)[tid] = reinterpret_cast<const uint4*>(spl_ + (int64_t)b * kMaxB)[tid];
   for (int k = tid; k < nb; k += kGrpNT) s_off[k] = 0;
+  if (tid == 0) s_tk = terminal_key(lg, E, bg, st0, st1, seed0, seed1);
   const uint32_t lmn = lut_base[2 * b];
   const int lsh = (int)lut_base[2 * b + 1];
-  const int blk0 = tile * kTileBlk, nbt = min(kTileBlk, nblk - blk0);
-  if (tid < 64) {  // one lane per select block: parallel loads, wave scan (fixed order)
-    const int c = tid < nbt ? blk_cnt[(int64_t)b * nblk + blk0 + tid] : 0;
-    double wr = tid < nbt ? blk_wrest[(int64_t)b * nblk + blk0 + tid] : 0.0;
-    const int incl = wave_incl_scan(c);
-    if (tid <= nbt) s_bpre[tid] = incl - c;
-    wr = wave_sum(wr);
-    if (tid == 0) tile_wrest[(int64_t)b * ntiles + tile] = wr;
+  const float lm = lmax[b];
+  const int a_t = tile * kTile;  // first action of the tile
+  const bool al16 = (reinterpret_cast<uintptr_t>(lg) & 15u) == 0;  // rows of E+1 floats need not be
+  __syncthreads();  // s_tk
+  PROF(0)
+  const float tk = s_tk;
+  // group g covers actions a_t + g * (4 * kGrpNT) + 4 * tid + 0..3 (coalesced float4 logits)
+  uint32_t ord[4 * kTileG];
+  uint32_t win = 0;  // bit 4g + s: action a_t + g * 4 * kGrpNT + 4 * tid + s is a winner
+  double wr = 0.0;
+#pragma unroll
+  for (int g = 0; g < kTileG; ++g) {
+    const int a0 = a_t + g * 4 * kGrpNT + 4 * tid;
+    float lv[4];
+    if (al16 && a0 + 3 < E) {
+      const float4 v = *reinterpret_cast<const float4*>(lg + a0);
+      lv[0] = v.x;
+      lv[1] = v.y;
+      lv[2] = v.z;
+      lv[3] = v.w;
+    } else {
+#pragma unroll
+      for (int s = 0; s < 4; ++s) lv[s] = a0 + s < E ? lg[a0 + s] : 0.0f;
+    }
+    const uint4 rr = philox4x32_10((uint32_t)a0 >> 2, bg, st0, st1, seed0, seed1);
+    uint32_t nib = 0;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      ord[4 * g + s] = 0u;
+      if (a0 + s < E) {
+        const float key = gumbel_key(lv[s], pick_word(rr, s));
+        if (key > tk) {
+          nib |= 1u << s;
+          ord[4 * g + s] = orderable(key);
+        } else {
+          wr += (double)__expf(lv[s] - lm);
+        }
+      }
+    }
+    win |= nib << (4 * g);
+    // removed bitmap: 8 adjacent threads make one 32-bit word
+    uint32_t x = nib << ((tid & 7) * 4);
+    x |= __shfl_xor(x, 1, kWave);
+    x |= __shfl_xor(x, 2, kWave);
+    x |= __shfl_xor(x, 4, kWave);
+    const int wi = a0 >> 5;
+    if ((tid & 7) == 0 && a0 < E && wi < words) removed[(int64_t)b * words + wi] = x;
+  }
+  wr = wave_sum(wr);
+  if (lane == 0) s_wr[wave] = wr;
+  PROF(1)
+  // bucket histogram of the winners; each winner keeps its bucket and its rank inside the
+  // bucket (the histogram atomic's return; any order: the level-2 sort orders buckets fully)
+  static_assert(kMaxB <= (1 << 11) && kTile <= (1 << 21), "bucket | rank << 11 packing");
+  uint32_t br[4 * kTileG];
+#pragma unroll
+  for (int q = 0; q < 4 * kTileG; ++q) {
+    br[q] = 0u;
+    if ((win >> q) & 1u) {
+      const int bk = bucket_lut(ord[q], s_lut, s_spl, lmn, lsh, nb);
+      br[q] = (uint32_t)bk | ((uint32_t)atomicAdd(&s_off[bk], 1) << 11);
+    }
   }
   __syncthreads();
-  const int64_t cbase = ((int64_t)b * nblk + blk0) * kBlk;
-  // this wave's records: select blocks wave*kWB .. +kWB, flattened
-  const int wb0 = min(wave * kWB, nbt), wb1 = min(wb0 + kWB, nbt);
-  const int wn = s_bpre[wb1] - s_bpre[wb0];
-  auto src = [&](int j) {  // j-th record of this wave -> index in the compacted streams
-    int bi = wb0;
+  PROF(2)
+  if (tid == 0) {
+    double t = 0.0;
 #pragma unroll
-    for (int q = 1; q < kWB; ++q) bi += (wb0 + q < wb1 && j >= s_bpre[wb0 + q] - s_bpre[wb0]) ? 1 : 0;
-    return cbase + (int64_t)bi * kBlk + (j - (s_bpre[bi] - s_bpre[wb0]));
-  };
-  for (int j0 = lane; j0 < wn; j0 += 64 * kR) {
-    uint32_t o[kR];
-#pragma unroll
-    for (int q = 0; q < kR; ++q) o[q] = j0 + 64 * q < wn ? c_ord[src(j0 + 64 * q)] : 0u;
-#pragma unroll
-    for (int q = 0; q < kR; ++q)
-      if (j0 + 64 * q < wn) atomicAdd(&s_off[bucket_lut(o[q], s_lut, s_spl, lmn, lsh, nb)], 1);
+    for (int w = 0; w < kGrpNT / 64; ++w) t += s_wr[w];
+    tile_wrest[(int64_t)b * ntiles + tile] = t;
   }
-  __syncthreads();
   // bucket offsets inside the tile (exclusive scan, kMaxB / kGrpNT buckets per thread)
   constexpr int kQ = kMaxB / kGrpNT;
   int hv[kQ], loc = 0;
@@ -566,62 +557,60 @@ __global__ __launch_bounds__(kGrpNT) void k_group(int32_t nblk, int32_t ntiles, 
   }
   if (tid == 0) s_off[nb] = tot;
   __syncthreads();
+  PROF(3)
+  // final tile-local position of every winner, two per VGPR
+  uint32_t pp[2 * kTileG];
+#pragma unroll
+  for (int q = 0; q < 4 * kTileG; ++q) {
+    const uint32_t pos = (win >> q) & 1u ? (uint32_t)s_off[br[q] & 0x7FFu] + (br[q] >> 11) : 0xFFFFu;
+    if (q & 1) pp[q >> 1] |= pos << 16;
+    else pp[q >> 1] = pos;
+  }
   uint64_t* st = staging + ((int64_t)b * ntiles + tile) * kTile;
   float* sl = stlog + ((int64_t)b * ntiles + tile) * kTile;
-  // windows of consecutive buckets whose records fit the LDS stage; a (tile, bucket) run
-  // longer than the stage is scattered directly (rare)
+  // positional windows of kWin records staged in LDS, written out as whole cache lines
 #pragma unroll 1
-  for (int kw = 0; kw < nb;) {
-    const int base = s_off[kw];
-    int lo = kw + 1, hi = nb;  // largest kw' with s_off[kw'] - base <= kWin
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (s_off[mid] - base <= kWin) lo = mid;
-      else hi = mid - 1;
-    }
-    const int kw2 = lo;
-    const bool direct = s_off[kw2] - base > kWin;  // single oversized bucket
-    for (int k = kw + tid; k < kw2; k += kGrpNT) s_cur[k] = s_off[k] - (direct ? 0 : base);
-    __syncthreads();
-    for (int j0 = lane; j0 < wn; j0 += 64 * kR) {
-      uint32_t o[kR];
-      int a[kR];
-      float lv[kR];
+  for (int w0 = 0; w0 < tot; w0 += kWin) {
+    int tv = tid;
+    asm volatile("" : "+v"(tv));  // opaque per window: keeps per-slot addresses out of registers
 #pragma unroll
-      for (int q = 0; q < kR; ++q) {
-        const bool in = j0 + 64 * q < wn;
-        const int64_t si = in ? src(j0 + 64 * q) : cbase;
-        o[q] = in ? c_ord[si] : 0u;
-        a[q] = in ? c_act[si] : 0;
-        lv[q] = in ? c_log[si] : 0.0f;
+    for (int q = 0; q < 4 * kTileG; ++q) {
+      const int p = (int)((pp[q >> 1] >> (16 * (q & 1))) & 0xFFFFu) - w0;
+      if ((unsigned)p < (unsigned)kWin) {  // (non-winners carry 0xFFFF, beyond every window)
+        const int a = a_t + (q >> 2) * 4 * kGrpNT + 4 * tv + (q & 3);
+        w_rec[p] = ((uint64_t)(~ord[q]) << 32) | (uint32_t)a;
+      }
+    }
+    __syncthreads();
+    PROF(4)
+    const int cnt = min(kWin, tot - w0);
+    // the logits are re-read here (L2-resident; every gather of the window in flight at once):
+    // keeping 32 logits per thread live through the phases above would cost occupancy
+    constexpr int kWU = 4;  // gathers in flight per thread
+#pragma unroll 1
+    for (int e0 = 0; e0 < cnt; e0 += kWU * kGrpNT) {
+      uint64_t rv[kWU];
+      float lw[kWU];
+#pragma unroll
+      for (int u = 0; u < kWU; ++u) {
+        const int e = e0 + u * kGrpNT + tid;
+        rv[u] = e < cnt ? w_rec[e] : 0ull;
       }
 #pragma unroll
-      for (int q = 0; q < kR; ++q) {
-        const int bk = j0 + 64 * q < wn ? bucket_lut(o[q], s_lut, s_spl, lmn, lsh, nb) : -1;
-        if (bk >= kw && bk < kw2) {
-          const int p = atomicAdd(&s_cur[bk], 1);
-          const uint64_t rec = ((uint64_t)(~o[q]) << 32) | (uint32_t)a[q];
-          if (direct) {
-            st[p] = rec;
-            sl[p] = lv[q];
-          } else {
-            w_rec[p] = rec;
-            w_log[p] = lv[q];
-          }
+      for (int u = 0; u < kWU; ++u) lw[u] = e0 + u * kGrpNT + tid < cnt ? lg[(uint32_t)rv[u]] : 0.0f;
+#pragma unroll
+      for (int u = 0; u < kWU; ++u) {
+        const int e = e0 + u * kGrpNT + tid;
+        if (e < cnt) {
+          st[w0 + e] = rv[u];
+          sl[w0 + e] = lw[u];
         }
       }
     }
     __syncthreads();
-    if (!direct) {
-      const int cnt = s_off[kw2] - base;
-      for (int e = tid; e < cnt; e += kGrpNT) {
-        st[base + e] = w_rec[e];
-        sl[base + e] = w_log[e];
-      }
-      __syncthreads();
-    }
-    kw = kw2;
+    PROF(5)
   }
+  PROF_END(32)
 }
 
 // ------------------------------------------------------------------ k_bscan
@@ -744,38 +733,6 @@ __global__ __launch_bounds__(256) void k_runs(int32_t ntiles, const int32_t* __r
 }
 
 // ------------------------------------------------------------------ k_sort2
-#ifdef SPAI_PROF  // phase timing of k_sort2 (variant builds only: make EXTRA=-DSPAI_PROF)
-__device__ unsigned long long g_sort2_prof[16];
-__device__ __forceinline__ uint64_t prof_stamp() {
-  uint64_t t;
-  __builtin_amdgcn_sched_barrier(0);
-  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-  __builtin_amdgcn_sched_barrier(0);
-  return t;
-}
-#define PROF_INIT uint64_t pf_t = prof_stamp(), pf_acc[12] = {};
-#define PROF(i)                          \
-  if (tid == 0) {                        \
-    const uint64_t pf_n = prof_stamp();   \
-    pf_acc[i] += pf_n - pf_t;            \
-    pf_t = pf_n;                         \
-  }
-#define PROF_END \
-  if (tid == 0)  \
-    for (int q = 0; q < 12; ++q) atomicAdd(&g_sort2_prof[q], (unsigned long long)pf_acc[q]);
-extern "C" int spai_debug_sort2_prof(unsigned long long* out, int reset) {
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sort2_prof), sizeof(g_sort2_prof)) != hipSuccess) return 2;
-  if (reset) {
-    static const unsigned long long z[16] = {};
-    if (hipMemcpyToSymbol(HIP_SYMBOL(g_sort2_prof), z, sizeof(z)) != hipSuccess) return 2;
-  }
-  return 0;
-}
-#else
-#define PROF_INIT
-#define PROF(i)
-#define PROF_END
-#endif
 
 // Oversized bucket (the sampled splitters missed; rare): gather into scratch, exact
 // in-block radix in global memory, then the same outputs as the LDS path.
@@ -1040,7 +997,7 @@ __global__ __launch_bounds__(kSortNT) void k_sort2(int32_t E, int32_t B, int32_t
       }
     lds_barrier();
     PROF(7)
-    // weights (computed by k_group) and fp64 in-bucket inclusive suffix sums: thread t owns
+    // weights (computed at the gather) and fp64 in-bucket inclusive suffix sums: thread t owns
     // the t-th chunk counted from the END (contiguous, fixed order -> deterministic)
     const int per = (n + kSortNT - 1) / kSortNT;
     const int hi_ = n - min(tid * per, n), lo_ = max(hi_ - per, 0);
@@ -1083,7 +1040,7 @@ __global__ __launch_bounds__(kSortNT) void k_sort2(int32_t E, int32_t B, int32_t
     PROF(9)
   }
   flush();
-  PROF_END
+  PROF_END(0)
 }
 
 // Buckets above the LDS capacity (rare): one block each, exact radix in global memory.
@@ -1261,12 +1218,9 @@ extern "C" int spai_rollout_select(const float* logits, int64_t bstride, int32_t
   SPAI_CHECK_LAUNCH();
   k_splitters<<<B, kSortNT, 0, s>>>(E, w.M, nsb, w.samp, w.samp_cnt, w.nb, w.spl, w.lut, w.lut_base);
   SPAI_CHECK_LAUNCH();
-  k_select<<<dim3(w.nblk, B), kNT, 0, s>>>(logits, bstride, E, w.nblk, s0, s1, t0, t1, sample_base, removed, words,
-                                           lmax, w.c_ord, w.c_act, w.c_log, w.blk_cnt, w.blk_wrest);
-  SPAI_CHECK_LAUNCH();
-  k_group<<<dim3(w.ntiles, B), kGrpNT, 0, s>>>(w.nblk, w.ntiles, w.c_ord, w.c_act, w.c_log, w.blk_cnt, w.blk_wrest,
-                                               w.nb, w.spl, w.lut, w.lut_base, w.staging, w.stlog, w.trun,
-                                               w.btot, w.tile_wrest);
+  k_tile<<<dim3(w.ntiles, B), kGrpNT, 0, s>>>(logits, bstride, E, w.ntiles, s0, s1, t0, t1, sample_base, removed,
+                                              words, lmax, w.nb, w.spl, w.lut, w.lut_base, w.staging, w.stlog,
+                                              w.trun, w.btot, w.tile_wrest);
   SPAI_CHECK_LAUNCH();
   k_bscan<<<B, 1024, 0, s>>>(E, w.ntiles, logits, bstride, lmax, w.nb, w.btot, w.tile_wrest, w.bstart,
                              counts, w.wrest, w.tdev);

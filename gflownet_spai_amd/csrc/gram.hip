@@ -97,7 +97,7 @@ __global__ __launch_bounds__(kNT) void k_gram_build(int32_t n, int32_t wrt, int3
 // squared line residuals of a chunk of kChunk samples go to LDS and are summed per sample
 // by one wave each in a fixed order (two barriers per chunk, none per sample).
 template <int W, typename TM, bool LSQ>
-__global__ __launch_bounds__(kNT) void k_gram_fill(int32_t n, int32_t line_begin, int32_t line_end, int32_t wrt,
+__global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(4))) void k_gram_fill(int32_t n, int32_t line_begin, int32_t line_end, int32_t wrt,
                                                    const int32_t* __restrict__ pat_act,
                                                    const float* __restrict__ pat_val,
                                                    const double* __restrict__ gram, int32_t B,
@@ -131,39 +131,54 @@ __global__ __launch_bounds__(kNT) void k_gram_fill(int32_t n, int32_t line_begin
   for (int p = 0; p < W; ++p) wofs[p] = act[p] >= 0 ? act[p] >> 5 : 0;
   TM* mo = m_out != nullptr ? m_out + (int64_t)(j - line_begin) * wrt : nullptr;
 
+  // the bitmap words of the next sample are loaded while the current one is solved
+  uint32_t wd[W];
+#pragma unroll
+  for (int p = 0; p < W; ++p) wd[p] = removed[wofs[p]];
 #pragma unroll 1
   for (int b0 = 0; b0 < B; b0 += kChunk) {
     const int nb = min(kChunk, B - b0);
 #pragma unroll 1
     for (int s = 0; s < nb; ++s) {
       const int b = b0 + s;
-      const uint32_t* rb = removed + (int64_t)b * words;
       bool keep[W];
 #pragma unroll
-      for (int p = 0; p < W; ++p) keep[p] = act[p] >= 0 && !((rb[wofs[p]] >> (act[p] & 31)) & 1u);
+      for (int p = 0; p < W; ++p) keep[p] = act[p] >= 0 && !((wd[p] >> (act[p] & 31)) & 1u);
+      if (b + 1 < B) {
+        const uint32_t* rn = removed + (int64_t)(b + 1) * words;
+#pragma unroll
+        for (int p = 0; p < W; ++p) wd[p] = rn[wofs[p]];
+      }
 
       double mr[W];
       double r2ls = 1.0;  // LSQ: 1 - c^T m* = 1 - sum_k y_k^2 / D_k (G m* = c on the kept slots)
       if constexpr (!LSQ) {
 #pragma unroll
         for (int p = 0; p < W; ++p) mr[p] = keep[p] ? (double)val[p] : 0.0;
+#ifdef FILL_NOCOMPUTE  // diagnostic variant: memory traffic without the solve
+      } else if (true) {
+#pragma unroll
+        for (int p = 0; p < W; ++p) mr[p] = keep[p] ? c[p] * G[gidx<W>(p, p)] : 0.0;
+        r2ls = mr[0] + mr[W - 1];
+#endif
       } else {
         // masked LDL^T of the normal equations: removed slots become identity rows, rhs 0
-        double L[W][W], D[W], iD[W], y[W];
+        // (EL[i][q] = L[i][q] * D[q] is the unscaled elimination value: one FMA per term)
+        double L[W][W], EL[W][W], iD[W], y[W];
 #pragma unroll
         for (int k = 0; k < W; ++k) {
           const double gkk = G[gidx<W>(k, k)];
           double dk = keep[k] ? gkk : 1.0;
           const double ref = dk;
 #pragma unroll
-          for (int q = 0; q < k; ++q) dk -= L[k][q] * L[k][q] * D[q];
-          D[k] = dk;
+          for (int q = 0; q < k; ++q) dk -= L[k][q] * EL[k][q];
           iD[k] = (dk > 1e-13 * ref) ? fast_rcp(dk) : 0.0;
 #pragma unroll
           for (int i = k + 1; i < W; ++i) {
             double v = (keep[k] && keep[i]) ? G[gidx<W>(k, i)] : 0.0;
 #pragma unroll
-            for (int q = 0; q < k; ++q) v -= L[i][q] * L[k][q] * D[q];
+            for (int q = 0; q < k; ++q) v -= L[i][q] * EL[k][q];
+            EL[i][k] = v;
             L[i][k] = v * iD[k];
           }
         }

@@ -105,6 +105,7 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(4))) void k
                                                    TM* __restrict__ m_out, double* __restrict__ partials) {
   constexpr int T = tri(W);
   __shared__ double s_r2[kChunk][kNT];
+  __shared__ __attribute__((aligned(16))) TM s_m[2][kNT * W];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int lb = blockIdx.x;
   const int j = line_begin + lb * kNT + t;
@@ -129,7 +130,7 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(4))) void k
   int wofs[W];  // bitmap word offsets / bit positions of the slots
 #pragma unroll
   for (int p = 0; p < W; ++p) wofs[p] = act[p] >= 0 ? act[p] >> 5 : 0;
-  TM* mo = m_out != nullptr ? m_out + (int64_t)(j - line_begin) * wrt : nullptr;
+  const int nvl = min(kNT, line_end - (line_begin + lb * kNT));  // valid lines of the block
 
   // the bitmap words of the next sample are loaded while the current one is solved
   uint32_t wd[W];
@@ -201,11 +202,26 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(4))) void k
 #pragma unroll
         for (int p = 0; p < W; ++p) mr[p] = keep[p] ? (double)(TM)mr[p] : 0.0;  // stored precision
       }
-      if (mo != nullptr && valid) {
-        TM* dst = mo + (int64_t)b * nloc * wrt;
+      if (m_out != nullptr) {
+        // M through LDS (double-buffered per sample): the block's lines of one sample are one
+        // contiguous run of nvl * wrt values, written with 16-byte stores
+        TM* sm = s_m[b & 1];
+        if (valid) {
 #pragma unroll
-        for (int p = 0; p < W; ++p)
-          if (p < wrt) dst[p] = (TM)mr[p];
+          for (int p = 0; p < W; ++p)
+            if (p < wrt) sm[t * wrt + p] = (TM)mr[p];
+        }
+        __syncthreads();
+        TM* dst = m_out + ((int64_t)b * nloc + (int64_t)lb * kNT) * wrt;
+        const int ne = nvl * wrt;
+        constexpr int V = 16 / sizeof(TM);
+        int e0 = 0;
+        if ((reinterpret_cast<uintptr_t>(dst) & 15u) == 0) {
+          for (int e = t; e < ne / V; e += kNT)
+            reinterpret_cast<uint4*>(dst)[e] = reinterpret_cast<const uint4*>(sm)[e];
+          e0 = ne / V * V;
+        }
+        for (int e = e0 + t; e < ne; e += kNT) dst[e] = sm[e];
       }
       double r2 = 0.0;
       if (valid) {

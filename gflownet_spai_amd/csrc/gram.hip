@@ -163,20 +163,23 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(4))) void k
         r2ls = mr[0] + mr[W - 1];
 #endif
       } else {
-        // masked LDL^T of the normal equations: removed slots become identity rows, rhs 0
+        // masked LDL^T of the normal equations. A removed slot k only gets iD[k] = 0: every
+        // L[.][k] = EL[.][k] * iD[k] is then exactly 0, so the kept unknowns see exactly the
+        // factorisation of G restricted to the kept slots (the removed rows' own values are
+        // finite and only ever multiplied by those zeros), and m[k] = 0 for the removed slots.
+        // No per-entry masking of G or c.
         // (EL[i][q] = L[i][q] * D[q] is the unscaled elimination value: one FMA per term)
         double L[W][W], EL[W][W], iD[W], y[W];
 #pragma unroll
         for (int k = 0; k < W; ++k) {
           const double gkk = G[gidx<W>(k, k)];
-          double dk = keep[k] ? gkk : 1.0;
-          const double ref = dk;
+          double dk = gkk;
 #pragma unroll
           for (int q = 0; q < k; ++q) dk -= L[k][q] * EL[k][q];
-          iD[k] = (dk > 1e-13 * ref) ? fast_rcp(dk) : 0.0;
+          iD[k] = (keep[k] && dk > 1e-13 * gkk) ? fast_rcp(dk) : 0.0;
 #pragma unroll
           for (int i = k + 1; i < W; ++i) {
-            double v = (keep[k] && keep[i]) ? G[gidx<W>(k, i)] : 0.0;
+            double v = G[gidx<W>(k, i)];
 #pragma unroll
             for (int q = 0; q < k; ++q) v -= L[i][q] * EL[k][q];
             EL[i][k] = v;
@@ -185,7 +188,7 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(4))) void k
         }
 #pragma unroll
         for (int k = 0; k < W; ++k) {
-          double v = keep[k] ? c[k] : 0.0;
+          double v = c[k];
 #pragma unroll
           for (int q = 0; q < k; ++q) v -= L[k][q] * y[q];
           y[k] = v;
@@ -199,8 +202,6 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(4))) void k
           for (int q = k + 1; q < W; ++q) v -= L[q][k] * mr[q];
           mr[k] = v;
         }
-#pragma unroll
-        for (int p = 0; p < W; ++p) mr[p] = keep[p] ? (double)(TM)mr[p] : 0.0;  // stored precision
       }
       if (m_out != nullptr) {
         // M through LDS (double-buffered per sample): the block's lines of one sample are one

@@ -36,8 +36,11 @@ namespace {
 
 constexpr int kTile = 16384;               // actions per tile (k_tile block; a run per bucket)
 static_assert(kTile <= 65535, "run offsets and counts are packed in 16 bits (k_tile, k_runs)");
-constexpr int kGrpNT = 512;                // threads of a k_tile block
-constexpr int kWin = 3584;                 // records per LDS output window of k_tile
+constexpr int kGrpNT = 1024;               // threads of a k_tile block (16 actions each)
+#ifndef KWIN
+#define KWIN 8192
+#endif
+constexpr int kWin = KWIN;                 // records per LDS output window of k_tile (1 block/CU)
 constexpr int kSampM = 65536;              // subset size (power of two, capped by E)
 constexpr int kSampNT = 256;
 constexpr int kSampCap = 32768;            // sampled winners behind the splitters
@@ -424,13 +427,13 @@ __device__ __forceinline__ int bucket_lut(uint32_t o, const uint16_t* s_lut, con
 
 // ------------------------------------------------------------------ k_tile
 // Selection and grouping fused, one 16384-action tile of one sample per block: Gumbel keys
-// of the tile (32 actions per thread, kept in registers), the removed bitmap, the rest mass
+// of the tile (16 actions per thread; keys and logits kept in registers), the removed bitmap, the rest mass
 // of the tile's non-winners, then the grouping steps on the register-resident winners:
 // bucket histogram, per-(bucket, tile) runs, and the winners re-written grouped by bucket
 // through LDS windows (whole cache lines out).  The splitter tables load while the keys are
 // computed, so the only exposed global trip is the logits read.
 constexpr int kTileG = kTile / (kGrpNT * 4);  // Philox groups (of 4 actions) per thread: 8
-__global__ __launch_bounds__(kGrpNT) __attribute__((amdgpu_waves_per_eu(4)))
+__global__ __launch_bounds__(kGrpNT)
 void k_tile(const float* __restrict__ logits, int64_t bstride, int32_t E,
                                                  int32_t ntiles, uint32_t seed0, uint32_t seed1, uint32_t st0,
                                                  uint32_t st1, int32_t sample_base, uint32_t* __restrict__ removed,
@@ -442,6 +445,7 @@ void k_tile(const float* __restrict__ logits, int64_t bstride, int32_t E,
                                                  uint32_t* __restrict__ trun, int32_t* __restrict__ btot,
                                                  double* __restrict__ tile_wrest) {
   __shared__ uint64_t w_rec[kWin];  // one window of the grouped output
+  __shared__ float w_log[kWin];
   __shared__ __attribute__((aligned(16))) uint32_t s_spl[kMaxB];
   __shared__ int s_off[kMaxB + 1];  // histogram, then tile-local bucket offsets
   __shared__ __attribute__((aligned(16))) uint16_t s_lut[kBins];
@@ -454,10 +458,11 @@ void k_tile(const float* __restrict__ logits, int64_t bstride, int32_t E,
   const uint32_t bg = (uint32_t)(sample_base + b);
   const int nb = nb_[b];
   // splitter tables (consumed only after the keys; their latency hides behind the Philox work)
-  static_assert(kBins * 2 == kGrpNT * 16 && kMaxB * 4 == kGrpNT * 16, "prologue vector widths");
-  reinterpret_cast<uint4*>(s_lut)[tid] = reinterpret_cast<const uint4*>(lut_ + (int64_t)b * kBins)[tid];
-  if (tid * 4 < nb - 1)
-    reinterpret_cast<uint4*>(s_spl)[tid] = reinterpret_cast<const uint4*>(spl_ + (int64_t)b * kMaxB)[tid];
+  static_assert(kBins * 2 == 512 * 16 && kMaxB * 4 == 512 * 16 && kGrpNT >= 1024, "prologue vector widths");
+  if (tid < 512)
+    reinterpret_cast<uint4*>(s_lut)[tid] = reinterpret_cast<const uint4*>(lut_ + (int64_t)b * kBins)[tid];
+  else if ((tid - 512) * 4 < nb - 1)
+    reinterpret_cast<uint4*>(s_spl)[tid - 512] = reinterpret_cast<const uint4*>(spl_ + (int64_t)b * kMaxB)[tid - 512];
   for (int k = tid; k < nb; k += kGrpNT) s_off[k] = 0;
   if (tid == 0) s_tk = terminal_key(lg, E, bg, st0, st1, seed0, seed1);
   const uint32_t lmn = lut_base[2 * b];
@@ -470,12 +475,13 @@ void k_tile(const float* __restrict__ logits, int64_t bstride, int32_t E,
   const float tk = s_tk;
   // group g covers actions a_t + g * (4 * kGrpNT) + 4 * tid + 0..3 (coalesced float4 logits)
   uint32_t ord[4 * kTileG];
+  float lvk[4 * kTileG];  // the logits stay in registers for the grouped logit stream
   uint32_t win = 0;  // bit 4g + s: action a_t + g * 4 * kGrpNT + 4 * tid + s is a winner
   double wr = 0.0;
 #pragma unroll
   for (int g = 0; g < kTileG; ++g) {
     const int a0 = a_t + g * 4 * kGrpNT + 4 * tid;
-    float lv[4];
+    float* lv = lvk + 4 * g;
     if (al16 && a0 + 3 < E) {
       const float4 v = *reinterpret_cast<const float4*>(lg + a0);
       lv[0] = v.x;
@@ -579,33 +585,15 @@ void k_tile(const float* __restrict__ logits, int64_t bstride, int32_t E,
       if ((unsigned)p < (unsigned)kWin) {  // (non-winners carry 0xFFFF, beyond every window)
         const int a = a_t + (q >> 2) * 4 * kGrpNT + 4 * tv + (q & 3);
         w_rec[p] = ((uint64_t)(~ord[q]) << 32) | (uint32_t)a;
+        w_log[p] = lvk[q];
       }
     }
     __syncthreads();
     PROF(4)
     const int cnt = min(kWin, tot - w0);
-    // the logits are re-read here (L2-resident; every gather of the window in flight at once):
-    // keeping 32 logits per thread live through the phases above would cost occupancy
-    constexpr int kWU = 4;  // gathers in flight per thread
-#pragma unroll 1
-    for (int e0 = 0; e0 < cnt; e0 += kWU * kGrpNT) {
-      uint64_t rv[kWU];
-      float lw[kWU];
-#pragma unroll
-      for (int u = 0; u < kWU; ++u) {
-        const int e = e0 + u * kGrpNT + tid;
-        rv[u] = e < cnt ? w_rec[e] : 0ull;
-      }
-#pragma unroll
-      for (int u = 0; u < kWU; ++u) lw[u] = e0 + u * kGrpNT + tid < cnt ? lg[(uint32_t)rv[u]] : 0.0f;
-#pragma unroll
-      for (int u = 0; u < kWU; ++u) {
-        const int e = e0 + u * kGrpNT + tid;
-        if (e < cnt) {
-          st[w0 + e] = rv[u];
-          sl[w0 + e] = lw[u];
-        }
-      }
+    for (int e = tid; e < cnt; e += kGrpNT) {
+      st[w0 + e] = w_rec[e];
+      sl[w0 + e] = w_log[e];
     }
     __syncthreads();
     PROF(5)

@@ -30,39 +30,70 @@ __device__ __forceinline__ uint32_t pick_word(const uint4& r, int s) {
 }
 
 // Deterministic ln(x) for positive normal fp32 x: bit-exact with oracle.det_logf.
-// Only separately rounded fp32 multiplies/adds (contraction disabled), so the
-// result does not depend on the compiler's FMA choices.
-__device__ __forceinline__ float det_logf(float x) {
-#pragma clang fp contract(off)
-  uint32_t bits = __float_as_uint(x);
+// Horner in single-rounded fp32 FMAs (IEEE fmaf; the oracle emulates it exactly) and no
+// other contraction, so the result never depends on the compiler's choices.
+constexpr uint32_t kLogC[9] = {0x3f800000u, 0xbefffffcu, 0x3eaaabc8u, 0xbe8002d3u, 0x3e4c5c05u,
+                               0xbe2994dfu, 0x3e191428u, 0xbe13394fu, 0x3db31375u};
+__device__ __forceinline__ void log_reduce(float x, float& t, float& ef) {
+  const uint32_t bits = __float_as_uint(x);
   int e = (int)(bits >> 23) - 127;
   uint32_t mb = (bits & 0x7FFFFFu) | 0x3F800000u;
   if (mb > 0x3FB504F3u) {
     mb -= 0x00800000u;
     e += 1;
   }
-  const float t = __uint_as_float(mb) - 1.0f;
-  float p = __uint_as_float(0x3db31375u);
-  p = p * t + __uint_as_float(0xbe13394fu);
-  p = p * t + __uint_as_float(0x3e191428u);
-  p = p * t + __uint_as_float(0xbe2994dfu);
-  p = p * t + __uint_as_float(0x3e4c5c05u);
-  p = p * t + __uint_as_float(0xbe8002d3u);
-  p = p * t + __uint_as_float(0x3eaaabc8u);
-  p = p * t + __uint_as_float(0xbefffffcu);
-  p = p * t + __uint_as_float(0x3f800000u);
+  t = __uint_as_float(mb) - 1.0f;  // exact
+  ef = (float)e;
+}
+__device__ __forceinline__ float det_logf(float x) {
+#pragma clang fp contract(off)
+  float t, ef;
+  log_reduce(x, t, ef);
+  float p = __uint_as_float(kLogC[8]);
+#pragma unroll
+  for (int i = 7; i >= 0; --i) p = __builtin_fmaf(p, t, __uint_as_float(kLogC[i]));
   p = p * t;
-  return (float)e * __uint_as_float(0x3f317218u) + p;
+  return __builtin_fmaf(ef, __uint_as_float(0x3f317218u), p);
+}
+
+// Two logs at once: the polynomial runs on packed fp32 (v_pk_fma_f32 / v_pk_mul_f32),
+// bit-identical to two det_logf calls.
+typedef float spai_f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ spai_f2 det_logf2(spai_f2 x) {
+#pragma clang fp contract(off)
+  float t0, t1, e0, e1;
+  log_reduce(x.x, t0, e0);
+  log_reduce(x.y, t1, e1);
+  const spai_f2 t = (spai_f2){t0, t1}, ef = (spai_f2){e0, e1};
+  spai_f2 p = (spai_f2){__uint_as_float(kLogC[8]), __uint_as_float(kLogC[8])};
+#pragma unroll
+  for (int i = 7; i >= 0; --i) {
+    const float c = __uint_as_float(kLogC[i]);
+    p = __builtin_elementwise_fma(p, t, (spai_f2){c, c});
+  }
+  p = p * t;
+  const float l2 = __uint_as_float(0x3f317218u);
+  return __builtin_elementwise_fma(ef, (spai_f2){l2, l2}, p);
 }
 
 // key = l - ln(-ln u), u = (2*(word >> 9) + 1) * 2^-24 (exact), canonical +0.
-__device__ __forceinline__ float gumbel_key(float logit, uint32_t word) {
+__device__ __forceinline__ float gumbel_u(uint32_t word) {
 #pragma clang fp contract(off)
   const uint32_t k = word >> 9;
-  const float u = (2.0f * (float)k + 1.0f) * 5.9604644775390625e-08f;
-  const float q = -det_logf(u);
+  return (2.0f * (float)k + 1.0f) * 5.9604644775390625e-08f;
+}
+__device__ __forceinline__ float gumbel_key(float logit, uint32_t word) {
+#pragma clang fp contract(off)
+  const float q = -det_logf(gumbel_u(word));
   const float key = logit - det_logf(q);
   return key + 0.0f;
+}
+// keys of two actions (words w0, w1) with the packed log
+__device__ __forceinline__ spai_f2 gumbel_key2(spai_f2 logit, uint32_t w0, uint32_t w1) {
+#pragma clang fp contract(off)
+  const spai_f2 q = -det_logf2((spai_f2){gumbel_u(w0), gumbel_u(w1)});
+  const spai_f2 key = logit - det_logf2(q);
+  return key + (spai_f2){0.0f, 0.0f};
 }
 
 // Monotone map float -> uint32 (larger float => larger uint).

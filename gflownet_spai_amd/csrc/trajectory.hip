@@ -493,12 +493,15 @@ void k_tile(const float* __restrict__ logits, int64_t bstride, int32_t E,
       for (int s = 0; s < 4; ++s) lv[s] = a0 + s < E ? lg[a0 + s] : 0.0f;
     }
     const uint4 rr = philox4x32_10((uint32_t)a0 >> 2, bg, st0, st1, seed0, seed1);
+    const spai_f2 k01 = gumbel_key2((spai_f2){lv[0], lv[1]}, rr.x, rr.y);
+    const spai_f2 k23 = gumbel_key2((spai_f2){lv[2], lv[3]}, rr.z, rr.w);
+    const float keys[4] = {k01.x, k01.y, k23.x, k23.y};
     uint32_t nib = 0;
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       ord[4 * g + s] = 0u;
       if (a0 + s < E) {
-        const float key = gumbel_key(lv[s], pick_word(rr, s));
+        const float key = keys[s];
         if (key > tk) {
           nib |= 1u << s;
           ord[4 * g + s] = orderable(key);

@@ -172,13 +172,37 @@ _LOG_C = np.array([0x3f800000, 0xbefffffc, 0x3eaaabc8, 0xbe8002d3, 0x3e4c5c05,
 _LN2F = np.array([0x3f317218], np.uint32).view(np.float32)[0]
 
 
+def fma32(a, b, c):
+    """IEEE single-rounded fp32 fused multiply-add, elementwise (the device's v_fma_f32 /
+    v_pk_fma_f32 and C fmaf).  a*b is exact in fp64; the fp64 sum s = a*b + c is rounded
+    once, and rounding s to fp32 can only differ from rounding the exact sum when s lands
+    exactly on a midpoint between two fp32 values - the exact TwoSum error of s then
+    decides the side."""
+    a = np.asarray(a, np.float32)
+    b = np.asarray(b, np.float32)
+    c = np.asarray(c, np.float32)
+    p = a.astype(np.float64) * b.astype(np.float64)
+    c64 = c.astype(np.float64)
+    s = p + c64
+    bb = s - p
+    err = (p - (s - bb)) + (c64 - bb)
+    r = s.astype(np.float32)
+    d = s - r.astype(np.float64)
+    # neighbour of r on the side of s, and the midpoint between them (exact in fp64)
+    n = np.nextafter(r, np.where(d > 0, np.float32(np.inf), np.float32(-np.inf))).astype(np.float32)
+    mid = (r.astype(np.float64) + n.astype(np.float64)) * 0.5
+    fix = (d != 0) & (s == mid) & (err != 0) & (np.sign(err) == np.sign(d))
+    return np.where(fix, n, r).astype(np.float32)
+
+
 def det_logf(x):
     """Deterministic natural log of positive normal float32 values.
 
     Exponent/mantissa split by bit operations, m in [sqrt(.5), sqrt(2)), t = m - 1
-    (exact), ln(1+t) = t * Q(t) with a degree-8 Q evaluated by Horner using only
-    separately rounded fp32 multiplies and adds (no FMA), then e*ln2 + that.
-    The HIP kernel (rollout.hip: det_logf) performs the identical op sequence.
+    (exact), ln(1+t) = t * Q(t) with a degree-8 Q evaluated by Horner in single-rounded
+    fp32 FMAs, then fma(e, ln2, t * Q).  The HIP kernels (spai_device.h: det_logf /
+    det_logf2, the latter two lanes per packed v_pk_fma_f32) perform the identical op
+    sequence.
     """
     x = np.asarray(x, np.float32)
     bits = x.view(np.uint32)
@@ -190,10 +214,9 @@ def det_logf(x):
     t = mb.view(np.float32) - np.float32(1.0)
     p = np.full_like(t, _LOG_C[8])
     for c in _LOG_C[7::-1]:
-        p = p * t
-        p = p + c
+        p = fma32(p, t, c)
     p = p * t
-    return e.astype(np.float32) * _LN2F + p
+    return fma32(e.astype(np.float32), _LN2F, p)
 
 
 def gumbel_keys(logits, b_global, seed, stream):

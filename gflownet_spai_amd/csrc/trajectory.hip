@@ -451,7 +451,6 @@ void k_tile(const float* __restrict__ logits, int64_t bstride, int32_t E,
   __shared__ __attribute__((aligned(16))) uint16_t s_lut[kBins];
   __shared__ int s_wc[kGrpNT / 64];
   __shared__ double s_wr[kGrpNT / 64];
-  __shared__ float s_tk;
   const int b = blockIdx.y, tile = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   PROF_INIT
   const float* lg = logits + (int64_t)b * bstride;
@@ -464,20 +463,14 @@ void k_tile(const float* __restrict__ logits, int64_t bstride, int32_t E,
   else if ((tid - 512) * 4 < nb - 1)
     reinterpret_cast<uint4*>(s_spl)[tid - 512] = reinterpret_cast<const uint4*>(spl_ + (int64_t)b * kMaxB)[tid - 512];
   for (int k = tid; k < nb; k += kGrpNT) s_off[k] = 0;
-  if (tid == 0) s_tk = terminal_key(lg, E, bg, st0, st1, seed0, seed1);
   const uint32_t lmn = lut_base[2 * b];
   const int lsh = (int)lut_base[2 * b + 1];
   const float lm = lmax[b];
   const int a_t = tile * kTile;  // first action of the tile
   const bool al16 = (reinterpret_cast<uintptr_t>(lg) & 15u) == 0;  // rows of E+1 floats need not be
-  __syncthreads();  // s_tk
-  PROF(0)
-  const float tk = s_tk;
-  // group g covers actions a_t + g * (4 * kGrpNT) + 4 * tid + 0..3 (coalesced float4 logits)
-  uint32_t ord[4 * kTileG];
+  // all logits of the thread in flight at once (group g: actions a_t + g * (4 * kGrpNT) +
+  // 4 * tid + 0..3, coalesced float4); no barrier before the keys
   float lvk[4 * kTileG];  // the logits stay in registers for the grouped logit stream
-  uint32_t win = 0;  // bit 4g + s: action a_t + g * 4 * kGrpNT + 4 * tid + s is a winner
-  double wr = 0.0;
 #pragma unroll
   for (int g = 0; g < kTileG; ++g) {
     const int a0 = a_t + g * 4 * kGrpNT + 4 * tid;
@@ -492,6 +485,17 @@ void k_tile(const float* __restrict__ logits, int64_t bstride, int32_t E,
 #pragma unroll
       for (int s = 0; s < 4; ++s) lv[s] = a0 + s < E ? lg[a0 + s] : 0.0f;
     }
+  }
+  // the terminal's key, redundantly per thread (one Philox call) instead of a barrier
+  const float tk = terminal_key(lg, E, bg, st0, st1, seed0, seed1);
+  PROF(0)
+  uint32_t ord[4 * kTileG];
+  uint32_t win = 0;  // bit 4g + s: action a_t + g * 4 * kGrpNT + 4 * tid + s is a winner
+  double wr = 0.0;
+#pragma unroll
+  for (int g = 0; g < kTileG; ++g) {
+    const int a0 = a_t + g * 4 * kGrpNT + 4 * tid;
+    const float* lv = lvk + 4 * g;
     const uint4 rr = philox4x32_10((uint32_t)a0 >> 2, bg, st0, st1, seed0, seed1);
     const spai_f2 k01 = gumbel_key2((spai_f2){lv[0], lv[1]}, rr.x, rr.y);
     const spai_f2 k23 = gumbel_key2((spai_f2){lv[2], lv[3]}, rr.z, rr.w);
@@ -521,6 +525,7 @@ void k_tile(const float* __restrict__ logits, int64_t bstride, int32_t E,
   }
   wr = wave_sum(wr);
   if (lane == 0) s_wr[wave] = wr;
+  __syncthreads();  // splitter tables, zeroed histogram
   PROF(1)
   // bucket histogram of the winners; each winner keeps its bucket and its rank inside the
   // bucket (the histogram atomic's return; any order: the level-2 sort orders buckets fully)

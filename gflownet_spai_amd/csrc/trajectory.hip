@@ -11,7 +11,7 @@
 //                (1.2 % of the Philox work at C4); winners kept in subset order.
 //   k_splitters  per sample: value-linear histogram quantiles of the sampled winner keys
 //                -> nb ~ est/4096 bucket splitters and a 4096-bin bucket lookup table.
-//   k_tile       one 16384-action tile of one sample per block: Philox4x32-10 +
+//   k_tile       one kTile (16384)-action tile of one sample per block: Philox4x32-10 +
 //                deterministic fp32 keys (in registers), removal bitmap words, the fp64
 //                mass of the untouched actions, bucket histogram with in-bucket ranks, and
 //                the tile's winners written grouped by bucket through LDS windows as one
@@ -34,9 +34,15 @@
 namespace spai {
 namespace {
 
-constexpr int kTile = 16384;               // actions per tile (k_tile block; a run per bucket)
+#ifndef KTILE
+#define KTILE 16384
+#endif
+constexpr int kTile = KTILE;               // actions per tile (k_tile block; a run per bucket)
 static_assert(kTile <= 65535, "run offsets and counts are packed in 16 bits (k_tile, k_runs)");
-constexpr int kGrpNT = 1024;               // threads of a k_tile block (16 actions each)
+#ifndef KGRPNT
+#define KGRPNT 1024
+#endif
+constexpr int kGrpNT = KGRPNT;             // threads of a k_tile block (16 actions each)
 #ifndef KWIN
 #define KWIN 8192
 #endif
@@ -49,7 +55,7 @@ constexpr int kMaxB = 2048;                // buckets per sample (11 bits in the
 constexpr int kCap2 = 8192;               // LDS capacity of k_sort2 (records per bucket)
 constexpr int kMaxSub = 4096;              // value sub-buckets per bucket in k_sort2
 constexpr int kSortNT = 1024;
-constexpr int kMaxTiles = 2048;            // E <= 33.5M actions
+constexpr int kMaxTiles = 2048;            // E <= kMaxTiles * kTile actions
 constexpr int kFinNT = 256;
 constexpr int kMaxSamples = 1024;          // B per rollout call
 constexpr int kBins = 4096;                // splitter histogram / bucket lookup table bins
@@ -457,11 +463,14 @@ void k_tile(const float* __restrict__ logits, int64_t bstride, int32_t E,
   const uint32_t bg = (uint32_t)(sample_base + b);
   const int nb = nb_[b];
   // splitter tables (consumed only after the keys; their latency hides behind the Philox work)
-  static_assert(kBins * 2 == 512 * 16 && kMaxB * 4 == 512 * 16 && kGrpNT >= 1024, "prologue vector widths");
-  if (tid < 512)
-    reinterpret_cast<uint4*>(s_lut)[tid] = reinterpret_cast<const uint4*>(lut_ + (int64_t)b * kBins)[tid];
-  else if ((tid - 512) * 4 < nb - 1)
-    reinterpret_cast<uint4*>(s_spl)[tid - 512] = reinterpret_cast<const uint4*>(spl_ + (int64_t)b * kMaxB)[tid - 512];
+  static_assert(kBins * 2 == 512 * 16 && kMaxB * 4 == 512 * 16 && kGrpNT % 512 == 0 || kGrpNT == 512,
+                "prologue vector widths");
+  for (int i = tid; i < 1024; i += kGrpNT) {
+    if (i < 512)
+      reinterpret_cast<uint4*>(s_lut)[i] = reinterpret_cast<const uint4*>(lut_ + (int64_t)b * kBins)[i];
+    else if ((i - 512) * 4 < nb - 1)
+      reinterpret_cast<uint4*>(s_spl)[i - 512] = reinterpret_cast<const uint4*>(spl_ + (int64_t)b * kMaxB)[i - 512];
+  }
   for (int k = tid; k < nb; k += kGrpNT) s_off[k] = 0;
   const uint32_t lmn = lut_base[2 * b];
   const int lsh = (int)lut_base[2 * b + 1];

@@ -1,7 +1,8 @@
 """Benchmark of the SPAI-via-GFlowNet hot path on MI355X (BASELINE.json metric).
 
 One step = one ``GFlowNet.sample_states`` call over a batch of B candidate preconditioners
-of the 1024^2 5-point Poisson matrix (config C4, fp32): throughput rollout (Gumbel-top-k,
+of the 1024^2 5-point Poisson matrix (config C4, fp32): ForwardPolicy logits (GATv2 x2 +
+mean pool + fc on the state graph, random-init weights), throughput rollout (Gumbel-top-k,
 20 % expected removal, ordered trajectory log + forward probabilities), least-squares fill
 of M (column SPAI) and the ||A M - I||_F reward, all inputs resident in HBM.
 columns/s = (B * N * world) / step time (max over ranks).  Multi-GPU: one process per
@@ -43,17 +44,26 @@ def terminal_logit(logits: np.ndarray, frac: float) -> float:
     return 0.5 * (lo + hi)
 
 
-class SyntheticLogits(torch.nn.Module):
-    """Fixed synthetic policy output (seeded N(0,1) logits, terminal logit
-    set for 20 % expected removal); same call contract as ForwardPolicy.logits."""
+def make_policy(env, A, dev, hid: int = 4):
+    """Random-init ForwardPolicy of the reference's architecture (policy.py:24-33:
+    node_features=-1, hidden_dim=4 as GFlowNet100.py:178-181), seeded; the terminal row's
+    fc bias is then set so the expected removed fraction is 20 %, so the
+    sampler's workload matches the configured one.  The policy runs inside every step."""
+    from gflownet_spai_amd import ForwardPolicy
+    from gflownet_spai_amd.preconditioner import Data
 
-    def __init__(self, logits: torch.Tensor):
-        super().__init__()
-        self.register_buffer("l", logits)
-        self.a = torch.tensor(0.5, device=logits.device)
-
-    def logits(self, data):
-        return self.l, self.a
+    torch.manual_seed(123)
+    E = env.num_actions - 1
+    pol = ForwardPolicy(-1, hid, E + 1).to(dev)
+    n = env.matrix_size
+    data = Data(x=torch.ones(2 * n, 1, device=dev), edge_index=A._indices().to(dev),
+                edge_attr=A._values().float().to(dev))
+    with torch.no_grad():
+        lg, _ = pol.logits(data)
+        lg = lg.reshape(-1).double().cpu().numpy()
+        pol.fc.bias[E] += terminal_logit(lg[:E], 0.2) - lg[E]
+    pol.requires_grad_(False)  # sampling only: no autograd bookkeeping in the step
+    return pol
 
 
 def fill_bytes(env, B, store_m: bool = True) -> float:
@@ -86,8 +96,9 @@ def measured_traffic(cfg: str, B: int, overlap: bool):
     return None
 
 
-def cpu_baseline(cfg, B, budget_s: float):
-    """The oracle (numpy, single thread) on a bounded sample of the same workload."""
+def cpu_baseline(cfg, B, budget_s: float, logits=None):
+    """The oracle (numpy, single thread) on a bounded sample of the same workload (the
+    policy's logits are taken as given: the CPU leg times the rollout, fill and residual)."""
     from oracle import spai_oracle as O
     import scipy.sparse as sp
 
@@ -95,8 +106,9 @@ def cpu_baseline(cfg, B, budget_s: float):
     npd = np.float32 if dtype == torch.float32 else np.float64
     r, c, v, n = O.poisson2d(grid, npd) if dims == 2 else O.poisson3d(grid, npd)
     E = len(r)
-    logits = torch.randn(E + 1, generator=torch.Generator().manual_seed(123)).numpy()
-    logits[E] = terminal_logit(logits[:E], 0.2)
+    if logits is None:
+        logits = torch.randn(E + 1, generator=torch.Generator().manual_seed(123)).numpy()
+        logits[E] = terminal_logit(logits[:E], 0.2)
     t0 = time.perf_counter()
     removed, actions, fwd, counts = O.throughput_rollout(logits, 1, seed=1234, stream=0)
     t_roll = time.perf_counter() - t0
@@ -121,8 +133,9 @@ def cpu_baseline(cfg, B, budget_s: float):
     per_col = t_fill / done
     t_sample = t_roll + per_col * n  # one candidate over all N columns
     return {"value": n / t_sample, "unit": "columns/s", "cores": 1, "kind": "port",
-            "sample": f"oracle/spai_oracle.py (numpy): 1 full rollout over E={E} ({t_roll:.2f}s) + LSQ fill and "
-                      f"||AM-I|| over the first {done} of {n} columns ({t_fill:.2f}s), extrapolated to N columns"}
+            "sample": f"oracle/spai_oracle.py (numpy): 1 full rollout over E={E} ({t_roll:.2f}s, the bench policy's "
+                      f"logits given) + LSQ fill and ||AM-I|| over the first {done} of {n} columns ({t_fill:.2f}s), "
+                      f"extrapolated to N columns; policy forward not included"}
 
 
 def main():
@@ -154,11 +167,8 @@ def main():
     n = A.shape[0]
     env = PreconditionerEnv(n, A, A, side="AM", fill="lsq", keep_m=True, device=dev)
     E = env.num_actions - 1
-    g = torch.Generator().manual_seed(123)
-    logits = torch.randn(E + 1, generator=g)
-    logits[E] = terminal_logit(logits[:E].numpy(), 0.2)
     B = args.batch
-    model = GFlowNet(SyntheticLogits(logits.to(dev)), None, env, mode="throughput", seed=1234, sample_base=rank * B,
+    model = GFlowNet(make_policy(env, A, dev), None, env, mode="throughput", seed=1234, sample_base=rank * B,
                      overlap=not args.no_overlap)
     s0 = [A] * B
 
@@ -206,8 +216,10 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32 storage, f64 solve/accumulate",
-            "data": "synthetic (seeded N(0,1) policy logits, 20% expected removal; Poisson matrix from its stencil)",
-            "config": {"workload": text + f", B={B} candidates per GPU: throughput rollout + LSQ fill + ||AM-I||_F",
+            "data": "synthetic (random-init seeded ForwardPolicy GATv2x2+fc, hid=4, evaluated on the state graph in "
+                    "every step; terminal fc bias set for 20% expected removal; Poisson matrix from its stencil)",
+            "config": {"workload": text + f", B={B} candidates per GPU: ForwardPolicy logits + throughput rollout + "
+                                        "LSQ fill + ||AM-I||_F",
                        "N": n, "E": E, "global_batch": B * world, "parallelism": f"candidates sharded x{world}"},
             "final_residual_fro": float(res[0]),
             "final_residual_fro_mean": float(res.mean()),
@@ -219,7 +231,9 @@ def main():
                          "traffic": traffic, "bytes_per_launch": fb, "avg_launch_ms": fill_ms},
         }
         if not args.no_cpu_baseline and world == 1:
-            out["cpu_baseline"] = cpu_baseline(args.config, B, args.cpu_budget)
+            with torch.no_grad():
+                lg_host = model.forward_policy.logits(model.state_to_data(s0[:1])[0])[0].reshape(-1).cpu().numpy()
+            out["cpu_baseline"] = cpu_baseline(args.config, B, args.cpu_budget, lg_host)
         print(json.dumps(out), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()

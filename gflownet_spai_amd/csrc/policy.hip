@@ -1,0 +1,449 @@
+// ForwardPolicy logits for gfx950 (reference: policy.py:14-73, BasePolicy + ForwardPolicy):
+//     logits = fc(mean_pool(relu(GATv2_2(relu(GATv2_1(x))))))[:E+1]
+// with the GATv2Conv semantics of PyG (heads 4 then 1, edge_dim 1, negative slope 0.2,
+// self loops replaced by loops whose attribute is the mean of the node's incoming
+// attributes, softmax over each target's incoming edges, concat heads, + bias):
+//     s_ij^h   = att_h . leaky_relu(W_l x_j + W_r x_i + W_e a_ij)_h
+//     alpha_ij = softmax_j(s_ij^h)            (over the incoming edges of target i)
+//     out_i^h  = sum_j alpha_ij^h (W_l x_j + b_l)_h + bias_h
+// The graph arrives as a CSR by target with the self loops already in place (built once
+// per state graph by the host, gflownet_spai_amd/policy.py), so each target's softmax is
+// a single pass over its row with an online (running max) normaliser.
+//
+//   k_gat1  one thread per node (hid <= 8; else per (node, head), 4 lanes per node):
+//           layer-1 attention in registers; epilogue relu + the layer-2 input transforms
+//           W_l2 h, W_r2 h (per-head partial products summed across a node's lanes in a
+//           fixed order) -> [n][2*hid] fp32.
+//   k_gat2  one thread per node: layer-2 attention over the gathered W_l2 h_j rows; epilogue
+//           relu + the block's fp64 pooled sum.  k_pool sums the block partials in block
+//           order (deterministic) into h = mean.
+//   k_fc    one thread per action: logit_a = b_a + W_a . h (W row-major [actions][hid],
+//           16-byte loads), the block max; k_max writes lmax.
+// Cross-block reductions are separate one-block kernels, not last-block-done counters: on
+// gfx950 a device-scope fence writes back the XCD's L2, which costs far more than a launch.
+// Every kernel is bound by HBM / L2 gathers; the only products are hid-wide dot products
+// per node or action (K <= 128, M = 1 for the fc), so there is no MFMA tile to fill.
+#include "spai_device.h"
+#include "spai_status.h"
+
+namespace spai {
+namespace {
+
+constexpr int kNT = 256;
+constexpr int kH1 = 4;  // BasePolicy.in_head (policy.py:20)
+
+// Offsets of the packed GATv2 parameter blocks (host packs them in this order):
+//   W_l [HC][F], b_l [HC], W_r [HC][F], b_r [HC], W_e [HC], att [HC], bias [HC]
+__host__ __device__ constexpr int gat_params(int HC, int F) { return 2 * HC * F + 5 * HC; }
+
+__device__ __forceinline__ float leaky(float v) { return v > 0.0f ? v : 0.2f * v; }
+
+constexpr int kEdgeChunk = 8;  // edges of one target whose loads are issued together
+constexpr int kRedNT = 1024;   // one-block reductions
+
+// Online softmax step: fold score s with value row v[0..C) into (m, den, acc).
+template <int C>
+__device__ __forceinline__ void online_step(float s, const float* v, float& m, float& den, float* acc) {
+  if (s > m) {  // rescale what was accumulated under the old maximum
+    const float r = __expf(m - s);
+    den = fmaf(den, r, 1.0f);
+#pragma unroll
+    for (int c = 0; c < C; ++c) acc[c] = fmaf(acc[c], r, v[c]);
+    m = s;
+  } else {
+    const float p = __expf(s - m);
+    den += p;
+#pragma unroll
+    for (int c = 0; c < C; ++c) acc[c] = fmaf(p, v[c], acc[c]);
+  }
+}
+
+// Layer 1.  HPT heads per thread (4 for hid <= 8: one thread per node; 1 above: one thread
+// per (node, head), the node's 4 lanes adjacent).  Per target: the edge ids, attributes
+// and source features of up to kEdgeChunk edges are loaded before any is used (one memory
+// round trip per chunk instead of three per edge).
+template <int F, int C, int HPT>
+__global__ __launch_bounds__(kNT) void k_gat1(int32_t n, const float* __restrict__ x, const int32_t* __restrict__ rp,
+                                              const int32_t* __restrict__ src, const float* __restrict__ ea,
+                                              const float* __restrict__ p1, const float* __restrict__ p2,
+                                              float* __restrict__ xlr2) {
+  constexpr int HC = kH1 * C;  // layer-1 width (heads concatenated)
+  constexpr int P1 = gat_params(HC, F);
+  constexpr int L = kH1 / HPT;  // lanes per node
+  constexpr int W2 = 2 * C * HC + 2 * C;  // W_l2, b_l2, W_r2, b_r2
+  __shared__ float s1[P1];
+  __shared__ float s2[W2];
+  for (int i = threadIdx.x; i < P1; i += kNT) s1[i] = p1[i];
+  for (int i = threadIdx.x; i < W2; i += kNT) s2[i] = p2[i];
+  __syncthreads();
+  const float* Wl = s1;
+  const float* bl = Wl + HC * F;
+  const float* Wr = bl + HC;
+  const float* br = Wr + HC * F;
+  const float* We = br + HC;
+  const float* att = We + HC;
+  const float* bias = att + HC;
+
+  const int64_t t = (int64_t)blockIdx.x * kNT + threadIdx.x;
+  const int node = (int)(t / L), lane_h = (int)(t % L);
+  const int hb = lane_h * HPT;  // first head of this thread
+  const bool live = node < n;
+  const int i = live ? node : n - 1;
+  const int e0 = rp[i], e1 = rp[i + 1];
+  float xi[F];
+#pragma unroll
+  for (int f = 0; f < F; ++f) xi[f] = x[(int64_t)i * F + f];
+  float xr[HPT][C], acc[HPT][C], m[HPT], den[HPT];
+#pragma unroll
+  for (int q = 0; q < HPT; ++q) {
+    m[q] = -INFINITY;
+    den[q] = 0.0f;
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      const int o = (hb + q) * C + c;
+      float v = br[o];
+#pragma unroll
+      for (int f = 0; f < F; ++f) v = fmaf(Wr[o * F + f], xi[f], v);
+      xr[q][c] = v;
+      acc[q][c] = 0.0f;
+    }
+  }
+  for (int eb = e0; eb < e1; eb += kEdgeChunk) {
+    int js[kEdgeChunk];
+    float as[kEdgeChunk], xj[kEdgeChunk][F];
+#pragma unroll
+    for (int k = 0; k < kEdgeChunk; ++k) {
+      const int e = min(eb + k, e1 - 1);  // clamped: every load is in bounds, extras unused
+      js[k] = src[e];
+      as[k] = ea[e];
+    }
+#pragma unroll
+    for (int k = 0; k < kEdgeChunk; ++k)
+#pragma unroll
+      for (int f = 0; f < F; ++f) xj[k][f] = x[(int64_t)js[k] * F + f];
+#pragma unroll
+    for (int k = 0; k < kEdgeChunk; ++k) {
+      if (eb + k >= e1) break;
+#pragma unroll
+      for (int q = 0; q < HPT; ++q) {
+        float xl[C], sc = 0.0f;
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+          const int o = (hb + q) * C + c;
+          float v = bl[o];
+#pragma unroll
+          for (int f = 0; f < F; ++f) v = fmaf(Wl[o * F + f], xj[k][f], v);
+          xl[c] = v;
+          sc = fmaf(att[o], leaky(v + xr[q][c] + We[o] * as[k]), sc);
+        }
+        online_step<C>(sc, xl, m[q], den[q], acc[q]);
+      }
+    }
+  }
+  // epilogue: relu(out) of this thread's heads, then its slice of W_l2 h1 and W_r2 h1
+  const float* Wl2 = s2;
+  const float* bl2 = Wl2 + C * HC;
+  const float* Wr2 = bl2 + C;
+  const float* br2 = Wr2 + C * HC;
+  float out[2 * C];
+#pragma unroll
+  for (int o = 0; o < 2 * C; ++o) out[o] = 0.0f;
+#pragma unroll
+  for (int q = 0; q < HPT; ++q) {
+    const float inv = den[q] > 0.0f ? 1.0f / den[q] : 0.0f;  // no incoming edge: out = bias (PyG)
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      const int k = (hb + q) * C + c;
+      const float h1 = fmaxf(fmaf(acc[q][c], inv, bias[k]), 0.0f);
+#pragma unroll
+      for (int o = 0; o < C; ++o) {
+        out[o] = fmaf(Wl2[o * HC + k], h1, out[o]);
+        out[C + o] = fmaf(Wr2[o * HC + k], h1, out[C + o]);
+      }
+    }
+  }
+  if constexpr (L == 4) {
+    // sum over the node's 4 lanes by xor shuffles, (h0+h1)+(h2+h3) in every lane
+#pragma unroll
+    for (int k = 0; k < 2 * C; ++k) {
+      const float a1 = __shfl_xor(out[k], 1, kWave);
+      const float lo = (lane_h & 1) ? a1 + out[k] : out[k] + a1;
+      const float a2 = __shfl_xor(lo, 2, kWave);
+      out[k] = (lane_h & 2) ? a2 + lo : lo + a2;
+    }
+  }
+  if (live) {
+    float* dst = xlr2 + (int64_t)node * 2 * C;
+    constexpr int per = 2 * C / L;  // components written by each lane of the node
+#pragma unroll
+    for (int k = 0; k < 2 * C; ++k)
+      if (k / per == lane_h) dst[k] = out[k] + (k < C ? bl2[k] : br2[k - C]);
+  }
+}
+
+// Layer 2 (one head), one thread per node: gathered W_l2 h_j rows (C floats, 16-byte
+// loads), chunked like layer 1; epilogue relu + the block's fp64 pooled sum.
+template <int C>
+__global__ __launch_bounds__(kNT) void k_gat2(int32_t n, const int32_t* __restrict__ rp,
+                                              const int32_t* __restrict__ src, const float* __restrict__ ea,
+                                              const float* __restrict__ p2, const float* __restrict__ xlr2,
+                                              double* __restrict__ part) {
+  constexpr int HC = kH1 * C;
+  constexpr int CH = C <= 8 ? kEdgeChunk : 4;  // gathered rows held in registers per chunk
+  const float* We = p2 + 2 * C * HC + 2 * C;
+  const float* att = We + C;
+  const float* bias = att + C;
+  const int node = blockIdx.x * kNT + threadIdx.x;
+  const bool live = node < n;
+  const int i = live ? node : n - 1;
+  const int e0 = rp[i], e1 = rp[i + 1];
+  float xr[C], acc[C];
+#pragma unroll
+  for (int c4 = 0; c4 < C / 4; ++c4) {
+    const float4 v = reinterpret_cast<const float4*>(xlr2 + (int64_t)i * 2 * C + C)[c4];
+    xr[4 * c4] = v.x;
+    xr[4 * c4 + 1] = v.y;
+    xr[4 * c4 + 2] = v.z;
+    xr[4 * c4 + 3] = v.w;
+  }
+#pragma unroll
+  for (int c = 0; c < C; ++c) acc[c] = 0.0f;
+  float m = -INFINITY, den = 0.0f;
+  for (int eb = e0; eb < e1; eb += CH) {
+    int js[CH];
+    float as[CH], xl[CH][C];
+#pragma unroll
+    for (int k = 0; k < CH; ++k) {
+      const int e = min(eb + k, e1 - 1);
+      js[k] = src[e];
+      as[k] = ea[e];
+    }
+#pragma unroll
+    for (int k = 0; k < CH; ++k) {
+      const float4* row = reinterpret_cast<const float4*>(xlr2 + (int64_t)js[k] * 2 * C);
+#pragma unroll
+      for (int c4 = 0; c4 < C / 4; ++c4) {
+        const float4 v = row[c4];
+        xl[k][4 * c4] = v.x;
+        xl[k][4 * c4 + 1] = v.y;
+        xl[k][4 * c4 + 2] = v.z;
+        xl[k][4 * c4 + 3] = v.w;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < CH; ++k) {
+      if (eb + k >= e1) break;
+      float sc = 0.0f;
+#pragma unroll
+      for (int c = 0; c < C; ++c) sc = fmaf(att[c], leaky(xl[k][c] + xr[c] + We[c] * as[k]), sc);
+      online_step<C>(sc, xl[k], m, den, acc);
+    }
+  }
+  const float inv = den > 0.0f ? 1.0f / den : 0.0f;
+  __shared__ double sred[kNT / 64][C];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    double v = live ? (double)fmaxf(fmaf(acc[c], inv, bias[c]), 0.0f) : 0.0;
+    v = wave_sum(v);
+    if (lane == 0) sred[wv][c] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < C) {
+    double v = 0.0;
+#pragma unroll
+    for (int k = 0; k < kNT / 64; ++k) v += sred[k][threadIdx.x];
+    part[(int64_t)blockIdx.x * C + threadIdx.x] = v;
+  }
+}
+
+// pooled mean over all n nodes from the k_gat2 block partials [nblk][C]: thread t sums a
+// contiguous run of blocks, then a fixed-order tree over the threads (deterministic)
+template <int C>
+__global__ __launch_bounds__(kRedNT) void k_pool(int32_t n, int32_t nblk, const double* __restrict__ part,
+                                                 float* __restrict__ hpool) {
+  const int per = (nblk + kRedNT - 1) / kRedNT;
+  const int b0 = threadIdx.x * per, b1 = min(b0 + per, nblk);
+  double v[C];
+#pragma unroll
+  for (int c = 0; c < C; ++c) v[c] = 0.0;
+#pragma unroll 8
+  for (int b = b0; b < b1; ++b)
+#pragma unroll
+    for (int c = 0; c < C; ++c) v[c] += part[(int64_t)b * C + c];
+  __shared__ double sred[kRedNT / 64][C];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    const double w = wave_sum(v[c]);
+    if (lane == 0) sred[wv][c] = w;
+  }
+  __syncthreads();
+  if (threadIdx.x < C) {
+    double r = 0.0;
+#pragma unroll
+    for (int k = 0; k < kRedNT / 64; ++k) r += sred[k][threadIdx.x];
+    hpool[threadIdx.x] = (float)(r / (double)n);
+  }
+}
+
+constexpr int kFcPer = 4;  // actions per thread of k_fc (strided by kNT inside a block)
+
+template <int C>
+__global__ __launch_bounds__(kNT) void k_fc(int32_t na, const float* __restrict__ W, const float* __restrict__ b,
+                                            const float* __restrict__ hpool, float* __restrict__ logits,
+                                            float* __restrict__ pmax) {
+  typedef float f4v __attribute__((ext_vector_type(4)));
+  float hv[C];
+#pragma unroll
+  for (int c = 0; c < C; ++c) hv[c] = hpool[c];
+  float l = -INFINITY;
+  f4v q[kFcPer][C / 4];
+  float bv[kFcPer];
+  const int base = blockIdx.x * (kNT * kFcPer) + threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < kFcPer; ++k) {  // all loads first: W is streamed once per rollout
+    const int a = min(base + k * kNT, na - 1);
+    const f4v* row = reinterpret_cast<const f4v*>(W + (int64_t)a * C);
+#pragma unroll
+    for (int c4 = 0; c4 < C / 4; ++c4) q[k][c4] = __builtin_nontemporal_load(row + c4);
+    bv[k] = __builtin_nontemporal_load(b + a);
+  }
+#pragma unroll
+  for (int k = 0; k < kFcPer; ++k) {
+    const int a = base + k * kNT;
+    float v = bv[k];
+#pragma unroll
+    for (int c4 = 0; c4 < C / 4; ++c4) {
+      v = fmaf(q[k][c4].x, hv[4 * c4], v);
+      v = fmaf(q[k][c4].y, hv[4 * c4 + 1], v);
+      v = fmaf(q[k][c4].z, hv[4 * c4 + 2], v);
+      v = fmaf(q[k][c4].w, hv[4 * c4 + 3], v);
+    }
+    if (a < na) {
+      logits[a] = v;
+      l = fmaxf(l, v);
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) l = fmaxf(l, __shfl_xor(l, o, kWave));
+  __shared__ float sm[kNT / 64];
+  if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = l;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float v = sm[0];
+#pragma unroll
+    for (int k = 1; k < kNT / 64; ++k) v = fmaxf(v, sm[k]);
+    pmax[blockIdx.x] = v;
+  }
+}
+
+// lmax[0..B-1] = max of the k_fc block maxima (a max: independent of the order)
+__global__ __launch_bounds__(kRedNT) void k_max(int32_t nblk, const float* __restrict__ pmax,
+                                                float* __restrict__ lmax, int32_t B) {
+  __shared__ float sm[kRedNT / 64];
+  float v = -INFINITY;
+  for (int k = threadIdx.x; k < nblk; k += kRedNT) v = fmaxf(v, pmax[k]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, kWave));
+  if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = v;
+  __syncthreads();
+  float r = sm[0];
+#pragma unroll
+  for (int k = 1; k < kRedNT / 64; ++k) r = fmaxf(r, sm[k]);
+  for (int bb = threadIdx.x; bb < B; bb += kRedNT) lmax[bb] = r;
+}
+
+struct PolicyWs {
+  float* xlr2;
+  double* part;
+  float* hpool;
+  float* pmax;
+};
+
+int fc_blocks(int32_t na) { return (na + kNT * kFcPer - 1) / (kNT * kFcPer); }
+
+size_t policy_ws(int32_t n, int32_t hid, int32_t na, void* base, PolicyWs* w) {
+  Carve c(base);
+  const int g2 = (n + kNT - 1) / kNT;
+  w->xlr2 = c.take<float>((size_t)n * 2 * hid);
+  w->part = c.take<double>((size_t)g2 * hid);
+  w->hpool = c.take<float>(hid);
+  w->pmax = c.take<float>(fc_blocks(na));
+  return c.off;
+}
+
+template <int F, int C>
+void launch_policy(int32_t n, const float* x, const int32_t* rp, const int32_t* src, const float* ea, const float* p1,
+                   const float* p2, const float* fw, const float* fb, int32_t na, float* logits, float* lmax,
+                   int32_t B, const PolicyWs& w, hipStream_t s) {
+  constexpr int HPT = C <= 8 ? kH1 : 1;
+  const int64_t t1 = (int64_t)n * (kH1 / HPT);
+  const int g2 = (n + kNT - 1) / kNT, gf = fc_blocks(na);
+  k_gat1<F, C, HPT><<<(int)((t1 + kNT - 1) / kNT), kNT, 0, s>>>(n, x, rp, src, ea, p1, p2, w.xlr2);
+  k_gat2<C><<<g2, kNT, 0, s>>>(n, rp, src, ea, p2, w.xlr2, w.part);
+  k_pool<C><<<1, kRedNT, 0, s>>>(n, g2, w.part, w.hpool);
+  k_fc<C><<<gf, kNT, 0, s>>>(na, fw, fb, w.hpool, logits, w.pmax);
+  k_max<<<1, kRedNT, 0, s>>>(gf, w.pmax, lmax, B);
+}
+
+template <int F>
+bool dispatch_hid(int32_t hid, int32_t n, const float* x, const int32_t* rp, const int32_t* src, const float* ea,
+                  const float* p1, const float* p2, const float* fw, const float* fb, int32_t na, float* logits,
+                  float* lmax, int32_t B, const PolicyWs& w, hipStream_t s) {
+  switch (hid) {
+    case 4: launch_policy<F, 4>(n, x, rp, src, ea, p1, p2, fw, fb, na, logits, lmax, B, w, s); return true;
+    case 8: launch_policy<F, 8>(n, x, rp, src, ea, p1, p2, fw, fb, na, logits, lmax, B, w, s); return true;
+    case 16: launch_policy<F, 16>(n, x, rp, src, ea, p1, p2, fw, fb, na, logits, lmax, B, w, s); return true;
+    case 32: launch_policy<F, 32>(n, x, rp, src, ea, p1, p2, fw, fb, na, logits, lmax, B, w, s); return true;
+    default: return false;
+  }
+}
+
+}  // namespace
+}  // namespace spai
+
+using namespace spai;
+
+extern "C" size_t spai_policy_params(int32_t layer, int32_t fin, int32_t hid) {
+  if (layer == 1) return (size_t)gat_params(kH1 * hid, fin);
+  if (layer == 2) return (size_t)gat_params(hid, kH1 * hid);
+  return 0;
+}
+
+extern "C" size_t spai_policy_workspace_bytes(int32_t n_nodes, int32_t hid, int32_t num_actions) {
+  PolicyWs w;
+  return policy_ws(n_nodes, hid, num_actions, nullptr, &w);
+}
+
+extern "C" int spai_policy_logits(int32_t n_nodes, int32_t fin, int32_t hid, const float* x, const int32_t* rowptr,
+                                  const int32_t* src, const float* eattr, const float* gat1, const float* gat2,
+                                  const float* fc_w, const float* fc_b, int32_t num_actions, float* logits,
+                                  float* lmax, int32_t B, void* workspace, size_t workspace_bytes, void* stream) {
+  SPAI_CHECK_ARG(x && rowptr && src && eattr && gat1 && gat2 && fc_w && fc_b && logits && lmax,
+                 "spai_policy_logits: null pointer");
+  SPAI_CHECK_ARG(n_nodes > 0 && num_actions > 0 && B > 0, "spai_policy_logits: bad shape");
+  SPAI_CHECK_ARG(((uintptr_t)fc_w & 15) == 0, "spai_policy_logits: fc weight must be 16-byte aligned");
+  SPAI_CHECK_ARG(workspace && workspace_bytes >= spai_policy_workspace_bytes(n_nodes, hid, num_actions),
+                 "spai_policy_logits: workspace too small");
+  PolicyWs w;
+  policy_ws(n_nodes, hid, num_actions, workspace, &w);
+  hipStream_t s = (hipStream_t)stream;
+  bool ok = false;
+  switch (fin) {
+    case 1: ok = dispatch_hid<1>(hid, n_nodes, x, rowptr, src, eattr, gat1, gat2, fc_w, fc_b, num_actions, logits,
+                                 lmax, B, w, s); break;
+    case 2: ok = dispatch_hid<2>(hid, n_nodes, x, rowptr, src, eattr, gat1, gat2, fc_w, fc_b, num_actions, logits,
+                                 lmax, B, w, s); break;
+    case 4: ok = dispatch_hid<4>(hid, n_nodes, x, rowptr, src, eattr, gat1, gat2, fc_w, fc_b, num_actions, logits,
+                                 lmax, B, w, s); break;
+    default: break;
+  }
+  if (!ok) {
+    set_error("spai_policy_logits: no kernel for node_features=%d hidden_dim=%d (compiled: 1/2/4 x 4/8/16/32)", fin,
+              hid);
+    return SPAI_ERR_UNSUPPORTED;
+  }
+  SPAI_CHECK_LAUNCH();
+  return SPAI_OK;
+}

@@ -45,19 +45,23 @@ class GFlowNet(nn.Module):
 
     # ------------------------------------------------------------------ policy
     def policy_logits(self, data, batch_size: int):
-        """(logits [E+1] fp32, alpha 0-d) for this rollout.
+        """(logits [E+1] fp32, alpha 0-d, lmax [B] or None) for this rollout.
 
-        Uses ``forward_policy.logits(data)`` when the policy provides it (ForwardPolicy
-        here), else the reference call contract ``forward(data, empty)`` -> probs and
-        logits = log(probs) (a constant shift, irrelevant to sampling).  alpha is the mean
-        of the B per-sample sigmoid(alpha) values, as gflownet.py:89."""
-        if hasattr(self.forward_policy, "logits"):
+        Uses ``forward_policy.logits_and_max(data, B)`` (ForwardPolicy here: the gfx950
+        kernels also return the logits' maximum), else ``.logits(data)``, else the reference
+        call contract ``forward(data, empty)`` -> probs and logits = log(probs) (a constant
+        shift, irrelevant to sampling).  alpha is the mean of the B per-sample
+        sigmoid(alpha) values, as gflownet.py:89."""
+        lmax = None
+        if hasattr(self.forward_policy, "logits_and_max"):
+            logits, a, lmax = self.forward_policy.logits_and_max(data, batch_size)
+        elif hasattr(self.forward_policy, "logits"):
             logits, a = self.forward_policy.logits(data)
         else:
             probs, a = self.forward_policy(data, torch.empty(0, dtype=torch.long))
             logits = torch.log(probs)
         alpha = torch.stack([a] * batch_size, dim=0).mean()
-        return logits.reshape(-1), alpha
+        return logits.reshape(-1), alpha, lmax
 
     def forward_probs(self, s, data_list, actions=None):
         """gflownet.py:47-123 (reference API; per-sample policy calls, not the hot path)."""
@@ -103,10 +107,13 @@ class GFlowNet(nn.Module):
         E = env.num_actions - 1
         log = Log(s0, self.backward_policy, self.total_flow, env)
         data_list = self.state_to_data(s0[:1])
-        logits, alpha = self.policy_logits(data_list[0], B)
+        logits, alpha, lmax = self.policy_logits(data_list[0], B)
         if logits.numel() != E + 1:
             raise ValueError(f"policy produced {logits.numel()} logits for {E + 1} actions")
-        lg, lmax, z = kernels.logits_stats(logits.detach().to(env.device), B)
+        if lmax is not None and self.mode == "throughput" and logits.is_cuda and logits.dtype == torch.float32:
+            lg = logits.detach()  # the throughput sampler needs only the maximum, which the policy kernels produced
+        else:
+            lg, lmax, z = kernels.logits_stats(logits.detach().to(env.device), B)
         if self.mode == "parity":
             actions_bt, fwd_bt = self._parity_rollout(lg, B, lmax, z)
             removed, counts = kernels.actions_to_removed(actions_bt, E)

@@ -1,10 +1,13 @@
 """Policies with the reference's constructors and call contracts (reference: policy.py:14-129).
 
-``ForwardPolicy`` restates the reference's GATv2 -> GATv2 -> mean-pool -> fc network
-(policy.py:14-73) in plain torch ops (no torch_geometric).  It is the logit producer of
-the rollout, NOT part of the HIP hot path yet, and its numerics
-are "parity unpinned": the reference's PyG version is unpinned and PyG is not installed,
-so no golden vectors exist for it.  GATv2 semantics restated: per head
+``ForwardPolicy`` is the reference's GATv2 -> GATv2 -> mean-pool -> fc network
+(policy.py:14-73) without torch_geometric: its forward runs on the gfx950 kernels of
+``spai_policy_logits`` (csrc/policy.hip); ``GATv2Layer`` below is the torch restatement
+that holds the parameters, gives the gradients and is the fp32 test reference.  The PyG
+version the reference ran is unpinned and PyG is not installed, so the GATv2 semantics
+are pinned by the numpy restatement in oracle/ and by a known answer (with x = ones, as
+state_to_data builds it, every node's output is W_l 1 + b_l + bias whatever the
+attention weights).  GATv2 semantics restated: per head
 e_ij = att . leaky_relu(W_l x_j + W_r x_i + W_e a_ij, 0.2), softmax over the incoming
 edges of i, out_i = sum_j alpha_ij W_l x_j (+ bias); self-loops replaced by loops whose
 edge attribute is the mean of the node's incoming attributes (fill_value="mean").
@@ -17,6 +20,8 @@ from typing import Tuple
 import torch
 import torch.nn.functional as F
 from torch import Tensor, nn
+
+from . import _lib, kernels
 
 
 class GATv2Layer(nn.Module):
@@ -70,21 +75,143 @@ class BasePolicy(nn.Module):
         self.gat1 = GATv2Layer(node_features if node_features > 0 else 1, self.hid, heads=self.in_head)
 
 
+def graph_csr(x: Tensor, edge_index: Tensor, edge_attr: Tensor):
+    """The state graph as the CSR by target that spai_policy_logits reads: self loops
+    removed, one loop per node re-added with the mean incoming attribute (GATv2Conv
+    add_self_loops(fill_value="mean")), edges grouped by target (edge_index[1]) in their
+    original order.  Built once per state graph (the graph is fixed within a rollout)."""
+    n = x.size(0)
+    dev = x.device
+    src, dst = edge_index[0].to(dev), edge_index[1].to(dev)
+    ea = edge_attr.reshape(-1).to(device=dev, dtype=torch.float32)
+    if src.numel() and (int(src.min()) < 0 or int(max(src.max(), dst.max())) >= n or int(dst.min()) < 0):
+        raise ValueError("edge_index out of range for x")
+    keep = src != dst
+    src, dst, ea = src[keep], dst[keep], ea[keep]
+    deg = torch.bincount(dst, minlength=n)
+    loop = torch.zeros(n, dtype=torch.float32, device=dev).index_add_(0, dst, ea) / deg.clamp(min=1).float()
+    ar = torch.arange(n, device=dev)
+    src, dst, ea = torch.cat([src, ar]), torch.cat([dst, ar]), torch.cat([ea, loop])
+    order = torch.sort(dst, stable=True).indices
+    rowptr = torch.zeros(n + 1, dtype=torch.int32, device=dev)
+    rowptr[1:] = torch.cumsum(torch.bincount(dst, minlength=n), 0).to(torch.int32)
+    return rowptr, src[order].to(torch.int32).contiguous(), ea[order].contiguous()
+
+
+def _pack(layer: GATv2Layer) -> Tensor:
+    """Packed parameter block of one layer in the order spai_policy_logits reads (cached
+    until a parameter is modified in place, e.g. by an optimizer step)."""
+    ps = (layer.lin_l.weight, layer.lin_l.bias, layer.lin_r.weight, layer.lin_r.bias, layer.lin_edge.weight,
+          layer.att, layer.bias)
+    key = tuple((p.data_ptr(), p._version) for p in ps)
+    hit = getattr(layer, "_packed", None)
+    if hit is not None and hit[0] == key:
+        return hit[1]
+    packed = torch.cat([layer.lin_l.weight.reshape(-1), layer.lin_l.bias, layer.lin_r.weight.reshape(-1),
+                      layer.lin_r.bias, layer.lin_edge.weight.reshape(-1), layer.att.reshape(-1),
+                      layer.bias]).detach().float().contiguous()
+    layer._packed = (key, packed)
+    return packed
+
+
+class _HipLogits(torch.autograd.Function):
+    """Forward on the gfx950 kernels; backward recomputes the torch restatement of the same
+    network (ForwardPolicy.torch_logits) and differentiates that: the gradient path of the
+    TB loss, not the sampler's hot path."""
+
+    @staticmethod
+    def forward(ctx, policy, data, B, *params):
+        ctx.policy, ctx.data = policy, data
+        logits, lmax = policy._hip_logits(data, B)
+        ctx.mark_non_differentiable(lmax)
+        return logits, lmax
+
+    @staticmethod
+    def backward(ctx, g, _g_lmax):
+        params = [p for p in ctx.policy.parameters()]
+        with torch.enable_grad():
+            out, _ = ctx.policy.torch_logits(ctx.data)
+            need = [p for p in params if p.requires_grad]
+            grads = torch.autograd.grad(out.reshape(-1), need, g.reshape(-1), allow_unused=True)
+        it = iter(grads)
+        full = [next(it) if p.requires_grad else None for p in params]
+        return (None, None, None, *full)
+
+
 class ForwardPolicy(BasePolicy):
+    """policy.py:24-73 on the MI355X: ``logits``/``forward`` run the three gfx950 kernels of
+    spai_policy_logits (GATv2 layer 1, GATv2 layer 2 + mean pool, fc + max); there is no CPU
+    path (``torch_logits`` is the torch restatement used for gradients and as the fp32
+    test reference)."""
+
     def __init__(self, node_features: int, hidden_dim: int, max_num_actions: int):
         super().__init__(node_features, hidden_dim)
         self.gat2 = GATv2Layer(self.hid * self.in_head, self.hid, heads=self.out_head)
         self.fc = nn.Linear(self.hid, max_num_actions)
         self.alpha = nn.Parameter(torch.tensor(0.0))
+        self._csr = {}
 
-    def logits(self, data) -> Tuple[Tensor, Tensor]:
-        """Unmasked logits [1, E+1] and sigmoid(alpha): everything of forward() but the mask."""
+    def torch_logits(self, data) -> Tuple[Tensor, Tensor]:
+        """Unmasked logits [1, E+1] and sigmoid(alpha) with torch ops (gradient path)."""
         x, edge_index, edge_attr = data.x, data.edge_index, data.edge_attr
         num_actions = edge_attr.size(0) + 1
         x = torch.relu(self.gat1(x, edge_index, edge_attr))
         x = torch.relu(self.gat2(x, edge_index, edge_attr))
         x = x.mean(dim=0, keepdim=True)
         return self.fc(x)[:, :num_actions], torch.sigmoid(self.alpha)
+
+    def _graph(self, data):
+        x, ei = data.x, data.edge_index
+        key = (ei.data_ptr(), ei.shape[1], data.edge_attr.data_ptr(), x.shape[0], str(x.device))
+        hit = self._csr.get(key)
+        if hit is None:
+            hit = self._csr[key] = (data,) + graph_csr(x, ei, data.edge_attr)  # data pins the key's storage
+            if len(self._csr) > 4:
+                self._csr.pop(next(iter(self._csr)))
+        return hit[1:]
+
+    def _hip_logits(self, data, B: int):
+        x = data.x
+        _lib.require_device(x)
+        n, fin = x.shape
+        num_actions = data.edge_attr.size(0) + 1
+        if num_actions > self.fc.out_features:
+            raise ValueError(f"{num_actions} actions > max_num_actions={self.fc.out_features}")
+        rowptr, src, ea = self._graph(data)
+        xf = x.detach().float().contiguous()
+        w = self.fc.weight.detach()
+        if w.dtype != torch.float32 or not w.is_contiguous():
+            w = w.float().contiguous()
+        fb = self.fc.bias.detach().float().contiguous()
+        p1, p2 = _pack(self.gat1), _pack(self.gat2)
+        lib = _lib.load()
+        if p1.numel() != lib.spai_policy_params(1, fin, self.hid) or p2.numel() != lib.spai_policy_params(2, fin, self.hid):
+            raise ValueError("policy parameter shapes do not match node_features/hidden_dim")
+        logits = torch.empty(1, num_actions, dtype=torch.float32, device=x.device)
+        lmax = torch.empty(B, dtype=torch.float32, device=x.device)
+        ws = _lib.workspace(lib.spai_policy_workspace_bytes(n, self.hid, num_actions), x.device, "policy")
+        with kernels._timed("policy"):
+            st = lib.spai_policy_logits(n, fin, self.hid, _lib.ptr(xf), _lib.ptr(rowptr), _lib.ptr(src),
+                                          _lib.ptr(ea), _lib.ptr(p1), _lib.ptr(p2), _lib.ptr(w), _lib.ptr(fb),
+                                          num_actions, _lib.ptr(logits), _lib.ptr(lmax), B, _lib.ptr(ws), ws.numel(),
+                                        _lib.stream_ptr(x.device))
+        _lib.check(st, "spai_policy_logits")
+        return logits, lmax
+
+    def logits_and_max(self, data, B: int = 1) -> Tuple[Tensor, Tensor, Tensor]:
+        """(logits [1, E+1], sigmoid(alpha), lmax [B]) — everything of forward() but the mask,
+        plus the logits' maximum for the sampler (no separate statistics pass)."""
+        params = tuple(self.parameters())
+        if torch.is_grad_enabled() and any(p.requires_grad for p in params):
+            logits, lmax = _HipLogits.apply(self, data, B, *params)
+        else:
+            logits, lmax = self._hip_logits(data, B)
+        return logits, torch.sigmoid(self.alpha), lmax
+
+    def logits(self, data) -> Tuple[Tensor, Tensor]:
+        """Unmasked logits [1, E+1] and sigmoid(alpha)."""
+        logits, a, _ = self.logits_and_max(data)
+        return logits, a
 
     def forward(self, data, actions: Tensor) -> Tuple[Tensor, Tensor]:
         x, a = self.logits(data)

@@ -164,6 +164,29 @@ int spai_fill_lines_gram(int32_t fill_mode, int32_t n, int32_t line_begin, int32
                          void* workspace, size_t workspace_bytes, void* stream);
 int spai_fill_reduce(int32_t n_lines, int32_t B, const void* workspace, double* res2_out, void* stream);
 
+/* ---------------------------------------------------------------- forward policy
+ * logits[a] = fc(mean_pool(relu(GATv2_2(relu(GATv2_1(x))))))[a] for a < num_actions and
+ * lmax[0..B-1] = max_a logits[a]: ForwardPolicy.forward up to the masked softmax
+ * (policy.py:34-73, BasePolicy policy.py:14-21; GATv2Conv heads 4 then 1, edge_dim 1,
+ * negative slope 0.2, concat, bias), evaluated once per rollout because the state graph
+ * of gflownet.py:223-257 does not change within a rollout (gflownet.py:133,145).
+ *   x       [n_nodes][fin] node features (state_to_data: ones(2N, 1))
+ *   rowptr/src/eattr  the graph as a CSR by TARGET (edge_index[1]) over n_nodes, with self
+ *           loops removed and one loop per node re-added whose attribute is the mean of the
+ *           node's incoming attributes (GATv2Conv add_self_loops fill_value="mean")
+ *   gat1/gat2  packed fp32 parameters of each layer: W_l [HC][F], b_l [HC], W_r [HC][F],
+ *           b_r [HC], W_e [HC], att [HC], bias [HC]  (layer 1: F = fin, HC = 4 hid;
+ *           layer 2: F = 4 hid, HC = hid); spai_policy_params(layer, fin, hid) floats each
+ *   fc_w    [num_actions][hid] row-major (nn.Linear weight rows, 16-byte aligned), fc_b [num_actions]
+ * Compiled for fin in {1, 2, 4} and hid in {4, 8, 16, 32} (else SPAI_ERR_UNSUPPORTED).
+ * Workspace: spai_policy_workspace_bytes(n_nodes, hid, num_actions). */
+size_t spai_policy_params(int32_t layer, int32_t fin, int32_t hid);
+size_t spai_policy_workspace_bytes(int32_t n_nodes, int32_t hid, int32_t num_actions);
+int spai_policy_logits(int32_t n_nodes, int32_t fin, int32_t hid, const float* x, const int32_t* rowptr,
+                       const int32_t* src, const float* eattr, const float* gat1, const float* gat2,
+                       const float* fc_w, const float* fc_b, int32_t num_actions, float* logits, float* lmax,
+                       int32_t B, void* workspace, size_t workspace_bytes, void* stream);
+
 /* ---------------------------------------------------------------- rewards
  * residual[b] = sqrt(res2[b]) and reward[b] = 1000 * (alpha (1 - r/r0) + (1 - alpha)(1 - f/f0))
  * with f = 2 n (nnz0 - removed_counts[b]) (preconditioner.py:55-66, 68-77, 137-165; alpha is

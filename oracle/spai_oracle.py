@@ -434,3 +434,68 @@ def trajectory_balance_loss(total_flow, rewards, fwd_probs, back_probs):
     lhs = torch.log(total_flow + eps) + lf
     rhs = torch.log(rewards + eps) + lb
     return ((lhs - rhs) ** 2).mean()
+
+
+# --------------------------------------------------------------------------------------
+# ForwardPolicy logits (policy.py:14-73) — GATv2Conv restated from PyG's published
+# algorithm (torch_geometric.nn.GATv2Conv, 2.x: lin_l / lin_r source and target
+# transforms, lin_edge without bias, leaky_relu 0.2, softmax over the incoming edges of
+# each target, concat heads, + bias; add_self_loops after remove_self_loops with
+# fill_value="mean" over edge_index[1]).  PARITY UNPINNED BY THE REFERENCE: PyG is not
+# installed and its version is unpinned (requirements.txt lists none), so this restatement
+# is pinned by the known answer gatv2_layer_ones_answer (x = ones, as state_to_data builds
+# it, gflownet/gflownet.py:247) and by the test-side torch restatement.
+# --------------------------------------------------------------------------------------
+
+
+def gatv2_layer(x, edge_index, edge_attr, W_l, b_l, W_r, b_r, W_e, att, bias, heads):
+    """One GATv2Conv (fp64, sequential loops over targets).  x [n, F]; W_l/W_r [H*C, F];
+    W_e [H*C, 1]; att [H, C]; bias [H*C].  Returns [n, H*C]."""
+    x = np.asarray(x, np.float64)
+    n = x.shape[0]
+    src, dst = np.asarray(edge_index[0]), np.asarray(edge_index[1])
+    ea = np.asarray(edge_attr, np.float64).reshape(-1)
+    keep = src != dst
+    src, dst, ea = src[keep], dst[keep], ea[keep]
+    deg = np.bincount(dst, minlength=n)
+    loop = np.bincount(dst, weights=ea, minlength=n) / np.maximum(deg, 1)
+    src = np.concatenate([src, np.arange(n)])
+    dst = np.concatenate([dst, np.arange(n)])
+    ea = np.concatenate([ea, loop])
+    HC = W_l.shape[0]
+    C = HC // heads
+    xl = (x @ np.asarray(W_l, np.float64).T + b_l).reshape(n, heads, C)
+    xr = (x @ np.asarray(W_r, np.float64).T + b_r).reshape(n, heads, C)
+    we = np.asarray(W_e, np.float64).reshape(heads, C)
+    att = np.asarray(att, np.float64).reshape(heads, C)
+    out = np.zeros((n, heads, C))
+    order = np.argsort(dst, kind="stable")
+    starts = np.searchsorted(dst[order], np.arange(n + 1))
+    for i in range(n):
+        es = order[starts[i]:starts[i + 1]]
+        if es.size == 0:
+            continue
+        z = xl[src[es]] + xr[i][None] + ea[es][:, None, None] * we[None]
+        z = np.where(z > 0, z, 0.2 * z)
+        s = (z * att[None]).sum(-1)  # [deg, H]
+        s = np.exp(s - s.max(0, keepdims=True))
+        a = s / s.sum(0, keepdims=True)
+        out[i] = (a[:, :, None] * xl[src[es]]).sum(0)
+    return out.reshape(n, HC) + np.asarray(bias, np.float64)
+
+
+def gatv2_layer_ones_answer(W_l, b_l, bias, n):
+    """Known answer for x = ones(n, 1): every node's incoming sources carry the same
+    W_l 1 + b_l, and the attention weights of a target sum to 1, so out_i = W_l 1 + b_l + bias
+    whatever the graph, edge attributes, att and W_e are."""
+    row = np.asarray(W_l, np.float64).sum(1) + np.asarray(b_l, np.float64) + np.asarray(bias, np.float64)
+    return np.tile(row, (n, 1))
+
+
+def forward_policy_logits(x, edge_index, edge_attr, p1, p2, fc_w, fc_b, num_actions):
+    """logits[a] = fc(mean_pool(relu(gat2(relu(gat1(x))))))[a], a < num_actions
+    (policy.py:40-69).  p1/p2: dicts with W_l b_l W_r b_r W_e att bias (numpy)."""
+    h = np.maximum(gatv2_layer(x, edge_index, edge_attr, heads=4, **p1), 0.0)
+    h = np.maximum(gatv2_layer(h, edge_index, edge_attr, heads=1, **p2), 0.0)
+    pooled = h.mean(0)
+    return (np.asarray(fc_w, np.float64)[:num_actions] @ pooled + np.asarray(fc_b, np.float64)[:num_actions])

@@ -253,6 +253,122 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(4))) void k
   }
 }
 
+// Wide lines (8 <= W <= 13, e.g. the 13-point 3-D star of config C3): the same stream and
+// outputs as k_gram_fill, but the factorisation runs in place on one packed copy of G per
+// sample (right-looking LDL^T, T = W(W+1)/2 doubles in registers, re-read from the Gram
+// cache for every sample: the block's Gram data stays in L2), one wave per SIMD.
+// Elimination order and masking are those of k_gram_fill: a removed slot k only gets
+// 1/D_k := 0, so L[.][k] = 0 and m_k = 0.
+template <int W, typename TM, bool LSQ>
+__global__ __launch_bounds__(kNT) void k_gram_fill_wide(int32_t n, int32_t line_begin, int32_t line_end, int32_t wrt,
+                                                        const int32_t* __restrict__ pat_act,
+                                                        const float* __restrict__ pat_val,
+                                                        const double* __restrict__ gram, int32_t B,
+                                                        const uint32_t* __restrict__ removed, int32_t words,
+                                                        TM* __restrict__ m_out, double* __restrict__ partials) {
+  constexpr int T = tri(W);
+  static_assert(W <= 32, "keep mask is one 32-bit word");
+  __shared__ double s_r2[kNT];
+  __shared__ __attribute__((aligned(16))) TM s_m[kNT * W];
+  __shared__ int32_t s_act[W][kNT];  // action ids of the slots (LDS, not registers: G needs them)
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int lb = blockIdx.x;
+  const int j = line_begin + lb * kNT + t;
+  const bool valid = j < line_end;
+  const int64_t nloc = line_end - line_begin;
+  const int jj = valid ? j : line_begin;
+#pragma unroll
+  for (int p = 0; p < W; ++p) s_act[p][t] = (valid && p < wrt) ? pat_act[(int64_t)jj * wrt + p] : -1;
+  const double* gp = gram + (int64_t)(jj >> 6) * (T + W) * 64 + (jj & 63);
+  const int nvl = min(kNT, line_end - (line_begin + lb * kNT));
+#pragma unroll 1
+  for (int b = 0; b < B; ++b) {
+    const uint32_t* rb = removed + (int64_t)b * words;
+    uint32_t keep = 0;
+#pragma unroll
+    for (int p = 0; p < W; ++p) {
+      const int ap = s_act[p][t];
+      if (ap >= 0 && !((rb[ap >> 5] >> (ap & 31)) & 1u)) keep |= 1u << p;
+    }
+    double a[T], y[W];
+#pragma unroll
+    for (int q = 0; q < T; ++q) a[q] = gp[q * 64];
+    double r2 = 1.0;
+    if constexpr (LSQ) {
+#pragma unroll
+      for (int k = 0; k < W; ++k) {
+        const double d = a[gidx<W>(k, k)];
+        const double ik = (((keep >> k) & 1u) && d > 1e-13 * gp[gidx<W>(k, k) * 64]) ? fast_rcp(d) : 0.0;
+        a[gidx<W>(k, k)] = ik;  // the diagonal slot now holds 1/D_k
+        // rows i descending: row i's multiplier L_ik = EL_ik / D_k replaces EL_ik only after
+        // every update that still reads it (rows j <= i use EL_jk)
+#pragma unroll
+        for (int i = W - 1; i > k; --i) {
+          const double li = a[gidx<W>(k, i)] * ik;
+#pragma unroll
+          for (int jx = k + 1; jx <= i; ++jx) a[gidx<W>(jx, i)] -= li * a[gidx<W>(k, jx)];
+          a[gidx<W>(k, i)] = li;
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < W; ++k) {
+        double v = gp[(T + k) * 64];
+#pragma unroll
+        for (int q = 0; q < k; ++q) v -= a[gidx<W>(q, k)] * y[q];
+        y[k] = v;
+      }
+#pragma unroll
+      for (int k = 0; k < W; ++k) r2 -= y[k] * y[k] * a[gidx<W>(k, k)];
+#pragma unroll
+      for (int k = W - 1; k >= 0; --k) {  // back substitution in place: y[q > k] already hold m_q
+        double v = y[k] * a[gidx<W>(k, k)];
+#pragma unroll
+        for (int q = k + 1; q < W; ++q) v -= a[gidx<W>(k, q)] * y[q];
+        y[k] = v;
+      }
+    } else {
+#pragma unroll
+      for (int p = 0; p < W; ++p)
+        y[p] = ((keep >> p) & 1u) ? (double)pat_val[(int64_t)jj * wrt + (p < wrt ? p : 0)] : 0.0;
+#pragma unroll
+      for (int p = 0; p < W; ++p) {
+        double acc = y[p] * a[gidx<W>(p, p)] - 2.0 * gp[(T + p) * 64];
+#pragma unroll
+        for (int q = p + 1; q < W; ++q) acc += 2.0 * y[q] * a[gidx<W>(p, q)];
+        r2 += y[p] * acc;
+      }
+    }
+    if (m_out != nullptr) {
+      if (valid) {
+#pragma unroll
+        for (int p = 0; p < W; ++p)
+          if (p < wrt) s_m[t * wrt + p] = (TM)y[p];
+      }
+      __syncthreads();
+      TM* dst = m_out + ((int64_t)b * nloc + (int64_t)lb * kNT) * wrt;
+      const int ne = nvl * wrt;
+      constexpr int V = 16 / sizeof(TM);
+      int e0 = 0;
+      if ((reinterpret_cast<uintptr_t>(dst) & 15u) == 0) {
+        for (int e = t; e < ne / V; e += kNT)
+          reinterpret_cast<uint4*>(dst)[e] = reinterpret_cast<const uint4*>(s_m)[e];
+        e0 = ne / V * V;
+      }
+      for (int e = e0 + t; e < ne; e += kNT) dst[e] = s_m[e];
+    }
+    s_r2[t] = valid ? r2 : 0.0;
+    __syncthreads();
+    if (wave == 0) {  // fixed-order block sum of this sample
+      double acc = 0.0;
+#pragma unroll
+      for (int q = 0; q < kNT / 64; ++q) acc += s_r2[q * 64 + lane];
+      acc = wave_sum(acc);
+      if (lane == 0) partials[(int64_t)b * gridDim.x + lb] = acc;
+    }
+    __syncthreads();
+  }
+}
+
 __global__ __launch_bounds__(kNT) void k_gram_reduce(const double* __restrict__ partials, int32_t nparts,
                                                      double* __restrict__ out) {
   __shared__ double sred[kNT / 64];
@@ -263,14 +379,18 @@ __global__ __launch_bounds__(kNT) void k_gram_reduce(const double* __restrict__ 
   if (threadIdx.x == 0) out[b] = s;
 }
 
-static int gram_width(int32_t W) { return W <= 5 ? 5 : (W <= 7 ? 7 : 0); }
+static int gram_width(int32_t W) { return W <= 5 ? 5 : (W <= 7 ? 7 : (W <= 13 ? 13 : 0)); }
 
 template <int W, typename TM, bool LSQ>
 hipError_t launch_fill(int32_t n, int32_t lb, int32_t le, int32_t wrt, const int32_t* pa, const float* pv,
                        const double* g, int32_t B, const uint32_t* rm, int32_t words, void* mo, double* partials,
                        int32_t nparts, hipStream_t s) {
-  k_gram_fill<W, TM, LSQ><<<nparts, kNT, 0, s>>>(n, lb, le, wrt, pa, pv, g, B, rm, words, static_cast<TM*>(mo),
-                                                  partials);
+  if constexpr (W > 7)
+    k_gram_fill_wide<W, TM, LSQ><<<nparts, kNT, 0, s>>>(n, lb, le, wrt, pa, pv, g, B, rm, words, static_cast<TM*>(mo),
+                                                       partials);
+  else
+    k_gram_fill<W, TM, LSQ><<<nparts, kNT, 0, s>>>(n, lb, le, wrt, pa, pv, g, B, rm, words, static_cast<TM*>(mo),
+                                                    partials);
   return hipGetLastError();
 }
 
@@ -291,7 +411,7 @@ extern "C" int spai_gram_build(int32_t n, int32_t W, const int32_t* pat_idx, int
   SPAI_CHECK_ARG(a_dtype == SPAI_DTYPE_F32 || a_dtype == SPAI_DTYPE_F64, "spai_gram_build: bad a_dtype");
   const int wc = gram_width(W);
   if (wc == 0 || WA > 7) {
-    set_error("spai_gram_build: widths W=%d WA=%d above the compiled 7", W, WA);
+    set_error("spai_gram_build: widths W=%d (max 13) WA=%d (max 7) above the compiled kernels", W, WA);
     return SPAI_ERR_UNSUPPORTED;
   }
   hipStream_t s = (hipStream_t)stream;
@@ -301,15 +421,19 @@ extern "C" int spai_gram_build(int32_t n, int32_t W, const int32_t* pat_idx, int
       k_gram_build<5, 5, float><<<grid, kNT, 0, s>>>(n, W, WA, pat_idx, a_idx, (const float*)a_val, gram);
     else if (wc == 5)
       k_gram_build<5, 7, float><<<grid, kNT, 0, s>>>(n, W, WA, pat_idx, a_idx, (const float*)a_val, gram);
-    else
+    else if (wc == 7)
       k_gram_build<7, 7, float><<<grid, kNT, 0, s>>>(n, W, WA, pat_idx, a_idx, (const float*)a_val, gram);
+    else
+      k_gram_build<13, 7, float><<<grid, kNT, 0, s>>>(n, W, WA, pat_idx, a_idx, (const float*)a_val, gram);
   } else {
     if (wc == 5 && WA <= 5)
       k_gram_build<5, 5, double><<<grid, kNT, 0, s>>>(n, W, WA, pat_idx, a_idx, (const double*)a_val, gram);
     else if (wc == 5)
       k_gram_build<5, 7, double><<<grid, kNT, 0, s>>>(n, W, WA, pat_idx, a_idx, (const double*)a_val, gram);
-    else
+    else if (wc == 7)
       k_gram_build<7, 7, double><<<grid, kNT, 0, s>>>(n, W, WA, pat_idx, a_idx, (const double*)a_val, gram);
+    else
+      k_gram_build<13, 7, double><<<grid, kNT, 0, s>>>(n, W, WA, pat_idx, a_idx, (const double*)a_val, gram);
   }
   SPAI_CHECK_LAUNCH();
   return SPAI_OK;
@@ -336,7 +460,7 @@ extern "C" int spai_fill_lines_gram(int32_t fill_mode, int32_t n, int32_t line_b
                  "spai_fill_lines_gram: null input");
   const int wc = gram_width(W);
   if (wc == 0) {
-    set_error("spai_fill_lines_gram: width W=%d above the compiled 7", W);
+    set_error("spai_fill_lines_gram: width W=%d above the compiled 13", W);
     return SPAI_ERR_UNSUPPORTED;
   }
   const int32_t nparts = (nl + kNT - 1) / kNT;
@@ -351,13 +475,20 @@ extern "C" int spai_fill_lines_gram(int32_t fill_mode, int32_t n, int32_t line_b
                                              m_out, partials, nparts, s)
               : launch_fill<5, float, true>(n, line_begin, line_end, W, pat_act, pat_val, gram, B, removed, words,
                                             m_out, partials, nparts, s);
-  } else {
+  } else if (wc == 7) {
     e = !lsq ? launch_fill<7, float, false>(n, line_begin, line_end, W, pat_act, pat_val, gram, B, removed, words,
                                             m_out, partials, nparts, s)
         : f64 ? launch_fill<7, double, true>(n, line_begin, line_end, W, pat_act, pat_val, gram, B, removed, words,
                                              m_out, partials, nparts, s)
               : launch_fill<7, float, true>(n, line_begin, line_end, W, pat_act, pat_val, gram, B, removed, words,
                                             m_out, partials, nparts, s);
+  } else {
+    e = !lsq ? launch_fill<13, float, false>(n, line_begin, line_end, W, pat_act, pat_val, gram, B, removed, words,
+                                             m_out, partials, nparts, s)
+        : f64 ? launch_fill<13, double, true>(n, line_begin, line_end, W, pat_act, pat_val, gram, B, removed, words,
+                                              m_out, partials, nparts, s)
+              : launch_fill<13, float, true>(n, line_begin, line_end, W, pat_act, pat_val, gram, B, removed, words,
+                                             m_out, partials, nparts, s);
   }
   SPAI_CHECK_HIP(e);
   return SPAI_OK;

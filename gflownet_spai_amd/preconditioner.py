@@ -79,10 +79,10 @@ class PreconditionerEnv(Env):
         self.a_lines: Lines = build_lines(ai[0], ai[1], a.values(), matrix_size, orient, self.device, a_dtype)
         self.last_m = None
         # Gram cache of the fixed pattern (G = A_J^T A_J, c = A[l, J] per line): the per-rollout
-        # fill then streams it instead of re-gathering A (widths <= 7; wider patterns use the
-        # generic kernels)
+        # fill then streams it instead of re-gathering A (pattern widths <= 13, A widths <= 7;
+        # wider patterns use the generic kernels)
         self.gram = (kernels.gram_build(self.pattern, self.a_lines)
-                     if self.pattern.width <= 7 and self.a_lines.width <= 7 else None)
+                     if self.pattern.width <= 13 and self.a_lines.width <= 7 else None)
 
         self.orig_residual = self.calculate_residual(self.original_matrix, self.original_matrix)
         self._r0 = float(self.orig_residual)  # host copy: no device sync inside the reward formula

@@ -142,12 +142,13 @@ int spai_fill_residual(int32_t fill_mode, int32_t n, int32_t line_begin, int32_t
  * pattern and A only, and the candidate pattern is fixed per PreconditionerEnv
  * (preconditioner.py:23-25).  spai_gram_build computes them once per env for all n lines
  * into `gram` (spai_gram_bytes(n, W) bytes, fp64, blocked [ceil(n/64)][T + Wc][64] with
- * Wc = 5 (W <= 5) or 7 (W <= 7), T = Wc(Wc+1)/2: the packed upper triangle of G, then c).
+ * Wc = 5 (W <= 5), 7 (W <= 7) or 13 (W <= 13; A widths WA <= 7), T = Wc(Wc+1)/2: the
+ * packed upper triangle of G, then c).
  * spai_fill_residual_gram then does what spai_fill_residual does (same fill modes,
  * res2_out / m_out semantics, line range, precision rules) from pat_act (+ pat_val for
  * COPY) and `gram` alone: per-rollout traffic is a stream of the line data and, per sample,
- * the mask bits and M values.  Widths above 7 return SPAI_ERR_UNSUPPORTED (use
- * spai_fill_residual).  Workspace: spai_fill_workspace_bytes(line_end - line_begin, B). */
+ * the mask bits and M values.  Widths above 13 (or WA above 7) return SPAI_ERR_UNSUPPORTED
+ * (use spai_fill_residual; its LSQ mode covers W <= 7).  Workspace: spai_fill_workspace_bytes(line_end - line_begin, B). */
 size_t spai_gram_bytes(int32_t n, int32_t W);
 int spai_gram_build(int32_t n, int32_t W, const int32_t* pat_idx, int32_t WA, const int32_t* a_idx,
                     const void* a_val, int32_t a_dtype, double* gram, void* stream);

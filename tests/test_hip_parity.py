@@ -361,3 +361,65 @@ def test_gram_cached_fill_matches_direct_kernel(side, fill, dims):
         res2, _ = kernels.fill_residual_gram(env.pattern, env.gram, removed, fill == "lsq", b, e)
         parts.append(res2)
     np.testing.assert_allclose(sum(parts).cpu().numpy(), got.cpu().numpy(), rtol=1e-12)
+
+
+def _wide_pattern(dims, g):
+    """13-wide candidate patterns (the nnz/col <= 13 rows of SURVEY §8a11): the 2-D A^2
+    13-point pattern, and in 3-D the 7-point star plus the +-2 axial neighbours."""
+    if dims == 2:
+        r, c, v, n = O.poisson2d(g)
+        A = sp.csr_matrix((v.astype(np.float64), (r, c)), shape=(n, n))
+        P = (A @ A).tocoo()
+        return A, P
+    r, c, v, n = O.poisson3d(g)
+    A = sp.csr_matrix((v, (r, c)), shape=(n, n))
+    one = sp.diags([1.0, 1.0], [-2, 2], shape=(g, g))
+    eye = sp.identity(g)
+    far = sp.kron(sp.kron(one, eye), eye) + sp.kron(sp.kron(eye, one), eye) + sp.kron(sp.kron(eye, eye), one)
+    P = (abs(A) + 0.5 * far).tocoo()
+    return A, P
+
+
+@pytest.mark.parametrize("dims,side,fill", [(2, "AM", "lsq"), (3, "AM", "lsq"), (2, "MA", "copy"), (3, "AM", "copy")])
+def test_wide_pattern_gram_fill_vs_oracle(dims, side, fill):
+    """Pattern width 13 (k_gram_fill_wide): LSQ values vs the oracle's Householder QR and the
+    residual vs the oracle's fp64 ||AM - I||; COPY residual vs the uncached LDS-hash kernel."""
+    from gflownet_spai_amd import PreconditionerEnv, kernels
+    g = 24 if dims == 2 else 9
+    A, P = _wide_pattern(dims, g)
+    n = A.shape[0]
+    dt = np.float32 if dims == 2 else np.float64
+    Ac = A.tocoo()
+    At = coo(Ac.row, Ac.col, Ac.data.astype(dt), n)
+    Pt = coo(P.row, P.col, P.data.astype(dt), n)
+    env = PreconditionerEnv(n, Pt, At, side=side, fill=fill, keep_m=True)
+    assert env.pattern.width == 13 and env.gram is not None
+    E = env.init_nnz
+    rng = np.random.default_rng(21)
+    rem = rng.random((3, E)) < np.array([[0.0], [0.3], [0.8]])
+    acts = torch.from_numpy(np.where(rem, np.arange(E), -1))
+    removed, counts = kernels.actions_to_removed(acts.to(DEV), E)
+    rw = env.rewards_from_removed(removed, counts, 0.5)
+    assert torch.isfinite(rw).all()
+    if fill == "lsq":
+        idx, act, _ = O.lines_from_coo(P.row, P.col, P.data, n, "col")
+        a_idx, _, a_val = O.lines_from_coo(Ac.row, Ac.col, Ac.data, n, "col")
+        Acsc = A.tocsc()
+        tol = 1e-6 if dt == np.float32 else 1e-11
+        for b in range(3):
+            keep = (idx >= 0) & ~rem[b][np.clip(act, 0, None)]
+            m_ref = O.lsq_fill(idx, keep, a_idx, a_val)
+            m_gpu = env.last_m[b].cpu().numpy().astype(np.float64)
+            assert np.linalg.norm(m_gpu - m_ref) / np.linalg.norm(m_ref) < tol
+            res = O.residual_fro_fp64(Acsc, O.m_to_csc(idx, env.last_m[b].cpu().numpy(), n, dt))
+            assert float(env.last_residual[b]) == pytest.approx(res, rel=1e-8)
+        j = n // 2 + 3  # one interior column against numpy lstsq as well
+        keep = (idx >= 0) & ~rem[1][np.clip(act, 0, None)]
+        m_ls, J = O.lsq_fill_lstsq(idx, keep, Acsc, j)
+        got = env.last_m[1][j].cpu().numpy().astype(np.float64)[keep[j] & (idx[j] >= 0)]
+        np.testing.assert_allclose(got, m_ls, rtol=tol * 10, atol=tol)
+    else:
+        ref, _ = kernels.fill_residual(env.pattern, env.a_lines, removed, False, store_m=False,
+                                       m_dtype=env.a_lines.val.dtype)
+        got, _ = kernels.fill_residual_gram(env.pattern, env.gram, removed, False)
+        np.testing.assert_allclose(got.cpu().numpy(), ref.cpu().numpy(), rtol=1e-12)

@@ -118,14 +118,14 @@ class GFlowNet(nn.Module):
             actions_bt, fwd_bt = self._parity_rollout(lg, B, lmax, z)
             removed, counts = kernels.actions_to_removed(actions_bt, E)
             rewards = env.rewards_from_removed(removed, counts, alpha)
-            log._set_rollout(logits, actions_bt, fwd_bt)
+            log._set_rollout(logits, actions_bt, fwd_bt, lmax=lmax)
         else:
             removed, counts, ws = kernels.rollout_select(lg, B, lmax, self.seed, self.rollouts, self.sample_base)
             self.rollouts += 1
             if not self.overlap:
                 actions_full, fwd_full, t_dev = kernels.rollout_order(lg, B, lmax, counts, ws)
                 rewards = env.rewards_from_removed(removed, counts, alpha)
-                log._set_rollout(logits, actions_full, fwd_full, t_dev)
+                log._set_rollout(logits, actions_full, fwd_full, t_dev, lmax=lmax)
                 log.removed, log.counts = removed, counts
                 log.rewards = rewards.detach().to(torch.float32)
                 return log if return_log else None
@@ -145,7 +145,7 @@ class GFlowNet(nn.Module):
             main.wait_stream(side)
             for t in (rewards, env.last_residual) + ((env.last_m,) if env.last_m is not None else ()):
                 t.record_stream(main)
-            log._set_rollout(logits, actions_full, fwd_full, t_dev)
+            log._set_rollout(logits, actions_full, fwd_full, t_dev, lmax=lmax)
         log.removed, log.counts = removed, counts
         log.rewards = rewards.detach().to(torch.float32)
         return log if return_log else None

@@ -199,3 +199,78 @@ def rewards(res2: torch.Tensor, counts: torch.Tensor, nnz0: int, n: int, r0: flo
     _lib.check(_l().spai_rewards(_lib.ptr(res2), _lib.ptr(counts), B, nnz0, n, float(r0), float(f0), _lib.ptr(a),
                                  _lib.ptr(residual), _lib.ptr(reward), _lib.stream_ptr(res2.device)), "spai_rewards")
     return residual, reward
+
+
+def logp_grad(logits: torch.Tensor, lmax: torch.Tensor, actions_bt: torch.Tensor, probs_bt: torch.Tensor,
+              gprobs_bt: torch.Tensor, removed: torch.Tensor) -> torch.Tensor:
+    """dL/dlogits from dL/dprobs of a rollout's logged forward probabilities (spai_logp_grad).
+
+    logits [E+1] or [1, E+1] (shared: the gradient is summed over the samples) or [B, E+1];
+    actions/probs/gprobs [B, T] (row stride may exceed T); removed [B, ceil(E/32)]."""
+    _lib.require_device(logits)
+    E1 = logits.shape[-1]
+    E = E1 - 1
+    B, T = actions_bt.shape
+    shared = logits.dim() == 1 or logits.shape[0] == 1
+    lg = logits.detach().float()
+    lg = lg.reshape(-1).contiguous() if shared else lg.contiguous()
+    if not shared and lg.shape[0] != B:
+        raise ValueError(f"per-sample logits {tuple(logits.shape)} for B={B}")
+
+    def rows(t, dt):
+        t = t.detach().to(dt)
+        return t if t.stride(1) == 1 and t.stride(0) >= T else t.contiguous()
+
+    a, p, g = rows(actions_bt, torch.int64), rows(probs_bt, torch.float32), rows(gprobs_bt, torch.float32)
+    if removed.shape[0] != B or p.shape != (B, T) or g.shape != (B, T):
+        raise ValueError("logp_grad: shapes of actions / probs / gprobs / removed disagree")
+    lm = lmax.detach().float().reshape(-1).expand(B).contiguous() if lmax.numel() == 1 else lmax.float().contiguous()
+    out = torch.empty(E1 if shared else (B, E1), dtype=torch.float32, device=lg.device)
+    nb = _l().spai_logp_grad_workspace_bytes(E, T, B, 0 if shared else 1)
+    ws = _lib.workspace(nb, lg.device, "logp_grad")
+    st = _l().spai_logp_grad(_lib.ptr(lg), 0 if shared else E1, E, B, _lib.ptr(lm), _lib.ptr(a), a.stride(0), T,
+                             _lib.ptr(p), p.stride(0), _lib.ptr(g), g.stride(0), _lib.ptr(removed), removed.shape[1],
+                             _lib.ptr(out), _lib.ptr(ws), ws.numel(), _lib.stream_ptr(lg.device))
+    _lib.check(st, "spai_logp_grad")
+    return out.view_as(logits) if shared else out
+
+
+def _lstm_params(w_ih, w_hh, b_ih, b_hh):
+    H = w_hh.shape[1]
+    if w_ih.shape != (4 * H, 1) or w_hh.shape != (4 * H, H) or b_ih.shape != (4 * H,) or b_hh.shape != (4 * H,):
+        raise ValueError("LSTM parameters must be input_dim=1: w_ih [4H,1], w_hh [4H,H], b_ih/b_hh [4H]")
+    return H, [t.detach().float().contiguous() for t in (w_ih, w_hh, b_ih, b_hh)]
+
+
+def lstm_forward(traj: torch.Tensor, lengths: torch.Tensor, w_ih, w_hh, b_ih, b_hh, keep_states: bool = False):
+    """(h_last [B, H], states [B, T, 2H] or None) of nn.LSTM(1, H) over each row's first lengths[b] ids."""
+    _lib.require_device(traj)
+    H, ps = _lstm_params(w_ih, w_hh, b_ih, b_hh)
+    tr = traj if traj.dtype == torch.int64 and traj.stride(1) == 1 else traj.to(torch.int64).contiguous()
+    B, T = tr.shape
+    n = lengths.to(device=tr.device, dtype=torch.int32).contiguous()
+    h = torch.empty(B, H, dtype=torch.float32, device=tr.device)
+    states = torch.empty(B, T, 2 * H, dtype=torch.float32, device=tr.device) if keep_states else None
+    with _timed("lstm_forward"):
+        st = _l().spai_lstm_forward(B, H, _lib.ptr(tr), tr.stride(0), _lib.ptr(n), T, *[_lib.ptr(p) for p in ps],
+                                    _lib.ptr(h), _lib.ptr(states), _lib.stream_ptr(tr.device))
+    _lib.check(st, "spai_lstm_forward")
+    return h, states
+
+
+def lstm_backward(traj: torch.Tensor, lengths: torch.Tensor, w_ih, w_hh, b_ih, b_hh, states: torch.Tensor,
+                  dh_last: torch.Tensor):
+    """Per-sample fp64 gradient rows [B, 4H + 4H*H + 4H] (d w_ih | d w_hh | d bias) by BPTT."""
+    H, ps = _lstm_params(w_ih, w_hh, b_ih, b_hh)
+    tr = traj if traj.dtype == torch.int64 and traj.stride(1) == 1 else traj.to(torch.int64).contiguous()
+    B, T = tr.shape
+    if states is None or states.shape != (B, T, 2 * H):
+        raise ValueError("lstm_backward needs the forward's states [B, T, 2H]")
+    n = lengths.to(device=tr.device, dtype=torch.int32).contiguous()
+    dh = dh_last.detach().float().contiguous()
+    g = torch.empty(B, 8 * H + 4 * H * H, dtype=torch.float64, device=tr.device)
+    with _timed("lstm_backward"):
+        st = _l().spai_lstm_backward(B, H, _lib.ptr(tr), tr.stride(0), _lib.ptr(n), T, *[_lib.ptr(p) for p in ps],
+                                     _lib.ptr(states), _lib.ptr(dh), _lib.ptr(g), _lib.stream_ptr(tr.device))
+    _lib.check(st, "spai_lstm_backward")
+    return g

@@ -6,9 +6,10 @@ After ``GFlowNet.sample_states`` the fields have the reference's shapes:
   ``back_probs``              [B, T] from the backward policy (log.py:123-164)
   ``rewards``                 [B] fp32 (gflownet.py:193: torch.tensor(..., dtype=log.rewards.dtype))
 ``fwd_probs`` is differentiable w.r.t. the policy logits when they require grad: the
-sampler kernels are not differentiable, so the probabilities of the sampled order are
-recomputed with torch ops from the fixed logits (closed form of the per-step masked
-softmax of policy.py:65-73: p_t = w_{a_t} / (Z - sum_{s<t} w_{a_s}), w = exp(l)).
+values are the sampler's, and the backward (``_TrajProbs``) is the gfx950 kernel
+spai_logp_grad — the closed-form derivative of the per-step masked softmax of
+policy.py:65-73 (p_t = w_{a_t} / (untouched mass + sum_{s>=t} w_{a_s}), w = exp(l)) in
+O(T + E) per sample, instead of autograd through [B, E+1] temporaries.
 """
 from __future__ import annotations
 
@@ -40,6 +41,24 @@ def trajectory_probs(logits: Tensor, actions_bt: Tensor) -> Tensor:
     return torch.where(valid, p, torch.ones((), dtype=p.dtype, device=p.device)).float()
 
 
+class _TrajProbs(torch.autograd.Function):
+    """fwd_probs [B, T] of a rollout as a differentiable function of the logits: forward
+    returns the sampler's probabilities, backward runs spai_logp_grad."""
+
+    @staticmethod
+    def forward(ctx, logits, probs_bt, actions_bt, removed, lmax):
+        ctx.save_for_backward(logits, probs_bt, actions_bt, removed, lmax)
+        return probs_bt.clone()
+
+    @staticmethod
+    def backward(ctx, g):
+        from . import kernels
+
+        logits, probs_bt, actions_bt, removed, lmax = ctx.saved_tensors
+        grad = kernels.logp_grad(logits, lmax, actions_bt, probs_bt, g, removed)
+        return grad.to(logits.dtype), None, None, None, None
+
+
 class Log:
     def __init__(self, s0, backward_policy, total_flow, env):
         self._fwd_probs = []
@@ -55,6 +74,7 @@ class Log:
         self._logits = None
         self._full = None  # (actions [B, cap] i64, fwd [B, cap] f32, T int32 device scalar)
         self._actions_bt = None
+        self._lmax = None
         self.removed = None
         self.counts = None
 
@@ -69,10 +89,13 @@ class Log:
         la[active] = actions.view(-1)[active]
         self._act_list.append(la)
 
-    def _set_rollout(self, logits: Tensor, actions_bt: Tensor, fwd_bt: Tensor, t_dev: Tensor | None = None):
+    def _set_rollout(self, logits: Tensor, actions_bt: Tensor, fwd_bt: Tensor, t_dev: Tensor | None = None,
+                     lmax: Tensor | None = None):
         """actions_bt / fwd_bt: [B, T] or, with t_dev, [B, cap] buffers of which the first
-        T = int(t_dev) columns are the trajectory (T is read lazily: no sync in the rollout)."""
+        T = int(t_dev) columns are the trajectory (T is read lazily: no sync in the rollout);
+        lmax: the logits' maximum the sampler used (the gradient kernel's weight scale)."""
         self._logits = logits
+        self._lmax = lmax
         if t_dev is None:
             self._actions_bt, self._fwd_probs, self._act_tb = actions_bt, fwd_bt, actions_bt.t()
         else:
@@ -100,6 +123,8 @@ class Log:
         if isinstance(self._fwd_probs, list):
             self._fwd_probs = torch.stack(self._fwd_probs, dim=0).t()
         if self._logits is not None and self._logits.requires_grad and torch.is_grad_enabled():
+            if self._logits.is_cuda and self.removed is not None and self._lmax is not None:
+                return _TrajProbs.apply(self._logits, self._fwd_probs, self._actions_bt, self.removed, self._lmax)
             return trajectory_probs(self._logits, self._actions_bt)
         return self._fwd_probs
 

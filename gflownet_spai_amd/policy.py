@@ -11,7 +11,8 @@ attention weights).  GATv2 semantics restated: per head
 e_ij = att . leaky_relu(W_l x_j + W_r x_i + W_e a_ij, 0.2), softmax over the incoming
 edges of i, out_i = sum_j alpha_ij W_l x_j (+ bias); self-loops replaced by loops whose
 edge attribute is the mean of the node's incoming attributes (fill_value="mean").
-``BackwardPolicy`` is the reference's LSTM policy (policy.py:75-129), batched.
+``BackwardPolicy`` is the reference's LSTM policy (policy.py:75-129), batched, with the
+recurrence (forward and BPTT) on the gfx950 kernels of csrc/train.hip.
 """
 from __future__ import annotations
 
@@ -222,9 +223,38 @@ class ForwardPolicy(BasePolicy):
         return torch.softmax(x, dim=1), a
 
 
+class _LstmLast(torch.autograd.Function):
+    """h at each row's last valid step of nn.LSTM(1, H) on the gfx950 kernels: forward
+    spai_lstm_forward (keeping (h_t, c_t) when a gradient is needed), backward
+    spai_lstm_backward (BPTT, per-sample fp64 rows summed here in sample order)."""
+
+    @staticmethod
+    def forward(ctx, traj, lengths, w_ih, w_hh, b_ih, b_hh):
+        need = any(ctx.needs_input_grad[2:])
+        h, states = kernels.lstm_forward(traj, lengths, w_ih, w_hh, b_ih, b_hh, keep_states=need)
+        if need:
+            ctx.save_for_backward(traj, lengths, w_ih, w_hh, b_ih, b_hh, states)
+        return h
+
+    @staticmethod
+    def backward(ctx, dh):
+        traj, lengths, w_ih, w_hh, b_ih, b_hh, states = ctx.saved_tensors
+        H = w_hh.shape[1]
+        rows = kernels.lstm_backward(traj, lengths, w_ih, w_hh, b_ih, b_hh, states, dh)
+        g = rows.sum(0)
+        R = 4 * H
+        d_ih = g[:R].view(R, 1).to(w_ih.dtype)
+        d_hh = g[R:R + R * H].view(R, H).to(w_hh.dtype)
+        d_b = g[R + R * H:].to(b_ih.dtype)
+        return None, None, d_ih, d_hh, d_b, d_b.clone()
+
+
 class BackwardPolicy(nn.Module):
     """LSTM over each trajectory's action ids; softmax over its first n_valid fc outputs,
-    padded with 1.0 to the trajectory length (policy.py:87-129), all samples in one call."""
+    padded with 1.0 to the trajectory length (policy.py:75-129), all samples in one call.
+    The recurrence runs on the gfx950 kernels (spai_lstm_forward / spai_lstm_backward);
+    the fc GEMM and the masked softmax are torch ops on the device.  ``torch_forward`` is
+    the nn.LSTM restatement (the fp32 test reference), not a fallback."""
 
     def __init__(self, input_dim: int, hidden_dim: int, max_num_actions: int):
         super().__init__()
@@ -233,13 +263,9 @@ class BackwardPolicy(nn.Module):
         self.lstm = nn.LSTM(input_dim, hidden_dim, batch_first=True)
         self.fc = nn.Linear(hidden_dim, max_num_actions)
 
-    def forward(self, trajectories: Tensor) -> Tensor:
-        B, T = trajectories.shape
-        n = (trajectories != -1).sum(1)
-        packed = nn.utils.rnn.pack_padded_sequence(trajectories.float().unsqueeze(-1), n.cpu(), batch_first=True,
-                                                   enforce_sorted=False)
-        _, (h, _) = self.lstm(packed)
-        out = self.fc(h[-1])
+    def _head(self, h: Tensor, n: Tensor, T: int) -> Tensor:
+        out = self.fc(h)
+        B = h.shape[0]
         width = min(T, out.shape[1])
         pos = torch.arange(width, device=out.device)
         valid = pos.view(1, -1) < n.view(-1, 1)
@@ -247,3 +273,24 @@ class BackwardPolicy(nn.Module):
         res = torch.ones(B, T, device=out.device, dtype=out.dtype)
         res[:, :width] = torch.where(valid, p, torch.ones((), device=out.device, dtype=out.dtype))
         return res.unsqueeze(1)
+
+    def forward(self, trajectories: Tensor) -> Tensor:
+        _lib.require_device(trajectories)
+        if self.lstm.input_size != 1:
+            raise ValueError("the trajectory is one feature per step (policy.py:100): input_dim must be 1")
+        B, T = trajectories.shape
+        n = (trajectories != -1).sum(1)
+        if bool((n == 0).any()):  # pack_padded_sequence rejects empty rows (one host sync)
+            raise RuntimeError("Length of all samples has to be greater than 0")
+        lstm = self.lstm
+        h = _LstmLast.apply(trajectories, n, lstm.weight_ih_l0, lstm.weight_hh_l0, lstm.bias_ih_l0, lstm.bias_hh_l0)
+        return self._head(h, n, T)
+
+    def torch_forward(self, trajectories: Tensor) -> Tensor:
+        """The same network with nn.LSTM over packed sequences (test reference)."""
+        B, T = trajectories.shape
+        n = (trajectories != -1).sum(1)
+        packed = nn.utils.rnn.pack_padded_sequence(trajectories.float().unsqueeze(-1), n.cpu(), batch_first=True,
+                                                   enforce_sorted=False)
+        _, (h, _) = self.lstm(packed)
+        return self._head(h[-1], n, T)

@@ -188,6 +188,37 @@ int spai_policy_logits(int32_t n_nodes, int32_t fin, int32_t hid, const float* x
                        const float* fc_w, const float* fc_b, int32_t num_actions, float* logits, float* lmax,
                        int32_t B, void* workspace, size_t workspace_bytes, void* stream);
 
+/* ---------------------------------------------------------------- training
+ * Gradient of the logged forward probabilities w.r.t. the logits (the backward of
+ * log.py:70 fwd_probs through policy.py:65-73's masked softmax, as trajectory_balance_loss
+ * gflownet/utils.py:228-278 differentiates it):
+ *   grad[a] (+)= sum_b sum_t gprobs[b,t] * d probs[b,t] / d logits[a]
+ * with probs[b,t] = w_{a_t} / (untouched mass + sum_{s>=t} w_{a_s}), w = exp(logits - lmax[b]).
+ *   logits   [E+1] (bstride 0: shared by all samples, grad_out [E+1] summed over b) or
+ *            [B][bstride] (grad_out [B][E+1])
+ *   actions  [B][lda] int64, the first T columns: removed actions, then E, then -1
+ *   probs    [B][ldp] the rollout's fwd_probs; gprobs [B][ldg] = dL/dprobs
+ *   removed  [B][words] the rollout's removal bitmaps (untouched = bit clear, a < E)
+ * Deterministic (fixed summation orders).  Workspace: spai_logp_grad_workspace_bytes. */
+size_t spai_logp_grad_workspace_bytes(int32_t E, int32_t T, int32_t B, int32_t per_sample);
+int spai_logp_grad(const float* logits, int64_t bstride, int32_t E, int32_t B, const float* lmax,
+                   const int64_t* actions, int64_t lda, int32_t T, const float* probs, int64_t ldp,
+                   const float* gprobs, int64_t ldg, const uint32_t* removed, int32_t words, float* grad_out,
+                   void* workspace, size_t workspace_bytes, void* stream);
+
+/* BackwardPolicy's LSTM (policy.py:75-129; nn.LSTM(1, H), gate order i, f, g, o): input
+ * x_t = (float)traj[b][t] for t < lengths[b] (the entries != -1, as pack_padded_sequence
+ * takes them).  Forward: h_last [B][H] and, when states != NULL, (h_t, c_t) of every step in
+ * states [B][T][2H].  Backward (BPTT from dh_last [B][H], dc = 0 at the end): one fp64 row
+ * per sample in grad [B][4H + 4H*H + 4H] = d w_ih [4H] | d w_hh [4H][H] | d bias [4H]
+ * (d b_ih = d b_hh = d bias).  H in {2, 4, 8}. */
+int spai_lstm_forward(int32_t B, int32_t H, const int64_t* traj, int64_t ldt, const int32_t* lengths, int32_t T,
+                      const float* w_ih, const float* w_hh, const float* b_ih, const float* b_hh, float* h_last,
+                      float* states, void* stream);
+int spai_lstm_backward(int32_t B, int32_t H, const int64_t* traj, int64_t ldt, const int32_t* lengths, int32_t T,
+                       const float* w_ih, const float* w_hh, const float* b_ih, const float* b_hh,
+                       const float* states, const float* dh_last, double* grad, void* stream);
+
 /* ---------------------------------------------------------------- rewards
  * residual[b] = sqrt(res2[b]) and reward[b] = 1000 * (alpha (1 - r/r0) + (1 - alpha)(1 - f/f0))
  * with f = 2 n (nnz0 - removed_counts[b]) (preconditioner.py:55-66, 68-77, 137-165; alpha is

@@ -23,6 +23,8 @@ Contents
   * reward                                              (preconditioner.py:55-66, 68-77, 137-165)
   * least-squares fill + ||AM-I||_F                    (north-star extension; parity unpinned by the reference)
   * trajectory balance loss                             (gflownet/utils.py:228-278)
+  * logged-probability gradient w.r.t. the logits       (log.py:70 + policy.py:65-73 under autograd)
+  * BackwardPolicy LSTM forward / BPTT                  (policy.py:75-129, torch nn.LSTM semantics)
 """
 from __future__ import annotations
 
@@ -434,6 +436,107 @@ def trajectory_balance_loss(total_flow, rewards, fwd_probs, back_probs):
     lhs = torch.log(total_flow + eps) + lf
     rhs = torch.log(rewards + eps) + lb
     return ((lhs - rhs) ** 2).mean()
+
+
+# --------------------------------------------------------------------------------------
+# Gradient of the logged forward probabilities w.r.t. the logits: what autograd computes
+# through the reference's per-step masked softmax (policy.py:65-73) and the gather of
+# log.py:70, in closed form.  p_t = w_{a_t} / R_t, R_t = untouched mass + sum_{s>=t} w_{a_s}:
+#   dL/dl_{a_t} += G_t - w_{a_t} S_t,  dL/dl_a += -w_a S_last (a untouched, a < E),
+#   G_t = gp_t p_t,  S_t = sum_{s<=t} G_s p_s / w_{a_s}.
+# Pinned by the reference's own logits.grad in the golden rollouts (tests/golden).
+# --------------------------------------------------------------------------------------
+
+
+def logp_grad(logits, actions_bt, probs_bt, gprobs_bt):
+    l = np.asarray(logits, np.float64).reshape(-1)
+    w = np.exp(l - l.max())
+    E = l.size - 1
+    grad = np.zeros(E + 1)
+    for a, p, g in zip(np.asarray(actions_bt), np.asarray(probs_bt, np.float64), np.asarray(gprobs_bt, np.float64)):
+        valid = a >= 0
+        av, pv, gv = a[valid], p[valid], g[valid]
+        G = gv * pv
+        S = np.cumsum(np.where(w[av] > 0, G * pv / np.where(w[av] > 0, w[av], 1.0), 0.0))
+        grad[av] += G - w[av] * S  # actions are distinct within one trajectory
+        untouched = np.ones(E + 1, np.bool_)
+        untouched[av] = False
+        untouched[E] = False
+        if S.size:
+            grad[untouched] -= w[untouched] * S[-1]
+    return grad
+
+
+# --------------------------------------------------------------------------------------
+# BackwardPolicy LSTM (policy.py:75-129): nn.LSTM(1, H) over each row's entries != -1
+# (pack_padded_sequence keeps the first n of them), gate order i, f, g, o (torch), then
+# fc(h_last) -> softmax over the first n outputs, padded with 1.  fp64 numpy restatement;
+# the BPTT gives d w_ih [4H, 1], d w_hh [4H, H], d bias [4H] (= d b_ih = d b_hh).
+# --------------------------------------------------------------------------------------
+
+
+def _sig(x):
+    return 1.0 / (1.0 + np.exp(-x))
+
+
+def lstm_forward(traj, w_ih, w_hh, b_ih, b_hh):
+    """(h_last [B, H], per-row lists of (h_t, c_t)) in fp64."""
+    w_ih, w_hh = np.asarray(w_ih, np.float64).reshape(-1), np.asarray(w_hh, np.float64)
+    bias = np.asarray(b_ih, np.float64) + np.asarray(b_hh, np.float64)
+    H = w_hh.shape[1]
+    outs, states = [], []
+    for row in np.asarray(traj):
+        n = int((row != -1).sum())
+        h, c, st = np.zeros(H), np.zeros(H), []
+        for t in range(n):
+            z = w_ih * float(row[t]) + bias + w_hh @ h
+            i, f, g, o = _sig(z[:H]), _sig(z[H:2 * H]), np.tanh(z[2 * H:3 * H]), _sig(z[3 * H:])
+            c = f * c + i * g
+            h = o * np.tanh(c)
+            st.append((h.copy(), c.copy()))
+        outs.append(h)
+        states.append(st)
+    return np.stack(outs), states
+
+
+def lstm_backward(traj, w_ih, w_hh, b_ih, b_hh, dh_last):
+    """Summed over rows: (d w_ih [4H, 1], d w_hh [4H, H], d bias [4H]) for dL/dh_last."""
+    w_ih1, w_hh = np.asarray(w_ih, np.float64).reshape(-1), np.asarray(w_hh, np.float64)
+    bias = np.asarray(b_ih, np.float64) + np.asarray(b_hh, np.float64)
+    H = w_hh.shape[1]
+    _, states = lstm_forward(traj, w_ih, w_hh, b_ih, b_hh)
+    g_ih, g_hh, g_b = np.zeros(4 * H), np.zeros((4 * H, H)), np.zeros(4 * H)
+    for row, st, dh0 in zip(np.asarray(traj), states, np.asarray(dh_last, np.float64)):
+        dh, dc = dh0.copy(), np.zeros(H)
+        for t in range(len(st) - 1, -1, -1):
+            hp, cp = (st[t - 1] if t > 0 else (np.zeros(H), np.zeros(H)))
+            x = float(row[t])
+            z = w_ih1 * x + bias + w_hh @ hp
+            i, f, g, o = _sig(z[:H]), _sig(z[H:2 * H]), np.tanh(z[2 * H:3 * H]), _sig(z[3 * H:])
+            tc = np.tanh(st[t][1])
+            dcc = dc + dh * o * (1 - tc * tc)
+            da = np.concatenate([dcc * g * i * (1 - i), dcc * cp * f * (1 - f), dcc * i * (1 - g * g),
+                                 dh * tc * o * (1 - o)])
+            g_ih += da * x
+            g_b += da
+            g_hh += np.outer(da, hp)
+            dc = dcc * f
+            dh = w_hh.T @ da
+    return g_ih.reshape(-1, 1), g_hh, g_b
+
+
+def backward_probs(traj, w_ih, w_hh, b_ih, b_hh, fc_w, fc_b):
+    """BackwardPolicy.forward (policy.py:87-129) -> [B, 1, T] in fp64."""
+    traj = np.asarray(traj)
+    B, T = traj.shape
+    h, _ = lstm_forward(traj, w_ih, w_hh, b_ih, b_hh)
+    out = h @ np.asarray(fc_w, np.float64).T + np.asarray(fc_b, np.float64)
+    res = np.ones((B, T))
+    for b in range(B):
+        n = min(int((traj[b] != -1).sum()), out.shape[1], T)
+        z = out[b, :n] - out[b, :n].max()
+        res[b, :n] = np.exp(z) / np.exp(z).sum()
+    return res[:, None, :]
 
 
 # --------------------------------------------------------------------------------------

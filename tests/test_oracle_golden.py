@@ -179,7 +179,7 @@ def test_trajectory_balance_loss_reference():
         np.testing.assert_allclose(fp.detach().numpy(), d["fwd_probs"], rtol=1e-6, atol=1e-9)
         torch.manual_seed(0)
         bwd = BackwardPolicy(1, 4, E + 1)
-        bp = bwd(acts_bt).reshape(B, -1)
+        bp = bwd.torch_forward(acts_bt).reshape(B, -1)
         np.testing.assert_allclose(bp.detach().numpy(), d["back_probs"], rtol=1e-5, atol=1e-7)
         loss = trajectory_balance_loss(torch.ones(1), torch.tensor(d["rewards"]), fp, bp)
         ref_loss = O.trajectory_balance_loss(torch.ones(1), torch.tensor(d["rewards"]), torch.tensor(d["fwd_probs"]),

@@ -59,8 +59,10 @@ SIGNATURES = {
                                       _c_i64, _c_p, _c_i32, _c_p, _c_p, _c_sz, _c_p]),
     "spai_lstm_forward": (ctypes.c_int, [_c_i32, _c_i32, _c_p, _c_i64, _c_p, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_p,
                                          _c_p, _c_p]),
+    "spai_lstm_states_floats": (_c_sz, [_c_i32, _c_i32, _c_i32]),
+    "spai_lstm_backward_workspace_bytes": (_c_sz, [_c_i32, _c_i32, _c_i32]),
     "spai_lstm_backward": (ctypes.c_int, [_c_i32, _c_i32, _c_p, _c_i64, _c_p, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_p,
-                                          _c_p, _c_p, _c_p]),
+                                          _c_p, _c_p, _c_p, _c_sz, _c_p]),
     "spai_fill_reduce": (ctypes.c_int, [_c_i32, _c_i32, _c_p, _c_p, _c_p]),
     "spai_fill_residual": (ctypes.c_int, [_c_i32, _c_i32, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_i32, _c_p, _c_p,
                                           _c_i32, _c_i32, _c_p, _c_i32, _c_p, _c_i32, _c_p, _c_p, _c_sz, _c_p]),

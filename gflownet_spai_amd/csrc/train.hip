@@ -375,200 +375,403 @@ __global__ __launch_bounds__(kLstmNT) void k_lstm_bwd(int32_t B, const int64_t* 
 }
 
 // ------------------------------------------------------------------ LSTM, H = 4 (the reference's size)
-// A step of one sample is 16 gate rows: one wave runs 4 samples, one 16-lane DPP row each.
-// Lane r of a row owns gate row q*H + k (unit k = r >> 2, gate type q = r & 3), so a unit's
-// four gates sit in one quad: quad_perm broadcasts hand i, f, g, o to the quad, which then
-// updates (c_k, h_k) redundantly; the recurrent product needs the other units' h, fetched
-// by row rotations (row_ror 4, 8, 12) against weights pre-rotated per lane at load time.
-// ~25 VALU instructions on the serial chain per step instead of ~1000 for a scalar step.
-// The rotation direction of row_ror is probed once (lane id through row_ror:1).
+// The recurrence is a chain of n_b dependent steps per sample, so the forward and the BPTT
+// adjoint chain each run one sample per wave on a 16-lane DPP row (exec = lanes 0-15) and
+// carry nothing else; all off-chain work runs as parallel passes over 16-step blocks.
+//
+// Forward (k_lstm_fwd4): lane r owns gate row q*H + k (unit k = r >> 2, gate q = r & 3), so a
+// unit's four gates sit in one quad: quad_perm broadcasts i, f, g, o to the quad, which
+// updates (c_k, h_k) redundantly; W_hh h takes the other units' h through row_ror 4, 8, 12
+// against weights pre-rotated per lane.  The activation's pre-scale (-log2 e, twice that
+// for tanh) is folded into the weights, so a gate is fma chain -> v_exp -> v_rcp -> fma.
+// Only a checkpoint (h, c) per 16-step block is stored ("states" = [B][ceil(T/16)][2H]);
+// the inputs are prefetched three blocks ahead.  Fwd4Step restates a step for one thread
+// with the same instructions in the same order (bit-identical states), so the backward
+// passes recompute any block from its checkpoint.
+//
+// Backward: the adjoint s_t = (dh_t, dc+_t) of BPTT obeys a LINEAR recurrence whose
+// coefficients depend only on the forward states:
+//    dc_t = dc+_t + gamma dh_t,  gamma = o (1 - tanh^2 c_t)
+//    dz_{q,k} = A_{q,k} dh_t[k] + B_{q,k} dc+_t[k]   (A = alpha gamma, B = alpha for i, f, g;
+//                                                    A = tanh(c_t) o (1 - o), B = 0 for o)
+//    dc+_{t-1} = f gamma dh_t + f dc+_t,   dh_{t-1} = W_hh^T dz
+//  k_lstm_coef4  (parallel, one thread per block) recomputes the block's states and folds
+//                W_hh into per-lane chain coefficients;
+//  k_lstm_adj4   runs the chain: per step 1 load, 2 fma, 3 row-rotated adds, 1 quad
+//                broadcast, 2 fma; it stores the adjoint once per block;
+//  k_lstm_grad4  (parallel, one thread per block) recomputes states and the adjoint inside
+//                the block from the two checkpoints, sums the gradient in fp64 in a fixed
+//                order; k_lstm_gsum4 adds the per-block partial rows in order.
+// Chain lane (k, j) [r = 4k + j] carries the partial of target unit u = (k - j) & 3:
+//    p = a1 dh[k] + a2 dc[k],  a1 = sum_q W_hh[q,k][u] A_{q,k},  a2 = sum_q W_hh[q,k][u] B_{q,k};
+// lane 4u collects lanes (4u + 5m) mod 16, m = 1..3 (one per other quad) by row_ror, and a
+// quad_perm broadcast returns dh_{t-1}[u] to its quad.  The row_ror direction is probed once
+// per kernel (ror_sign).
 constexpr int kH4 = 4;
-constexpr int kPre4 = 16;  // steps of inputs prefetched ahead
+constexpr int kBlk4 = 16;        // steps per block (checkpoint interval, prefetch unit)
+constexpr int kGrad4NT = 256;    // k_lstm_grad4 threads per block
+constexpr int kGrad4Blocks = 64; // k_lstm_grad4 blocks per sample
+constexpr int kNG4 = 8 * kH4 + 4 * kH4 * kH4;  // 96 gradient entries per sample
+constexpr float kLog2e = 1.4426950408889634f;
 
+// DPP move within a row whose 16 lanes are all active (row_ror, quad_perm): every source is
+// valid, so the old value is never read and need not be materialised
 template <int CTRL>
 __device__ __forceinline__ float dppf(float v) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, true));
 }
 __device__ __forceinline__ float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
-__device__ __forceinline__ float fsig(float y) { return frcp(1.0f + __expf(-y)); }
-__device__ __forceinline__ float ftanh(float y) { return fmaf(2.0f, fsig(2.0f * y), -1.0f); }
+__device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
+// sigmoid of y given -log2(e) y
+__device__ __forceinline__ float fsig_pre(float ny) { return frcp(1.0f + fexp2(ny)); }
+__device__ __forceinline__ float ftanh(float y) { return fmaf(2.0f, fsig_pre((-2.0f * kLog2e) * y), -1.0f); }
 
-struct Lane4 {
-  int r, k, q, d;  // lane in row, unit, gate type, row_ror:1 source offset (1 or 15)
-  __device__ __forceinline__ void init() {
-    r = threadIdx.x & 15;
-    k = r >> 2;
-    q = r & 3;
-    const int probe = __builtin_amdgcn_update_dpp(0, r, 0x121, 0xF, 0xF, false);  // row_ror:1
-    d = (r - probe) & 15;
+// +1 if row_ror:N hands lane i the value of lane i + N, -1 if that of lane i - N.  Lane 0 must
+// be active; the DPP result goes straight to readfirstlane (no arithmetic it could fold into).
+__device__ __forceinline__ int ror_sign() {
+  const int src = __builtin_amdgcn_update_dpp(0, (int)(threadIdx.x & 15), 0x121, 0xF, 0xF, false);  // row_ror:1
+  return __builtin_amdgcn_readfirstlane(src) == 1 ? 1 : -1;
+}
+
+__device__ __forceinline__ int nblocks4(int n) { return (n + kBlk4 - 1) / kBlk4; }
+
+// a gate row's scaled weights, as the forward lane (q, k) holds them
+struct Row4 {
+  float wx, bs, A2, Bm, wr[4];
+  __device__ __forceinline__ void load(const float* w_ih, const float* w_hh, const float* b_ih, const float* b_hh,
+                                       int q, int k, int sg) {
+    const int row = q * kH4 + k;
+    const float sc = (q == 2 ? -2.0f : -1.0f) * kLog2e;
+    wx = w_ih[row] * sc;
+    bs = (b_ih[row] + b_hh[row]) * sc;
+    A2 = q == 2 ? 2.0f : 1.0f;
+    Bm = q == 2 ? -1.0f : 0.0f;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) wr[m] = w_hh[row * kH4 + ((k + m * sg) & 3)] * sc;  // unit row_ror(4m) brings
   }
-  // unit whose h row_ror(4m) brings to this lane
-  __device__ __forceinline__ int unit_rot(int m) const { return (k - m * d) & 3; }
-  // lane whose value row_ror(m) brings to this lane
-  __device__ __forceinline__ int lane_rot(int m) const { return (r - m * d) & 15; }
+  // fma order: own unit, then the units row_ror 4, 8, 12 bring (k + sg, k + 2sg, k + 3sg)
+  __device__ __forceinline__ float act(float x, float h0, float h1, float h2, float h3) const {
+    float z = fmaf(wx, x, bs);
+    z = fmaf(wr[0], h0, z);
+    z = fmaf(wr[1], h1, z);
+    z = fmaf(wr[2], h2, z);
+    z = fmaf(wr[3], h3, z);
+    return fmaf(fsig_pre(z), A2, Bm);
+  }
 };
 
-__device__ __forceinline__ float gate_act(float z, int q) {
-  const float s = fsig(q == 2 ? 2.0f * z : z);
-  return q == 2 ? fmaf(2.0f, s, -1.0f) : s;
-}
+// one thread's bit-identical restatement of k_lstm_fwd4's step (all 16 rows); weights in LDS
+struct Fwd4Step {
+  Row4 row[16];  // [q * 4 + k]
+  __device__ __forceinline__ void load(const float* w_ih, const float* w_hh, const float* b_ih, const float* b_hh,
+                                       int sg) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) row[q * 4 + k].load(w_ih, w_hh, b_ih, b_hh, q, k, sg);
+  }
+  // gates g[q][k] and the step update of h, c
+  __device__ __forceinline__ void step(float x, float* h, float* c, float (*g)[4], int sg) const {
+    float hn[4], cn[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        g[q][k] = row[q * 4 + k].act(x, h[k], h[(k + sg) & 3], h[(k + 2 * sg) & 3], h[(k + 3 * sg) & 3]);
+      cn[k] = fmaf(g[1][k], c[k], g[0][k] * g[2][k]);
+      hn[k] = g[3][k] * ftanh(cn[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) h[k] = hn[k], c[k] = cn[k];
+  }
+};
 
-// pre-activation of this lane's gate row from x and the quad-resident h
-__device__ __forceinline__ float gate_z(float wx, float bb, const float* wr, float x, float h) {
-  float z = fmaf(wx, x, bb);
-  z = fmaf(wr[0], h, z);
-  z = fmaf(wr[1], dppf<0x124>(h), z);  // row_ror:4
-  z = fmaf(wr[2], dppf<0x128>(h), z);  // row_ror:8
-  z = fmaf(wr[3], dppf<0x12C>(h), z);  // row_ror:12
-  return z;
-}
-
-__global__ __launch_bounds__(64) void k_lstm_fwd4(int32_t B, const int64_t* __restrict__ traj, int64_t ldt,
+__global__ __launch_bounds__(64) void k_lstm_fwd4(const int64_t* __restrict__ traj, int64_t ldt,
                                                   const int32_t* __restrict__ lengths, int32_t T,
                                                   const float* __restrict__ w_ih, const float* __restrict__ w_hh,
                                                   const float* __restrict__ b_ih, const float* __restrict__ b_hh,
                                                   float* __restrict__ h_last, float* __restrict__ states) {
-  constexpr int H = kH4;
-  Lane4 L;
-  L.init();
-  const int b = blockIdx.x * 4 + (threadIdx.x >> 4);
-  const bool live = b < B;
-  const int bb = live ? b : B - 1;
-  const int row = L.q * H + L.k;
-  const float wx = w_ih[row], bs = b_ih[row] + b_hh[row];
-  float wr[4];
-#pragma unroll
-  for (int m = 0; m < 4; ++m) wr[m] = w_hh[row * H + L.unit_rot(m)];
-  const int n = live ? min(lengths[bb], T) : 0;
-  int nmax = n;  // the wave runs to its longest row; finished rows hold their state
-#pragma unroll
-  for (int o = 16; o < 64; o <<= 1) nmax = max(nmax, __shfl_xor(nmax, o, kWave));
-  const int64_t* tr = traj + (int64_t)bb * ldt;
-  float* st = states ? states + (int64_t)bb * T * 2 * H : nullptr;
+  if (threadIdx.x >= 16) return;
+  const int r = threadIdx.x, k = r >> 2, q = r & 3, sg = ror_sign();
+  const int b = blockIdx.x;
+  Row4 R;
+  R.load(w_ih, w_hh, b_ih, b_hh, q, k, sg);
+  const int n = min(lengths[b], T);
+  const int32_t* x32 = reinterpret_cast<const int32_t*>(traj + (int64_t)b * ldt);  // ids < 2^31: low words
+  float* ck = states ? states + (int64_t)b * nblocks4(T) * 2 * kH4 + (q & 1) * kH4 + k : nullptr;
   float h = 0.0f, c = 0.0f;
-  float xc[kPre4], xn[kPre4];
+  auto step = [&](int32_t xi) {
+    const float a = R.act((float)xi, h, dppf<0x124>(h), dppf<0x128>(h), dppf<0x12C>(h));  // row_ror 4, 8, 12
+    const float ig = dppf<0x00>(a), fg = dppf<0x55>(a), gg = dppf<0xAA>(a), og = dppf<0xFF>(a);  // quad_perm
+    c = fmaf(fg, c, ig * gg);
+    h = og * ftanh(c);
+  };
+  auto ckpt = [&](int m) {
+    if (ck) ck[(int64_t)m * 2 * kH4] = (q & 1) ? c : h;
+  };
+  const int nb = n / kBlk4;
+  auto ldblk = [&](int32_t* dst, int m) {
+    if (nb == 0) return;  // no full block: nothing in the ring is read
+    const int32_t* p = x32 + 2 * kBlk4 * min(m, nb - 1);
 #pragma unroll
-  for (int i = 0; i < kPre4; ++i) xc[i] = i < n ? (float)tr[i] : 0.0f;
-  for (int t0 = 0; t0 < nmax; t0 += kPre4) {
+    for (int i = 0; i < kBlk4; ++i) dst[i] = p[2 * i];
+  };
+  auto runblk = [&](const int32_t* xs, int m) {
+    ckpt(m);
 #pragma unroll
-    for (int i = 0; i < kPre4; ++i) xn[i] = t0 + kPre4 + i < n ? (float)tr[t0 + kPre4 + i] : 0.0f;
-#pragma unroll
-    for (int i = 0; i < kPre4; ++i) {
-      const int t = t0 + i;
-      const float a = gate_act(gate_z(wx, bs, wr, xc[i], h), L.q);
-      const float ig = dppf<0x00>(a), fg = dppf<0x55>(a), gg = dppf<0xAA>(a), og = dppf<0xFF>(a);  // quad_perm
-      const float cn = fmaf(fg, c, ig * gg);
-      const float hn = og * ftanh(cn);
-      const bool act = t < n;
-      c = act ? cn : c;
-      h = act ? hn : h;
-      if (st != nullptr && act && L.q < 2) st[(int64_t)t * 2 * H + L.q * H + L.k] = L.q == 0 ? h : c;
-    }
-#pragma unroll
-    for (int i = 0; i < kPre4; ++i) xc[i] = xn[i];
+    for (int i = 0; i < kBlk4; ++i) step(xs[i]);
+  };
+  int32_t x0[kBlk4], x1[kBlk4], x2[kBlk4];
+  ldblk(x0, 0);
+  ldblk(x1, 1);
+  ldblk(x2, 2);
+  int m = 0;
+  for (; m + 3 <= nb; m += 3) {
+    runblk(x0, m);
+    ldblk(x0, m + 3);
+    runblk(x1, m + 1);
+    ldblk(x1, m + 4);
+    runblk(x2, m + 2);
+    ldblk(x2, m + 5);
   }
-  if (live && L.q == 0) h_last[(int64_t)b * H + L.k] = h;
+  if (m < nb) runblk(x0, m);
+  if (m + 1 < nb) runblk(x1, m + 1);
+  if (nb * kBlk4 < n) {
+    ckpt(nb);
+    for (int t = nb * kBlk4; t < n; ++t) step(x32[2 * t]);
+  }
+  if (q == 0) h_last[(int64_t)b * kH4 + k] = h;
 }
 
-__global__ __launch_bounds__(64) void k_lstm_bwd4(int32_t B, const int64_t* __restrict__ traj, int64_t ldt,
-                                                  const int32_t* __restrict__ lengths, int32_t T,
-                                                  const float* __restrict__ w_ih, const float* __restrict__ w_hh,
-                                                  const float* __restrict__ b_ih, const float* __restrict__ b_hh,
-                                                  const float* __restrict__ states,
-                                                  const float* __restrict__ dh_last, double* __restrict__ grad) {
-  constexpr int H = kH4, R = 4 * H, NG = 2 * R + R * H;
-  Lane4 L;
-  L.init();
-  const int b = blockIdx.x * 4 + (threadIdx.x >> 4);
-  const bool live = b < B;
-  const int bb = live ? b : B - 1;
-  const int row = L.q * H + L.k;
-  const float wx = w_ih[row], bs = b_ih[row] + b_hh[row];
-  float wr[4], wt[16];
+__device__ __forceinline__ void load_ckpt4(const float* ck, float* h, float* c) {
+  const float4 h4 = reinterpret_cast<const float4*>(ck)[0], c4 = reinterpret_cast<const float4*>(ck)[1];
+  h[0] = h4.x, h[1] = h4.y, h[2] = h4.z, h[3] = h4.w;
+  c[0] = c4.x, c[1] = c4.y, c[2] = c4.z, c[3] = c4.w;
+}
+
+// per step, A and B of each gate row: dz_{q,k} = A dh[k] + B dc+[k]; gamma of each unit
+__device__ __forceinline__ void adj_coef4(const float (*g)[4], const float* cp, const float* ct, float* A, float* Bc,
+                                          float* gam) {
 #pragma unroll
-  for (int m = 0; m < 4; ++m) wr[m] = w_hh[row * H + L.unit_rot(m)];
-#pragma unroll
-  for (int m = 0; m < 16; ++m) {  // W_hh[row of the lane row_ror(m) reads][k]
-    const int lr = L.lane_rot(m);
-    wt[m] = w_hh[((lr & 3) * H + (lr >> 2)) * H + L.k];
+  for (int k = 0; k < 4; ++k) {
+    const float i = g[0][k], f = g[1][k], gg = g[2][k], o = g[3][k];
+    const float tc = ftanh(ct[k]);
+    gam[k] = o * (1.0f - tc * tc);
+    const float ai = gg * i * (1.0f - i), af = cp[k] * f * (1.0f - f), ag = i * (1.0f - gg * gg);
+    A[0 * 4 + k] = ai * gam[k];
+    A[1 * 4 + k] = af * gam[k];
+    A[2 * 4 + k] = ag * gam[k];
+    A[3 * 4 + k] = tc * o * (1.0f - o);
+    Bc[0 * 4 + k] = ai;
+    Bc[1 * 4 + k] = af;
+    Bc[2 * 4 + k] = ag;
+    Bc[3 * 4 + k] = 0.0f;
   }
-  const int n = live ? min(lengths[bb], T) : 0;
-  int nmax = n;
+}
+
+// coef [B][T][16 lanes] float4 (a1, a2, f gamma, f) for chain lane (k, j), target u = (k - j) & 3
+__global__ __launch_bounds__(256) void k_lstm_coef4(const int64_t* __restrict__ traj, int64_t ldt,
+                                                    const int32_t* __restrict__ lengths, int32_t T,
+                                                    const float* __restrict__ w_ih, const float* __restrict__ w_hh,
+                                                    const float* __restrict__ b_ih, const float* __restrict__ b_hh,
+                                                    const float* __restrict__ states, float4* __restrict__ coef) {
+  const int sg = ror_sign();  // before any lane leaves
+  const int b = blockIdx.y;
+  const int n = min(lengths[b], T);
+  const int m = blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= nblocks4(n)) return;
+  Fwd4Step F;
+  F.load(w_ih, w_hh, b_ih, b_hh, sg);
+  float whh[64];
 #pragma unroll
-  for (int o = 16; o < 64; o <<= 1) nmax = max(nmax, __shfl_xor(nmax, o, kWave));
-  const int64_t* tr = traj + (int64_t)bb * ldt;
-  const float* st = states + (int64_t)bb * T * 2 * H;
-  float dh = live ? dh_last[(int64_t)b * H + L.k] : 0.0f, dc = 0.0f;
-  double gx = 0.0, gbias = 0.0, gh[4] = {0.0, 0.0, 0.0, 0.0};
-  // step t needs x_t, (h, c)_{t-1} of unit k, c_t of unit k; t descends from nmax - 1
-  auto ld = [&](int t, float& x, float& hp, float& cp) {
-    x = (t >= 0 && t < n) ? (float)tr[t] : 0.0f;
-    hp = (t >= 1 && t - 1 < n) ? st[(int64_t)(t - 1) * 2 * H + L.k] : 0.0f;
-    cp = (t >= 1 && t - 1 < n) ? st[(int64_t)(t - 1) * 2 * H + H + L.k] : 0.0f;
+  for (int e = 0; e < 64; ++e) whh[e] = w_hh[e];
+  float h[4], c[4];
+  load_ckpt4(states + ((int64_t)b * nblocks4(T) + m) * 8, h, c);
+  const int32_t* x32 = reinterpret_cast<const int32_t*>(traj + (int64_t)b * ldt);
+  float4* out = coef + ((int64_t)b * T + (int64_t)m * kBlk4) * 16;
+  const int steps = min(kBlk4, n - m * kBlk4);
+  for (int i = 0; i < steps; ++i) {
+    float cp[4] = {c[0], c[1], c[2], c[3]}, g[4][4];
+    F.step((float)x32[2 * (m * kBlk4 + i)], h, c, g, sg);
+    float A[16], Bc[16], gam[4];
+    adj_coef4(g, cp, c, A, Bc, gam);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int k = r >> 2, u = (k - (r & 3)) & 3;
+      float a1 = 0.0f, a2 = 0.0f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float wqu = whh[(q * 4 + k) * 4 + u];
+        a1 = fmaf(wqu, A[q * 4 + k], a1);
+        a2 = fmaf(wqu, Bc[q * 4 + k], a2);
+      }
+      out[i * 16 + r] = make_float4(a1, a2, g[1][k] * gam[k], g[1][k]);
+    }
+  }
+}
+
+// the adjoint chain; cka [B][ceil(T/16)][8] = (dh, dc+) entering step min(16m + 15, n - 1)
+template <bool PLUS>  // PLUS: row_ror:N hands lane i the value of lane i + N
+__device__ __forceinline__ void adj_chain4(const float4* __restrict__ cf, float* __restrict__ ck, int n, int r,
+                                           float dh, float dc) {
+  constexpr int N1 = PLUS ? 5 : 11, N2 = PLUS ? 10 : 6, N3 = PLUS ? 15 : 1;
+  const int j = r & 3;
+  float* ckl = ck + (j & 1) * 4 + (r >> 2);
+  auto step = [&](const float4 c) {
+    const float p = fmaf(c.x, dh, c.y * dc);
+    const float s = p + dppf<0x120 + N1>(p) + dppf<0x120 + N2>(p) + dppf<0x120 + N3>(p);
+    dc = fmaf(c.z, dh, c.w * dc);
+    dh = dppf<0x00>(s);  // quad_perm [0,0,0,0]
   };
-  float ct = (nmax - 1 < n && nmax >= 1) ? st[(int64_t)(nmax - 1) * 2 * H + H + L.k] : 0.0f;
-  float xc[kPre4], hc[kPre4], cc[kPre4], xn[kPre4], hn[kPre4], cn[kPre4];
+  auto ckpt = [&](int m) { ckl[(int64_t)m * 8] = (j & 1) ? dc : dh; };
+  const int nb = n / kBlk4;
+  if (nb * kBlk4 < n) {  // the partial top block first
+    ckpt(nb);
+    for (int t = n - 1; t >= nb * kBlk4; --t) step(cf[(int64_t)t * 16]);
+  }
+  auto ldblk = [&](float4* dst, int m) {  // coefficients of steps 16m + 15 .. 16m
+    if (nb == 0) return;
+    const float4* p = cf + (int64_t)max(m, 0) * kBlk4 * 16;
 #pragma unroll
-  for (int i = 0; i < kPre4; ++i) ld(nmax - 1 - i, xc[i], hc[i], cc[i]);
-  for (int t0 = nmax - 1; t0 >= 0; t0 -= kPre4) {
+    for (int i = 0; i < kBlk4; ++i) dst[i] = p[(kBlk4 - 1 - i) * 16];
+  };
+  auto runblk = [&](const float4* cs, int m) {
+    ckpt(m);
 #pragma unroll
-    for (int i = 0; i < kPre4; ++i) ld(t0 - kPre4 - i, xn[i], hn[i], cn[i]);
+    for (int i = 0; i < kBlk4; ++i) step(cs[i]);
+  };
+  float4 c0[kBlk4], c1[kBlk4], c2[kBlk4];
+  ldblk(c0, nb - 1);
+  ldblk(c1, nb - 2);
+  ldblk(c2, nb - 3);
+  int m = nb - 1;
+  for (; m >= 2; m -= 3) {
+    runblk(c0, m);
+    ldblk(c0, m - 3);
+    runblk(c1, m - 1);
+    ldblk(c1, m - 4);
+    runblk(c2, m - 2);
+    ldblk(c2, m - 5);
+  }
+  if (m >= 0) runblk(c0, m);
+  if (m >= 1) runblk(c1, m - 1);
+}
+
+__global__ __launch_bounds__(64) void k_lstm_adj4(const int32_t* __restrict__ lengths, int32_t T,
+                                                  const float* __restrict__ dh_last, const float4* __restrict__ coef,
+                                                  float* __restrict__ cka) {
+  if (threadIdx.x >= 16) return;
+  const int r = threadIdx.x, b = blockIdx.x;
+  const int n = min(lengths[b], T);
+  const float4* cf = coef + (int64_t)b * T * 16 + r;
+  float* ck = cka + (int64_t)b * nblocks4(T) * 8;
+  const float dh = dh_last[(int64_t)b * kH4 + (r >> 2)];
+  if (ror_sign() == 1)
+    adj_chain4<true>(cf, ck, n, r, dh, 0.0f);
+  else
+    adj_chain4<false>(cf, ck, n, r, dh, 0.0f);
+}
+
+// gradient partial rows [B][kGrad4Blocks][96]: block-strided threads, fp64 sums, fixed-order reductions
+__global__ __launch_bounds__(kGrad4NT) void k_lstm_grad4(const int64_t* __restrict__ traj, int64_t ldt,
+                                                         const int32_t* __restrict__ lengths, int32_t T,
+                                                         const float* __restrict__ w_ih, const float* __restrict__ w_hh,
+                                                         const float* __restrict__ b_ih, const float* __restrict__ b_hh,
+                                                         const float* __restrict__ states,
+                                                         const float* __restrict__ cka, double* __restrict__ part) {
+  __shared__ double red[kGrad4NT / kWave][kNG4];
+  const int sg = ror_sign();
+  const int b = blockIdx.y;
+  const int n = min(lengths[b], T);
+  Fwd4Step F;
+  F.load(w_ih, w_hh, b_ih, b_hh, sg);
+  float whh[64];
 #pragma unroll
-    for (int i = 0; i < kPre4; ++i) {
-      const int t = t0 - i;
-      if (t < 0) break;  // wave-uniform
-      const float x = xc[i], hp = hc[i], cp = cc[i];
-      const float a = gate_act(gate_z(wx, bs, wr, x, hp), L.q);
-      const float ig = dppf<0x00>(a), fg = dppf<0x55>(a), gg = dppf<0xAA>(a), og = dppf<0xFF>(a);
-      const float tc = ftanh(ct);
-      const float dcc = fmaf(dh * og, 1.0f - tc * tc, dc);
-      const float P = L.q == 0 ? dcc * gg : (L.q == 1 ? dcc * cp : (L.q == 2 ? dcc * ig : dh * tc));
-      const float D = L.q == 2 ? 1.0f - a * a : a * (1.0f - a);
-      const bool act = t < n;
-      const float da = act ? P * D : 0.0f;
-      // dh_{t-1}[k] = sum over the 16 gate rows of W_hh[row][k] * da_row
-      float v = wt[0] * da;
-      v = fmaf(wt[1], dppf<0x121>(da), v);
-      v = fmaf(wt[2], dppf<0x122>(da), v);
-      v = fmaf(wt[3], dppf<0x123>(da), v);
-      v = fmaf(wt[4], dppf<0x124>(da), v);
-      v = fmaf(wt[5], dppf<0x125>(da), v);
-      v = fmaf(wt[6], dppf<0x126>(da), v);
-      v = fmaf(wt[7], dppf<0x127>(da), v);
-      v = fmaf(wt[8], dppf<0x128>(da), v);
-      v = fmaf(wt[9], dppf<0x129>(da), v);
-      v = fmaf(wt[10], dppf<0x12A>(da), v);
-      v = fmaf(wt[11], dppf<0x12B>(da), v);
-      v = fmaf(wt[12], dppf<0x12C>(da), v);
-      v = fmaf(wt[13], dppf<0x12D>(da), v);
-      v = fmaf(wt[14], dppf<0x12E>(da), v);
-      v = fmaf(wt[15], dppf<0x12F>(da), v);
-      const float h1 = dppf<0x124>(hp), h2 = dppf<0x128>(hp), h3 = dppf<0x12C>(hp);
-      const double dd = (double)da;
-      gx = fma(dd, (double)x, gx);
-      gbias += dd;
-      gh[0] = fma(dd, (double)hp, gh[0]);
-      gh[1] = fma(dd, (double)h1, gh[1]);
-      gh[2] = fma(dd, (double)h2, gh[2]);
-      gh[3] = fma(dd, (double)h3, gh[3]);
-      dc = act ? dcc * fg : dc;
-      dh = act ? v : dh;
-      ct = act || t - 1 < n ? cp : ct;
+  for (int e = 0; e < 64; ++e) whh[e] = w_hh[e];
+  const int32_t* x32 = reinterpret_cast<const int32_t*>(traj + (int64_t)b * ldt);
+  const int nbt = nblocks4(T);
+  double gi[16], gb[16], gh[64];
+#pragma unroll
+  for (int e = 0; e < 16; ++e) gi[e] = gb[e] = 0.0;
+#pragma unroll
+  for (int e = 0; e < 64; ++e) gh[e] = 0.0;
+  for (int m = blockIdx.x * kGrad4NT + threadIdx.x; m < nblocks4(n); m += kGrad4Blocks * kGrad4NT) {
+    const int t0 = m * kBlk4, steps = min(kBlk4, n - t0);
+    float hs[kBlk4 + 1][4], cs[kBlk4 + 1][4], xs[kBlk4];
+    load_ckpt4(states + ((int64_t)b * nbt + m) * 8, hs[0], cs[0]);
+#pragma unroll
+    for (int i = 0; i < kBlk4; ++i) {
+      if (i < steps) {
+        float g[4][4];
+        xs[i] = (float)x32[2 * (t0 + i)];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) hs[i + 1][k] = hs[i][k], cs[i + 1][k] = cs[i][k];
+        F.step(xs[i], hs[i + 1], cs[i + 1], g, sg);
+      }
     }
+    float dh[4], dc[4];
+    load_ckpt4(cka + ((int64_t)b * nbt + m) * 8, dh, dc);
 #pragma unroll
-    for (int i = 0; i < kPre4; ++i) {
-      xc[i] = xn[i];
-      hc[i] = hn[i];
-      cc[i] = cn[i];
+    for (int i = kBlk4 - 1; i >= 0; --i) {
+      if (i < steps) {
+        float hh[4] = {hs[i][0], hs[i][1], hs[i][2], hs[i][3]}, cc[4] = {cs[i][0], cs[i][1], cs[i][2], cs[i][3]};
+        float g[4][4];
+        F.step(xs[i], hh, cc, g, sg);  // gates of step t0 + i (h, c of step t0 + i - 1 in)
+        float A[16], Bc[16], gam[4];
+        adj_coef4(g, cs[i], cs[i + 1], A, Bc, gam);
+        float dz[16];
+#pragma unroll
+        for (int row = 0; row < 16; ++row) {
+          const int k = row & 3;
+          dz[row] = fmaf(A[row], dh[k], Bc[row] * dc[k]);
+          const double dd = (double)dz[row];
+          gi[row] = fma(dd, (double)xs[i], gi[row]);
+          gb[row] += dd;
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) gh[row * 4 + jj] = fma(dd, (double)hs[i][jj], gh[row * 4 + jj]);
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          float v = 0.0f;
+#pragma unroll
+          for (int row = 0; row < 16; ++row) v = fmaf(whh[row * 4 + k], dz[row], v);
+          dc[k] = fmaf(g[1][k] * gam[k], dh[k], g[1][k] * dc[k]);
+          dh[k] = v;
+        }
+      }
     }
   }
-  if (live) {
-    double* g = grad + (int64_t)b * NG;
-    g[row] = gx;
+  const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
+  auto wsum = [&](double v) {
 #pragma unroll
-    for (int m = 0; m < 4; ++m) g[R + row * H + L.unit_rot(m)] = gh[m];
-    g[R + R * H + row] = gbias;
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+    return v;
+  };
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const double a = wsum(gi[e]), c = wsum(gb[e]);
+    if (lane == 0) red[wv][e] = a, red[wv][80 + e] = c;
   }
+#pragma unroll
+  for (int e = 0; e < 64; ++e) {
+    const double a = wsum(gh[e]);
+    if (lane == 0) red[wv][16 + e] = a;
+  }
+  __syncthreads();
+  if (threadIdx.x < kNG4) {
+    double s = 0.0;
+#pragma unroll
+    for (int v = 0; v < kGrad4NT / kWave; ++v) s += red[v][threadIdx.x];
+    part[((int64_t)b * kGrad4Blocks + blockIdx.x) * kNG4 + threadIdx.x] = s;
+  }
+}
+
+__global__ __launch_bounds__(128) void k_lstm_gsum4(const double* __restrict__ part, double* __restrict__ grad) {
+  const int b = blockIdx.x, e = threadIdx.x;
+  if (e >= kNG4) return;
+  double s = 0.0;
+  for (int i = 0; i < kGrad4Blocks; ++i) s += part[((int64_t)b * kGrad4Blocks + i) * kNG4 + e];
+  grad[(int64_t)b * kNG4 + e] = s;
 }
 
 }  // namespace
@@ -623,6 +826,11 @@ extern "C" int spai_logp_grad(const float* logits, int64_t bstride, int32_t E, i
   return SPAI_OK;
 }
 
+extern "C" size_t spai_lstm_states_floats(int32_t B, int32_t H, int32_t T) {
+  if (B <= 0 || T <= 0 || H <= 0) return 0;
+  return H == kH4 ? (size_t)B * ((T + kBlk4 - 1) / kBlk4) * 2 * H : (size_t)B * T * 2 * H;
+}
+
 extern "C" int spai_lstm_forward(int32_t B, int32_t H, const int64_t* traj, int64_t ldt, const int32_t* lengths,
                                  int32_t T, const float* w_ih, const float* w_hh, const float* b_ih,
                                  const float* b_hh, float* h_last, float* states, void* stream) {
@@ -632,7 +840,7 @@ extern "C" int spai_lstm_forward(int32_t B, int32_t H, const int64_t* traj, int6
   const int g = (B + kLstmNT - 1) / kLstmNT;
   switch (H) {
     case 2: k_lstm_fwd<2><<<g, kLstmNT, 0, s>>>(B, traj, ldt, lengths, T, w_ih, w_hh, b_ih, b_hh, h_last, states); break;
-    case 4: k_lstm_fwd4<<<(B + 3) / 4, 64, 0, s>>>(B, traj, ldt, lengths, T, w_ih, w_hh, b_ih, b_hh, h_last, states); break;
+    case 4: k_lstm_fwd4<<<B, 64, 0, s>>>(traj, ldt, lengths, T, w_ih, w_hh, b_ih, b_hh, h_last, states); break;
     case 8: k_lstm_fwd<8><<<g, kLstmNT, 0, s>>>(B, traj, ldt, lengths, T, w_ih, w_hh, b_ih, b_hh, h_last, states); break;
     default:
       set_error("spai_lstm_forward: hidden_dim %d not compiled (2, 4, 8)", H);
@@ -642,10 +850,25 @@ extern "C" int spai_lstm_forward(int32_t B, int32_t H, const int64_t* traj, int6
   return SPAI_OK;
 }
 
+// H = 4 backward workspace: chain coefficients, adjoint checkpoints, per-block gradient rows
+static size_t lstm4_ws(int32_t B, int32_t T, float4** coef, float** adj, double** part, void* base) {
+  Carve c(base);
+  float4* cf = c.take<float4>((size_t)B * T * 16);
+  float* ad = c.take<float>((size_t)B * ((T + kBlk4 - 1) / kBlk4) * 8);
+  double* pt = c.take<double>((size_t)B * kGrad4Blocks * kNG4);
+  if (coef) *coef = cf, *adj = ad, *part = pt;
+  return c.off;
+}
+
+extern "C" size_t spai_lstm_backward_workspace_bytes(int32_t B, int32_t H, int32_t T) {
+  if (H != kH4 || B <= 0 || T <= 0) return 0;
+  return lstm4_ws(B, T, nullptr, nullptr, nullptr, nullptr);
+}
+
 extern "C" int spai_lstm_backward(int32_t B, int32_t H, const int64_t* traj, int64_t ldt, const int32_t* lengths,
                                   int32_t T, const float* w_ih, const float* w_hh, const float* b_ih,
                                   const float* b_hh, const float* states, const float* dh_last, double* grad,
-                                  void* stream) {
+                                  void* workspace, size_t workspace_bytes, void* stream) {
   SPAI_CHECK_ARG(traj && lengths && w_ih && w_hh && b_ih && b_hh && states && dh_last && grad,
                  "spai_lstm_backward: null pointer");
   SPAI_CHECK_ARG(B > 0 && T > 0 && ldt >= T, "spai_lstm_backward: bad shape B=%d T=%d", B, T);
@@ -653,7 +876,20 @@ extern "C" int spai_lstm_backward(int32_t B, int32_t H, const int64_t* traj, int
   const int g = B;  // one block per sample
   switch (H) {
     case 2: k_lstm_bwd<2><<<g, kLstmNT, 0, s>>>(B, traj, ldt, lengths, T, w_ih, w_hh, b_ih, b_hh, states, dh_last, grad); break;
-    case 4: k_lstm_bwd4<<<(B + 3) / 4, 64, 0, s>>>(B, traj, ldt, lengths, T, w_ih, w_hh, b_ih, b_hh, states, dh_last, grad); break;
+    case 4: {
+      SPAI_CHECK_ARG(workspace && workspace_bytes >= spai_lstm_backward_workspace_bytes(B, H, T),
+                     "spai_lstm_backward: workspace too small");
+      float4* coef;
+      float* adj;
+      double* part;
+      lstm4_ws(B, T, &coef, &adj, &part, workspace);
+      k_lstm_coef4<<<dim3((T + 255) / 256, B), 256, 0, s>>>(traj, ldt, lengths, T, w_ih, w_hh, b_ih, b_hh, states, coef);
+      k_lstm_adj4<<<B, 64, 0, s>>>(lengths, T, dh_last, coef, adj);
+      k_lstm_grad4<<<dim3(kGrad4Blocks, B), kGrad4NT, 0, s>>>(traj, ldt, lengths, T, w_ih, w_hh, b_ih, b_hh, states,
+                                                              adj, part);
+      k_lstm_gsum4<<<B, 128, 0, s>>>(part, grad);
+      break;
+    }
     case 8: k_lstm_bwd<8><<<g, kLstmNT, 0, s>>>(B, traj, ldt, lengths, T, w_ih, w_hh, b_ih, b_hh, states, dh_last, grad); break;
     default:
       set_error("spai_lstm_backward: hidden_dim %d not compiled (2, 4, 8)", H);

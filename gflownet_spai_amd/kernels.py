@@ -243,14 +243,16 @@ def _lstm_params(w_ih, w_hh, b_ih, b_hh):
 
 
 def lstm_forward(traj: torch.Tensor, lengths: torch.Tensor, w_ih, w_hh, b_ih, b_hh, keep_states: bool = False):
-    """(h_last [B, H], states [B, T, 2H] or None) of nn.LSTM(1, H) over each row's first lengths[b] ids."""
+    """(h_last [B, H], states or None) of nn.LSTM(1, H) over each row's first lengths[b] ids; states
+    is the flat buffer spai_lstm_backward reads (per-step (h, c), or 16-step checkpoints for H = 4)."""
     _lib.require_device(traj)
     H, ps = _lstm_params(w_ih, w_hh, b_ih, b_hh)
     tr = traj if traj.dtype == torch.int64 and traj.stride(1) == 1 else traj.to(torch.int64).contiguous()
     B, T = tr.shape
     n = lengths.to(device=tr.device, dtype=torch.int32).contiguous()
     h = torch.empty(B, H, dtype=torch.float32, device=tr.device)
-    states = torch.empty(B, T, 2 * H, dtype=torch.float32, device=tr.device) if keep_states else None
+    states = (torch.empty(_l().spai_lstm_states_floats(B, H, T), dtype=torch.float32, device=tr.device)
+              if keep_states else None)
     with _timed("lstm_forward"):
         st = _l().spai_lstm_forward(B, H, _lib.ptr(tr), tr.stride(0), _lib.ptr(n), T, *[_lib.ptr(p) for p in ps],
                                     _lib.ptr(h), _lib.ptr(states), _lib.stream_ptr(tr.device))
@@ -264,13 +266,16 @@ def lstm_backward(traj: torch.Tensor, lengths: torch.Tensor, w_ih, w_hh, b_ih, b
     H, ps = _lstm_params(w_ih, w_hh, b_ih, b_hh)
     tr = traj if traj.dtype == torch.int64 and traj.stride(1) == 1 else traj.to(torch.int64).contiguous()
     B, T = tr.shape
-    if states is None or states.shape != (B, T, 2 * H):
-        raise ValueError("lstm_backward needs the forward's states [B, T, 2H]")
+    if states is None or states.numel() != _l().spai_lstm_states_floats(B, H, T):
+        raise ValueError("lstm_backward needs the states buffer of lstm_forward(keep_states=True) for this B, H, T")
     n = lengths.to(device=tr.device, dtype=torch.int32).contiguous()
     dh = dh_last.detach().float().contiguous()
     g = torch.empty(B, 8 * H + 4 * H * H, dtype=torch.float64, device=tr.device)
+    nws = _l().spai_lstm_backward_workspace_bytes(B, H, T)
+    ws = _lib.workspace(nws, tr.device, "lstm_backward") if nws else None
     with _timed("lstm_backward"):
         st = _l().spai_lstm_backward(B, H, _lib.ptr(tr), tr.stride(0), _lib.ptr(n), T, *[_lib.ptr(p) for p in ps],
-                                     _lib.ptr(states), _lib.ptr(dh), _lib.ptr(g), _lib.stream_ptr(tr.device))
+                                     _lib.ptr(states), _lib.ptr(dh), _lib.ptr(g), _lib.ptr(ws), nws,
+                                     _lib.stream_ptr(tr.device))
     _lib.check(st, "spai_lstm_backward")
     return g

@@ -208,16 +208,23 @@ int spai_logp_grad(const float* logits, int64_t bstride, int32_t E, int32_t B, c
 
 /* BackwardPolicy's LSTM (policy.py:75-129; nn.LSTM(1, H), gate order i, f, g, o): input
  * x_t = (float)traj[b][t] for t < lengths[b] (the entries != -1, as pack_padded_sequence
- * takes them).  Forward: h_last [B][H] and, when states != NULL, (h_t, c_t) of every step in
- * states [B][T][2H].  Backward (BPTT from dh_last [B][H], dc = 0 at the end): one fp64 row
+ * takes them).  Forward: h_last [B][H] and, when states != NULL, what the backward needs in
+ * states (spai_lstm_states_floats(B, H, T) floats): (h_t, c_t) of every step, [B][T][2H], for
+ * H = 2, 8; for H = 4 the (h, c) checkpoint entering every 16-step block, [B][ceil(T/16)][2H]
+ * (the backward recomputes the steps inside a block bit for bit).  Backward (BPTT from dh_last [B][H], dc = 0 at the end): one fp64 row
  * per sample in grad [B][4H + 4H*H + 4H] = d w_ih [4H] | d w_hh [4H][H] | d bias [4H]
- * (d b_ih = d b_hh = d bias).  H in {2, 4, 8}. */
+ * (d b_ih = d b_hh = d bias).  H in {2, 4, 8}.  H = 4 runs the adjoint as a linear recurrence
+ * over per-step coefficients kept in the workspace (spai_lstm_backward_workspace_bytes:
+ * 288 B per (sample, step) + 48 KB per sample; 0 for H = 2, 8, where workspace may be NULL). */
+size_t spai_lstm_backward_workspace_bytes(int32_t B, int32_t H, int32_t T);
+size_t spai_lstm_states_floats(int32_t B, int32_t H, int32_t T);
 int spai_lstm_forward(int32_t B, int32_t H, const int64_t* traj, int64_t ldt, const int32_t* lengths, int32_t T,
                       const float* w_ih, const float* w_hh, const float* b_ih, const float* b_hh, float* h_last,
                       float* states, void* stream);
 int spai_lstm_backward(int32_t B, int32_t H, const int64_t* traj, int64_t ldt, const int32_t* lengths, int32_t T,
                        const float* w_ih, const float* w_hh, const float* b_ih, const float* b_hh,
-                       const float* states, const float* dh_last, double* grad, void* stream);
+                       const float* states, const float* dh_last, double* grad, void* workspace,
+                       size_t workspace_bytes, void* stream);
 
 /* ---------------------------------------------------------------- rewards
  * residual[b] = sqrt(res2[b]) and reward[b] = 1000 * (alpha (1 - r/r0) + (1 - alpha)(1 - f/f0))

@@ -132,13 +132,18 @@ def _lstm_case(H, B, T, lens, hi, seed):
     return lstm, traj
 
 
-@pytest.mark.parametrize("H", [2, 4, 8])
-def test_lstm_forward_backward_vs_oracle(H):
+@pytest.mark.parametrize("H,hi,lens", [(2, 100, None), (4, 100, None), (8, 100, None),
+                                       # action-id-sized inputs (gates saturate, a cell counts steps)
+                                       (4, 5_000_000, None),
+                                       # block edges of the H = 4 checkpointed path (16-step blocks)
+                                       (4, 1000, [16, 15, 17, 47, 48, 49, 32, 2])])
+def test_lstm_forward_backward_vs_oracle(H, hi, lens):
     from gflownet_spai_amd import kernels
 
-    B, T = 5, 3000
-    lens = [T, 2999, 1500, 64, 1]
-    lstm, traj = _lstm_case(H, B, T, lens, 100, H)
+    T = 3000 if lens is None else max(lens)
+    lens = lens or [T, 2999, 1500, 64, 1]
+    B = len(lens)
+    lstm, traj = _lstm_case(H, B, T, lens, hi, H)
     P = [lstm.weight_ih_l0, lstm.weight_hh_l0, lstm.bias_ih_l0, lstm.bias_hh_l0]
     Pd = [p.detach().to(DEV) for p in P]
     tr = torch.tensor(traj, device=DEV)

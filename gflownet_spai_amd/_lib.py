@@ -21,7 +21,7 @@ if os.environ.get("SPAI_LIB_VARIANT"):  # A/B timing of kernel variants built un
 SPAI_OK, SPAI_ERR_INVALID, SPAI_ERR_HIP, SPAI_ERR_UNSUPPORTED = 0, 1, 2, 3
 FILL_COPY, FILL_LSQ = 0, 1
 DTYPE_F32, DTYPE_F64 = 0, 1
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 _c_i32, _c_i64, _c_u64, _c_sz, _c_p = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_size_t, ctypes.c_void_p
 
@@ -59,6 +59,8 @@ SIGNATURES = {
                                       _c_i64, _c_p, _c_i32, _c_p, _c_p, _c_sz, _c_p]),
     "spai_lstm_forward": (ctypes.c_int, [_c_i32, _c_i32, _c_p, _c_i64, _c_p, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_p,
                                          _c_p, _c_p]),
+    "spai_mtx_header": (ctypes.c_int, [ctypes.c_char_p, _c_p, _c_p]),
+    "spai_mtx_read": (ctypes.c_int, [ctypes.c_char_p, _c_p, _c_p, _c_p, _c_i64, _c_i32, _c_p]),
     "spai_lstm_states_floats": (_c_sz, [_c_i32, _c_i32, _c_i32]),
     "spai_lstm_backward_workspace_bytes": (_c_sz, [_c_i32, _c_i32, _c_i32]),
     "spai_lstm_backward": (ctypes.c_int, [_c_i32, _c_i32, _c_p, _c_i64, _c_p, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_p,

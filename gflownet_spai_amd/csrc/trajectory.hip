@@ -463,7 +463,7 @@ void k_tile(const float* __restrict__ logits, int64_t bstride, int32_t E,
   const uint32_t bg = (uint32_t)(sample_base + b);
   const int nb = nb_[b];
   // splitter tables (consumed only after the keys; their latency hides behind the Philox work)
-  static_assert(kBins * 2 == 512 * 16 && kMaxB * 4 == 512 * 16 && kGrpNT % 512 == 0 || kGrpNT == 512,
+  static_assert((kBins * 2 == 512 * 16 && kMaxB * 4 == 512 * 16 && kGrpNT % 512 == 0) || kGrpNT == 512,
                 "prologue vector widths");
   for (int i = tid; i < 1024; i += kGrpNT) {
     if (i < 512)

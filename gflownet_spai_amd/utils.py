@@ -1,6 +1,8 @@
 """Host-side helpers with the reference's names (reference: gflownet/utils.py)."""
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 from torch import Tensor
@@ -18,13 +20,62 @@ def trajectory_balance_loss(total_flow: Tensor, rewards: Tensor, fwd_probs: Tens
     return (lhs - rhs).pow(2).mean()
 
 
-def market_matrix_to_sparse_tensor(file_path: str) -> Tensor:
-    """gflownet/utils.py:54-63: Matrix Market file -> fp64 COO tensor (raw file order)."""
-    import scipy.io
+def read_mtx(file_path: str, threads: int = 0):
+    """Matrix Market file -> (rows, cols, values float64, shape) host arrays in the order of
+    scipy.io.mmread(path).tocoo(), parsed by the native multi-threaded reader (spai_mtx_read)."""
+    import ctypes
 
-    m = scipy.io.mmread(file_path).tocoo()
-    idx = torch.from_numpy(np.vstack([m.row, m.col]).astype(np.int64))
-    return torch.sparse_coo_tensor(idx, torch.from_numpy(m.data.astype(np.float64)), m.shape)
+    from . import _lib
+
+    lib = _lib.load()
+    path = os.fsencode(file_path)
+    dims = np.zeros(4, np.int64)
+    kinds = np.zeros(2, np.int32)
+    _lib.check(lib.spai_mtx_header(path, dims.ctypes.data_as(ctypes.c_void_p), kinds.ctypes.data_as(ctypes.c_void_p)),
+               "spai_mtx_header")
+    cap = int(dims[3])
+    rows, cols = np.empty(cap, np.int64), np.empty(cap, np.int64)
+    vals = np.empty(cap, np.float64)
+    nnz = ctypes.c_int64(0)
+    _lib.check(lib.spai_mtx_read(path, rows.ctypes.data_as(ctypes.c_void_p), cols.ctypes.data_as(ctypes.c_void_p),
+                                 vals.ctypes.data_as(ctypes.c_void_p), cap, int(threads), ctypes.byref(nnz)),
+               "spai_mtx_read")
+    k = nnz.value
+    return rows[:k], cols[:k], vals[:k], (int(dims[0]), int(dims[1]))
+
+
+def market_matrix_to_sparse_tensor(file_path: str) -> Tensor:
+    """gflownet/utils.py:54-63: Matrix Market file -> fp64 COO tensor (uncoalesced, in mmread's
+    raw order, which defines the action ids), read by the native parser."""
+    rows, cols, vals, shape = read_mtx(file_path)
+    idx = torch.from_numpy(np.vstack([rows, cols]))
+    return torch.sparse_coo_tensor(idx, torch.from_numpy(vals), shape)
+
+
+def load_mtx_file(file_path: str):
+    """GFlowNet100.py:44-46: csr_matrix(mmread(path)) (scipy CSR, duplicates summed), from the
+    native reader."""
+    import scipy.sparse as sp
+
+    rows, cols, vals, shape = read_mtx(file_path)
+    return sp.csr_matrix((vals, (rows, cols)), shape=shape)
+
+
+def lu_candidate_matrix(A) -> Tensor:
+    """GFlowNet100.py:126-153: the candidate pattern the driver samples from.  spilu(A) with
+    scipy's defaults (SuperLU ILUTP), L = tril(ilu.L), U = triu(ilu.U), LU = L @ U (the factors in
+    SuperLU's permuted order, as the driver takes them), as an fp32 COO tensor in LU.tocoo()
+    order.  One-time host preprocessing, as in the reference; the rollout then runs on the GPU
+    with this tensor as initial_matrix = original_matrix (GFlowNet100.py:173)."""
+    import scipy.sparse as sp
+    import scipy.sparse.linalg as spla
+
+    ilu = spla.spilu(sp.csc_matrix(A))
+    L = sp.tril(ilu.L, format="csr")
+    U = sp.triu(ilu.U, format="csr")
+    coo = (L @ U).tocoo()
+    idx = torch.from_numpy(np.vstack((coo.row, coo.col)).astype(np.int64))
+    return torch.sparse_coo_tensor(idx, torch.from_numpy(coo.data.astype(np.float32)), coo.shape)
 
 
 def poisson_2d(grid: int, dtype=torch.float32) -> Tensor:

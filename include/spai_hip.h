@@ -234,6 +234,27 @@ int spai_lstm_backward(int32_t B, int32_t H, const int64_t* traj, int64_t ldt, c
 int spai_rewards(const double* res2, const int32_t* removed_counts, int32_t B, int64_t nnz0, int32_t n,
                  double r0, double f0, const float* alpha, double* residual, double* reward, void* stream);
 
+/* ---------------------------------------------------------------- Matrix Market ingest (host)
+ * gflownet/utils.py:54-63 market_matrix_to_sparse_tensor / GFlowNet100.py:44-46 load_mtx_file:
+ * scipy.io.mmread(path).tocoo().  Coordinate format; field real / integer / pattern; symmetry
+ * general / symmetric / skew-symmetric.  The COO written is mmread's entry for entry: the file
+ * entries in file order (0-based), then the mirror (j, i) of every off-diagonal entry of a
+ * (skew-)symmetric file in file order (value negated for skew), i.e. the raw order that defines
+ * the action ids (preconditioner.py:23-25).  Host memory, no GPU.
+ * spai_mtx_header: dims = {rows, cols, file entries, capacity spai_mtx_read needs},
+ *                  kinds = {SPAI_MTX_REAL | _INTEGER | _PATTERN, SPAI_MTX_GENERAL | _SYMMETRIC | _SKEW}.
+ * spai_mtx_read:   fills row/col (int64) and val (double), *nnz_out = entries written;
+ *                  threads <= 0 = all hardware threads. */
+#define SPAI_MTX_REAL 0
+#define SPAI_MTX_INTEGER 1
+#define SPAI_MTX_PATTERN 2
+#define SPAI_MTX_GENERAL 0
+#define SPAI_MTX_SYMMETRIC 1
+#define SPAI_MTX_SKEW 2
+int spai_mtx_header(const char* path, int64_t* dims, int32_t* kinds);
+int spai_mtx_read(const char* path, int64_t* row, int64_t* col, double* val, int64_t capacity, int32_t threads,
+                  int64_t* nnz_out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -234,6 +234,13 @@ int spai_lstm_backward(int32_t B, int32_t H, const int64_t* traj, int64_t ldt, c
 int spai_rewards(const double* res2, const int32_t* removed_counts, int32_t B, int64_t nnz0, int32_t n,
                  double r0, double f0, const float* alpha, double* residual, double* reward, void* stream);
 
+/* ---------------------------------------------------------------- Krylov evaluation
+ * y = A x (fp64 x, y; fp32 or fp64 values) over row-ELL lines idx/val [n][W] (-1 = padding),
+ * slot order, fp64 fma: the products of GFlowNet100.py:61-93's GMRES (A v and the SPAI M v),
+ * driven by gflownet_spai_amd/gmres.py. */
+int spai_ell_spmv(int32_t n, int32_t W, const int32_t* idx, const void* val, int32_t val_dtype, const double* x,
+                  double* y, void* stream);
+
 /* ---------------------------------------------------------------- Matrix Market ingest (host)
  * gflownet/utils.py:54-63 market_matrix_to_sparse_tensor / GFlowNet100.py:44-46 load_mtx_file:
  * scipy.io.mmread(path).tocoo().  Coordinate format; field real / integer / pattern; symmetry

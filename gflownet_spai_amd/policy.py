@@ -25,6 +25,16 @@ from torch import Tensor, nn
 from . import _lib, kernels
 
 
+def _small_linear(x: Tensor, weight: Tensor, bias: Tensor | None) -> Tensor:
+    """nn.Linear for a small input width, as in_features broadcast multiply-adds."""
+    out = weight[:, 0].unsqueeze(0) * x[:, 0:1]
+    if bias is not None:
+        out = out + bias
+    for k in range(1, x.shape[1]):
+        out = torch.addcmul(out, x[:, k:k + 1], weight[:, k].unsqueeze(0))
+    return out
+
+
 class GATv2Layer(nn.Module):
     def __init__(self, in_channels: int, out_channels: int, heads: int = 1, edge_dim: int = 1,
                  negative_slope: float = 0.2):
@@ -51,9 +61,12 @@ class GATv2Layer(nn.Module):
         loop_attr = torch.zeros(n, 1, device=x.device, dtype=x.dtype).index_add_(0, dst, ea) / deg.clamp(min=1).view(-1, 1)
         ar = torch.arange(n, device=x.device)
         src, dst, ea = torch.cat([src, ar]), torch.cat([dst, ar]), torch.cat([ea, loop_attr])
-        xl = self.lin_l(x).view(n, self.h, self.c)
-        xr = self.lin_r(x).view(n, self.h, self.c)
-        e = F.leaky_relu(xl[src] + xr[dst] + self.lin_edge(ea).view(-1, self.h, self.c), self.slope)
+        # the three linears as broadcast multiply-adds (K = in_channels <= 16, edge_dim 1): the
+        # BLAS tiles these skinny GEMMs badly (~8 ms each at C4), elementwise they are bandwidth
+        xl = _small_linear(x, self.lin_l.weight, self.lin_l.bias).view(n, self.h, self.c)
+        xr = _small_linear(x, self.lin_r.weight, self.lin_r.bias).view(n, self.h, self.c)
+        xe = _small_linear(ea, self.lin_edge.weight, None).view(-1, self.h, self.c)
+        e = F.leaky_relu(xl[src] + xr[dst] + xe, self.slope)
         score = (e * self.att).sum(-1)  # [E', H]
         smax = torch.full((n, self.h), float("-inf"), device=x.device, dtype=score.dtype)
         smax = smax.scatter_reduce(0, dst.view(-1, 1).expand_as(score), score, reduce="amax", include_self=True)
@@ -97,6 +110,17 @@ def graph_csr(x: Tensor, edge_index: Tensor, edge_attr: Tensor):
     rowptr = torch.zeros(n + 1, dtype=torch.int32, device=dev)
     rowptr[1:] = torch.cumsum(torch.bincount(dst, minlength=n), 0).to(torch.int32)
     return rowptr, src[order].to(torch.int32).contiguous(), ea[order].contiguous()
+
+
+def skinny_linear(h: Tensor, weight: Tensor, bias: Tensor, width: int) -> Tensor:
+    """nn.Linear(h)[:, :width] for a short hidden size: the first ``width`` output columns only,
+    as hid broadcast multiply-adds over [rows, width] (bandwidth-bound elementwise work, and so
+    is its autograd), instead of a full [rows, max_num_actions] GEMM whose skinny shape
+    (K = hid = 4) the BLAS tiles badly."""
+    out = bias[:width].unsqueeze(0).expand(h.shape[0], width)
+    for k in range(h.shape[1]):
+        out = torch.addcmul(out, h[:, k:k + 1], weight[:width, k].unsqueeze(0))
+    return out
 
 
 def _pack(layer: GATv2Layer) -> Tensor:
@@ -159,7 +183,7 @@ class ForwardPolicy(BasePolicy):
         x = torch.relu(self.gat1(x, edge_index, edge_attr))
         x = torch.relu(self.gat2(x, edge_index, edge_attr))
         x = x.mean(dim=0, keepdim=True)
-        return self.fc(x)[:, :num_actions], torch.sigmoid(self.alpha)
+        return skinny_linear(x, self.fc.weight, self.fc.bias, num_actions), torch.sigmoid(self.alpha)
 
     def _graph(self, data):
         x, ei = data.x, data.edge_index
@@ -264,9 +288,9 @@ class BackwardPolicy(nn.Module):
         self.fc = nn.Linear(hidden_dim, max_num_actions)
 
     def _head(self, h: Tensor, n: Tensor, T: int) -> Tensor:
-        out = self.fc(h)
         B = h.shape[0]
-        width = min(T, out.shape[1])
+        width = min(T, self.fc.out_features)
+        out = skinny_linear(h, self.fc.weight, self.fc.bias, width)
         pos = torch.arange(width, device=out.device)
         valid = pos.view(1, -1) < n.view(-1, 1)
         p = torch.softmax(out[:, :width].masked_fill(~valid, float("-inf")), dim=1)

@@ -70,12 +70,13 @@ def fill_bytes(env, B, store_m: bool = True) -> float:
     """Algorithmic HBM bytes of one fill + ||AM-I|| launch.
 
     Gram-cached path (the env's default for widths <= 7): per line the action ids and the
-    Gram values (T + Wc fp64), per sample the removal bitmap and the stored values of M."""
+    Gram values (T + Wc, fp32 when the cache round-trips exactly, else fp64), per sample the
+    removal bitmap and the stored values of M."""
     n, W = env.pattern.n, env.pattern.width
     s = env.a_lines.val.element_size() if env.fill == "lsq" else 4
     per_sample = math.ceil(env.init_nnz / 32) * 4 + (n * W * s if store_m else 0) + 8
     if getattr(env, "gram", None) is not None:
-        line = n * W * 4 + env.gram.numel() * 8 + (n * W * 4 if env.fill == "copy" else 0)
+        line = n * W * 4 + env.gram.numel() * env.gram.element_size() + (n * W * 4 if env.fill == "copy" else 0)
     else:
         sa = env.a_lines.val.element_size()
         line = n * W * (4 + 4 + 4) + n * env.a_lines.width * (4 + sa)

@@ -96,11 +96,11 @@ __global__ __launch_bounds__(kNT) void k_gram_build(int32_t n, int32_t wrt, int3
 // consecutive lines are consecutive doubles), then the thread solves every sample; the
 // squared line residuals of a chunk of kChunk samples go to LDS and are summed per sample
 // by one wave each in a fixed order (two barriers per chunk, none per sample).
-template <int W, typename TM, bool LSQ>
+template <int W, typename TM, bool LSQ, typename GT>
 __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(4))) void k_gram_fill(int32_t n, int32_t line_begin, int32_t line_end, int32_t wrt,
                                                    const int32_t* __restrict__ pat_act,
                                                    const float* __restrict__ pat_val,
-                                                   const double* __restrict__ gram, int32_t B,
+                                                   const GT* __restrict__ gram, int32_t B,
                                                    const uint32_t* __restrict__ removed, int32_t words,
                                                    TM* __restrict__ m_out, double* __restrict__ partials) {
   constexpr int T = tri(W);
@@ -122,11 +122,11 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(4))) void k
     val[p] = (!LSQ && valid && p < wrt) ? pat_val[(int64_t)jj * wrt + p] : 0.0f;
   }
   double G[T], c[W];
-  const double* gp = gram + (int64_t)(jj >> 6) * (T + W) * 64 + (jj & 63);  // blocked: one 64-line block contiguous
+  const GT* gp = gram + (int64_t)(jj >> 6) * (T + W) * 64 + (jj & 63);  // blocked: one 64-line block contiguous
 #pragma unroll
-  for (int q = 0; q < T; ++q) G[q] = gp[q * 64];
+  for (int q = 0; q < T; ++q) G[q] = (double)gp[q * 64];  // fp32 storage only when exact (spai_gram_compact)
 #pragma unroll
-  for (int p = 0; p < W; ++p) c[p] = gp[(T + p) * 64];
+  for (int p = 0; p < W; ++p) c[p] = (double)gp[(T + p) * 64];
   int wofs[W];  // bitmap word offsets / bit positions of the slots
 #pragma unroll
   for (int p = 0; p < W; ++p) wofs[p] = act[p] >= 0 ? act[p] >> 5 : 0;
@@ -383,15 +383,29 @@ static int gram_width(int32_t W) { return W <= 5 ? 5 : (W <= 7 ? 7 : (W <= 13 ? 
 
 template <int W, typename TM, bool LSQ>
 hipError_t launch_fill(int32_t n, int32_t lb, int32_t le, int32_t wrt, const int32_t* pa, const float* pv,
-                       const double* g, int32_t B, const uint32_t* rm, int32_t words, void* mo, double* partials,
-                       int32_t nparts, hipStream_t s) {
+                       const void* g, bool g32, int32_t B, const uint32_t* rm, int32_t words, void* mo,
+                       double* partials, int32_t nparts, hipStream_t s) {
   if constexpr (W > 7)
-    k_gram_fill_wide<W, TM, LSQ><<<nparts, kNT, 0, s>>>(n, lb, le, wrt, pa, pv, g, B, rm, words, static_cast<TM*>(mo),
-                                                       partials);
+    k_gram_fill_wide<W, TM, LSQ><<<nparts, kNT, 0, s>>>(n, lb, le, wrt, pa, pv, static_cast<const double*>(g), B, rm,
+                                                       words, static_cast<TM*>(mo), partials);
+  else if (g32)
+    k_gram_fill<W, TM, LSQ, float><<<nparts, kNT, 0, s>>>(n, lb, le, wrt, pa, pv, static_cast<const float*>(g), B, rm,
+                                                           words, static_cast<TM*>(mo), partials);
   else
-    k_gram_fill<W, TM, LSQ><<<nparts, kNT, 0, s>>>(n, lb, le, wrt, pa, pv, g, B, rm, words, static_cast<TM*>(mo),
-                                                    partials);
+    k_gram_fill<W, TM, LSQ, double><<<nparts, kNT, 0, s>>>(n, lb, le, wrt, pa, pv, static_cast<const double*>(g), B,
+                                                            rm, words, static_cast<TM*>(mo), partials);
   return hipGetLastError();
+}
+
+// fp32 copy of the Gram cache; *exact is cleared if any entry does not survive the round trip
+__global__ __launch_bounds__(kNT) void k_gram_compact(int64_t count, const double* __restrict__ g,
+                                                      float* __restrict__ g32, int32_t* __restrict__ exact) {
+  const int64_t i = (int64_t)blockIdx.x * kNT + threadIdx.x;
+  if (i >= count) return;
+  const double v = g[i];
+  const float f = (float)v;
+  g32[i] = f;
+  if ((double)f != v) *exact = 0;  // benign race: every writer stores 0
 }
 
 }  // namespace
@@ -439,9 +453,22 @@ extern "C" int spai_gram_build(int32_t n, int32_t W, const int32_t* pat_idx, int
   return SPAI_OK;
 }
 
+extern "C" int spai_gram_compact(int32_t n, int32_t W, const double* gram, float* gram32, int32_t* exact,
+                                 void* stream) {
+  SPAI_CHECK_ARG(n >= 1 && gram && gram32 && exact, "spai_gram_compact: bad arguments");
+  const int wc = gram_width(W);
+  SPAI_CHECK_ARG(wc != 0, "spai_gram_compact: width %d above 13", W);
+  const int64_t count = (int64_t)(tri(wc) + wc) * ((n + 63) / 64 * 64);
+  hipStream_t s = (hipStream_t)stream;
+  k_gram_compact<<<(int)((count + kNT - 1) / kNT), kNT, 0, s>>>(count, gram, gram32, exact);
+  SPAI_CHECK_LAUNCH();
+  return SPAI_OK;
+}
+
 // Fill + per-block partial sums only (res2 partials stay in the workspace for spai_fill_reduce).
 extern "C" int spai_fill_lines_gram(int32_t fill_mode, int32_t n, int32_t line_begin, int32_t line_end, int32_t W,
-                                    const int32_t* pat_act, const float* pat_val, const double* gram, int32_t B,
+                                    const int32_t* pat_act, const float* pat_val, const void* gram,
+                                    int32_t gram_dtype, int32_t B,
                                     const uint32_t* removed, int32_t words, void* m_out, int32_t m_dtype,
                                     void* workspace, size_t workspace_bytes, void* stream) {
   SPAI_CHECK_ARG(fill_mode == SPAI_FILL_COPY || fill_mode == SPAI_FILL_LSQ,
@@ -463,31 +490,34 @@ extern "C" int spai_fill_lines_gram(int32_t fill_mode, int32_t n, int32_t line_b
     set_error("spai_fill_lines_gram: width W=%d above the compiled 13", W);
     return SPAI_ERR_UNSUPPORTED;
   }
+  SPAI_CHECK_ARG(gram_dtype == SPAI_DTYPE_F64 || (gram_dtype == SPAI_DTYPE_F32 && wc <= 7),
+                 "spai_fill_lines_gram: gram dtype %d (fp32 only for widths <= 7)", gram_dtype);
+  const bool g32 = gram_dtype == SPAI_DTYPE_F32;
   const int32_t nparts = (nl + kNT - 1) / kNT;
   SPAI_CHECK_ARG(workspace_bytes >= sizeof(double) * (size_t)nparts * B, "spai_fill_lines_gram: workspace too small");
   double* partials = static_cast<double*>(workspace);
   hipError_t e;
   const bool lsq = fill_mode == SPAI_FILL_LSQ, f64 = m_dtype == SPAI_DTYPE_F64;
   if (wc == 5) {
-    e = !lsq ? launch_fill<5, float, false>(n, line_begin, line_end, W, pat_act, pat_val, gram, B, removed, words,
+    e = !lsq ? launch_fill<5, float, false>(n, line_begin, line_end, W, pat_act, pat_val, gram, g32, B, removed, words,
                                             m_out, partials, nparts, s)
-        : f64 ? launch_fill<5, double, true>(n, line_begin, line_end, W, pat_act, pat_val, gram, B, removed, words,
+        : f64 ? launch_fill<5, double, true>(n, line_begin, line_end, W, pat_act, pat_val, gram, g32, B, removed, words,
                                              m_out, partials, nparts, s)
-              : launch_fill<5, float, true>(n, line_begin, line_end, W, pat_act, pat_val, gram, B, removed, words,
+              : launch_fill<5, float, true>(n, line_begin, line_end, W, pat_act, pat_val, gram, g32, B, removed, words,
                                             m_out, partials, nparts, s);
   } else if (wc == 7) {
-    e = !lsq ? launch_fill<7, float, false>(n, line_begin, line_end, W, pat_act, pat_val, gram, B, removed, words,
+    e = !lsq ? launch_fill<7, float, false>(n, line_begin, line_end, W, pat_act, pat_val, gram, g32, B, removed, words,
                                             m_out, partials, nparts, s)
-        : f64 ? launch_fill<7, double, true>(n, line_begin, line_end, W, pat_act, pat_val, gram, B, removed, words,
+        : f64 ? launch_fill<7, double, true>(n, line_begin, line_end, W, pat_act, pat_val, gram, g32, B, removed, words,
                                              m_out, partials, nparts, s)
-              : launch_fill<7, float, true>(n, line_begin, line_end, W, pat_act, pat_val, gram, B, removed, words,
+              : launch_fill<7, float, true>(n, line_begin, line_end, W, pat_act, pat_val, gram, g32, B, removed, words,
                                             m_out, partials, nparts, s);
   } else {
-    e = !lsq ? launch_fill<13, float, false>(n, line_begin, line_end, W, pat_act, pat_val, gram, B, removed, words,
+    e = !lsq ? launch_fill<13, float, false>(n, line_begin, line_end, W, pat_act, pat_val, gram, g32, B, removed, words,
                                              m_out, partials, nparts, s)
-        : f64 ? launch_fill<13, double, true>(n, line_begin, line_end, W, pat_act, pat_val, gram, B, removed, words,
+        : f64 ? launch_fill<13, double, true>(n, line_begin, line_end, W, pat_act, pat_val, gram, g32, B, removed, words,
                                               m_out, partials, nparts, s)
-              : launch_fill<13, float, true>(n, line_begin, line_end, W, pat_act, pat_val, gram, B, removed, words,
+              : launch_fill<13, float, true>(n, line_begin, line_end, W, pat_act, pat_val, gram, g32, B, removed, words,
                                              m_out, partials, nparts, s);
   }
   SPAI_CHECK_HIP(e);
@@ -507,11 +537,13 @@ extern "C" int spai_fill_reduce(int32_t n_lines, int32_t B, const void* workspac
 }
 
 extern "C" int spai_fill_residual_gram(int32_t fill_mode, int32_t n, int32_t line_begin, int32_t line_end, int32_t W,
-                                       const int32_t* pat_act, const float* pat_val, const double* gram, int32_t B,
+                                       const int32_t* pat_act, const float* pat_val, const void* gram,
+                                       int32_t gram_dtype, int32_t B,
                                        const uint32_t* removed, int32_t words, void* m_out, int32_t m_dtype,
                                        double* res2_out, void* workspace, size_t workspace_bytes, void* stream) {
   SPAI_CHECK_ARG(res2_out != nullptr, "spai_fill_residual_gram: null res2_out");
-  const int st = spai_fill_lines_gram(fill_mode, n, line_begin, line_end, W, pat_act, pat_val, gram, B, removed,
+  const int st = spai_fill_lines_gram(fill_mode, n, line_begin, line_end, W, pat_act, pat_val, gram, gram_dtype, B,
+                                      removed,
                                       words, m_out, m_dtype, workspace, workspace_bytes, stream);
   if (st != SPAI_OK) return st;
   return spai_fill_reduce(line_end - line_begin, B, workspace, res2_out, stream);

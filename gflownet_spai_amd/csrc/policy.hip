@@ -39,6 +39,7 @@ __host__ __device__ constexpr int gat_params(int HC, int F) { return 2 * HC * F 
 __device__ __forceinline__ float leaky(float v) { return v > 0.0f ? v : 0.2f * v; }
 
 constexpr int kEdgeChunk = 8;  // edges of one target whose loads are issued together
+constexpr int kCh1 = 4;        // k_gat1 chunk: fewer registers than kEdgeChunk (occupancy 6 waves/SIMD at hid 4)
 constexpr int kRedNT = 1024;   // one-block reductions
 
 // Online softmax step: fold score s with value row v[0..C) into (m, den, acc).
@@ -60,10 +61,12 @@ __device__ __forceinline__ void online_step(float s, const float* v, float& m, f
 
 // Layer 1.  HPT heads per thread (4 for hid <= 8: one thread per node; 1 above: one thread
 // per (node, head), the node's 4 lanes adjacent).  Per target: the edge ids, attributes
-// and source features of up to kEdgeChunk edges are loaded before any is used (one memory
-// round trip per chunk instead of three per edge).
+// and source features of up to kCh1 edges are loaded before any is used (one memory
+// round trip per chunk instead of three per edge).  Latency-bound gathers: occupancy is the
+// lever (hid 4, fin 1: 80 VGPRs, 6 waves/SIMD; 76 -> 57 us at C4).
 template <int F, int C, int HPT>
-__global__ __launch_bounds__(kNT) void k_gat1(int32_t n, const float* __restrict__ x, const int32_t* __restrict__ rp,
+__global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(C <= 4 && F == 1 ? 6 : 1)))
+void k_gat1(int32_t n, const float* __restrict__ x, const int32_t* __restrict__ rp,
                                               const int32_t* __restrict__ src, const float* __restrict__ ea,
                                               const float* __restrict__ p1, const float* __restrict__ p2,
                                               float* __restrict__ xlr2) {
@@ -83,6 +86,11 @@ __global__ __launch_bounds__(kNT) void k_gat1(int32_t n, const float* __restrict
   const float* We = br + HC;
   const float* att = We + HC;
   const float* bias = att + HC;
+  // the per-edge weights straight from the kernel argument: uniform addresses -> scalar
+  // loads, SGPR operands (the LDS copies would be hoisted into ~50 VGPRs and cost occupancy)
+  const float* gWl = p1;
+  const float* gWe = p1 + 2 * HC * F + 2 * HC;
+  const float* gatt = gWe + HC;
 
   const int64_t t = (int64_t)blockIdx.x * kNT + threadIdx.x;
   const int node = (int)(t / L), lane_h = (int)(t % L);
@@ -108,38 +116,90 @@ __global__ __launch_bounds__(kNT) void k_gat1(int32_t n, const float* __restrict
       acc[q][c] = 0.0f;
     }
   }
-  for (int eb = e0; eb < e1; eb += kEdgeChunk) {
-    int js[kEdgeChunk];
-    float as[kEdgeChunk], xj[kEdgeChunk][F];
+  // Per chunk: all scores first, one maximum per head, then the weights: no data-dependent
+  // rescaling branch per edge.  The aggregation is affine in the source features,
+  //     sum_j p_j (W_l x_j + b_l) = W_l (sum_j p_j x_j) + b_l sum_j p_j,
+  // so a head accumulates F weighted features and the weight sum instead of C products.
+  float kc[HPT][C];  // b_l + W_r x_i: the per-target constant of every channel
 #pragma unroll
-    for (int k = 0; k < kEdgeChunk; ++k) {
+  for (int q = 0; q < HPT; ++q)
+#pragma unroll
+    for (int c = 0; c < C; ++c) kc[q][c] = bl[(hb + q) * C + c] + xr[q][c];
+  float sx[HPT][F];
+#pragma unroll
+  for (int q = 0; q < HPT; ++q)
+#pragma unroll
+    for (int f = 0; f < F; ++f) sx[q][f] = 0.0f;
+  for (int eb = e0; eb < e1; eb += kCh1) {
+    int js[kCh1];
+    float as[kCh1], xj[kCh1][F];
+#pragma unroll
+    for (int k = 0; k < kCh1; ++k) {
       const int e = min(eb + k, e1 - 1);  // clamped: every load is in bounds, extras unused
       js[k] = src[e];
       as[k] = ea[e];
     }
 #pragma unroll
-    for (int k = 0; k < kEdgeChunk; ++k)
+    for (int k = 0; k < kCh1; ++k)
 #pragma unroll
       for (int f = 0; f < F; ++f) xj[k][f] = x[(int64_t)js[k] * F + f];
+    const int nv = min(kCh1, e1 - eb);
+    float sc[kCh1][HPT];
+    float mc[HPT];
 #pragma unroll
-    for (int k = 0; k < kEdgeChunk; ++k) {
-      if (eb + k >= e1) break;
+    for (int q = 0; q < HPT; ++q) mc[q] = m[q];
+#pragma unroll
+    for (int k = 0; k < kCh1; ++k) {
 #pragma unroll
       for (int q = 0; q < HPT; ++q) {
-        float xl[C], sc = 0.0f;
+        float v = -INFINITY;
+        if (k < nv) {
+          v = 0.0f;
 #pragma unroll
-        for (int c = 0; c < C; ++c) {
-          const int o = (hb + q) * C + c;
-          float v = bl[o];
+          for (int c = 0; c < C; ++c) {
+            const int o = (hb + q) * C + c;
+            float z = fmaf(gWe[o], as[k], kc[q][c]);
 #pragma unroll
-          for (int f = 0; f < F; ++f) v = fmaf(Wl[o * F + f], xj[k][f], v);
-          xl[c] = v;
-          sc = fmaf(att[o], leaky(v + xr[q][c] + We[o] * as[k]), sc);
+            for (int f = 0; f < F; ++f) z = fmaf(gWl[o * F + f], xj[k][f], z);
+            v = fmaf(gatt[o], leaky(z), v);
+          }
         }
-        online_step<C>(sc, xl, m[q], den[q], acc[q]);
+        sc[k][q] = v;
+        mc[q] = fmaxf(mc[q], v);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < HPT; ++q) {  // rescale what earlier chunks accumulated (exp(-inf) = 0 first)
+      const float r = __expf(m[q] - mc[q]);
+      den[q] *= r;
+#pragma unroll
+      for (int f = 0; f < F; ++f) sx[q][f] *= r;
+      m[q] = mc[q];
+    }
+#pragma unroll
+    for (int k = 0; k < kCh1; ++k) {
+      if (k < nv) {
+#pragma unroll
+        for (int q = 0; q < HPT; ++q) {
+          const float pk = __expf(sc[k][q] - m[q]);
+          den[q] += pk;
+#pragma unroll
+          for (int f = 0; f < F; ++f) sx[q][f] = fmaf(pk, xj[k][f], sx[q][f]);
+        }
       }
     }
   }
+  // acc[q][c] = sum_j p_j xl_j[c] from the affine form
+#pragma unroll
+  for (int q = 0; q < HPT; ++q)
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      const int o = (hb + q) * C + c;
+      float v = bl[o] * den[q];
+#pragma unroll
+      for (int f = 0; f < F; ++f) v = fmaf(Wl[o * F + f], sx[q][f], v);
+      acc[q][c] = v;
+    }
   // epilogue: relu(out) of this thread's heads, then its slice of W_l2 h1 and W_r2 h1
   const float* Wl2 = s2;
   const float* bl2 = Wl2 + C * HC;

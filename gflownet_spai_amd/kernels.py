@@ -157,11 +157,25 @@ def gram_build(pattern: Lines, a_lines: Lines) -> torch.Tensor:
     nb = _l().spai_gram_bytes(pattern.n, pattern.width)
     if nb == 0:
         raise NotImplementedError(f"no Gram kernel for width {pattern.width}")
-    gram = torch.empty(nb // 8, dtype=torch.float64, device=pattern.idx.device)
+    # zeroed: the padding lines of the last 64-line block stay exactly 0 (spai_gram_compact checks every entry)
+    gram = torch.zeros(nb // 8, dtype=torch.float64, device=pattern.idx.device)
     _lib.check(_l().spai_gram_build(pattern.n, pattern.width, _lib.ptr(pattern.idx), a_lines.width,
                                     _lib.ptr(a_lines.idx), _lib.ptr(a_lines.val), _DT[a_lines.val.dtype],
                                     _lib.ptr(gram), _lib.stream_ptr(pattern.idx.device)), "spai_gram_build")
     return gram
+
+
+def gram_compact(gram: torch.Tensor, pattern: Lines):
+    """fp32 copy of an fp64 Gram cache if every entry survives the round trip exactly (then the
+    fill is bit-identical from it and streams half the Gram bytes), else None.  One host sync
+    (once per env)."""
+    if pattern.width > 7:
+        return None
+    g32 = torch.empty(gram.numel(), dtype=torch.float32, device=gram.device)
+    exact = torch.ones(1, dtype=torch.int32, device=gram.device)
+    _lib.check(_l().spai_gram_compact(pattern.n, pattern.width, _lib.ptr(gram), _lib.ptr(g32), _lib.ptr(exact),
+                                      _lib.stream_ptr(gram.device)), "spai_gram_compact")
+    return g32 if int(exact.item()) == 1 else None
 
 
 def fill_residual_gram(pattern: Lines, gram: torch.Tensor, removed: torch.Tensor, lsq: bool, line_begin: int = 0,
@@ -181,7 +195,8 @@ def fill_residual_gram(pattern: Lines, gram: torch.Tensor, removed: torch.Tensor
     ws = _lib.workspace(nb, removed.device, "fill")
     with _timed("fill_residual"):  # the fill kernel alone (the bench's roofline kernel)
         st = _l().spai_fill_lines_gram(mode, pattern.n, line_begin, line_end, pattern.width, _lib.ptr(pattern.act),
-                                       _lib.ptr(pattern.val), _lib.ptr(gram), B, _lib.ptr(removed), words,
+                                       _lib.ptr(pattern.val), _lib.ptr(gram), _DT[gram.dtype], B, _lib.ptr(removed),
+                                       words,
                                        _lib.ptr(m), _DT[m_dtype], _lib.ptr(ws), ws.numel(),
                                        _lib.stream_ptr(removed.device))
     _lib.check(st, "spai_fill_lines_gram")

@@ -51,7 +51,7 @@ def _default_device():
 
 class PreconditionerEnv(Env):
     def __init__(self, matrix_size: int, initial_matrix: Tensor, original_matrix: Tensor, *, side: str = "MA",
-                 fill: str = "copy", keep_m: bool = False, device=None):
+                 fill: str = "copy", keep_m: bool = False, device=None, compact_gram: bool = True):
         if side not in ("MA", "AM"):
             raise ValueError("side must be 'MA' or 'AM'")
         if fill not in ("copy", "lsq"):
@@ -83,6 +83,11 @@ class PreconditionerEnv(Env):
         # wider patterns use the generic kernels)
         self.gram = (kernels.gram_build(self.pattern, self.a_lines)
                      if self.pattern.width <= 13 and self.a_lines.width <= 7 else None)
+        if self.gram is not None and compact_gram:
+            # integer stencils (and any A whose G, c are fp32-exact): the same cache in fp32
+            g32 = kernels.gram_compact(self.gram, self.pattern)
+            if g32 is not None:
+                self.gram = g32
 
         self.orig_residual = self.calculate_residual(self.original_matrix, self.original_matrix)
         self._r0 = float(self.orig_residual)  # host copy: no device sync inside the reward formula

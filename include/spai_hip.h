@@ -148,19 +148,26 @@ int spai_fill_residual(int32_t fill_mode, int32_t n, int32_t line_begin, int32_t
  * res2_out / m_out semantics, line range, precision rules) from pat_act (+ pat_val for
  * COPY) and `gram` alone: per-rollout traffic is a stream of the line data and, per sample,
  * the mask bits and M values.  Widths above 13 (or WA above 7) return SPAI_ERR_UNSUPPORTED
- * (use spai_fill_residual; its LSQ mode covers W <= 7).  Workspace: spai_fill_workspace_bytes(line_end - line_begin, B). */
+ * (use spai_fill_residual; its LSQ mode covers W <= 7).  Workspace: spai_fill_workspace_bytes(line_end - line_begin, B).
+ * spai_gram_compact writes the same entries as fp32 (same blocked layout, half the bytes) and
+ * clears *exact (caller sets it to 1) if any entry changes in the fp64 -> fp32 -> fp64 round
+ * trip; only an exact copy may be used (gram_dtype SPAI_DTYPE_F32, widths W <= 7): the fill
+ * then computes bit for bit what it computes from the fp64 cache (e.g. integer stencils,
+ * whose G and c are small integers), with 80 instead of 160 bytes per 5-wide line. */
 size_t spai_gram_bytes(int32_t n, int32_t W);
 int spai_gram_build(int32_t n, int32_t W, const int32_t* pat_idx, int32_t WA, const int32_t* a_idx,
                     const void* a_val, int32_t a_dtype, double* gram, void* stream);
+int spai_gram_compact(int32_t n, int32_t W, const double* gram, float* gram32, int32_t* exact, void* stream);
 int spai_fill_residual_gram(int32_t fill_mode, int32_t n, int32_t line_begin, int32_t line_end, int32_t W,
-                            const int32_t* pat_act, const float* pat_val, const double* gram, int32_t B,
+                            const int32_t* pat_act, const float* pat_val, const void* gram, int32_t gram_dtype,
+                            int32_t B,
                             const uint32_t* removed, int32_t words, void* m_out, int32_t m_dtype,
                             double* res2_out, void* workspace, size_t workspace_bytes, void* stream);
 /* The two halves of spai_fill_residual_gram: the fill kernel leaves per-block fp64 partial
  * sums in the workspace; spai_fill_reduce (n_lines = line_end - line_begin of that call)
  * sums them per sample in a fixed order into res2_out. */
 int spai_fill_lines_gram(int32_t fill_mode, int32_t n, int32_t line_begin, int32_t line_end, int32_t W,
-                         const int32_t* pat_act, const float* pat_val, const double* gram, int32_t B,
+                         const int32_t* pat_act, const float* pat_val, const void* gram, int32_t gram_dtype, int32_t B,
                          const uint32_t* removed, int32_t words, void* m_out, int32_t m_dtype,
                          void* workspace, size_t workspace_bytes, void* stream);
 int spai_fill_reduce(int32_t n_lines, int32_t B, const void* workspace, double* res2_out, void* stream);

@@ -363,6 +363,33 @@ def test_gram_cached_fill_matches_direct_kernel(side, fill, dims):
     np.testing.assert_allclose(sum(parts).cpu().numpy(), got.cpu().numpy(), rtol=1e-12)
 
 
+@pytest.mark.parametrize("side,fill,dims", [("AM", "lsq", 2), ("MA", "copy", 2), ("AM", "lsq", 3)])
+def test_fp32_gram_cache_is_bit_identical(side, fill, dims):
+    """The fp32 Gram cache (spai_gram_compact: integer stencils round-trip exactly) gives the
+    fp64 cache's residuals and M values bit for bit; a matrix with non-fp32-exact products
+    keeps the fp64 cache."""
+    from gflownet_spai_amd import PreconditionerEnv, kernels, poisson_2d, poisson_3d
+    A = poisson_2d(40) if dims == 2 else poisson_3d(9)
+    n = A.shape[0]
+    env32 = PreconditionerEnv(n, A, A, side=side, fill=fill)
+    env64 = PreconditionerEnv(n, A, A, side=side, fill=fill, compact_gram=False)
+    assert env32.gram.dtype == torch.float32 and env64.gram.dtype == torch.float64
+    assert torch.equal(env32.gram.double(), env64.gram)
+    E = env32.init_nnz
+    rng = np.random.default_rng(5)
+    acts = torch.from_numpy(np.where(rng.random((6, E)) < 0.3, np.arange(E), -1))
+    removed, _ = kernels.actions_to_removed(acts.to(DEV), E)
+    mdt = env64.a_lines.val.dtype
+    r32, m32 = kernels.fill_residual_gram(env32.pattern, env32.gram, removed, fill == "lsq", store_m=True, m_dtype=mdt)
+    r64, m64 = kernels.fill_residual_gram(env64.pattern, env64.gram, removed, fill == "lsq", store_m=True, m_dtype=mdt)
+    assert torch.equal(r32, r64) and torch.equal(m32, m64)
+    # a random-valued A: products are not fp32-exact, the env keeps fp64
+    c = A.coalesce()
+    vals = torch.from_numpy(np.random.default_rng(1).standard_normal(c._nnz()).astype(np.float32))
+    R = torch.sparse_coo_tensor(c.indices(), vals.to(c.dtype), c.shape)
+    assert PreconditionerEnv(n, R, R, side=side, fill=fill).gram.dtype == torch.float64
+
+
 def _wide_pattern(dims, g):
     """13-wide candidate patterns (the nnz/col <= 13 rows of SURVEY §8a11): the 2-D A^2
     13-point pattern, and in 3-D the 7-point star plus the +-2 axial neighbours."""

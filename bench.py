@@ -148,6 +148,10 @@ def main():
     ap.add_argument("--batch", type=int, default=8)
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--shard", default="candidates", choices=["candidates", "columns"],
+                    help="candidates: B candidates per rank (weak scaling, no collective); columns: the same B "
+                         "candidates on every rank, lines of M split across ranks, one all_reduce of the squared "
+                         "residuals and one all_gather of M per step (strong scaling)")
     ap.add_argument("--no-overlap", action="store_true",
                     help="run the fill/reward after the trajectory sort on one stream (isolated kernel timing)")
     args = ap.parse_args()
@@ -169,12 +173,21 @@ def main():
     env = PreconditionerEnv(n, A, A, side="AM", fill="lsq", keep_m=True, device=dev)
     E = env.num_actions - 1
     B = args.batch
-    model = GFlowNet(make_policy(env, A, dev), None, env, mode="throughput", seed=1234, sample_base=rank * B,
-                     overlap=not args.no_overlap)
+    columns = args.shard == "columns"
+    shard = None
+    if columns and world > 1:
+        from gflownet_spai_amd.distributed import allgather_lines, shard_lines
+        lb, le = shard_lines(n, rank, world)
+        shard = (lb, le, None)
+    model = GFlowNet(make_policy(env, A, dev), None, env, mode="throughput", seed=1234,
+                     sample_base=0 if columns else rank * B, overlap=not args.no_overlap, line_shard=shard)
     s0 = [A] * B
 
     def step():
-        return model.sample_states(s0, return_log=True)
+        log = model.sample_states(s0, return_log=True)
+        if shard is not None:
+            log.m_full = allgather_lines(env.last_m, n)  # M of every candidate on every rank (one all_gather)
+        return log
 
     for _ in range(args.warmup):
         step()
@@ -203,25 +216,30 @@ def main():
     if rank == 0:
         fill_ms = phases.get("fill_residual", float("nan"))
         fb = fill_bytes(env, B)
+        if shard is not None:  # the rank's fill covers its own lines only (rank 0: the first, largest shard)
+            fb *= (shard[1] - shard[0]) / n
         achieved = fb / (fill_ms * 1e-3) / 1e9
         traffic = measured_traffic(args.config, B, not args.no_overlap)
         out = {
             "metric": "SPAI columns/sec + final ||AM-I||_F, 2D Poisson 1024^2, at 1/2/4/8 GPU",
-            "value": B * n * world / dt,
+            "value": B * n * (1 if columns else world) / dt,
             "unit": "columns/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": dt * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if columns else "weak",
             "vs_baseline": None,
             "dtype": "f32 storage, f64 solve/accumulate",
             "data": "synthetic (random-init seeded ForwardPolicy GATv2x2+fc, hid=4, evaluated on the state graph in "
                     "every step; terminal fc bias set for 20% expected removal; Poisson matrix from its stencil)",
-            "config": {"workload": text + f", B={B} candidates per GPU: ForwardPolicy logits + throughput rollout + "
-                                        "LSQ fill + ||AM-I||_F",
-                       "N": n, "E": E, "global_batch": B * world, "parallelism": f"candidates sharded x{world}"},
+            "config": {"workload": text + (f", B={B} candidates, lines of M sharded over the GPUs (all_reduce of "
+                                               "||.||^2, all_gather of M)" if columns else
+                                               f", B={B} candidates per GPU") +
+                                   ": ForwardPolicy logits + throughput rollout + LSQ fill + ||AM-I||_F",
+                       "N": n, "E": E, "global_batch": B * (1 if columns else world),
+                       "parallelism": f"{'columns' if columns else 'candidates'} sharded x{world}"},
             "final_residual_fro": float(res[0]),
             "final_residual_fro_mean": float(res.mean()),
             "removed_per_candidate_mean": float(counts.mean()),

@@ -27,7 +27,7 @@ from .preconditioner import Data
 
 class GFlowNet(nn.Module):
     def __init__(self, forward_policy, backward_policy, env, *, mode: str = "parity", seed: int | None = None,
-                 sample_base: int = 0, overlap: bool = True):
+                 sample_base: int = 0, overlap: bool = True, line_shard: tuple | None = None):
         super().__init__()
         if mode not in ("parity", "throughput"):
             raise ValueError("mode must be 'parity' or 'throughput'")
@@ -42,6 +42,11 @@ class GFlowNet(nn.Module):
         self._data_cache = {}
         self._side = None  # HIP stream for the fill/reward, overlapped with the trajectory sort
         self.overlap = overlap  # False: fill/reward on the main stream after the sort (isolated kernel timing)
+        # (line_begin, line_end, group): this rank fills and scores only lines [begin, end) of
+        # every candidate and the squared residuals are summed over the group (one all_reduce);
+        # every rank draws the same candidates (same seed and sample_base), so no exchange of
+        # the rollout is needed (columns sharded)
+        self.line_shard = line_shard
 
     # ------------------------------------------------------------------ policy
     def policy_logits(self, data, batch_size: int):
@@ -100,6 +105,12 @@ class GFlowNet(nn.Module):
             out.append(hit[1])
         return out
 
+    def _rewards(self, removed, counts, alpha):
+        if self.line_shard is None:
+            return self.env.rewards_from_removed(removed, counts, alpha)
+        b, e, group = self.line_shard
+        return self.env.rewards_from_removed(removed, counts, alpha, b, e, group)
+
     # ------------------------------------------------------------------ sampler
     def sample_states(self, s0, return_log: bool = False):
         env = self.env
@@ -117,14 +128,14 @@ class GFlowNet(nn.Module):
         if self.mode == "parity":
             actions_bt, fwd_bt = self._parity_rollout(lg, B, lmax, z)
             removed, counts = kernels.actions_to_removed(actions_bt, E)
-            rewards = env.rewards_from_removed(removed, counts, alpha)
+            rewards = self._rewards(removed, counts, alpha)
             log._set_rollout(logits, actions_bt, fwd_bt, lmax=lmax)
         else:
             removed, counts, ws = kernels.rollout_select(lg, B, lmax, self.seed, self.rollouts, self.sample_base)
             self.rollouts += 1
             if not self.overlap:
                 actions_full, fwd_full, t_dev = kernels.rollout_order(lg, B, lmax, counts, ws)
-                rewards = env.rewards_from_removed(removed, counts, alpha)
+                rewards = self._rewards(removed, counts, alpha)
                 log._set_rollout(logits, actions_full, fwd_full, t_dev, lmax=lmax)
                 log.removed, log.counts = removed, counts
                 log.rewards = rewards.detach().to(torch.float32)
@@ -137,7 +148,7 @@ class GFlowNet(nn.Module):
             side = self._side
             side.wait_stream(main)
             with torch.cuda.stream(side):
-                rewards = env.rewards_from_removed(removed, counts, alpha)
+                rewards = self._rewards(removed, counts, alpha)
             for t in (removed, counts, alpha):
                 if torch.is_tensor(t) and t.is_cuda:
                     t.record_stream(side)

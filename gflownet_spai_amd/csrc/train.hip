@@ -383,7 +383,8 @@ __global__ __launch_bounds__(kLstmNT) void k_lstm_bwd(int32_t B, const int64_t* 
 // unit's four gates sit in one quad: quad_perm broadcasts i, f, g, o to the quad, which
 // updates (c_k, h_k) redundantly; W_hh h takes the other units' h through row_ror 4, 8, 12
 // against weights pre-rotated per lane.  The activation's pre-scale (-log2 e, twice that
-// for tanh) is folded into the weights, so a gate is fma chain -> v_exp -> v_rcp -> fma.
+// for tanh) is folded into the weights, so a gate is a two-deep fma tree -> v_exp -> v_rcp; the
+// quad receives the raw sigmoids and applies g = 2 s_g - 1 and tanh inside two fmas (cell4, hid4).
 // Only a checkpoint (h, c) per 16-step block is stored ("states" = [B][ceil(T/16)][2H]);
 // the inputs are prefetched three blocks ahead.  Fwd4Step restates a step for one thread
 // with the same instructions in the same order (bit-identical states), so the backward
@@ -437,30 +438,37 @@ __device__ __forceinline__ int nblocks4(int n) { return (n + kBlk4 - 1) / kBlk4;
 
 // a gate row's scaled weights, as the forward lane (q, k) holds them
 struct Row4 {
-  float wx, bs, A2, Bm, wr[4];
+  float wx, bs, wr[4];
   __device__ __forceinline__ void load(const float* w_ih, const float* w_hh, const float* b_ih, const float* b_hh,
                                        int q, int k, int sg) {
     const int row = q * kH4 + k;
     const float sc = (q == 2 ? -2.0f : -1.0f) * kLog2e;
     wx = w_ih[row] * sc;
     bs = (b_ih[row] + b_hh[row]) * sc;
-    A2 = q == 2 ? 2.0f : 1.0f;
-    Bm = q == 2 ? -1.0f : 0.0f;
 #pragma unroll
     for (int m = 0; m < 4; ++m) wr[m] = w_hh[row * kH4 + ((k + m * sg) & 3)] * sc;  // unit row_ror(4m) brings
   }
-  // fma order: own unit, then the units row_ror 4, 8, 12 bring (k + sg, k + 2sg, k + 3sg)
-  __device__ __forceinline__ float act(float x, float h0, float h1, float h2, float h3) const {
-    float z = fmaf(wx, x, bs);
-    z = fmaf(wr[0], h0, z);
-    z = fmaf(wr[1], h1, z);
-    z = fmaf(wr[2], h2, z);
-    z = fmaf(wr[3], h3, z);
-    return fmaf(fsig_pre(z), A2, Bm);
+  // sigmoid of the (pre-scaled) gate pre-activation: sigma(z) for i, f, o; sigma(2z) for g.
+  // Two-deep tree: (own unit, +2sg) and (+sg, +3sg), the units row_ror 4, 8, 12 bring.
+  __device__ __forceinline__ float sig(float x, float h0, float h1, float h2, float h3) const {
+    float z1 = fmaf(wr[0], h0, fmaf(wx, x, bs));
+    float z2 = wr[1] * h1;
+    z1 = fmaf(wr[2], h2, z1);
+    z2 = fmaf(wr[3], h3, z2);
+    return fsig_pre(z1 + z2);
   }
 };
 
-// one thread's bit-identical restatement of k_lstm_fwd4's step (all 16 rows); weights in LDS
+// the cell update from the four gate sigmoids (s_g = sigma(2 z_g), so g = 2 s_g - 1):
+//   c' = f c + i (2 s_g - 1) = fma(2i, s_g, fma(f, c, -i)),  h' = o tanh(c') = fma(2o, sigma(2c'), -o)
+__device__ __forceinline__ float cell4(float si, float sf, float sgg, float c) {
+  return fmaf(si + si, sgg, fmaf(sf, c, -si));
+}
+__device__ __forceinline__ float hid4(float so, float c) {
+  return fmaf(so + so, fsig_pre((-2.0f * kLog2e) * c), -so);
+}
+
+// one thread's bit-identical restatement of k_lstm_fwd4's step (all 16 rows)
 struct Fwd4Step {
   Row4 row[16];  // [q * 4 + k]
   __device__ __forceinline__ void load(const float* w_ih, const float* w_hh, const float* b_ih, const float* b_hh,
@@ -470,16 +478,18 @@ struct Fwd4Step {
 #pragma unroll
       for (int k = 0; k < 4; ++k) row[q * 4 + k].load(w_ih, w_hh, b_ih, b_hh, q, k, sg);
   }
-  // gates g[q][k] and the step update of h, c
+  // gate values g[q][k] (i, f, g = tanh, o) and the step update of h, c
   __device__ __forceinline__ void step(float x, float* h, float* c, float (*g)[4], int sg) const {
     float hn[4], cn[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
+      float sq[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q)
-        g[q][k] = row[q * 4 + k].act(x, h[k], h[(k + sg) & 3], h[(k + 2 * sg) & 3], h[(k + 3 * sg) & 3]);
-      cn[k] = fmaf(g[1][k], c[k], g[0][k] * g[2][k]);
-      hn[k] = g[3][k] * ftanh(cn[k]);
+        sq[q] = row[q * 4 + k].sig(x, h[k], h[(k + sg) & 3], h[(k + 2 * sg) & 3], h[(k + 3 * sg) & 3]);
+      cn[k] = cell4(sq[0], sq[1], sq[2], c[k]);
+      hn[k] = hid4(sq[3], cn[k]);
+      g[0][k] = sq[0], g[1][k] = sq[1], g[2][k] = fmaf(2.0f, sq[2], -1.0f), g[3][k] = sq[3];
     }
 #pragma unroll
     for (int k = 0; k < 4; ++k) h[k] = hn[k], c[k] = cn[k];
@@ -501,10 +511,10 @@ __global__ __launch_bounds__(64) void k_lstm_fwd4(const int64_t* __restrict__ tr
   float* ck = states ? states + (int64_t)b * nblocks4(T) * 2 * kH4 + (q & 1) * kH4 + k : nullptr;
   float h = 0.0f, c = 0.0f;
   auto step = [&](int32_t xi) {
-    const float a = R.act((float)xi, h, dppf<0x124>(h), dppf<0x128>(h), dppf<0x12C>(h));  // row_ror 4, 8, 12
-    const float ig = dppf<0x00>(a), fg = dppf<0x55>(a), gg = dppf<0xAA>(a), og = dppf<0xFF>(a);  // quad_perm
-    c = fmaf(fg, c, ig * gg);
-    h = og * ftanh(c);
+    const float a = R.sig((float)xi, h, dppf<0x124>(h), dppf<0x128>(h), dppf<0x12C>(h));  // row_ror 4, 8, 12
+    const float si = dppf<0x00>(a), sf = dppf<0x55>(a), sgg = dppf<0xAA>(a), so = dppf<0xFF>(a);  // quad_perm
+    c = cell4(si, sf, sgg, c);
+    h = hid4(so, c);
   };
   auto ckpt = [&](int m) {
     if (ck) ck[(int64_t)m * 2 * kH4] = (q & 1) ? c : h;

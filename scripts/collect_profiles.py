@@ -14,7 +14,7 @@ import os
 import shutil
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-ROOF_KERNEL = "k_gram_fill<5, float, true>"
+ROOF_KERNEL = "k_gram_fill<5, float, true"  # any Gram storage type (fp32 exact or fp64)
 
 
 def short(name):

@@ -227,6 +227,26 @@ def test_throughput_sample_states_end_to_end():
         assert float(env.last_residual[b]) == pytest.approx(res, rel=1e-10)
 
 
+def test_overlapped_and_serial_fill_agree():
+    """GFlowNet(overlap=True) (fill/reward on a side stream during the sort) and the default
+    serial order give identical trajectories, probabilities, M and rewards."""
+    from gflownet_spai_amd import GFlowNet, PreconditionerEnv, poisson_2d
+    A = poisson_2d(40)
+    n = 40 * 40
+    outs = []
+    for overlap in (False, True):
+        env = PreconditionerEnv(n, A, A, side="AM", fill="lsq", keep_m=True)
+        E = env.num_actions - 1
+        logits = torch.randn(E + 1, generator=torch.Generator().manual_seed(7))
+        logits[E] = 7.0
+        g = GFlowNet(FixedLogits(logits), None, env, mode="throughput", seed=5, overlap=overlap)
+        log = g.sample_states([A] * 3, return_log=True)
+        torch.cuda.synchronize()
+        outs.append((log.actions.cpu(), log.fwd_probs.detach().cpu(), env.last_m.cpu(), log.rewards.cpu()))
+    for x, y in zip(*outs):
+        assert torch.equal(x, y)
+
+
 def test_lsq_fp64_3d_vs_oracle():
     """64^3 is the C3 config; a 12^3 7-pt fp64 lattice checks the fp64 LSQ kernel exactly."""
     from gflownet_spai_amd import GFlowNet, PreconditionerEnv, poisson_3d

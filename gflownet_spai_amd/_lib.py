@@ -60,7 +60,10 @@ SIGNATURES = {
                                       _c_i64, _c_p, _c_i32, _c_p, _c_p, _c_sz, _c_p]),
     "spai_lstm_forward": (ctypes.c_int, [_c_i32, _c_i32, _c_p, _c_i64, _c_p, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_p,
                                          _c_p, _c_p]),
-    "spai_ell_spmv": (ctypes.c_int, [_c_i32, _c_i32, _c_p, _c_p, _c_i32, _c_p, _c_p, _c_p]),
+    "spai_policy_backward_workspace_bytes": (_c_sz, [_c_i32, _c_i32, _c_i32, _c_i32, _c_i32]),
+    "spai_policy_backward": (ctypes.c_int, [_c_i32, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p,
+                                            _c_p, _c_p, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_sz, _c_p]),
+    "spai_ell_spmv":(ctypes.c_int, [_c_i32, _c_i32, _c_p, _c_p, _c_i32, _c_p, _c_p, _c_p]),
     "spai_mtx_header": (ctypes.c_int, [ctypes.c_char_p, _c_p, _c_p]),
     "spai_mtx_read": (ctypes.c_int, [ctypes.c_char_p, _c_p, _c_p, _c_p, _c_i64, _c_i32, _c_p]),
     "spai_lstm_states_floats": (_c_sz, [_c_i32, _c_i32, _c_i32]),

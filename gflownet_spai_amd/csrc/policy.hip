@@ -243,8 +243,11 @@ void k_gat1(int32_t n, const float* __restrict__ x, const int32_t* __restrict__ 
 
 // Layer 2 (one head), one thread per node: gathered W_l2 h_j rows (C floats, 16-byte
 // loads), chunked like layer 1; epilogue relu + the block's fp64 pooled sum.
+#ifndef GAT2_WPE4
+#define GAT2_WPE4 7  // waves/SIMD of k_gat2 at hid 4 (66 VGPRs, no spills)
+#endif
 template <int C>
-__global__ __launch_bounds__(kNT) void k_gat2(int32_t n, const int32_t* __restrict__ rp,
+__global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(C <= 4 ? GAT2_WPE4 : 1))) void k_gat2(int32_t n, const int32_t* __restrict__ rp,
                                               const int32_t* __restrict__ src, const float* __restrict__ ea,
                                               const float* __restrict__ p2, const float* __restrict__ xlr2,
                                               double* __restrict__ part) {
@@ -460,6 +463,8 @@ bool dispatch_hid(int32_t hid, int32_t n, const float* x, const int32_t* rp, con
   }
 }
 
+#include "policy_bwd.inc"
+
 }  // namespace
 }  // namespace spai
 
@@ -503,6 +508,48 @@ extern "C" int spai_policy_logits(int32_t n_nodes, int32_t fin, int32_t hid, con
     set_error("spai_policy_logits: no kernel for node_features=%d hidden_dim=%d (compiled: 1/2/4 x 4/8/16/32)", fin,
               hid);
     return SPAI_ERR_UNSUPPORTED;
+  }
+  SPAI_CHECK_LAUNCH();
+  return SPAI_OK;
+}
+
+extern "C" size_t spai_policy_backward_workspace_bytes(int32_t n_nodes, int32_t n_edges, int32_t fin, int32_t hid,
+                                                       int32_t num_actions) {
+  PolicyWs w;
+  PolicyBwdWs v;
+  const size_t a = align_up(policy_ws(n_nodes, hid, num_actions, nullptr, &w));
+  return a + policy_bwd_ws(n_nodes, n_edges, fin, hid, num_actions, nullptr, &v);
+}
+
+extern "C" int spai_policy_backward(int32_t n_nodes, int32_t n_edges, int32_t fin, int32_t hid, const float* x,
+                                    const int32_t* rowptr, const int32_t* src, const float* eattr,
+                                    const int32_t* rev_ptr, const int32_t* rev_eid, const float* gat1,
+                                    const float* gat2, const float* fc_w, int32_t num_actions, const float* dlogits,
+                                    float* g_gat1, float* g_gat2, float* g_fc_w, float* g_fc_b, void* workspace,
+                                    size_t workspace_bytes, void* stream) {
+  SPAI_CHECK_ARG(x && rowptr && src && eattr && rev_ptr && rev_eid && gat1 && gat2 && fc_w && dlogits && g_gat1 &&
+                     g_gat2 && g_fc_w && g_fc_b,
+                 "spai_policy_backward: null pointer");
+  SPAI_CHECK_ARG(n_nodes > 0 && n_edges >= 0 && num_actions > 0, "spai_policy_backward: bad shape");
+  if ((fin != 1 && fin != 2 && fin != 4) || (hid != 4 && hid != 8)) {
+    set_error("spai_policy_backward: no kernel for node_features=%d hidden_dim=%d (compiled: 1/2/4 x 4/8)", fin, hid);
+    return SPAI_ERR_UNSUPPORTED;
+  }
+  SPAI_CHECK_ARG(workspace && workspace_bytes >= spai_policy_backward_workspace_bytes(n_nodes, n_edges, fin, hid,
+                                                                                      num_actions),
+                 "spai_policy_backward: workspace too small");
+  PolicyWs w;
+  PolicyBwdWs v;
+  const size_t a = align_up(policy_ws(n_nodes, hid, num_actions, workspace, &w));
+  policy_bwd_ws(n_nodes, n_edges, fin, hid, num_actions, static_cast<char*>(workspace) + a, &v);
+  hipStream_t s = (hipStream_t)stream;
+  switch (fin) {
+    case 1: dispatch_bwd<1>(hid, n_nodes, x, rowptr, src, eattr, rev_ptr, rev_eid, gat1, gat2, fc_w, num_actions,
+                            dlogits, g_gat1, g_gat2, g_fc_w, g_fc_b, w, v, s); break;
+    case 2: dispatch_bwd<2>(hid, n_nodes, x, rowptr, src, eattr, rev_ptr, rev_eid, gat1, gat2, fc_w, num_actions,
+                            dlogits, g_gat1, g_gat2, g_fc_w, g_fc_b, w, v, s); break;
+    default: dispatch_bwd<4>(hid, n_nodes, x, rowptr, src, eattr, rev_ptr, rev_eid, gat1, gat2, fc_w, num_actions,
+                             dlogits, g_gat1, g_gat2, g_fc_w, g_fc_b, w, v, s); break;
   }
   SPAI_CHECK_LAUNCH();
   return SPAI_OK;

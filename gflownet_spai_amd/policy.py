@@ -139,10 +139,22 @@ def _pack(layer: GATv2Layer) -> Tensor:
     return packed
 
 
+def reverse_csr(src: Tensor, n: int):
+    """The target-CSR edges grouped by SOURCE node (stable): rev_ptr [n+1], rev_eid [E'] = edge
+    positions in the target CSR.  The policy backward gathers each source's gradient messages
+    through it in a fixed order (no atomics)."""
+    s = src.long()
+    rev_eid = torch.sort(s, stable=True).indices.to(torch.int32).contiguous()
+    rev_ptr = torch.zeros(n + 1, dtype=torch.int32, device=src.device)
+    rev_ptr[1:] = torch.cumsum(torch.bincount(s, minlength=n), 0).to(torch.int32)
+    return rev_ptr, rev_eid
+
+
 class _HipLogits(torch.autograd.Function):
-    """Forward on the gfx950 kernels; backward recomputes the torch restatement of the same
-    network (ForwardPolicy.torch_logits) and differentiates that: the gradient path of the
-    TB loss, not the sampler's hot path."""
+    """Forward on the gfx950 kernels.  Backward on the gfx950 kernels too (spai_policy_backward,
+    hid 4 or 8 and node_features 1/2/4: the GATv2 softmax and message gradients, fc, pooling);
+    other sizes differentiate the torch restatement ForwardPolicy.torch_logits on the device.
+    The gradient path of the TB loss, not the sampler's hot path."""
 
     @staticmethod
     def forward(ctx, policy, data, B, *params):
@@ -153,6 +165,14 @@ class _HipLogits(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g, _g_lmax):
+        pol = ctx.policy
+        if pol._hip_backward_ok(ctx.data):
+            grads = pol._hip_backward(ctx.data, g.reshape(-1))
+            return (None, None, None, *[grads.get(id(p)) if p.requires_grad else None for p in pol.parameters()])
+        return _HipLogits._torch_backward(ctx, g)
+
+    @staticmethod
+    def _torch_backward(ctx, g):
         params = [p for p in ctx.policy.parameters()]
         with torch.enable_grad():
             out, _ = ctx.policy.torch_logits(ctx.data)
@@ -222,6 +242,54 @@ class ForwardPolicy(BasePolicy):
                                         _lib.stream_ptr(x.device))
         _lib.check(st, "spai_policy_logits")
         return logits, lmax
+
+    def _hip_backward_ok(self, data) -> bool:
+        return self.hid in (4, 8) and data.x.shape[1] in (1, 2, 4)
+
+    def _hip_backward(self, data, g: Tensor) -> dict:
+        """{id(parameter): gradient} of sum_a g_a logit_a by spai_policy_backward."""
+        x = data.x
+        n, fin = x.shape
+        A = g.numel()
+        rowptr, src, ea = self._graph(data)
+        key = (rowptr.data_ptr(), src.data_ptr())
+        rev = getattr(self, "_rev", None)
+        if rev is None or rev[0] != key:
+            rev = self._rev = (key, *reverse_csr(src, n))
+        rev_ptr, rev_eid = rev[1], rev[2]
+        xf = x.detach().float().contiguous()
+        p1, p2 = _pack(self.gat1), _pack(self.gat2)
+        w = self.fc.weight.detach()
+        if w.dtype != torch.float32 or not w.is_contiguous():
+            w = w.float().contiguous()
+        gf = g.detach().float().contiguous()
+        g1, g2 = torch.empty_like(p1), torch.empty_like(p2)
+        dW = torch.empty(A, self.hid, dtype=torch.float32, device=x.device)
+        db = torch.empty(A, dtype=torch.float32, device=x.device)
+        lib = _lib.load()
+        ne = src.numel()
+        ws = _lib.workspace(lib.spai_policy_backward_workspace_bytes(n, ne, fin, self.hid, A), x.device,
+                            "policy_bwd")
+        with kernels._timed("policy_backward"):
+            st = lib.spai_policy_backward(n, ne, fin, self.hid, _lib.ptr(xf), _lib.ptr(rowptr), _lib.ptr(src),
+                                          _lib.ptr(ea), _lib.ptr(rev_ptr), _lib.ptr(rev_eid), _lib.ptr(p1),
+                                          _lib.ptr(p2), _lib.ptr(w), A, _lib.ptr(gf), _lib.ptr(g1), _lib.ptr(g2),
+                                          _lib.ptr(dW), _lib.ptr(db), _lib.ptr(ws), ws.numel(),
+                                          _lib.stream_ptr(x.device))
+        _lib.check(st, "spai_policy_backward")
+        grads = {}
+        for layer, flat in ((self.gat1, g1), (self.gat2, g2)):
+            off = 0
+            for p in (layer.lin_l.weight, layer.lin_l.bias, layer.lin_r.weight, layer.lin_r.bias,
+                      layer.lin_edge.weight, layer.att, layer.bias):
+                grads[id(p)] = flat[off:off + p.numel()].view(p.shape).to(p.dtype)
+                off += p.numel()
+        fw = torch.zeros_like(self.fc.weight)
+        fw[:A] = dW.to(fw.dtype)
+        fb = torch.zeros_like(self.fc.bias)
+        fb[:A] = db.to(fb.dtype)
+        grads[id(self.fc.weight)], grads[id(self.fc.bias)] = fw, fb
+        return grads
 
     def logits_and_max(self, data, B: int = 1) -> Tuple[Tensor, Tensor, Tensor]:
         """(logits [1, E+1], sigmoid(alpha), lmax [B]) — everything of forward() but the mask,

@@ -194,6 +194,20 @@ int spai_policy_logits(int32_t n_nodes, int32_t fin, int32_t hid, const float* x
                        const int32_t* src, const float* eattr, const float* gat1, const float* gat2,
                        const float* fc_w, const float* fc_b, int32_t num_actions, float* logits, float* lmax,
                        int32_t B, void* workspace, size_t workspace_bytes, void* stream);
+/* Backward of the same network (the TB loss's path into ForwardPolicy's parameters, autograd
+ * through policy.py:34-73): given dlogits [num_actions], the gradients in the parameter packs'
+ * layouts (g_gat1 / g_gat2: spai_policy_params floats each) and of the fc rows < num_actions
+ * (g_fc_w [num_actions][hid], g_fc_b [num_actions]).  The forward is recomputed inside.
+ * rev_ptr [n+1] / rev_eid [n_edges]: the CSR's edges grouped by source node (edge positions),
+ * n_edges = rowptr[n] (self loops included).  hid 4 or 8, fin 1/2/4 (else SPAI_ERR_UNSUPPORTED).
+ * Deterministic (fixed-order fp64 sums).  Workspace: spai_policy_backward_workspace_bytes. */
+size_t spai_policy_backward_workspace_bytes(int32_t n_nodes, int32_t n_edges, int32_t fin, int32_t hid,
+                                            int32_t num_actions);
+int spai_policy_backward(int32_t n_nodes, int32_t n_edges, int32_t fin, int32_t hid, const float* x,
+                         const int32_t* rowptr, const int32_t* src, const float* eattr, const int32_t* rev_ptr,
+                         const int32_t* rev_eid, const float* gat1, const float* gat2, const float* fc_w,
+                         int32_t num_actions, const float* dlogits, float* g_gat1, float* g_gat2, float* g_fc_w,
+                         float* g_fc_b, void* workspace, size_t workspace_bytes, void* stream);
 
 /* ---------------------------------------------------------------- training
  * Gradient of the logged forward probabilities w.r.t. the logits (the backward of

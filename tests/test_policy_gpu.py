@@ -82,13 +82,17 @@ def test_policy_logits_state_graph(grid):
     close(got.cpu(), lg)
 
 
-def test_policy_gradients_match_torch():
+@pytest.mark.parametrize("fin,hid", [(1, 4), (2, 8), (4, 4), (1, 16)])
+def test_policy_gradients_match_torch(fin, hid):
+    """spai_policy_backward (hid 4, 8) and the torch-restatement path (hid 16) against autograd
+    through the torch restatement of the same network."""
     torch.manual_seed(3)
     n = 200
     ei, ea = random_graph(n // 2, 700, seed=3)
-    x = torch.randn(n, 1)
-    pol = randomise(ForwardPolicy(1, 4, 800), 11).to(DEV)
+    x = torch.randn(n, fin)
+    pol = randomise(ForwardPolicy(fin, hid, 800), 11).to(DEV)
     data = Data(x=x.to(DEV), edge_index=torch.from_numpy(ei).to(DEV), edge_attr=torch.from_numpy(ea).to(DEV))
+    assert pol._hip_backward_ok(data) == (hid in (4, 8))
     w = torch.randn(1, 701, device=DEV)
     lg, a, _ = pol.logits_and_max(data)
     ((lg * w).sum() + a).backward()

@@ -15,9 +15,9 @@
 //                deterministic fp32 keys (in registers), removal bitmap words, the fp64
 //                mass of the untouched actions, bucket histogram with in-bucket ranks, and
 //                the tile's winners written grouped by bucket through LDS windows as one
-//                contiguous 8 B record stream + 4 B logit stream; per-(bucket, tile) runs.
+//                contiguous 8 B record stream + 4 B logit stream; per-(bucket, tile) runs
+//                in a bucket-major table (one contiguous row per bucket).
 //   k_bscan      per sample: bucket starts, winner count, untouched mass, T.
-//   k_runs       run table transposed bucket-major (one contiguous row per bucket).
 //   k_sort2      persistent; per bucket: one-round-trip gather of its runs (one per tile)
 //                into registers, value-linear sub-buckets + rank counting in LDS, fp32
 //                weights w = exp(l - lmax), fp64 in-bucket suffix sums.  Outputs stored
@@ -38,7 +38,7 @@ namespace {
 #define KTILE 16384
 #endif
 constexpr int kTile = KTILE;               // actions per tile (k_tile block; a run per bucket)
-static_assert(kTile <= 65535, "run offsets and counts are packed in 16 bits (k_tile, k_runs)");
+static_assert(kTile <= 65535, "run offsets and counts are packed in 16 bits (k_tile, k_sort2)");
 #ifndef KGRPNT
 #define KGRPNT 1024
 #endif
@@ -73,8 +73,7 @@ struct TrajWs {
   uint32_t* lut_base;     // [B][2] (min key, shift) of the table
   uint64_t* staging;      // [B][ntiles][kTile] (~ord << 32 | action), grouped by bucket per tile
   float* stlog;           // [B][ntiles][kTile] logit of each staged record
-  uint32_t* trun;         // [B][ntiles][kMaxB] run of bucket k in tile t: offset << 16 | count
-  uint32_t* runs;         // [B][kMaxB][ntiles] the same, bucket-major (k_runs)
+  uint32_t* runs;         // [B][kMaxB][ntiles] run of bucket k in tile t: offset << 16 | count (k_tile)
   double* tile_wrest;     // [B][ntiles]
   int32_t* bstart;        // [B][kMaxB + 1]
   double* wrest;          // [B]
@@ -104,8 +103,7 @@ static void traj_ws(void* base, int32_t E, int32_t B, TrajWs* w) {
   w->lut_base = c.take<uint32_t>((size_t)B * 2);
   w->staging = c.take<uint64_t>((size_t)B * w->ntiles * kTile);
   w->stlog = c.take<float>((size_t)B * w->ntiles * kTile);
-  w->trun = c.take<uint32_t>((size_t)B * kMaxB * w->ntiles);
-  w->runs = c.take<uint32_t>((size_t)B * kMaxB * w->ntiles);
+  w->runs =c.take<uint32_t>((size_t)B * kMaxB * w->ntiles);
   w->tile_wrest = c.take<double>((size_t)B * w->ntiles);
   w->bstart = c.take<int32_t>((size_t)B * (kMaxB + 1));
   w->wrest = c.take<double>(B);
@@ -448,7 +446,7 @@ void k_tile(const float* __restrict__ logits, int64_t bstride, int32_t E,
                                                  const uint16_t* __restrict__ lut_,
                                                  const uint32_t* __restrict__ lut_base,
                                                  uint64_t* __restrict__ staging, float* __restrict__ stlog,
-                                                 uint32_t* __restrict__ trun, int32_t* __restrict__ btot,
+                                                 uint32_t* __restrict__ runs, int32_t* __restrict__ btot,
                                                  double* __restrict__ tile_wrest) {
   __shared__ uint64_t w_rec[kWin];  // one window of the grouped output
   __shared__ float w_log[kWin];
@@ -567,13 +565,16 @@ void k_tile(const float* __restrict__ logits, int64_t bstride, int32_t E,
   }
   int tot;
   int run = block_excl_scan<kGrpNT>(loc, s_wc, &tot);
-  const int64_t trow = ((int64_t)b * ntiles + tile) * kMaxB;  // tile-major: one contiguous row per tile
+  // bucket-major run table [b][bucket][tile] written directly (k_sort2 reads one bucket's runs
+  // as a contiguous row): neighbouring tiles fill neighbouring words of a row, so the scattered
+  // 4-byte stores merge in L2; this replaced a separate transpose kernel (k_runs, 26 us at C4)
+  uint32_t* rcol = runs + (int64_t)b * kMaxB * ntiles + tile;
 #pragma unroll
   for (int q = 0; q < kQ; ++q) {
     const int k = tid * kQ + q;
     if (k < nb) {
       s_off[k] = run;
-      trun[trow + k] = ((uint32_t)run << 16) | (uint32_t)hv[q];
+      rcol[(int64_t)k * ntiles] = ((uint32_t)run << 16) | (uint32_t)hv[q];
       if (hv[q]) atomicAdd(&btot[(int64_t)b * kMaxB + k], hv[q]);
     }
     run += hv[q];
@@ -717,25 +718,6 @@ __device__ void big_bucket_sort(uint64_t* __restrict__ s0, uint64_t* __restrict_
   }
 }
 
-// ------------------------------------------------------------------ k_runs
-// Run table transposed to bucket-major, so the level-2 sort reads one bucket's runs as a
-// contiguous row: block (tile chunk of 64, bucket chunk of 64, sample) through LDS.
-constexpr int kRunT = 64;
-__global__ __launch_bounds__(256) void k_runs(int32_t ntiles, const int32_t* __restrict__ nb_,
-                                              const uint32_t* __restrict__ trun, uint32_t* __restrict__ runs) {
-  __shared__ uint32_t t[kRunT][kRunT + 1];
-  const int b = blockIdx.z, t0 = blockIdx.x * kRunT, k0 = blockIdx.y * kRunT;
-  const int nb = nb_[b];
-  if (k0 >= nb) return;
-  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-  const uint32_t* src = trun + (int64_t)b * ntiles * kMaxB;
-  for (int r = ty; r < kRunT; r += 4)
-    t[r][tx] = (t0 + r < ntiles && k0 + tx < nb) ? src[(int64_t)(t0 + r) * kMaxB + k0 + tx] : 0u;
-  __syncthreads();
-  uint32_t* dst = runs + (int64_t)b * kMaxB * ntiles;
-  for (int r = ty; r < kRunT; r += 4)
-    if (k0 + r < nb && t0 + tx < ntiles) dst[(int64_t)(k0 + r) * ntiles + t0 + tx] = t[tx][r];
-}
 
 // ------------------------------------------------------------------ k_sort2
 
@@ -1225,7 +1207,7 @@ extern "C" int spai_rollout_select(const float* logits, int64_t bstride, int32_t
   SPAI_CHECK_LAUNCH();
   k_tile<<<dim3(w.ntiles, B), kGrpNT, 0, s>>>(logits, bstride, E, w.ntiles, s0, s1, t0, t1, sample_base, removed,
                                               words, lmax, w.nb, w.spl, w.lut, w.lut_base, w.staging, w.stlog,
-                                              w.trun, w.btot, w.tile_wrest);
+                                              w.runs, w.btot, w.tile_wrest);
   SPAI_CHECK_LAUNCH();
   k_bscan<<<B, 1024, 0, s>>>(E, w.ntiles, logits, bstride, lmax, w.nb, w.btot, w.tile_wrest, w.bstart,
                              counts, w.wrest, w.tdev);
@@ -1248,7 +1230,6 @@ extern "C" int spai_rollout_order(const float* logits, int64_t bstride, int32_t 
   hipStream_t s = (hipStream_t)stream;
   const int nbm = max_buckets(E);
   const int g2 = std::max(1, std::min(nbm * B, num_cus()));
-  k_runs<<<dim3((w.ntiles + kRunT - 1) / kRunT, kMaxB / kRunT, B), 256, 0, s>>>(w.ntiles, w.nb, w.trun, w.runs);
   k_sort2<<<g2, kSortNT, 0, s>>>(E, B, w.ntiles, w.nb, w.bstart, w.runs, w.staging, w.stlog, lmax, t_cap,
                                  actions, w.out_w, w.out_suf, w.bwsum);
   SPAI_CHECK_LAUNCH();

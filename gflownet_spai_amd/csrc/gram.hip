@@ -24,6 +24,9 @@ namespace {
 
 constexpr int kNT = 256;
 constexpr int kChunk = 8;  // samples per LDS residual chunk of the fill kernel
+#ifndef FILL_WPE5
+#define FILL_WPE5 4  // waves/SIMD of the 5-wide fill (7-wide: 2, no spills)
+#endif
 
 __host__ __device__ constexpr int tri(int w) { return w * (w + 1) / 2; }
 
@@ -97,7 +100,7 @@ __global__ __launch_bounds__(kNT) void k_gram_build(int32_t n, int32_t wrt, int3
 // squared line residuals of a chunk of kChunk samples go to LDS and are summed per sample
 // by one wave each in a fixed order (two barriers per chunk, none per sample).
 template <int W, typename TM, bool LSQ, typename GT>
-__global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(4))) void k_gram_fill(int32_t n, int32_t line_begin, int32_t line_end, int32_t wrt,
+__global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(W <= 5 ? FILL_WPE5 : 2))) void k_gram_fill(int32_t n, int32_t line_begin, int32_t line_end, int32_t wrt,
                                                    const int32_t* __restrict__ pat_act,
                                                    const float* __restrict__ pat_val,
                                                    const GT* __restrict__ gram, int32_t B,

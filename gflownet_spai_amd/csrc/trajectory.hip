@@ -62,7 +62,9 @@ constexpr int kBins = 4096;                // splitter histogram / bucket lookup
 
 struct TrajWs {
   int32_t ntiles, M;
-  int32_t* ctl;           // zeroed per rollout: btot [B][kMaxB] | reserved [B] | tdev
+  int32_t* ctl;           // zeroed per rollout: btot [B][kMaxB] | bigcnt, reserved [B] | tdev
+  int32_t* bigcnt;        // number of oversized buckets (k_sort2 -> k_sort2_big)
+  int32_t* biglist;       // [B][kMaxB] their flattened (sample, bucket) indices
   int32_t* btot;          // [B][kMaxB] winners per bucket (atomic sums over tiles)
   int32_t* tdev;
   int32_t* samp_cnt;      // [B][M / kSampNT] winners per presample block
@@ -95,6 +97,8 @@ static void traj_ws(void* base, int32_t E, int32_t B, TrajWs* w) {
   w->ctl = c.take<int32_t>((size_t)B * kMaxB + B + 1);
   w->btot = w->ctl;
   w->tdev = w->ctl + (size_t)B * kMaxB + B;
+  w->bigcnt = w->ctl + (size_t)B * kMaxB;  // first reserved slot: oversized buckets found by k_sort2
+  w->biglist = c.take<int32_t>((size_t)B * kMaxB);
   w->samp_cnt = c.take<int32_t>((size_t)B * nsb);
   w->samp = c.take<uint32_t>((size_t)B * M);
   w->nb = c.take<int32_t>(B);
@@ -774,7 +778,8 @@ __global__ __launch_bounds__(kSortNT) void k_sort2(int32_t E, int32_t B, int32_t
                                                    const float* __restrict__ stlog, const float* __restrict__ lmax_,
                                                    int64_t t_cap, int64_t* __restrict__ actions,
                                                    float* __restrict__ out_w, float* __restrict__ out_suf,
-                                                   double* __restrict__ bwsum) {
+                                                   double* __restrict__ bwsum, int32_t* __restrict__ bigcnt,
+                                                   int32_t* __restrict__ biglist) {
   __shared__ uint64_t A[kCap2];  // low half: gather map; high half: actions awaiting store
   __shared__ float L[kCap2];     // weights in trajectory order
   __shared__ float S[kCap2];     // suffix sums awaiting store
@@ -866,6 +871,7 @@ __global__ __launch_bounds__(kSortNT) void k_sort2(int32_t E, int32_t B, int32_t
     PROF(0)
     if (n == 0 || n > kCap2) {
       if (n == 0 && tid == 0) bwsum[(int64_t)b * kMaxB + k] = 0.0;
+      if (n > kCap2 && tid == 0) biglist[atomicAdd(bigcnt, 1)] = f;  // for k_sort2_big (rare)
       __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): retire the fetch (see above)
       continue;
     }
@@ -1040,7 +1046,8 @@ __global__ __launch_bounds__(kSortNT) void k_sort2_big(int32_t E, int32_t B, int
                                                        const float* __restrict__ lmax_, int64_t t_cap,
                                                        int64_t* __restrict__ actions, float* __restrict__ out_w,
                                                        float* __restrict__ out_suf, uint64_t* __restrict__ scratch,
-                                                       double* __restrict__ bwsum) {
+                                                       double* __restrict__ bwsum, const int32_t* __restrict__ bigcnt,
+                                                       const int32_t* __restrict__ biglist) {
   __shared__ int s_nbp[kMaxSamples + 1];
   __shared__ int s_pre[kMaxTiles + 1];
   __shared__ int s_loc[kMaxTiles];
@@ -1048,6 +1055,8 @@ __global__ __launch_bounds__(kSortNT) void k_sort2_big(int32_t E, int32_t B, int
   __shared__ double s_wd[kSortNT / 64];
   __shared__ uint32_t s_red[4 * (kSortNT / 64)];
   const int tid = threadIdx.x;
+  const int nbig = *bigcnt;  // oversized buckets k_sort2 skipped (usually none: the whole grid exits here)
+  if (nbig == 0) return;
   {  // prefix of the bucket counts over the samples (parallel loads)
     const int v = tid < B ? nb_[tid] : 0;
     int tot;
@@ -1056,9 +1065,9 @@ __global__ __launch_bounds__(kSortNT) void k_sort2_big(int32_t E, int32_t B, int
     if (tid == 0) s_nbp[B] = tot;
   }
   __syncthreads();
-  const int total = s_nbp[B];
 #pragma unroll 1
-  for (int f = blockIdx.x; f < total; f += gridDim.x) {
+  for (int q = blockIdx.x; q < nbig; q += gridDim.x) {
+    const int f = biglist[q];
     int b = 0;
     while (s_nbp[b + 1] <= f) ++b;
     const int k = f - s_nbp[b];
@@ -1231,10 +1240,11 @@ extern "C" int spai_rollout_order(const float* logits, int64_t bstride, int32_t 
   const int nbm = max_buckets(E);
   const int g2 = std::max(1, std::min(nbm * B, num_cus()));
   k_sort2<<<g2, kSortNT, 0, s>>>(E, B, w.ntiles, w.nb, w.bstart, w.runs, w.staging, w.stlog, lmax, t_cap,
-                                 actions, w.out_w, w.out_suf, w.bwsum);
+                                 actions, w.out_w, w.out_suf, w.bwsum, w.bigcnt, w.biglist);
   SPAI_CHECK_LAUNCH();
   k_sort2_big<<<g2, kSortNT, 0, s>>>(E, B, w.ntiles, w.nb, w.bstart, w.runs, w.staging, logits, bstride,
-                                     lmax, t_cap, actions, w.out_w, w.out_suf, w.scratch, w.bwsum);
+                                     lmax, t_cap, actions, w.out_w, w.out_suf, w.scratch, w.bwsum, w.bigcnt,
+                                     w.biglist);
   SPAI_CHECK_LAUNCH();
   k_wscan<<<B, 1024, 0, s>>>(w.nb, w.bwsum, w.bwsuf);
   SPAI_CHECK_LAUNCH();

@@ -237,8 +237,14 @@ __device__ __forceinline__ uint64_t block_excl_scan_u64(uint64_t c, uint64_t* ld
 __global__ __launch_bounds__(kSampNT) void k_presample(const float* __restrict__ logits, int64_t bstride, int32_t E,
                                                        int32_t M, uint32_t seed0, uint32_t seed1, uint32_t st0,
                                                        uint32_t st1, int32_t sample_base,
-                                                       uint32_t* __restrict__ samp, int32_t* __restrict__ samp_cnt) {
+                                                       uint32_t* __restrict__ samp, int32_t* __restrict__ samp_cnt,
+                                                       int32_t* __restrict__ ctl, int32_t nctl) {
   const int b = blockIdx.y, tid = threadIdx.x;
+  {  // the rollout's control block (bucket totals, oversized-bucket list count, tdev) starts at 0;
+     // its first users (k_tile, k_sort2, k_bscan) run after this launch on the same stream
+    const int nthr = gridDim.x * gridDim.y * kSampNT;
+    for (int q = (blockIdx.y * gridDim.x + blockIdx.x) * kSampNT + tid; q < nctl; q += nthr) ctl[q] = 0;
+  }
   const float* lg = logits + (int64_t)b * bstride;
   const uint32_t bg = (uint32_t)(sample_base + b);
   __shared__ float s_tk;
@@ -1207,10 +1213,9 @@ extern "C" int spai_rollout_select(const float* logits, int64_t bstride, int32_t
   hipStream_t s = (hipStream_t)stream;
   const uint32_t s0 = (uint32_t)seed, s1 = (uint32_t)(seed >> 32);
   const uint32_t t0 = (uint32_t)stream_id, t1 = (uint32_t)(stream_id >> 32);
-  SPAI_CHECK_HIP(hipMemsetAsync(w.ctl, 0, sizeof(int32_t) * ((size_t)B * kMaxB + B + 1), s));
   const int nsb = (w.M + kSampNT - 1) / kSampNT;
   k_presample<<<dim3(nsb, B), kSampNT, 0, s>>>(logits, bstride, E, w.M, s0, s1, t0, t1, sample_base, w.samp,
-                                              w.samp_cnt);
+                                              w.samp_cnt, w.ctl, B * kMaxB + B + 1);
   SPAI_CHECK_LAUNCH();
   k_splitters<<<B, kSortNT, 0, s>>>(E, w.M, nsb, w.samp, w.samp_cnt, w.nb, w.spl, w.lut, w.lut_base);
   SPAI_CHECK_LAUNCH();

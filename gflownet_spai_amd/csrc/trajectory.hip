@@ -429,16 +429,6 @@ extern "C" int spai_debug_prof(unsigned long long* out, int reset) {
 #define PROF_END(base)
 #endif
 
-// Bucket of a winner's orderable key: value-linear lookup table, then the splitters
-// (usually 0-1 steps); buckets are numbered in trajectory order (descending key).
-__device__ __forceinline__ int bucket_lut(uint32_t o, const uint16_t* s_lut, const uint32_t* s_spl, uint32_t lmn,
-                                          int lsh, int nb) {
-  const uint32_t bin = o < lmn ? 0u : min((uint32_t)(kBins - 1), (o - lmn) >> lsh);
-  int c = s_lut[bin];
-  while (c < nb - 1 && s_spl[c] <= o) ++c;
-  return nb - 1 - c;
-}
-
 // ------------------------------------------------------------------ k_tile
 // Selection and grouping fused, one 16384-action tile of one sample per block: Gumbel keys
 // of the tile (16 actions per thread; keys and logits kept in registers), the removed bitmap, the rest mass
@@ -547,12 +537,35 @@ void k_tile(const float* __restrict__ logits, int64_t bstride, int32_t E,
   // bucket histogram of the winners; each winner keeps its bucket and its rank inside the
   // bucket (the histogram atomic's return; any order: the level-2 sort orders buckets fully)
   static_assert(kMaxB <= (1 << 11) && kTile <= (1 << 21), "bucket | rank << 11 packing");
+  // bucket of a winner's orderable key (buckets numbered in trajectory order, descending key):
+  // value-linear lookup table, then the splitters, for all the thread's slots at once: the table guesses of every slot are read
+  // together, then wave-uniform correction rounds over the splitters (usually one step and one
+  // check), so the LDS reads of the slots overlap instead of forming one dependent chain each
+  int bc[4 * kTileG];
+#pragma unroll
+  for (int q = 0; q < 4 * kTileG; ++q) {
+    const uint32_t o = ord[q];
+    const uint32_t bin = o < lmn ? 0u : min((uint32_t)(kBins - 1), (o - lmn) >> lsh);
+    bc[q] = s_lut[bin];
+  }
+  const int nbl = nb - 1;
+  bool more;
+  do {
+    more = false;
+#pragma unroll
+    for (int q = 0; q < 4 * kTileG; ++q) {
+      const uint32_t sv = s_spl[max(0, min(bc[q], nbl - 1))];
+      const bool step = ((win >> q) & 1u) && bc[q] < nbl && sv <= ord[q];
+      bc[q] += step;
+      more |= step;
+    }
+  } while (__any(more));
   uint32_t br[4 * kTileG];
 #pragma unroll
   for (int q = 0; q < 4 * kTileG; ++q) {
     br[q] = 0u;
     if ((win >> q) & 1u) {
-      const int bk = bucket_lut(ord[q], s_lut, s_spl, lmn, lsh, nb);
+      const int bk = nbl - bc[q];
       br[q] = (uint32_t)bk | ((uint32_t)atomicAdd(&s_off[bk], 1) << 11);
     }
   }

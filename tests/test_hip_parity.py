@@ -174,10 +174,32 @@ def test_throughput_rollout_clustered_keys_overflow_path():
     actions, fwd, t_dev = kernels.rollout_order(lg, B, lmax, counts, ws)
     T = int(t_dev)
     r_o, a_o, f_o, c_o = O.throughput_rollout(logits, B, 99, 1)
-    assert c_o.max() > 4096  # buckets beyond the 2048-element LDS capacity
+    assert c_o.max() > 4096  # more winners than one 4096-record presample bucket
     assert np.array_equal(counts.cpu().numpy(), c_o)
     assert np.array_equal(actions[:, :T].cpu().numpy(), a_o.T)
     np.testing.assert_allclose(fwd[:, :T].cpu().numpy(), f_o, rtol=1e-6)
+
+
+def test_throughput_rollout_tied_keys_oversized_bucket():
+    """All 20,000 actions win with one and the same fp32 key (logit 1e30 swamps its Gumbel
+    noise; the terminal's 9.9e29 loses to it) and fall into one bucket beyond k_sort2's
+    8192-record LDS capacity: k_sort2 lists it and k_sort2_big orders it (ties by action id,
+    as the oracle).  The terminal's own probability is 0/0 in both and is not compared."""
+    from gflownet_spai_amd import kernels
+    E, B = 20000, 2
+    logits = np.full(E + 1, 1e30, np.float32)
+    logits[E] = 9.9e29
+    lg, lmax, z = kernels.logits_stats(torch.from_numpy(logits).to(DEV), B)
+    removed, counts, ws = kernels.rollout_select(lg, B, lmax, 5, 3)
+    actions, fwd, t_dev = kernels.rollout_order(lg, B, lmax, counts, ws)
+    T = int(t_dev)
+    big = int(ws[: 4 * (B * 2048 + 1)].view(torch.int32)[B * 2048])  # ctl: btot [B][2048] | oversized count
+    assert big >= B  # the big path ran for every sample
+    r_o, a_o, f_o, c_o = O.throughput_rollout(logits, B, 5, 3)
+    assert (c_o == E).all()
+    assert np.array_equal(counts.cpu().numpy(), c_o)
+    assert np.array_equal(actions[:, :T].cpu().numpy(), a_o.T)
+    np.testing.assert_allclose(fwd[:, :T - 1].cpu().numpy(), f_o[:, :T - 1], rtol=1e-6)
 
 
 def test_full_size_c4_rollout_vs_oracle():

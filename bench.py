@@ -25,11 +25,23 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 CONFIGS = {
-    # name: (dims, grid, dtype, workload text)
-    "c4": (2, 1024, torch.float32, "C4: 1024^2 5-pt Poisson (1,048,576 x 1,048,576 CSR, fp32)"),
-    "c2": (2, 256, torch.float32, "C2: 256^2 5-pt Poisson (65,536 x 65,536 CSR, fp32)"),
-    "c3": (3, 64, torch.float64, "C3: 64^3 7-pt 3-D Laplacian (262,144 x 262,144, fp64)"),
+    # name: (dims, grid, dtype, workload text); candidate pattern = A (2-D) or the 13-wide axial
+    # pattern (C3: nnz/col <= 13, utils.axial_pattern_3d)
+    "c4": (2, 1024, torch.float32, "C4: 1024^2 5-pt Poisson (1,048,576 x 1,048,576 CSR, fp32), pattern = A"),
+    "c2": (2, 256, torch.float32, "C2: 256^2 5-pt Poisson (65,536 x 65,536 CSR, fp32), pattern = A"),
+    "c3": (3, 64, torch.float64, "C3: 64^3 7-pt 3-D Laplacian (262,144 x 262,144, fp64), 13-wide axial pattern "
+                                 "(nnz/col <= 13)"),
 }
+
+
+def config_matrices(cfg: str):
+    """(A, candidate pattern) of a bench config."""
+    from gflownet_spai_amd import axial_pattern_3d, poisson_2d, poisson_3d
+    dims, grid, dtype, _ = CONFIGS[cfg]
+    if dims == 2:
+        A = poisson_2d(grid, dtype)
+        return A, A
+    return poisson_3d(grid, dtype), axial_pattern_3d(grid, 2, dtype)
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec (6.29 TB/s measured copy)
 
 
@@ -139,6 +151,23 @@ def cpu_baseline(cfg, B, budget_s: float, logits=None):
                       f"extrapolated to N columns; policy forward not included"}
 
 
+def launch_ranks(n: int) -> int:
+    """`bench.py --gpus N` run directly: start the N ranks (one process per GPU) under
+    torch.distributed.run on 127.0.0.1 as child processes and return their exit status.
+    The parent has not initialised the GPU (no HIP call before this point)."""
+    import socket
+    import subprocess
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.run(cmd, env=env).returncode
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -158,7 +187,12 @@ def main():
     ap.add_argument("--no-overlap", action="store_true", help="(default; kept for old command lines)")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))  # one child process per GPU; nothing here touched the GPU
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; launch with "
+                 f"torch.distributed.run --nproc-per-node {args.gpus} or without WORLD_SIZE")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
@@ -170,9 +204,9 @@ def main():
     from gflownet_spai_amd import GFlowNet, PreconditionerEnv, kernels, poisson_2d, poisson_3d
 
     dims, grid, dtype, text = CONFIGS[args.config]
-    A = poisson_2d(grid, dtype) if dims == 2 else poisson_3d(grid, dtype)
+    A, P = config_matrices(args.config)
     n = A.shape[0]
-    env = PreconditionerEnv(n, A, A, side="AM", fill="lsq", keep_m=True, device=dev)
+    env = PreconditionerEnv(n, P, A, side="AM", fill="lsq", keep_m=True, device=dev)
     E = env.num_actions - 1
     B = args.batch
     columns = args.shard == "columns"
@@ -181,9 +215,9 @@ def main():
         from gflownet_spai_amd.distributed import allgather_lines, shard_lines
         lb, le = shard_lines(n, rank, world)
         shard = (lb, le, None)
-    model = GFlowNet(make_policy(env, A, dev), None, env, mode="throughput", seed=1234,
+    model = GFlowNet(make_policy(env, P, dev), None, env, mode="throughput", seed=1234,
                      sample_base=0 if columns else rank * B, overlap=args.overlap and not args.no_overlap, line_shard=shard)
-    s0 = [A] * B
+    s0 = [P] * B
 
     def step():
         log = model.sample_states(s0, return_log=True)

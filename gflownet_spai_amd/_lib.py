@@ -21,7 +21,7 @@ if os.environ.get("SPAI_LIB_VARIANT"):  # A/B timing of kernel variants built un
 SPAI_OK, SPAI_ERR_INVALID, SPAI_ERR_HIP, SPAI_ERR_UNSUPPORTED = 0, 1, 2, 3
 FILL_COPY, FILL_LSQ = 0, 1
 DTYPE_F32, DTYPE_F64 = 0, 1
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 _c_i32, _c_i64, _c_u64, _c_sz, _c_p = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_size_t, ctypes.c_void_p
 
@@ -54,7 +54,9 @@ SIGNATURES = {
     "spai_policy_params": (_c_sz, [_c_i32, _c_i32, _c_i32]),
     "spai_policy_workspace_bytes": (_c_sz, [_c_i32, _c_i32, _c_i32]),
     "spai_policy_logits": (ctypes.c_int, [_c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p,
-                                          _c_i32, _c_p, _c_p, _c_i32, _c_p, _c_sz, _c_p]),
+                                          _c_i32, _c_p, _c_p, _c_i32, _c_i32, _c_p, _c_sz, _c_p]),
+    "spai_policy_rows_constant": (ctypes.c_int, [_c_i32, _c_i32, _c_p, _c_p, _c_p]),
+    "spai_rollout_ws_offset": (_c_i64, [_c_i32, _c_i32, _c_i32]),
     "spai_logp_grad_workspace_bytes": (_c_sz, [_c_i32, _c_i32, _c_i32, _c_i32]),
     "spai_logp_grad": (ctypes.c_int, [_c_p, _c_i64, _c_i32, _c_i32, _c_p, _c_p, _c_i64, _c_i32, _c_p, _c_i64, _c_p,
                                       _c_i64, _c_p, _c_i32, _c_p, _c_p, _c_sz, _c_p]),

@@ -417,6 +417,49 @@ __global__ __launch_bounds__(kRedNT) void k_max(int32_t nblk, const float* __res
   for (int bb = threadIdx.x; bb < B; bb += kRedNT) lmax[bb] = r;
 }
 
+// ------------------------------------------------------------------ constant node features
+// state_to_data builds x = ones(2N, 1) (gflownet.py:247): every source a target aggregates
+// carries the same W_l x_j + b_l, and the softmax weights of a target sum to 1 (its self
+// loop guarantees an in-edge), so each layer's output is the same for every node:
+//     h1 = relu(W_l1 x0 + b_l1 + bias1),  h2 = relu(W_l2 h1 + b_l2 + bias2),  pool = h2.
+// The whole GATv2 stack then collapses to these two small products (one block), and only
+// the fc GEMV streams memory.  The general kernels above remain the path for any other x.
+
+// flag stays 1 iff every row of x [n][F] equals row 0 (a benign race: writers only store 0).
+__global__ __launch_bounds__(kNT) void k_rows_const(int32_t n, int32_t F, const float* __restrict__ x,
+                                                    int32_t* __restrict__ flag) {
+  const int64_t total = (int64_t)n * F;
+  bool same = true;
+  for (int64_t i = (int64_t)blockIdx.x * kNT + threadIdx.x; i < total; i += (int64_t)gridDim.x * kNT)
+    same &= x[i] == x[i % F];
+  if (__any(!same) && (threadIdx.x & 63) == 0) *flag = 0;
+}
+
+template <int F, int C>
+__global__ __launch_bounds__(64) void k_const_pool(const float* __restrict__ x0, const float* __restrict__ p1,
+                                                   const float* __restrict__ p2, float* __restrict__ hpool) {
+  constexpr int HC = kH1 * C;
+  __shared__ float h1[HC];
+  const float* Wl = p1;
+  const float* bl = Wl + HC * F;
+  const float* bias1 = p1 + 2 * HC * F + 5 * HC - HC;
+  for (int k = threadIdx.x; k < HC; k += 64) {
+    float v = bl[k];
+#pragma unroll
+    for (int f = 0; f < F; ++f) v = fmaf(Wl[k * F + f], x0[f], v);
+    h1[k] = fmaxf(v + bias1[k], 0.0f);
+  }
+  __syncthreads();
+  const float* Wl2 = p2;
+  const float* bl2 = Wl2 + C * HC;
+  const float* bias2 = p2 + 2 * C * HC + 5 * C - C;
+  for (int o = threadIdx.x; o < C; o += 64) {
+    float v = 0.0f;
+    for (int k = 0; k < HC; ++k) v = fmaf(Wl2[o * HC + k], h1[k], v);
+    hpool[o] = fmaxf((v + bl2[o]) + bias2[o], 0.0f);
+  }
+}
+
 struct PolicyWs {
   float* xlr2;
   double* part;
@@ -439,13 +482,17 @@ size_t policy_ws(int32_t n, int32_t hid, int32_t na, void* base, PolicyWs* w) {
 template <int F, int C>
 void launch_policy(int32_t n, const float* x, const int32_t* rp, const int32_t* src, const float* ea, const float* p1,
                    const float* p2, const float* fw, const float* fb, int32_t na, float* logits, float* lmax,
-                   int32_t B, const PolicyWs& w, hipStream_t s) {
+                   int32_t B, const PolicyWs& w, hipStream_t s, bool const_rows) {
   constexpr int HPT = C <= 8 ? kH1 : 1;
   const int64_t t1 = (int64_t)n * (kH1 / HPT);
   const int g2 = (n + kNT - 1) / kNT, gf = fc_blocks(na);
-  k_gat1<F, C, HPT><<<(int)((t1 + kNT - 1) / kNT), kNT, 0, s>>>(n, x, rp, src, ea, p1, p2, w.xlr2);
-  k_gat2<C><<<g2, kNT, 0, s>>>(n, rp, src, ea, p2, w.xlr2, w.part);
-  k_pool<C><<<1, kRedNT, 0, s>>>(n, g2, w.part, w.hpool);
+  if (const_rows) {
+    k_const_pool<F, C><<<1, 64, 0, s>>>(x, p1, p2, w.hpool);
+  } else {
+    k_gat1<F, C, HPT><<<(int)((t1 + kNT - 1) / kNT), kNT, 0, s>>>(n, x, rp, src, ea, p1, p2, w.xlr2);
+    k_gat2<C><<<g2, kNT, 0, s>>>(n, rp, src, ea, p2, w.xlr2, w.part);
+    k_pool<C><<<1, kRedNT, 0, s>>>(n, g2, w.part, w.hpool);
+  }
   k_fc<C><<<gf, kNT, 0, s>>>(na, fw, fb, w.hpool, logits, w.pmax);
   k_max<<<1, kRedNT, 0, s>>>(gf, w.pmax, lmax, B);
 }
@@ -453,12 +500,12 @@ void launch_policy(int32_t n, const float* x, const int32_t* rp, const int32_t* 
 template <int F>
 bool dispatch_hid(int32_t hid, int32_t n, const float* x, const int32_t* rp, const int32_t* src, const float* ea,
                   const float* p1, const float* p2, const float* fw, const float* fb, int32_t na, float* logits,
-                  float* lmax, int32_t B, const PolicyWs& w, hipStream_t s) {
+                  float* lmax, int32_t B, const PolicyWs& w, hipStream_t s, bool cr) {
   switch (hid) {
-    case 4: launch_policy<F, 4>(n, x, rp, src, ea, p1, p2, fw, fb, na, logits, lmax, B, w, s); return true;
-    case 8: launch_policy<F, 8>(n, x, rp, src, ea, p1, p2, fw, fb, na, logits, lmax, B, w, s); return true;
-    case 16: launch_policy<F, 16>(n, x, rp, src, ea, p1, p2, fw, fb, na, logits, lmax, B, w, s); return true;
-    case 32: launch_policy<F, 32>(n, x, rp, src, ea, p1, p2, fw, fb, na, logits, lmax, B, w, s); return true;
+    case 4: launch_policy<F, 4>(n, x, rp, src, ea, p1, p2, fw, fb, na, logits, lmax, B, w, s, cr); return true;
+    case 8: launch_policy<F, 8>(n, x, rp, src, ea, p1, p2, fw, fb, na, logits, lmax, B, w, s, cr); return true;
+    case 16: launch_policy<F, 16>(n, x, rp, src, ea, p1, p2, fw, fb, na, logits, lmax, B, w, s, cr); return true;
+    case 32: launch_policy<F, 32>(n, x, rp, src, ea, p1, p2, fw, fb, na, logits, lmax, B, w, s, cr); return true;
     default: return false;
   }
 }
@@ -481,11 +528,27 @@ extern "C" size_t spai_policy_workspace_bytes(int32_t n_nodes, int32_t hid, int3
   return policy_ws(n_nodes, hid, num_actions, nullptr, &w);
 }
 
+extern "C" int spai_policy_rows_constant(int32_t n_nodes, int32_t fin, const float* x, int32_t* flag, void* stream) {
+  SPAI_CHECK_ARG(x && flag && n_nodes > 0 && fin > 0, "spai_policy_rows_constant: bad argument");
+  hipStream_t s = (hipStream_t)stream;
+  const int32_t one = 1;
+  if (hipMemcpyAsync(flag, &one, sizeof(one), hipMemcpyHostToDevice, s) != hipSuccess) {
+    set_error("spai_policy_rows_constant: hipMemcpyAsync failed");
+    return SPAI_ERR_HIP;
+  }
+  const int64_t total = (int64_t)n_nodes * fin;
+  const int grid = (int)std::min<int64_t>(2048, (total + kNT - 1) / kNT);
+  k_rows_const<<<grid, kNT, 0, s>>>(n_nodes, fin, x, flag);
+  SPAI_CHECK_LAUNCH();
+  return SPAI_OK;
+}
+
 extern "C" int spai_policy_logits(int32_t n_nodes, int32_t fin, int32_t hid, const float* x, const int32_t* rowptr,
                                   const int32_t* src, const float* eattr, const float* gat1, const float* gat2,
                                   const float* fc_w, const float* fc_b, int32_t num_actions, float* logits,
-                                  float* lmax, int32_t B, void* workspace, size_t workspace_bytes, void* stream) {
-  SPAI_CHECK_ARG(x && rowptr && src && eattr && gat1 && gat2 && fc_w && fc_b && logits && lmax,
+                                  float* lmax, int32_t B, int32_t const_rows, void* workspace, size_t workspace_bytes,
+                                  void* stream) {
+  SPAI_CHECK_ARG(x && gat1 && gat2 && fc_w && fc_b && logits && lmax && (const_rows || (rowptr && src && eattr)),
                  "spai_policy_logits: null pointer");
   SPAI_CHECK_ARG(n_nodes > 0 && num_actions > 0 && B > 0, "spai_policy_logits: bad shape");
   SPAI_CHECK_ARG(((uintptr_t)fc_w & 15) == 0, "spai_policy_logits: fc weight must be 16-byte aligned");
@@ -497,11 +560,11 @@ extern "C" int spai_policy_logits(int32_t n_nodes, int32_t fin, int32_t hid, con
   bool ok = false;
   switch (fin) {
     case 1: ok = dispatch_hid<1>(hid, n_nodes, x, rowptr, src, eattr, gat1, gat2, fc_w, fc_b, num_actions, logits,
-                                 lmax, B, w, s); break;
+                                 lmax, B, w, s, const_rows != 0); break;
     case 2: ok = dispatch_hid<2>(hid, n_nodes, x, rowptr, src, eattr, gat1, gat2, fc_w, fc_b, num_actions, logits,
-                                 lmax, B, w, s); break;
+                                 lmax, B, w, s, const_rows != 0); break;
     case 4: ok = dispatch_hid<4>(hid, n_nodes, x, rowptr, src, eattr, gat1, gat2, fc_w, fc_b, num_actions, logits,
-                                 lmax, B, w, s); break;
+                                 lmax, B, w, s, const_rows != 0); break;
     default: break;
   }
   if (!ok) {

@@ -62,8 +62,9 @@ constexpr int kBins = 4096;                // splitter histogram / bucket lookup
 
 struct TrajWs {
   int32_t ntiles, M;
-  int32_t* ctl;           // zeroed per rollout: btot [B][kMaxB] | bigcnt, reserved [B] | tdev
-  int32_t* bigcnt;        // number of oversized buckets (k_sort2 -> k_sort2_big)
+  int32_t* ctl;           // zeroed per rollout: btot [B][kMaxB] | bigcnt, reserved [B] | tdev | lastbig
+  int32_t* bigcnt;        // number of oversized buckets (k_sort2 -> k_sort2_big); back to 0 after each order
+  int32_t* lastbig;       // bigcnt of the last order phase (kept for tests / diagnostics)
   int32_t* biglist;       // [B][kMaxB] their flattened (sample, bucket) indices
   int32_t* btot;          // [B][kMaxB] winners per bucket (atomic sums over tiles)
   int32_t* tdev;
@@ -94,9 +95,10 @@ static void traj_ws(void* base, int32_t E, int32_t B, TrajWs* w) {
   while (M * 2 <= E && M * 2 <= kSampM) M *= 2;
   w->M = M;
   const int nsb = (M + kSampNT - 1) / kSampNT;
-  w->ctl = c.take<int32_t>((size_t)B * kMaxB + B + 1);
+  w->ctl = c.take<int32_t>((size_t)B * kMaxB + B + 2);
   w->btot = w->ctl;
   w->tdev = w->ctl + (size_t)B * kMaxB + B;
+  w->lastbig = w->tdev + 1;
   w->bigcnt = w->ctl + (size_t)B * kMaxB;  // first reserved slot: oversized buckets found by k_sort2
   w->biglist = c.take<int32_t>((size_t)B * kMaxB);
   w->samp_cnt = c.take<int32_t>((size_t)B * nsb);
@@ -1119,9 +1121,17 @@ __global__ __launch_bounds__(kSortNT) void k_sort2_big(int32_t E, int32_t B, int
 }
 
 // bwsuf[k] = sum of the weights of all buckets after k (exclusive suffix, fixed order).
+// Also retires the oversized-bucket list of this order phase: k_sort2_big (the only reader)
+// ran before this launch on the same stream, so the count goes back to 0 and a second order
+// call on the same select (k_sort2 appends to the list) starts from an empty list.
 __global__ __launch_bounds__(1024) void k_wscan(const int32_t* __restrict__ nb_, const double* __restrict__ bwsum,
-                                                double* __restrict__ bwsuf) {
+                                                double* __restrict__ bwsuf, int32_t* __restrict__ bigcnt,
+                                                int32_t* __restrict__ lastbig) {
   const int b = blockIdx.x, tid = threadIdx.x;
+  if (b == 0 && tid == 0) {
+    *lastbig = *bigcnt;
+    *bigcnt = 0;
+  }
   __shared__ double sd[16];
   const int nb = nb_[b];
   const int per = (nb + 1023) / 1024;
@@ -1211,6 +1221,18 @@ extern "C" size_t spai_rollout_workspace_bytes(int32_t E, int32_t B) {
   return w.total_bytes;
 }
 
+// Byte offset of a diagnostic word inside the rollout workspace (tests read it from the
+// caller-owned buffer instead of hard-coding the carve): 0 = oversized buckets of the last
+// order phase (k_sort2 -> k_sort2_big), 1 = T of the last rollout.  -1 for a bad field.
+extern "C" int64_t spai_rollout_ws_offset(int32_t E, int32_t B, int32_t field) {
+  if (E <= 0 || B <= 0) return -1;
+  TrajWs w;
+  traj_ws(nullptr, E, B, &w);
+  if (field == 0) return (int64_t)reinterpret_cast<uintptr_t>(w.lastbig);
+  if (field == 1) return (int64_t)reinterpret_cast<uintptr_t>(w.tdev);
+  return -1;
+}
+
 extern "C" int spai_rollout_select(const float* logits, int64_t bstride, int32_t E, int32_t B, const float* lmax,
                                    uint64_t seed, uint64_t stream_id, int32_t sample_base, uint32_t* removed,
                                    int32_t words, int32_t* counts, void* workspace, size_t workspace_bytes,
@@ -1218,6 +1240,7 @@ extern "C" int spai_rollout_select(const float* logits, int64_t bstride, int32_t
   SPAI_CHECK_ARG(logits && lmax && removed && counts && workspace, "spai_rollout_select: null pointer");
   SPAI_CHECK_ARG(E > 0 && B > 0 && bstride >= 0 && sample_base >= 0, "spai_rollout_select: bad shape");
   SPAI_CHECK_ARG((int64_t)E <= (int64_t)kMaxTiles * kTile, "spai_rollout_select: E=%d too large", E);
+  SPAI_CHECK_ARG(B <= kMaxSamples, "spai_rollout_select: B=%d above %d", B, kMaxSamples);
   SPAI_CHECK_ARG(words == (E + 31) / 32, "spai_rollout_select: words must be ceil(E/32)");
   TrajWs w;
   traj_ws(workspace, E, B, &w);
@@ -1228,7 +1251,7 @@ extern "C" int spai_rollout_select(const float* logits, int64_t bstride, int32_t
   const uint32_t t0 = (uint32_t)stream_id, t1 = (uint32_t)(stream_id >> 32);
   const int nsb = (w.M + kSampNT - 1) / kSampNT;
   k_presample<<<dim3(nsb, B), kSampNT, 0, s>>>(logits, bstride, E, w.M, s0, s1, t0, t1, sample_base, w.samp,
-                                              w.samp_cnt, w.ctl, B * kMaxB + B + 1);
+                                              w.samp_cnt, w.ctl, B * kMaxB + B + 2);
   SPAI_CHECK_LAUNCH();
   k_splitters<<<B, kSortNT, 0, s>>>(E, w.M, nsb, w.samp, w.samp_cnt, w.nb, w.spl, w.lut, w.lut_base);
   SPAI_CHECK_LAUNCH();
@@ -1264,7 +1287,7 @@ extern "C" int spai_rollout_order(const float* logits, int64_t bstride, int32_t 
                                      lmax, t_cap, actions, w.out_w, w.out_suf, w.scratch, w.bwsum, w.bigcnt,
                                      w.biglist);
   SPAI_CHECK_LAUNCH();
-  k_wscan<<<B, 1024, 0, s>>>(w.nb, w.bwsum, w.bwsuf);
+  k_wscan<<<B, 1024, 0, s>>>(w.nb, w.bwsum, w.bwsuf, w.bigcnt, w.lastbig);
   SPAI_CHECK_LAUNCH();
   k_final<<<dim3(nbm, B), kFinNT, 0, s>>>(E, w.nb, w.bstart, w.bwsuf, w.out_w, w.out_suf, w.wrest, t_cap, fwd_probs);
   SPAI_CHECK_LAUNCH();

@@ -108,6 +108,35 @@ class GFlowNet(nn.Module):
             out.append(hit[1])
         return out
 
+    def _same_states(self, s0) -> bool:
+        """True when every initial state is the same matrix (the drivers pass clones of one
+        matrix, GFlowNet100.py:276): same storage, or equal indices and values (compared once per
+        set of storages and versions).  Then one policy call serves every sample (the logits
+        depend on the state only)."""
+        key = tuple((m._indices().data_ptr(), m._values().data_ptr(), m._values()._version, m._nnz())
+                    if m.is_sparse else id(m) for m in s0)
+        memo = getattr(self, "_same_memo", None)
+        if memo is not None and memo[0] == key:
+            return memo[1]
+        same = self._compare_states(s0)
+        self._same_memo = (key, same, list(s0))  # the list pins the storages the key names
+        return same
+
+    @staticmethod
+    def _compare_states(s0) -> bool:
+        m0 = s0[0]
+        for m in s0[1:]:
+            if m is m0:
+                continue
+            if not (m.is_sparse and m0.is_sparse) or m.shape != m0.shape or m._nnz() != m0._nnz():
+                return False
+            i0, v0, i1, v1 = m0._indices(), m0._values(), m._indices(), m._values()
+            if i0.data_ptr() == i1.data_ptr() and v0.data_ptr() == v1.data_ptr():
+                continue
+            if not (torch.equal(i0, i1.to(i0.device)) and torch.equal(v0, v1.to(v0.device))):
+                return False
+        return True
+
     def _rewards(self, removed, counts, alpha):
         if self.line_shard is None:
             return self.env.rewards_from_removed(removed, counts, alpha)
@@ -120,10 +149,22 @@ class GFlowNet(nn.Module):
         B = len(s0)
         E = env.num_actions - 1
         log = Log(s0, self.backward_policy, self.total_flow, env)
-        data_list = self.state_to_data(s0[:1])
-        logits, alpha, lmax = self.policy_logits(data_list[0], B)
-        if logits.numel() != E + 1:
-            raise ValueError(f"policy produced {logits.numel()} logits for {E + 1} actions")
+        if self._same_states(s0):
+            data_list = self.state_to_data(s0[:1])
+            logits, alpha, lmax = self.policy_logits(data_list[0], B)
+            if logits.numel() != E + 1:
+                raise ValueError(f"policy produced {logits.numel()} logits for {E + 1} actions")
+        else:
+            # distinct initial states: one policy call per sample (gflownet.py:70-74 builds one
+            # Data per sample), per-sample logit rows [B, E+1] for the sampler
+            rows, alphas = [], []
+            for d in self.state_to_data(s0):
+                l, a, _ = self.policy_logits(d, 1)
+                if l.numel() != E + 1:
+                    raise ValueError(f"policy produced {l.numel()} logits for {E + 1} actions")
+                rows.append(l)
+                alphas.append(a)
+            logits, alpha, lmax = torch.stack(rows, 0), torch.stack(alphas).mean(), None
         if lmax is not None and self.mode == "throughput" and logits.is_cuda and logits.dtype == torch.float32:
             lg = logits.detach()  # the throughput sampler needs only the maximum, which the policy kernels produced
         else:

@@ -77,15 +77,15 @@ def build_lines(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor, n: i
     return Lines(n, width, idx.view(n, width), act.view(n, width), val.view(n, width), orient)
 
 
-def lines_to_coo(lines: Lines, values: torch.Tensor, n: int) -> torch.Tensor:
-    """Assemble a [n, n] sparse COO matrix from per-line values aligned with ``lines``.
-
-    Entries whose value is exactly 0 because the slot was removed are dropped via the
-    ``keep`` mask the caller bakes into ``values`` being NaN-free; padding is dropped.
-    """
+def lines_to_coo(lines: Lines, values: torch.Tensor, n: int, keep: torch.Tensor | None = None) -> torch.Tensor:
+    """Assemble a coalesced [n, n] sparse COO matrix from per-line values aligned with
+    ``lines``: padding slots and the slots where ``keep`` ([n, W] bool) is False are dropped,
+    so the result holds exactly the kept entries (gflownet/utils.py:323-353)."""
     li = torch.arange(n, device=lines.idx.device).repeat_interleave(lines.width)
     oi = lines.idx.reshape(-1).long()
     ok = oi >= 0
+    if keep is not None:
+        ok &= keep.reshape(-1)
     li, oi, v = li[ok], oi[ok], values.reshape(-1)[ok]
     rows, cols = (li, oi) if lines.orient == "row" else (oi, li)
     return torch.sparse_coo_tensor(torch.stack([rows, cols]), v, (n, n)).coalesce()

@@ -78,6 +78,7 @@ class PreconditionerEnv(Env):
         ai = a.indices()
         self.a_lines: Lines = build_lines(ai[0], ai[1], a.values(), matrix_size, orient, self.device, a_dtype)
         self.last_m = None
+        self.last_removed = None  # removal bitmaps [B, ceil(E/32)] of the last batch (assemble)
         # Gram cache of the fixed pattern (G = A_J^T A_J, c = A[l, J] per line): the per-rollout
         # fill then streams it instead of re-gathering A (pattern widths <= 13, A widths <= 7;
         # wider patterns use the generic kernels)
@@ -118,6 +119,7 @@ class PreconditionerEnv(Env):
             dist.all_reduce(res2, group=group)
         if self.keep_m:
             self.last_m = m
+        self.last_removed = removed
         if not torch.is_tensor(alpha):
             alpha = torch.tensor(float(alpha), dtype=torch.float32)
         self.last_residual, reward = kernels.rewards(res2, counts, self.init_nnz, self.matrix_size, self._r0,
@@ -177,14 +179,19 @@ class PreconditionerEnv(Env):
 
     # ------------------------------------------------------------------ products
     def assemble(self, b: int = 0, removed: Tensor | None = None) -> Tensor:
-        """Sparse M of sample b of the last batch (LSQ: stored values; COPY: needs ``removed``)."""
-        if self.fill == "lsq":
-            if self.last_m is None:
-                raise ValueError("construct with keep_m=True to keep M")
-            return lines_to_coo(self.pattern, self.last_m[b], self.matrix_size)
+        """Sparse M of sample b of the last batch, as update_edges_and_convert_to_sparse returns
+        it (gflownet/utils.py:295-356 + resize :89-126): coalesced [N, N] COO holding exactly the
+        kept pattern entries (COPY: their pattern values; LSQ: the fitted values).  ``removed``
+        defaults to the last batch's removal bitmaps."""
         if removed is None:
-            raise ValueError("copy fill: pass the removal bitmaps")
-        bits = removed[b]
-        act = self.pattern.act.long().clamp(min=0)
-        gone = ((bits[act >> 5] >> (act & 31)) & 1).bool() | (self.pattern.act < 0)
-        return lines_to_coo(self.pattern, torch.where(gone, 0.0, self.pattern.val), self.matrix_size)
+            removed = self.last_removed
+        if removed is None:
+            raise ValueError("no removal bitmaps: run update / rewards_from_removed first or pass removed")
+        if self.fill == "lsq" and self.last_m is None:
+            raise ValueError("construct with keep_m=True to keep M")
+        bits = removed[b].to(self.device)
+        act = self.pattern.act.long()
+        a = act.clamp(min=0)
+        keep = (act >= 0) & (((bits[a >> 5] >> (a & 31)) & 1) == 0)
+        vals = self.last_m[b] if self.fill == "lsq" else self.pattern.val
+        return lines_to_coo(self.pattern, vals, self.matrix_size, keep)

@@ -108,3 +108,24 @@ def poisson_3d(grid: int, dtype=torch.float64) -> Tensor:
     rows, cols, vals = torch.cat(rows), torch.cat(cols), torch.cat(vals)
     order = torch.argsort(rows * n + cols)
     return torch.sparse_coo_tensor(torch.stack([rows[order], cols[order]]), vals[order].to(dtype), (n, n))
+
+
+def axial_pattern_3d(grid: int, reach: int = 2, dtype=torch.float64) -> Tensor:
+    """Candidate pattern of config C3 ("deeper learned pattern, nnz/col <= 13"): the 7-point
+    star plus the axial neighbours at distance 2..reach on a grid^3 lattice (13 entries per
+    interior column at reach 2, a subset of A^2's 25-point pattern, so it contains A).
+    Values: A's stencil values (6 / -1) on A's entries, 0 beyond; the COPY fill copies them,
+    the LSQ fill ignores them.  Row-major COO (action id = position)."""
+    n = grid ** 3
+    i = torch.arange(n)
+    x, y, z = i % grid, (i // grid) % grid, i // (grid * grid)
+    rows, cols, vals = [i], [i], [torch.full((n,), 6.0)]
+    for d in range(1, reach + 1):
+        for dx, dy, dz in ((d, 0, 0), (-d, 0, 0), (0, d, 0), (0, -d, 0), (0, 0, d), (0, 0, -d)):
+            ok = (x + dx >= 0) & (x + dx < grid) & (y + dy >= 0) & (y + dy < grid) & (z + dz >= 0) & (z + dz < grid)
+            rows.append(i[ok])
+            cols.append(((z + dz) * grid * grid + (y + dy) * grid + (x + dx))[ok])
+            vals.append(torch.full((int(ok.sum()),), -1.0 if d == 1 else 0.0))
+    rows, cols, vals = torch.cat(rows), torch.cat(cols), torch.cat(vals)
+    order = torch.argsort(rows * n + cols)
+    return torch.sparse_coo_tensor(torch.stack([rows[order], cols[order]]), vals[order].to(dtype), (n, n))

@@ -104,6 +104,10 @@ int spai_rollout_select(const float* logits, int64_t bstride, int32_t E, int32_t
 int spai_rollout_order(const float* logits, int64_t bstride, int32_t E, int32_t B, const float* lmax,
                        const int32_t* counts, int64_t t_cap, int64_t* actions, float* fwd_probs,
                        int32_t* t_out, void* workspace, size_t workspace_bytes, void* stream);
+/* Byte offset inside the rollout workspace of a diagnostic int32 (tests/diagnostics):
+ * field 0 = oversized buckets the last order phase handed to the global-memory sort,
+ * field 1 = T of the last rollout.  -1 for an unknown field or bad shape. */
+int64_t spai_rollout_ws_offset(int32_t E, int32_t B, int32_t field);
 
 /* ---------------------------------------------------------------- actions -> removal sets
  * removed[b] = { a : 0 <= a < E, a in actions[b, :] } (preconditioner.py:37-43 +
@@ -186,14 +190,21 @@ int spai_fill_reduce(int32_t n_lines, int32_t B, const void* workspace, double* 
  *           b_r [HC], W_e [HC], att [HC], bias [HC]  (layer 1: F = fin, HC = 4 hid;
  *           layer 2: F = 4 hid, HC = hid); spai_policy_params(layer, fin, hid) floats each
  *   fc_w    [num_actions][hid] row-major (nn.Linear weight rows, 16-byte aligned), fc_b [num_actions]
+ *   const_rows  non-zero when every row of x equals row 0 (spai_policy_rows_constant; the
+ *           reference's x = ones(2N, 1) is): both GATv2 layers then give every node
+ *           relu(W_l x0 + b_l + bias) (the attention weights of a target sum to 1), so the
+ *           stack collapses to two small products and only the fc GEMV runs (rowptr, src,
+ *           eattr may be null).  0: the general GATv2 kernels.
  * Compiled for fin in {1, 2, 4} and hid in {4, 8, 16, 32} (else SPAI_ERR_UNSUPPORTED).
  * Workspace: spai_policy_workspace_bytes(n_nodes, hid, num_actions). */
 size_t spai_policy_params(int32_t layer, int32_t fin, int32_t hid);
 size_t spai_policy_workspace_bytes(int32_t n_nodes, int32_t hid, int32_t num_actions);
+/* *flag = 1 if every row of x [n_nodes][fin] equals row 0, else 0 (asynchronous, on stream). */
+int spai_policy_rows_constant(int32_t n_nodes, int32_t fin, const float* x, int32_t* flag, void* stream);
 int spai_policy_logits(int32_t n_nodes, int32_t fin, int32_t hid, const float* x, const int32_t* rowptr,
                        const int32_t* src, const float* eattr, const float* gat1, const float* gat2,
                        const float* fc_w, const float* fc_b, int32_t num_actions, float* logits, float* lmax,
-                       int32_t B, void* workspace, size_t workspace_bytes, void* stream);
+                       int32_t B, int32_t const_rows, void* workspace, size_t workspace_bytes, void* stream);
 /* Backward of the same network (the TB loss's path into ForwardPolicy's parameters, autograd
  * through policy.py:34-73): given dlogits [num_actions], the gradients in the parameter packs'
  * layouts (g_gat1 / g_gat2: spai_policy_params floats each) and of the fc rows < num_actions

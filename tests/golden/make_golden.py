@@ -27,6 +27,8 @@ Harness-side workarounds for the reference's latent bugs:
     reference's logits are state-independent within a rollout.
 
 Usage:  python tests/golden/make_golden.py            (writes *.npz + meta.json)
+        python tests/golden/make_golden.py g6         (C2/C4 parity rollouts, appended)
+        python tests/golden/make_golden.py g7         (C1 assembled M of three removal sets, appended)
 """
 import gc
 import json
@@ -246,5 +248,75 @@ def main():
         json.dump(meta, f, indent=1)
 
 
+def parity_rollouts_large():
+    """G6: reference rollouts at C2 (256^2) and C4 (1024^2) through GFlowNet.sample_states.
+
+    Terminal-biased fixed logits keep T small (the reference loop costs a policy call and a
+    [B, E+1] multinomial per step).  Stored: the recipe of the logits (regenerable from the
+    seed), the torch seed of the rollout (the sampler's Exp(1) noise is regenerable from it),
+    and the reference's actions, fwd_probs and rewards.  Appends to meta.json."""
+    preconditioner, policy, gfn_mod, ref_utils = _import_reference()
+    meta_path = os.path.join(HERE, "meta.json")
+    meta = json.load(open(meta_path))
+    for tag, grid, logit_seed, term_logit, seed, B in (("c2", 256, 7, 11.5, 11, 2), ("c4", 1024, 8, 14.2, 12, 2)):
+        A = poisson2d(grid)
+        order = np.lexsort((A.col, A.row))
+        rows, cols, vals = A.row[order].astype(np.int64), A.col[order].astype(np.int64), A.data[order].astype(np.float32)
+        n = grid * grid
+        A_t = to_torch_coo(rows, cols, vals, n)
+        env = make_env(preconditioner, A_t, n)
+        E = env.num_actions - 1
+        logits = torch.randn(E + 1, generator=torch.Generator().manual_seed(logit_seed))
+        logits[E] = term_logit
+        model = gfn_mod.GFlowNet(FixedLogitPolicy(logits), None, env)
+        s0 = [A_t.clone() for _ in range(B)]
+        torch.manual_seed(seed)
+        t0 = time.time()
+        lg = model.sample_states(s0, return_log=True)
+        dt = time.time() - t0
+        np.savez_compressed(os.path.join(HERE, f"{tag}_rollout.npz"), grid=grid, logit_seed=logit_seed,
+                            terminal_logit=term_logit, seed=seed, B=B, actions=lg.actions.numpy(),
+                            fwd_probs=lg.fwd_probs.detach().numpy(), rewards=lg.rewards.numpy())
+        meta["cases"][f"{tag}_rollout"] = {
+            "B": B, "T": int(lg.actions.shape[0]), "E": E, "grid": grid,
+            "logits": f"torch.randn(E + 1, generator=torch.Generator().manual_seed({logit_seed})); [E] = {term_logit}",
+            "rollout_seed": f"torch.manual_seed({seed}) before sample_states", "seconds": round(dt, 3)}
+        print(tag, "T", lg.actions.shape[0], "rewards", lg.rewards.tolist(), "s", round(dt, 1))
+    with open(meta_path, "w") as f:
+        json.dump(meta, f, indent=1)
+
+
+def assembled_m():
+    """G7: the reference's M (update_edges_and_convert_to_sparse + resize_sparse_tensor,
+    utils.py:295-356, 89-126) for three removal sets of the permuted-raw-order C1 pattern
+    (c1p_removal.npz sets 2, 5, 20): coalesced indices and values, concatenated."""
+    preconditioner, policy, gfn_mod, ref_utils = _import_reference()
+    d = np.load(os.path.join(HERE, "c1p_removal.npz"))
+    n = int(d["n"])
+    A_t = to_torch_coo(d["rows"], d["cols"], d["vals"], n)
+    env = make_env(preconditioner, A_t, n)
+    sets, idx, vals, nnz = [2, 5, 20], [], [], []
+    for k in sets:
+        acts = [torch.tensor(int(a)) for a in np.flatnonzero(d["removed"][k])]
+        M = ref_utils.resize_sparse_tensor(ref_utils.update_edges_and_convert_to_sparse(env.data, acts, n), (n, n))
+        M = M.coalesce()
+        idx.append(M.indices().numpy())
+        vals.append(M.values().numpy())
+        nnz.append(M._nnz())
+    np.savez_compressed(os.path.join(HERE, "c1p_assembled.npz"), sets=np.array(sets), nnz=np.array(nnz),
+                        indices=np.concatenate(idx, 1), values=np.concatenate(vals))
+    meta_path = os.path.join(HERE, "meta.json")
+    meta = json.load(open(meta_path))
+    meta["cases"]["c1p_assembled"] = {"removal_sets": sets, "nnz": nnz, "dtype": str(vals[0].dtype)}
+    with open(meta_path, "w") as f:
+        json.dump(meta, f, indent=1)
+    print("assembled", nnz)
+
+
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 1 and sys.argv[1] == "g6":
+        parity_rollouts_large()
+    elif len(sys.argv) > 1 and sys.argv[1] == "g7":
+        assembled_m()
+    else:
+        main()

@@ -49,6 +49,24 @@ def test_parity_rollout_matches_reference(name):
     assert np.array_equal(fwd.numpy(), d["fwd_probs"])
 
 
+def large_rollout_logits(d):
+    E = int(d["grid"]) ** 2 * 5 - 4 * int(d["grid"])
+    logits = torch.randn(E + 1, generator=torch.Generator().manual_seed(int(d["logit_seed"])))
+    logits[E] = float(d["terminal_logit"])
+    return logits
+
+
+@pytest.mark.parametrize("name", ["c2_rollout.npz", "c4_rollout.npz"])
+def test_parity_rollout_matches_reference_large(name):
+    """C2 / C4 reference rollouts (G6): the oracle's sequential sampler with the reference's
+    normalisation chain reproduces actions and fwd_probs bit for bit from the seeds."""
+    d = load(name)
+    torch.manual_seed(int(d["seed"]))
+    acts, fwd = O.parity_rollout(large_rollout_logits(d), int(d["B"]))
+    assert np.array_equal(acts.numpy(), d["actions"])
+    assert np.array_equal(fwd.numpy(), d["fwd_probs"])
+
+
 @pytest.mark.parametrize("name", REMOVALS)
 def test_copy_fill_residual_reward_match_reference(name):
     d = load(name)

@@ -59,18 +59,21 @@ def test_policy_logits_random_features(fin, hid):
     close(got.cpu(), orc)
 
 
-@pytest.mark.parametrize("grid", [16, 256])
-def test_policy_logits_state_graph(grid):
-    """The reference's own input: state_to_data's x = ones(2N, 1) over A's raw COO pattern."""
+@pytest.mark.parametrize("grid,fast", [(16, True), (256, True), (16, False), (256, False)])
+def test_policy_logits_state_graph(grid, fast):
+    """The reference's own input: state_to_data's x = ones(2N, 1) over A's raw COO pattern,
+    through the constant-row closed form (fast) and through the general GATv2 kernels."""
     A = poisson_2d(grid)
     n = grid * grid
     E = A._nnz()
     pol = randomise(ForwardPolicy(-1, 4, E + 7), grid).to(DEV)
+    pol.const_fast_path = fast
     data = Data(x=torch.ones(2 * n, 1, device=DEV), edge_index=A._indices().to(DEV),
                 edge_attr=A._values().float().to(DEV))
     with torch.no_grad():
         got, _, lmax = pol.logits_and_max(data, 2)
         ref, _ = pol.torch_logits(data)
+    assert pol.rows_constant(data.x)
     close(got.cpu(), ref.cpu())
     assert float(lmax[0]) == float(got.max())
     # known answer: with x = ones the pooled embedding is graph-independent
@@ -129,3 +132,47 @@ def test_sample_states_with_forward_policy():
     loss = torch.log(log.fwd_probs).sum()
     loss.backward()
     assert pol.fc.weight.grad is not None and float(pol.fc.weight.grad.abs().sum()) > 0
+
+
+def lp(layer):
+    import copy
+    return layer_params(copy.deepcopy(layer).cpu().double())
+
+
+@pytest.mark.parametrize("fin,hid", [(1, 4), (2, 8), (4, 16), (1, 32)])
+def test_policy_const_rows_closed_form_matches_general(fin, hid):
+    """Identical non-unit rows (x = c for every node): the closed form and the general kernels
+    agree with each other and with the fp64 oracle; a single differing row is detected and
+    takes the general kernels."""
+    n = 400
+    ei, ea = random_graph(n // 2, 1500, seed=fin + hid)
+    row = np.random.default_rng(hid).standard_normal(fin).astype(np.float32)
+    x = np.tile(row, (n, 1))
+    pol = randomise(ForwardPolicy(fin, hid, 1700), 7 * hid).to(DEV)
+    data = Data(x=torch.from_numpy(x).to(DEV), edge_index=torch.from_numpy(ei).to(DEV),
+                edge_attr=torch.from_numpy(ea).to(DEV))
+    outs = []
+    for fast in (True, False):
+        pol.const_fast_path = fast
+        with torch.no_grad():
+            got, _, lmax = pol.logits_and_max(data, 2)
+        assert float(lmax[1]) == float(got.max())
+        outs.append(got.cpu())
+    assert pol.rows_constant(data.x)
+    close(outs[0], outs[1])
+    orc = O.forward_policy_logits(x, ei, ea, lp(pol.gat1),
+                                  lp(pol.gat2), pol.fc.weight.detach().cpu().numpy(),
+                                  pol.fc.bias.detach().cpu().numpy(), 1501)
+    close(outs[0], orc)
+    # one row differs -> not constant (re-checked after the in-place change), general path
+    pol.const_fast_path = True
+    with torch.no_grad():
+        data.x[n - 1, 0] += 1.0
+    assert not pol.rows_constant(data.x)
+    x2 = data.x.cpu().numpy()
+    with torch.no_grad():
+        got, _, _ = pol.logits_and_max(data, 1)
+    orc2 = O.forward_policy_logits(x2, ei, ea, lp(pol.gat1),
+                                   lp(pol.gat2), pol.fc.weight.detach().cpu().numpy(),
+                                   pol.fc.bias.detach().cpu().numpy(), 1501)
+    close(got.cpu(), orc2)

@@ -5,9 +5,18 @@ of the 1024^2 5-point Poisson matrix (config C4, fp32): ForwardPolicy logits (GA
 mean pool + fc on the state graph, random-init weights), throughput rollout (Gumbel-top-k,
 20 % expected removal, ordered trajectory log + forward probabilities), least-squares fill
 of M (column SPAI) and the ||A M - I||_F reward, all inputs resident in HBM.
-columns/s = (B * N * world) / step time (max over ranks).  Multi-GPU: one process per
-GPU, each rank samples its own B candidates (Philox sample ids rank*B..), no collective in
-the step (weak scaling).  Prints ONE JSON line on rank 0.
+
+Multi-GPU (one process per GPU; `--gpus N` starts the N ranks itself, or run it under
+torch.distributed.run):
+  --shard columns (default; the north star's and BASELINE C4's split, strong scaling): the
+      same B candidates on every rank; rank r orders the r-th slice of every trajectory and
+      fills lines shard_lines(N, r, P) of every candidate's M; ONE all_reduce per step (bucket
+      weight sums + residual partials); the best candidate's M is assembled with ONE all_gather
+      (--assemble best; `all` gathers every candidate, `none` skips it).  value = B*N / step.
+  --shard candidates (weak scaling): B candidates per rank, no collective.  value = P*B*N / step.
+The timed steps replay HIP graphs of the collective-free phases (the rollout's Philox stream
+id lives on the device, so every replay draws a fresh rollout); the per-phase HIP-event
+timings come from an eager pass of the same step.  Prints ONE JSON line on rank 0.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config c4|c2|c3] [--batch B]
 """
@@ -95,7 +104,7 @@ def fill_bytes(env, B, store_m: bool = True) -> float:
     return line + B * per_sample
 
 
-def measured_traffic(cfg: str, B: int, overlap: bool):
+def measured_traffic(cfg: str, B: int):
     """HBM bytes per launch of the roofline kernel from the committed PMC profile of this
     exact workload (profiles/fill_traffic.json, written by scripts/collect_profiles.py from
     separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of `bench.py`), else None."""
@@ -109,63 +118,71 @@ def measured_traffic(cfg: str, B: int, overlap: bool):
     return None
 
 
-def cpu_baseline(cfg, B, budget_s: float, logits=None):
-    """The oracle (numpy, single thread) on a bounded sample of the same workload (the
-    policy's logits are taken as given: the CPU leg times the rollout, fill and residual)."""
+def cpu_baseline(cfg, B, budget_s: float, logits, T_mean: float):
+    """The reference's CPU path restated with its own torch ops (oracle/spai_oracle.py:
+    reference_step = masked softmax + renormalisations + Categorical(probs).sample() per step,
+    gflownet.py:116-148, policy.py:65-73; reference_update_residual = keep-mask COO M +
+    coalesce + sparse torch.mm + identity subtraction + torch.norm, utils.py:315-353,
+    preconditioner.py:79-93), on all the threads torch uses on this host, over a BOUNDED sample
+    of the same workload: a few sampler steps over the full [B, E+1] action space and one
+    candidate's env.update, extrapolated to the batch (T_mean steps: the GPU run's mean
+    trajectory length; B updates).  The reference has no least-squares fill: its env.update is
+    the copy fill (the ForwardPolicy forward is not timed: PyG is absent).  A secondary field
+    times the oracle's numpy Gumbel-top-k rollout + LSQ fill (1 thread) on part of the columns."""
     from oracle import spai_oracle as O
-    import scipy.sparse as sp
 
-    dims, grid, dtype, _ = CONFIGS[cfg]
-    npd = np.float32 if dtype == torch.float32 else np.float64
-    r, c, v, n = O.poisson2d(grid, npd) if dims == 2 else O.poisson3d(grid, npd)
+    A, P = config_matrices(cfg)
+    Pc, Ac = P.coalesce(), A.coalesce()
+    r, c = (t.numpy() for t in Pc.indices())
+    v = Pc.values().float().numpy()
+    n = A.shape[0]
     E = len(r)
-    if logits is None:
-        logits = torch.randn(E + 1, generator=torch.Generator().manual_seed(123)).numpy()
-        logits[E] = terminal_logit(logits[:E], 0.2)
-    t0 = time.perf_counter()
-    removed, actions, fwd, counts = O.throughput_rollout(logits, 1, seed=1234, stream=0)
-    t_roll = time.perf_counter() - t0
-    idx, act, _ = O.lines_from_coo(r, c, v, n, "col")
-    a_idx, _, a_val = O.lines_from_coo(r, c, v.astype(np.float64), n, "col")
-    keep = (idx >= 0) & ~removed[0][np.clip(act, 0, None)]
-    cols = min(n, 16384)
-    done, t_fill = 0, 0.0
-    A = sp.csc_matrix((v.astype(np.float64), (r, c)), shape=(n, n))
-    while done < n and t_fill < budget_s:
-        ids = np.arange(done, min(done + cols, n))
+    lg_t = torch.as_tensor(np.asarray(logits, np.float32)).view(1, -1)
+    assert lg_t.shape[1] == E + 1
+    threads = torch.get_num_threads()
+    g = torch.Generator().manual_seed(0)
+    hist, t_steps, steps = [], 0.0, 0
+    t_budget = 0.4 * budget_s
+    while steps < 3 or (t_steps < t_budget and steps < 40):
         t0 = time.perf_counter()
-        m = O.lsq_fill(idx, keep, a_idx, a_val, ids)
-        sub = idx[ids]
-        ok = sub >= 0
-        Ms = sp.csc_matrix((m[ok], (sub[ok], np.nonzero(ok)[0])), shape=(n, ids.size))
-        P = (A @ Ms).tocoo()
-        diag = P.data[P.row == ids[P.col]].sum()
-        _ = np.sqrt(max((P.data ** 2).sum() - 2 * diag + ids.size, 0.0))
-        t_fill += time.perf_counter() - t0
-        done = ids[-1] + 1
-    per_col = t_fill / done
-    t_sample = t_roll + per_col * n  # one candidate over all N columns
-    return {"value": n / t_sample, "unit": "columns/s", "cores": 1, "kind": "port",
-            "sample": f"oracle/spai_oracle.py (numpy): 1 full rollout over E={E} ({t_roll:.2f}s, the bench policy's "
-                      f"logits given) + LSQ fill and ||AM-I|| over the first {done} of {n} columns ({t_fill:.2f}s), "
-                      f"extrapolated to N columns; policy forward not included"}
+        a, _ = O.reference_step(lg_t, B, hist, g)
+        t_steps += time.perf_counter() - t0
+        hist.append(a.view(B))
+        steps += 1
+    t_step = t_steps / steps
+    A_t = torch.sparse_coo_tensor(Ac.indices(), Ac.values().float(), (n, n))
+    removed = np.random.default_rng(1).random(E) < 0.2
+    t0 = time.perf_counter()
+    O.reference_update_residual(r, c, v, removed, n, A_t)
+    t_upd = time.perf_counter() - t0
+    t_batch = T_mean * t_step + B * t_upd
+    out = {"value": B * n / t_batch, "unit": "columns/s", "cores": threads, "kind": "port",
+           "host_cpus": os.cpu_count(), "torch_threads": threads,
+           "sample": f"reference ops in torch-CPU ({threads} threads of {os.cpu_count()} CPUs): {steps} sampler steps "
+                     f"over [B={B}, E+1={E + 1}] ({t_step * 1e3:.1f} ms/step) and one env.update copy fill + "
+                     f"||MA-I||_F ({t_upd:.2f} s), extrapolated to the batch: {T_mean:.0f} steps (the GPU run's "
+                     f"mean trajectory length) + {B} updates"}
+    if A.shape == P.shape and Ac._nnz() == E:  # secondary (pattern = A): numpy Gumbel-top-k + LSQ fill, 1 thread
+        idx, act, _ = O.lines_from_coo(r, c, v, n, "col")
+        a_idx, _, a_val = O.lines_from_coo(r, c, v.astype(np.float64), n, "col")
+        t0 = time.perf_counter()
+        rem, *_ = O.throughput_rollout(np.asarray(logits, np.float32), 1, 1234, 0)
+        t_roll = time.perf_counter() - t0
+        keep = (idx >= 0) & ~rem[0][np.clip(act, 0, None)]
+        cols = min(n, 65536)
+        t0 = time.perf_counter()
+        O.lsq_fill(idx, keep, a_idx, a_val, np.arange(cols))
+        t_fill = (time.perf_counter() - t0) * n / cols
+        out["numpy_gumbel_lsq"] = {"value": n / (t_roll + t_fill), "unit": "columns/s", "cores": 1,
+                                   "sample": f"oracle numpy Gumbel-top-k rollout ({t_roll:.2f} s) + LSQ fill of "
+                                             f"{cols} columns extrapolated to {n}"}
+    return out
 
 
-def launch_ranks(n: int) -> int:
-    """`bench.py --gpus N` run directly: start the N ranks (one process per GPU) under
-    torch.distributed.run on 127.0.0.1 as child processes and return their exit status.
-    The parent has not initialised the GPU (no HIP call before this point)."""
-    import socket
-    import subprocess
-
-    with socket.socket() as sk:
-        sk.bind(("127.0.0.1", 0))
-        port = sk.getsockname()[1]
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
-           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
-    env = dict(os.environ)
-    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-    return subprocess.run(cmd, env=env).returncode
+def roofline_obj(kernel, nbytes, ms, traffic=None):
+    achieved = nbytes / (ms * 1e-3) / 1e9
+    return {"kernel": kernel, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "bytes_per_launch": nbytes, "avg_launch_ms": ms}
 
 
 def main():
@@ -175,16 +192,11 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c4", choices=sorted(CONFIGS))
     ap.add_argument("--batch", type=int, default=8)
-    ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--shard", default="candidates", choices=["candidates", "columns"],
-                    help="candidates: B candidates per rank (weak scaling, no collective); columns: the same B "
-                         "candidates on every rank, lines of M split across ranks, one all_reduce of the squared "
-                         "residuals and one all_gather of M per step (strong scaling)")
-    ap.add_argument("--overlap", action="store_true",
-                    help="run the fill/reward on a side stream concurrent with the trajectory sort (measured ~1%% "
-                         "slower: the sort's persistent blocks hold nearly all LDS, so the two serialise anyway)")
-    ap.add_argument("--no-overlap", action="store_true", help="(default; kept for old command lines)")
+    ap.add_argument("--shard", default="columns", choices=["columns", "candidates"])
+    ap.add_argument("--assemble", default="best", choices=["best", "all", "none"])
+    ap.add_argument("--no-graph", action="store_true", help="time eager steps (host launches) instead of graph replays")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -201,7 +213,8 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=dev)
 
-    from gflownet_spai_amd import GFlowNet, PreconditionerEnv, kernels, poisson_2d, poisson_3d
+    from gflownet_spai_amd import GFlowNet, PreconditionerEnv, kernels
+    from gflownet_spai_amd.distributed import allgather_lines
 
     dims, grid, dtype, text = CONFIGS[args.config]
     A, P = config_matrices(args.config)
@@ -210,52 +223,106 @@ def main():
     E = env.num_actions - 1
     B = args.batch
     columns = args.shard == "columns"
-    shard = None
-    if columns and world > 1:
-        from gflownet_spai_amd.distributed import allgather_lines, shard_lines
-        lb, le = shard_lines(n, rank, world)
-        shard = (lb, le, None)
+    split = columns and world > 1
     model = GFlowNet(make_policy(env, P, dev), None, env, mode="throughput", seed=1234,
-                     sample_base=0 if columns else rank * B, overlap=args.overlap and not args.no_overlap, line_shard=shard)
+                     sample_base=0 if columns else rank * B, shard=(rank, world, None) if split else None)
     s0 = [P] * B
+    assembled = {}
 
-    def step():
-        log = model.sample_states(s0, return_log=True)
-        if shard is not None:
-            log.m_full = allgather_lines(env.last_m, n)  # M of every candidate on every rank (one all_gather)
+    def assemble(log):
+        if not split or args.assemble == "none":
+            return
+        m = env.last_m
+        if args.assemble == "best":  # the candidate with the highest reward: the preconditioner kept
+            m = m.index_select(0, torch.argmax(log.rewards).view(1))
+        assembled["m"] = allgather_lines(m, n)
+
+    def eager_step():
+        with kernels._timed("begin"):
+            st = model.rollout_begin(s0)
+        with kernels._timed("exchange"):
+            model.rollout_exchange(st)
+        with kernels._timed("end"):
+            log = model.rollout_end(st)
+        with kernels._timed("assemble"):
+            assemble(log)
         return log
-
-    for _ in range(args.warmup):
-        step()
 
     def barrier():
         if world > 1:
             torch.distributed.barrier()
         torch.cuda.synchronize()
 
-    kernels.TIMERS = {}
-    barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        log = step()
-    barrier()
-    dt = (time.perf_counter() - t0) / args.steps
-    phases = {k: float(np.mean(kernels.timer_ms(k))) for k in kernels.TIMERS}
-    kernels.TIMERS = None
+    with torch.no_grad():
+        for _ in range(args.warmup):
+            log = eager_step()
+        # eager pass with per-phase HIP events (on the stream the kernels run on)
+        kernels.TIMERS = {}
+        k_eager = max(1, min(args.steps, 10))
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(k_eager):
+            log = eager_step()
+        barrier()
+        dt_eager = (time.perf_counter() - t0) / k_eager
+        phases = {k: float(np.mean(kernels.timer_ms(k))) for k in kernels.TIMERS}
+        kernels.TIMERS = None
+
+        use_graph = not args.no_graph
+        if use_graph:
+            # capture: world 1 -> one graph of the whole step; split -> the collective-free
+            # phases (begin, end) as two graphs around the eager all_reduce and all_gather
+            side = torch.cuda.Stream(dev)
+            side.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(side):
+                eager_step()
+            torch.cuda.current_stream(dev).wait_stream(side)
+            barrier()
+            g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+            if not split:
+                with torch.cuda.graph(g1):
+                    st = model.rollout_begin(s0)
+                    model.rollout_exchange(st)
+                    glog = model.rollout_end(st)
+            else:
+                with torch.cuda.graph(g1):
+                    st = model.rollout_begin(s0)
+                model.rollout_exchange(st)  # allocates the persistent exchange buffer the end phase reads
+                with torch.cuda.graph(g2, pool=g1.pool()):
+                    glog = model.rollout_end(st)
+
+            def step():
+                g1.replay()
+                if split:
+                    model.rollout_exchange(st)
+                    g2.replay()
+                    assemble(glog)
+                return glog
+
+            for _ in range(max(1, args.warmup)):
+                log = step()
+        else:
+            step = eager_step
+
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            log = step()
+        barrier()
+        dt = (time.perf_counter() - t0) / args.steps
     if world > 1:
-        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        t = torch.tensor([dt, dt_eager], device=dev, dtype=torch.float64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        dt = float(t)
+        dt, dt_eager = float(t[0]), float(t[1])
     res = env.last_residual.double().cpu().numpy()
     counts = log.counts.cpu().numpy()
 
     if rank == 0:
         fill_ms = phases.get("fill_residual", float("nan"))
         fb = fill_bytes(env, B)
-        if shard is not None:  # the rank's fill covers its own lines only (rank 0: the first, largest shard)
-            fb *= (shard[1] - shard[0]) / n
-        achieved = fb / (fill_ms * 1e-3) / 1e9
-        traffic = measured_traffic(args.config, B, args.overlap and not args.no_overlap)
+        if split:  # the rank's fill covers its own lines only (rank 0: the first, largest shard)
+            fb *= (model.lines[1] - model.lines[0]) / n
+        gram_t = "f32" if env.gram is not None and env.gram.dtype == torch.float32 else "f64"
         out = {
             "metric": "SPAI columns/sec + final ||AM-I||_F, 2D Poisson 1024^2, at 1/2/4/8 GPU",
             "value": B * n * (1 if columns else world) / dt,
@@ -267,28 +334,29 @@ def main():
             "higher_is_better": True,
             "scaling": "strong" if columns else "weak",
             "vs_baseline": None,
-            "dtype": "f32 storage, f64 solve/accumulate",
+            "dtype": "f32 storage, f64 solve/accumulate" if dtype == torch.float32 else "f64",
             "data": "synthetic (random-init seeded ForwardPolicy GATv2x2+fc, hid=4, evaluated on the state graph in "
-                    "every step; terminal fc bias set for 20% expected removal; Poisson matrix from its stencil)",
-            "config": {"workload": text + (f", B={B} candidates, lines of M sharded over the GPUs (all_reduce of "
-                                               "||.||^2, all_gather of M)" if columns else
-                                               f", B={B} candidates per GPU") +
+                    "every step; terminal fc bias set for 20% expected removal; matrix from its stencil)",
+            "config": {"workload": text + (f", B={B} candidates, columns split over {world} GPUs (trajectory slices + "
+                                           f"lines of M per rank, one all_reduce, {args.assemble} M all_gather)"
+                                           if columns else f", B={B} candidates per GPU") +
                                    ": ForwardPolicy logits + throughput rollout + LSQ fill + ||AM-I||_F",
                        "N": n, "E": E, "global_batch": B * (1 if columns else world),
                        "parallelism": f"{'columns' if columns else 'candidates'} sharded x{world}"},
+            "graph": use_graph,
+            "ms_per_step_eager": dt_eager * 1e3,
             "final_residual_fro": float(res[0]),
             "final_residual_fro_mean": float(res.mean()),
             "removed_per_candidate_mean": float(counts.mean()),
             "phases_ms": phases,
-            "roofline": {"kernel": "k_gram_fill<5,f32,LSQ> (spai_fill_residual_gram: LSQ fill of M + ||AM-I||^2)",
-                         "bound": "hbm",
-                         "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": traffic, "bytes_per_launch": fb, "avg_launch_ms": fill_ms},
+            "roofline": roofline_obj(f"k_gram_fill<{env.pattern.width},{gram_t},LSQ> (LSQ fill of M + ||AM-I||^2; A "
+                                     f"reaches it through the env-constant Gram cache)", fb, fill_ms,
+                                     measured_traffic(args.config, B)),
         }
         if not args.no_cpu_baseline and world == 1:
             with torch.no_grad():
                 lg_host = model.forward_policy.logits(model.state_to_data(s0[:1])[0])[0].reshape(-1).cpu().numpy()
-            out["cpu_baseline"] = cpu_baseline(args.config, B, args.cpu_budget, lg_host)
+            out["cpu_baseline"] = cpu_baseline(args.config, B, args.cpu_budget, lg_host, float(counts.mean()) + 1)
         print(json.dumps(out), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()

@@ -212,6 +212,9 @@ __device__ __forceinline__ int32_t subset_action(int i, int M, int32_t E) {
   return (int32_t)(lo + (int64_t)(h % (uint32_t)(hi - lo)));
 }
 
+// First bucket of part p of np (buckets in trajectory order; part p orders [lo(p), lo(p+1))).
+__host__ __device__ __forceinline__ int part_lo(int nb, int p, int np) { return (int)(((int64_t)nb * p) / np); }
+
 // Block-wide exclusive scan of one uint64 per thread (packed 16-bit fields never overflow).
 template <int NT>
 __device__ __forceinline__ uint64_t block_excl_scan_u64(uint64_t c, uint64_t* lds /* NT/64 */, uint64_t* total) {
@@ -236,12 +239,24 @@ __device__ __forceinline__ uint64_t block_excl_scan_u64(uint64_t c, uint64_t* ld
 }
 
 // ------------------------------------------------------------------ k_presample
+// Philox stream id of this rollout: the kernel argument, or the device counter when the caller
+// keeps one (graph replays draw fresh rollouts; k_bscan advances it after the select phase).
+__device__ __forceinline__ void stream_words(const uint64_t* sctr, uint32_t& st0, uint32_t& st1) {
+  if (sctr) {
+    const uint64_t v = *sctr;
+    st0 = (uint32_t)v;
+    st1 = (uint32_t)(v >> 32);
+  }
+}
+
 __global__ __launch_bounds__(kSampNT) void k_presample(const float* __restrict__ logits, int64_t bstride, int32_t E,
                                                        int32_t M, uint32_t seed0, uint32_t seed1, uint32_t st0,
-                                                       uint32_t st1, int32_t sample_base,
+                                                       uint32_t st1, const uint64_t* __restrict__ sctr,
+                                                       int32_t sample_base,
                                                        uint32_t* __restrict__ samp, int32_t* __restrict__ samp_cnt,
                                                        int32_t* __restrict__ ctl, int32_t nctl) {
   const int b = blockIdx.y, tid = threadIdx.x;
+  stream_words(sctr, st0, st1);
   {  // the rollout's control block (bucket totals, oversized-bucket list count, tdev) starts at 0;
      // its first users (k_tile, k_sort2, k_bscan) run after this launch on the same stream
     const int nthr = gridDim.x * gridDim.y * kSampNT;
@@ -442,7 +457,9 @@ constexpr int kTileG = kTile / (kGrpNT * 4);  // Philox groups (of 4 actions) pe
 __global__ __launch_bounds__(kGrpNT)
 void k_tile(const float* __restrict__ logits, int64_t bstride, int32_t E,
                                                  int32_t ntiles, uint32_t seed0, uint32_t seed1, uint32_t st0,
-                                                 uint32_t st1, int32_t sample_base, uint32_t* __restrict__ removed,
+                                                 uint32_t st1, const uint64_t* __restrict__ sctr,
+                                                 int32_t sample_base, int32_t part, int32_t nparts,
+                                                 uint32_t* __restrict__ removed,
                                                  int32_t words, const float* __restrict__ lmax,
                                                  const int32_t* __restrict__ nb_, const uint32_t* __restrict__ spl_,
                                                  const uint16_t* __restrict__ lut_,
@@ -459,9 +476,13 @@ void k_tile(const float* __restrict__ logits, int64_t bstride, int32_t E,
   __shared__ double s_wr[kGrpNT / 64];
   const int b = blockIdx.y, tile = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   PROF_INIT
+  stream_words(sctr, st0, st1);
   const float* lg = logits + (int64_t)b * bstride;
   const uint32_t bg = (uint32_t)(sample_base + b);
   const int nb = nb_[b];
+  // buckets [k0, k1) are ordered by this part (the others only counted: the removal bitmap,
+  // the bucket totals and the untouched mass cover every action in every part)
+  const int k0 = part_lo(nb, part, nparts), k1 = part_lo(nb, part + 1, nparts);
   // splitter tables (consumed only after the keys; their latency hides behind the Philox work)
   static_assert((kBins * 2 == 512 * 16 && kMaxB * 4 == 512 * 16 && kGrpNT % 512 == 0) || kGrpNT == 512,
                 "prologue vector widths");
@@ -586,7 +607,7 @@ void k_tile(const float* __restrict__ logits, int64_t bstride, int32_t E,
   for (int q = 0; q < kQ; ++q) {
     const int k = tid * kQ + q;
     hv[q] = k < nb ? s_off[k] : 0;
-    loc += hv[q];
+    loc += (k >= k0 && k < k1) ? hv[q] : 0;
   }
   int tot;
   int run = block_excl_scan<kGrpNT>(loc, s_wc, &tot);
@@ -597,12 +618,13 @@ void k_tile(const float* __restrict__ logits, int64_t bstride, int32_t E,
 #pragma unroll
   for (int q = 0; q < kQ; ++q) {
     const int k = tid * kQ + q;
+    const bool mine = k >= k0 && k < k1;
     if (k < nb) {
-      s_off[k] = run;
-      rcol[(int64_t)k * ntiles] = ((uint32_t)run << 16) | (uint32_t)hv[q];
+      s_off[k] = mine ? run : 0xFFFF;  // other parts' winners are not staged (beyond every window)
+      if (mine) rcol[(int64_t)k * ntiles] = ((uint32_t)run << 16) | (uint32_t)hv[q];
       if (hv[q]) atomicAdd(&btot[(int64_t)b * kMaxB + k], hv[q]);
     }
-    run += hv[q];
+    run += mine ? hv[q] : 0;
   }
   if (tid == 0) s_off[nb] = tot;
   __syncthreads();
@@ -611,7 +633,7 @@ void k_tile(const float* __restrict__ logits, int64_t bstride, int32_t E,
   uint32_t pp[2 * kTileG];
 #pragma unroll
   for (int q = 0; q < 4 * kTileG; ++q) {
-    const uint32_t pos = (win >> q) & 1u ? (uint32_t)s_off[br[q] & 0x7FFu] + (br[q] >> 11) : 0xFFFFu;
+    const uint32_t pos = (win >> q) & 1u ? min((uint32_t)s_off[br[q] & 0x7FFu] + (br[q] >> 11), 0xFFFFu) : 0xFFFFu;
     if (q & 1) pp[q >> 1] |= pos << 16;
     else pp[q >> 1] = pos;
   }
@@ -650,8 +672,14 @@ __global__ __launch_bounds__(1024) void k_bscan(int32_t E, int32_t ntiles, const
                                                 const int32_t* __restrict__ nb_, const int32_t* __restrict__ btot,
                                                 const double* __restrict__ tile_wrest, int32_t* __restrict__ bstart,
                                                 int32_t* __restrict__ counts, double* __restrict__ wrest,
-                                                int32_t* __restrict__ tdev) {
+                                                int32_t* __restrict__ tdev, uint64_t* __restrict__ sctr,
+                                                double* __restrict__ bwsum) {
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // every k_presample / k_tile block has read the stream id: the next rollout draws the next one
+  if (sctr && b == 0 && tid == 0) *sctr += 1;
+  // bucket weight sums start at 0: the order phase fills its part's buckets (the other parts'
+  // stay 0, so a sum over the parts reproduces the single-part array exactly)
+  for (int k = tid; k < kMaxB; k += 1024) bwsum[(int64_t)b * kMaxB + k] = 0.0;
   __shared__ int s_wc[16];
   __shared__ double s_wr[16];
   const int nb = nb_[b];
@@ -800,7 +828,7 @@ __global__ __launch_bounds__(kSortNT) void k_sort2(int32_t E, int32_t B, int32_t
                                                    int64_t t_cap, int64_t* __restrict__ actions,
                                                    float* __restrict__ out_w, float* __restrict__ out_suf,
                                                    double* __restrict__ bwsum, int32_t* __restrict__ bigcnt,
-                                                   int32_t* __restrict__ biglist) {
+                                                   int32_t* __restrict__ biglist, int32_t part, int32_t nparts) {
   __shared__ uint64_t A[kCap2];  // low half: gather map; high half: actions awaiting store
   __shared__ float L[kCap2];     // weights in trajectory order
   __shared__ float S[kCap2];     // suffix sums awaiting store
@@ -811,8 +839,9 @@ __global__ __launch_bounds__(kSortNT) void k_sort2(int32_t E, int32_t B, int32_t
   __shared__ double s_wd[kSortNT / 64];
   __shared__ uint32_t s_red[2 * (kSortNT / 64)];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  {  // prefix of the bucket counts over the samples (parallel loads)
-    const int v = tid < B ? nb_[tid] : 0;
+  {  // prefix of the part's bucket counts over the samples (parallel loads)
+    const int nbb = tid < B ? nb_[tid] : 0;
+    const int v = part_lo(nbb, part + 1, nparts) - part_lo(nbb, part, nparts);
     int tot;
     const int ex = block_excl_scan<kSortNT>(v, s_wc, &tot);
     if (tid < B) s_lm[tid] = lmax_[tid];
@@ -829,7 +858,7 @@ __global__ __launch_bounds__(kSortNT) void k_sort2(int32_t E, int32_t B, int32_t
     bb = kk = s0 = s1 = 0;
     if (f < total) {
       while (s_nbp[bb + 1] <= f) ++bb;
-      kk = f - s_nbp[bb];
+      kk = f - s_nbp[bb] + part_lo(nb_[bb], part, nparts);
       const int32_t* bs = bstart + (int64_t)bb * (kMaxB + 1);
       s0 = bs[kk];
       s1 = bs[kk + 1];
@@ -892,7 +921,7 @@ __global__ __launch_bounds__(kSortNT) void k_sort2(int32_t E, int32_t B, int32_t
     PROF(0)
     if (n == 0 || n > kCap2) {
       if (n == 0 && tid == 0) bwsum[(int64_t)b * kMaxB + k] = 0.0;
-      if (n > kCap2 && tid == 0) biglist[atomicAdd(bigcnt, 1)] = f;  // for k_sort2_big (rare)
+      if (n > kCap2 && tid == 0) biglist[atomicAdd(bigcnt, 1)] = (b << 16) | k;  // for k_sort2_big (rare)
       __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): retire the fetch (see above)
       continue;
     }
@@ -1069,7 +1098,6 @@ __global__ __launch_bounds__(kSortNT) void k_sort2_big(int32_t E, int32_t B, int
                                                        float* __restrict__ out_suf, uint64_t* __restrict__ scratch,
                                                        double* __restrict__ bwsum, const int32_t* __restrict__ bigcnt,
                                                        const int32_t* __restrict__ biglist) {
-  __shared__ int s_nbp[kMaxSamples + 1];
   __shared__ int s_pre[kMaxTiles + 1];
   __shared__ int s_loc[kMaxTiles];
   __shared__ int s_wc[kSortNT / 64];
@@ -1078,20 +1106,10 @@ __global__ __launch_bounds__(kSortNT) void k_sort2_big(int32_t E, int32_t B, int
   const int tid = threadIdx.x;
   const int nbig = *bigcnt;  // oversized buckets k_sort2 skipped (usually none: the whole grid exits here)
   if (nbig == 0) return;
-  {  // prefix of the bucket counts over the samples (parallel loads)
-    const int v = tid < B ? nb_[tid] : 0;
-    int tot;
-    const int ex = block_excl_scan<kSortNT>(v, s_wc, &tot);
-    if (tid < B) s_nbp[tid] = ex;
-    if (tid == 0) s_nbp[B] = tot;
-  }
-  __syncthreads();
 #pragma unroll 1
   for (int q = blockIdx.x; q < nbig; q += gridDim.x) {
     const int f = biglist[q];
-    int b = 0;
-    while (s_nbp[b + 1] <= f) ++b;
-    const int k = f - s_nbp[b];
+    const int b = f >> 16, k = f & 0xFFFF;
     const int32_t* bs = bstart + (int64_t)b * (kMaxB + 1);
     const int s = bs[k], n = bs[k + 1] - s;
     if (n <= kCap2) continue;
@@ -1154,9 +1172,10 @@ __global__ __launch_bounds__(kFinNT) void k_final(int32_t E, const int32_t* __re
                                                   const double* __restrict__ bwsuf, const float* __restrict__ out_w,
                                                   const float* __restrict__ out_suf,
                                                   const double* __restrict__ wrest, int64_t t_cap,
-                                                  float* __restrict__ fwd) {
+                                                  float* __restrict__ fwd, int32_t part, int32_t nparts) {
   const int k = blockIdx.x, b = blockIdx.y;
-  if (k >= nb_[b]) return;
+  const int nb = nb_[b];
+  if (k < part_lo(nb, part, nparts) || k >= part_lo(nb, part + 1, nparts)) return;
   const int32_t* bs = bstart + (int64_t)b * (kMaxB + 1);
   const int s = bs[k], e = bs[k + 1];
   const double later = wrest[b] + bwsuf[(int64_t)b * kMaxB + k];
@@ -1173,10 +1192,11 @@ __global__ __launch_bounds__(kFinNT) void k_pad(int32_t E, const int32_t* __rest
                                                 const float* __restrict__ logits, int64_t bstride,
                                                 const float* __restrict__ lmax, int64_t t_cap,
                                                 int64_t* __restrict__ actions, float* __restrict__ fwd,
-                                                int32_t* __restrict__ t_out) {
+                                                int32_t* __restrict__ t_out, int32_t do_pad) {
   const int b = blockIdx.y;
   const int k = counts[b], T = *tdev;
   if (t_out && b == 0 && blockIdx.x == 0 && threadIdx.x == 0) *t_out = T;
+  if (!do_pad) return;  // the terminal step and the padding belong to the last part
   int64_t* ab = actions + (int64_t)b * t_cap;
   float* fb = fwd + (int64_t)b * t_cap;
   for (int t = k + blockIdx.x * kFinNT + threadIdx.x; t < T; t += gridDim.x * kFinNT) {
@@ -1221,26 +1241,40 @@ extern "C" size_t spai_rollout_workspace_bytes(int32_t E, int32_t B) {
   return w.total_bytes;
 }
 
-// Byte offset of a diagnostic word inside the rollout workspace (tests read it from the
-// caller-owned buffer instead of hard-coding the carve): 0 = oversized buckets of the last
-// order phase (k_sort2 -> k_sort2_big), 1 = T of the last rollout.  -1 for a bad field.
+// Byte offset of a diagnostic / exchange array inside the rollout workspace (tests and the
+// multi-part exchange address it in the caller-owned buffer instead of hard-coding the carve):
+//   0 = int32 oversized buckets of the last order phase (k_sort2 -> k_sort2_big)
+//   1 = int32 T of the last rollout
+//   2 = fp64 [B][kMaxB] bucket weight sums (a part fills its own buckets, the rest stay 0)
+//   3 = kMaxB (the row length of field 2), as a value, not an offset
+//   4 = int32 [B][kMaxB + 1] trajectory position of each bucket's first winner (bucket nb: count)
+//   5 = int32 [B] buckets of each sample
+// -1 for a bad field or shape.
 extern "C" int64_t spai_rollout_ws_offset(int32_t E, int32_t B, int32_t field) {
   if (E <= 0 || B <= 0) return -1;
   TrajWs w;
-  traj_ws(nullptr, E, B, &w);
-  if (field == 0) return (int64_t)reinterpret_cast<uintptr_t>(w.lastbig);
-  if (field == 1) return (int64_t)reinterpret_cast<uintptr_t>(w.tdev);
-  return -1;
+  char* base = reinterpret_cast<char*>((uintptr_t)1 << 20);  // any aligned non-null base: offsets only
+  traj_ws(base, E, B, &w);
+  switch (field) {
+    case 0: return reinterpret_cast<char*>(w.lastbig) - base;
+    case 1: return reinterpret_cast<char*>(w.tdev) - base;
+    case 2: return reinterpret_cast<char*>(w.bwsum) - base;
+    case 3: return kMaxB;
+    case 4: return reinterpret_cast<char*>(w.bstart) - base;
+    case 5: return reinterpret_cast<char*>(w.nb) - base;
+    default: return -1;
+  }
 }
 
 extern "C" int spai_rollout_select(const float* logits, int64_t bstride, int32_t E, int32_t B, const float* lmax,
-                                   uint64_t seed, uint64_t stream_id, int32_t sample_base, uint32_t* removed,
-                                   int32_t words, int32_t* counts, void* workspace, size_t workspace_bytes,
-                                   void* stream) {
+                                   uint64_t seed, uint64_t stream_id, uint64_t* stream_ctr, int32_t sample_base,
+                                   int32_t part, int32_t nparts, uint32_t* removed, int32_t words, int32_t* counts,
+                                   void* workspace, size_t workspace_bytes, void* stream) {
   SPAI_CHECK_ARG(logits && lmax && removed && counts && workspace, "spai_rollout_select: null pointer");
   SPAI_CHECK_ARG(E > 0 && B > 0 && bstride >= 0 && sample_base >= 0, "spai_rollout_select: bad shape");
   SPAI_CHECK_ARG((int64_t)E <= (int64_t)kMaxTiles * kTile, "spai_rollout_select: E=%d too large", E);
   SPAI_CHECK_ARG(B <= kMaxSamples, "spai_rollout_select: B=%d above %d", B, kMaxSamples);
+  SPAI_CHECK_ARG(nparts >= 1 && part >= 0 && part < nparts, "spai_rollout_select: part %d of %d", part, nparts);
   SPAI_CHECK_ARG(words == (E + 31) / 32, "spai_rollout_select: words must be ceil(E/32)");
   TrajWs w;
   traj_ws(workspace, E, B, &w);
@@ -1250,17 +1284,74 @@ extern "C" int spai_rollout_select(const float* logits, int64_t bstride, int32_t
   const uint32_t s0 = (uint32_t)seed, s1 = (uint32_t)(seed >> 32);
   const uint32_t t0 = (uint32_t)stream_id, t1 = (uint32_t)(stream_id >> 32);
   const int nsb = (w.M + kSampNT - 1) / kSampNT;
-  k_presample<<<dim3(nsb, B), kSampNT, 0, s>>>(logits, bstride, E, w.M, s0, s1, t0, t1, sample_base, w.samp,
-                                              w.samp_cnt, w.ctl, B * kMaxB + B + 2);
+  k_presample<<<dim3(nsb, B), kSampNT, 0, s>>>(logits, bstride, E, w.M, s0, s1, t0, t1, stream_ctr, sample_base,
+                                              w.samp, w.samp_cnt, w.ctl, B * kMaxB + B + 2);
   SPAI_CHECK_LAUNCH();
   k_splitters<<<B, kSortNT, 0, s>>>(E, w.M, nsb, w.samp, w.samp_cnt, w.nb, w.spl, w.lut, w.lut_base);
   SPAI_CHECK_LAUNCH();
-  k_tile<<<dim3(w.ntiles, B), kGrpNT, 0, s>>>(logits, bstride, E, w.ntiles, s0, s1, t0, t1, sample_base, removed,
-                                              words, lmax, w.nb, w.spl, w.lut, w.lut_base, w.staging, w.stlog,
-                                              w.runs, w.btot, w.tile_wrest);
+  k_tile<<<dim3(w.ntiles, B), kGrpNT, 0, s>>>(logits, bstride, E, w.ntiles, s0, s1, t0, t1, stream_ctr,
+                                              sample_base, part, nparts, removed, words, lmax, w.nb, w.spl, w.lut,
+                                              w.lut_base, w.staging, w.stlog, w.runs, w.btot, w.tile_wrest);
   SPAI_CHECK_LAUNCH();
   k_bscan<<<B, 1024, 0, s>>>(E, w.ntiles, logits, bstride, lmax, w.nb, w.btot, w.tile_wrest, w.bstart,
-                             counts, w.wrest, w.tdev);
+                             counts, w.wrest, w.tdev, stream_ctr, w.bwsum);
+  SPAI_CHECK_LAUNCH();
+  return SPAI_OK;
+}
+
+static int order_args(const float* logits, const float* lmax, const void* actions, const void* workspace, int32_t E,
+                      int32_t B, int64_t t_cap, int32_t part, int32_t nparts, size_t workspace_bytes, TrajWs* w,
+                      const char* who) {
+  SPAI_CHECK_ARG(logits && lmax && actions && workspace, "%s: null pointer", who);
+  SPAI_CHECK_ARG(E > 0 && B > 0 && t_cap >= (int64_t)E + 1, "%s: bad shape (E=%d B=%d t_cap=%lld)", who, E, B,
+                 (long long)t_cap);
+  SPAI_CHECK_ARG((int64_t)E <= (int64_t)kMaxTiles * kTile, "%s: E=%d too large", who, E);
+  SPAI_CHECK_ARG(B <= kMaxSamples, "%s: B=%d above %d", who, B, kMaxSamples);
+  SPAI_CHECK_ARG(nparts >= 1 && part >= 0 && part < nparts, "%s: part %d of %d", who, part, nparts);
+  traj_ws(const_cast<void*>(workspace), E, B, w);
+  SPAI_CHECK_ARG(workspace_bytes >= w->total_bytes, "%s: workspace too small", who);
+  return SPAI_OK;
+}
+
+extern "C" int spai_rollout_sort(const float* logits, int64_t bstride, int32_t E, int32_t B, const float* lmax,
+                                 int32_t part, int32_t nparts, int64_t t_cap, int64_t* actions, void* workspace,
+                                 size_t workspace_bytes, void* stream) {
+  TrajWs w;
+  const int st = order_args(logits, lmax, actions, workspace, E, B, t_cap, part, nparts, workspace_bytes, &w,
+                            "spai_rollout_sort");
+  if (st != SPAI_OK) return st;
+  hipStream_t s = (hipStream_t)stream;
+  const int nbm = max_buckets(E);
+  const int g2 = std::max(1, std::min((nbm + nparts - 1) / nparts * B, num_cus()));
+  k_sort2<<<g2, kSortNT, 0, s>>>(E, B, w.ntiles, w.nb, w.bstart, w.runs, w.staging, w.stlog, lmax, t_cap,
+                                 actions, w.out_w, w.out_suf, w.bwsum, w.bigcnt, w.biglist, part, nparts);
+  SPAI_CHECK_LAUNCH();
+  k_sort2_big<<<g2, kSortNT, 0, s>>>(E, B, w.ntiles, w.nb, w.bstart, w.runs, w.staging, logits, bstride,
+                                     lmax, t_cap, actions, w.out_w, w.out_suf, w.scratch, w.bwsum, w.bigcnt,
+                                     w.biglist);
+  SPAI_CHECK_LAUNCH();
+  return SPAI_OK;
+}
+
+extern "C" int spai_rollout_finish(const float* logits, int64_t bstride, int32_t E, int32_t B, const float* lmax,
+                                   const int32_t* counts, int32_t part, int32_t nparts, int64_t t_cap,
+                                   int64_t* actions, float* fwd_probs, int32_t* t_out, void* workspace,
+                                   size_t workspace_bytes, void* stream) {
+  TrajWs w;
+  const int st = order_args(logits, lmax, actions, workspace, E, B, t_cap, part, nparts, workspace_bytes, &w,
+                            "spai_rollout_finish");
+  if (st != SPAI_OK) return st;
+  SPAI_CHECK_ARG(counts && fwd_probs, "spai_rollout_finish: null pointer");
+  hipStream_t s = (hipStream_t)stream;
+  const int nbm = max_buckets(E);
+  k_wscan<<<B, 1024, 0, s>>>(w.nb, w.bwsum, w.bwsuf, w.bigcnt, w.lastbig);
+  SPAI_CHECK_LAUNCH();
+  k_final<<<dim3(nbm, B), kFinNT, 0, s>>>(E, w.nb, w.bstart, w.bwsuf, w.out_w, w.out_suf, w.wrest, t_cap, fwd_probs,
+                                          part, nparts);
+  SPAI_CHECK_LAUNCH();
+  const int last = part == nparts - 1;
+  k_pad<<<dim3(last ? std::max(1, 1024 / B) : 1, B), kFinNT, 0, s>>>(E, counts, w.tdev, w.wrest, logits, bstride,
+                                                                     lmax, t_cap, actions, fwd_probs, t_out, last);
   SPAI_CHECK_LAUNCH();
   return SPAI_OK;
 }
@@ -1268,31 +1359,9 @@ extern "C" int spai_rollout_select(const float* logits, int64_t bstride, int32_t
 extern "C" int spai_rollout_order(const float* logits, int64_t bstride, int32_t E, int32_t B, const float* lmax,
                                   const int32_t* counts, int64_t t_cap, int64_t* actions, float* fwd_probs,
                                   int32_t* t_out, void* workspace, size_t workspace_bytes, void* stream) {
-  SPAI_CHECK_ARG(logits && lmax && counts && actions && fwd_probs && workspace,
-                 "spai_rollout_order: null pointer");
-  SPAI_CHECK_ARG(E > 0 && B > 0 && t_cap >= (int64_t)E + 1, "spai_rollout_order: bad shape (E=%d B=%d t_cap=%lld)",
-                 E, B, (long long)t_cap);
-  SPAI_CHECK_ARG((int64_t)E <= (int64_t)kMaxTiles * kTile, "spai_rollout_order: E=%d too large", E);
-  SPAI_CHECK_ARG(B <= kMaxSamples, "spai_rollout_order: B=%d above %d", B, kMaxSamples);
-  TrajWs w;
-  traj_ws(workspace, E, B, &w);
-  SPAI_CHECK_ARG(workspace_bytes >= w.total_bytes, "spai_rollout_order: workspace too small");
-  hipStream_t s = (hipStream_t)stream;
-  const int nbm = max_buckets(E);
-  const int g2 = std::max(1, std::min(nbm * B, num_cus()));
-  k_sort2<<<g2, kSortNT, 0, s>>>(E, B, w.ntiles, w.nb, w.bstart, w.runs, w.staging, w.stlog, lmax, t_cap,
-                                 actions, w.out_w, w.out_suf, w.bwsum, w.bigcnt, w.biglist);
-  SPAI_CHECK_LAUNCH();
-  k_sort2_big<<<g2, kSortNT, 0, s>>>(E, B, w.ntiles, w.nb, w.bstart, w.runs, w.staging, logits, bstride,
-                                     lmax, t_cap, actions, w.out_w, w.out_suf, w.scratch, w.bwsum, w.bigcnt,
-                                     w.biglist);
-  SPAI_CHECK_LAUNCH();
-  k_wscan<<<B, 1024, 0, s>>>(w.nb, w.bwsum, w.bwsuf, w.bigcnt, w.lastbig);
-  SPAI_CHECK_LAUNCH();
-  k_final<<<dim3(nbm, B), kFinNT, 0, s>>>(E, w.nb, w.bstart, w.bwsuf, w.out_w, w.out_suf, w.wrest, t_cap, fwd_probs);
-  SPAI_CHECK_LAUNCH();
-  k_pad<<<dim3(std::max(1, 1024 / B), B), kFinNT, 0, s>>>(E, counts, w.tdev, w.wrest, logits, bstride, lmax, t_cap,
-                                                          actions, fwd_probs, t_out);
-  SPAI_CHECK_LAUNCH();
-  return SPAI_OK;
+  const int st = spai_rollout_sort(logits, bstride, E, B, lmax, 0, 1, t_cap, actions, workspace, workspace_bytes,
+                                   stream);
+  if (st != SPAI_OK) return st;
+  return spai_rollout_finish(logits, bstride, E, B, lmax, counts, 0, 1, t_cap, actions, fwd_probs, t_out, workspace,
+                             workspace_bytes, stream);
 }

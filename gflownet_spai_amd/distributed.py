@@ -1,14 +1,16 @@
 """Multi-GPU layout of the hot path: one process per GPU, torch.distributed (RCCL over xGMI on
 MI355X, gloo in the CPU tests).
 
-Two ways to spread work (DESIGN.md §5):
-  * candidates (default, weak scaling): rank r samples candidates with Philox sample ids
+Two ways to spread work (DESIGN.md §6):
+  * columns (default of bench.py, the north star's split, strong scaling): every rank draws
+    the same B candidates; rank r orders the r-th slice of every trajectory (rollout parts:
+    a contiguous range of the presampled key buckets) and fills lines shard_lines(n, r, P) of
+    every candidate's M.  ONE all_reduce per step carries the parts' bucket weight sums and the
+    squared residual partials (``exchange_parts``); the chosen M is assembled with ONE
+    all_gather of equal-size ELL blocks (``allgather_lines``).
+  * candidates (weak scaling): rank r samples candidates with Philox sample ids
     r*B .. r*B+B-1 (``GFlowNet(sample_base=r*B)``); every candidate's trajectory, fill and
     reward live on one rank, so the step needs no collective.
-  * columns of one candidate (strong scaling of a single huge M): rank r owns lines
-    [shard_lines(n, r, P)); the per-sample squared residuals are summed with ONE
-    all_reduce of B fp64 (``PreconditionerEnv.rewards_from_removed(..., group=...)``) and M
-    is assembled with ONE all_gather of equal-size ELL blocks (``allgather_lines``).
 The reference has no parallelism at all.
 """
 from __future__ import annotations
@@ -57,3 +59,32 @@ def gather_rewards(rewards: torch.Tensor, group=None) -> torch.Tensor:
     out = torch.empty(world * rewards.numel(), dtype=rewards.dtype, device=rewards.device)
     dist.all_gather_into_tensor(out, rewards.contiguous(), group=group)
     return out
+
+
+def exchange_parts(bucket_sums: torch.Tensor, res2: torch.Tensor, group=None,
+                   packed: torch.Tensor | None = None) -> torch.Tensor:
+    """The split rollout's one collective: sum the parts' bucket weight sums ([B, kMaxB] fp64,
+    each part non-zero on its own buckets only, so the sum is exact and equals the one-GPU
+    array) into ``bucket_sums`` in place, and the lines' squared residual partials [B]; returns
+    the summed residuals (a view of ``packed``, reused when given).  Packed into one buffer:
+    one all_reduce instead of two."""
+    nb = bucket_sums.numel()
+    if packed is None:
+        packed = torch.empty(nb + res2.numel(), dtype=torch.float64, device=bucket_sums.device)
+    packed[:nb].copy_(bucket_sums.reshape(-1))
+    packed[nb:].copy_(res2.reshape(-1))
+    dist.all_reduce(packed, op=dist.ReduceOp.SUM, group=group)
+    bucket_sums.copy_(packed[:bucket_sums.numel()].view_as(bucket_sums))
+    return packed[bucket_sums.numel():]
+
+
+def gather_slices(actions: torch.Tensor, fwd: torch.Tensor, bounds: torch.Tensor, T: int, group=None):
+    """Full [B, T] trajectories from every rank's slice [bounds[b, 0], bounds[b, 1]) (the slices
+    partition [0, T)): zero outside the slice, one all_reduce each (exact: one non-zero term)."""
+    pos = torch.arange(T, device=actions.device).view(1, -1)
+    mine = (pos >= bounds[:, :1]) & (pos < bounds[:, 1:])
+    a = torch.where(mine, actions[:, :T], torch.zeros((), dtype=actions.dtype, device=actions.device)).contiguous()
+    f = torch.where(mine, fwd[:, :T], torch.zeros((), dtype=fwd.dtype, device=fwd.device)).contiguous()
+    dist.all_reduce(a, group=group)
+    dist.all_reduce(f, group=group)
+    return a, f

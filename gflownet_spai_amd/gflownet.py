@@ -27,7 +27,7 @@ from .preconditioner import Data
 
 class GFlowNet(nn.Module):
     def __init__(self, forward_policy, backward_policy, env, *, mode: str = "parity", seed: int | None = None,
-                 sample_base: int = 0, overlap: bool = False, line_shard: tuple | None = None):
+                 sample_base: int = 0, shard: tuple | None = None):
         super().__init__()
         if mode not in ("parity", "throughput"):
             raise ValueError("mode must be 'parity' or 'throughput'")
@@ -38,18 +38,18 @@ class GFlowNet(nn.Module):
         self.mode = mode
         self.seed = int(torch.initial_seed() if seed is None else seed) & (2**64 - 1)
         self.sample_base = sample_base
-        self.rollouts = 0  # Philox stream id of the next throughput rollout
+        self.rollouts = 0  # Philox stream id of the next throughput rollout (host mirror)
+        self._ctr = None   # the same counter on the device (advanced by the select phase itself)
         self._data_cache = {}
-        self._side = None  # HIP stream for the fill/reward, overlapped with the trajectory sort
-        # True: fill/reward on a side stream while the main stream sorts the trajectories.  Off by
-        # default: k_sort2's persistent blocks hold ~156 KB of each CU's LDS, so the fill's blocks
-        # wait for them anyway and the serial order measured ~1% faster (r1f: 0.722 vs 0.731 ms/step)
-        self.overlap = overlap
-        # (line_begin, line_end, group): this rank fills and scores only lines [begin, end) of
-        # every candidate and the squared residuals are summed over the group (one all_reduce);
-        # every rank draws the same candidates (same seed and sample_base), so no exchange of
-        # the rollout is needed (columns sharded)
-        self.line_shard = line_shard
+        # (rank, world, group): the columns split of DESIGN.md §6 (throughput mode).  Every rank
+        # draws the same B candidates; rank r orders the r-th slice of every trajectory
+        # (rollout parts) and fills lines shard_lines(n, r, world) of every candidate's M; one
+        # all_reduce carries the parts' bucket weight sums and the squared residual partials.
+        self.shard = shard
+        if shard is not None:
+            from .distributed import shard_lines
+            rank, world, _ = shard
+            self.lines = shard_lines(env.matrix_size, rank, world) if env is not None else None
 
     # ------------------------------------------------------------------ policy
     def policy_logits(self, data, batch_size: int):
@@ -138,17 +138,34 @@ class GFlowNet(nn.Module):
         return True
 
     def _rewards(self, removed, counts, alpha):
-        if self.line_shard is None:
-            return self.env.rewards_from_removed(removed, counts, alpha)
-        b, e, group = self.line_shard
-        return self.env.rewards_from_removed(removed, counts, alpha, b, e, group)
+        return self.env.rewards_from_removed(removed, counts, alpha)
 
     # ------------------------------------------------------------------ sampler
     def sample_states(self, s0, return_log: bool = False):
+        """gflownet.py:125-197: sample B trajectories from the initial states, score them, log."""
+        if self.mode == "throughput":
+            st = self.rollout_begin(s0)
+            self.rollout_exchange(st)
+            log = self.rollout_end(st)
+            return log if return_log else None
         env = self.env
         B = len(s0)
         E = env.num_actions - 1
         log = Log(s0, self.backward_policy, self.total_flow, env)
+        logits, alpha, lg, lmax, z = self._logits(s0, need_z=True)
+        actions_bt, fwd_bt = self._parity_rollout(lg, B, lmax, z)
+        removed, counts = kernels.actions_to_removed(actions_bt, E)
+        rewards = self._rewards(removed, counts, alpha)
+        log._set_rollout(logits, actions_bt, fwd_bt, lmax=lmax)
+        log.removed, log.counts = removed, counts
+        log.rewards = rewards.detach().to(torch.float32)
+        return log if return_log else None
+
+    def _logits(self, s0, need_z: bool = False):
+        """(logits, alpha, sampler logits fp32 on the device, lmax [B], z [B] or None)."""
+        env = self.env
+        B = len(s0)
+        E = env.num_actions - 1
         if self._same_states(s0):
             data_list = self.state_to_data(s0[:1])
             logits, alpha, lmax = self.policy_logits(data_list[0], B)
@@ -165,45 +182,61 @@ class GFlowNet(nn.Module):
                 rows.append(l)
                 alphas.append(a)
             logits, alpha, lmax = torch.stack(rows, 0), torch.stack(alphas).mean(), None
-        if lmax is not None and self.mode == "throughput" and logits.is_cuda and logits.dtype == torch.float32:
-            lg = logits.detach()  # the throughput sampler needs only the maximum, which the policy kernels produced
-        else:
-            lg, lmax, z = kernels.logits_stats(logits.detach().to(env.device), B)
-        if self.mode == "parity":
-            actions_bt, fwd_bt = self._parity_rollout(lg, B, lmax, z)
-            removed, counts = kernels.actions_to_removed(actions_bt, E)
-            rewards = self._rewards(removed, counts, alpha)
-            log._set_rollout(logits, actions_bt, fwd_bt, lmax=lmax)
-        else:
-            removed, counts, ws = kernels.rollout_select(lg, B, lmax, self.seed, self.rollouts, self.sample_base)
-            self.rollouts += 1
-            if not self.overlap:
-                actions_full, fwd_full, t_dev = kernels.rollout_order(lg, B, lmax, counts, ws)
-                rewards = self._rewards(removed, counts, alpha)
-                log._set_rollout(logits, actions_full, fwd_full, t_dev, lmax=lmax)
-                log.removed, log.counts = removed, counts
-                log.rewards = rewards.detach().to(torch.float32)
-                return log if return_log else None
-            # the fill + ||.||_F reward needs only the removal bitmaps: run it on a second
-            # HIP stream while the main stream sorts the trajectories
-            main = torch.cuda.current_stream(lg.device)
-            if self._side is None or self._side.device != lg.device:
-                self._side = torch.cuda.Stream(lg.device)
-            side = self._side
-            side.wait_stream(main)
-            with torch.cuda.stream(side):
-                rewards = self._rewards(removed, counts, alpha)
-            for t in (removed, counts, alpha):
-                if torch.is_tensor(t) and t.is_cuda:
-                    t.record_stream(side)
-            actions_full, fwd_full, t_dev = kernels.rollout_order(lg, B, lmax, counts, ws)
-            main.wait_stream(side)
-            for t in (rewards, env.last_residual) + ((env.last_m,) if env.last_m is not None else ()):
-                t.record_stream(main)
-            log._set_rollout(logits, actions_full, fwd_full, t_dev, lmax=lmax)
-        log.removed, log.counts = removed, counts
+        if lmax is not None and not need_z and logits.is_cuda and logits.dtype == torch.float32:
+            return logits, alpha, logits.detach(), lmax, None  # the policy kernels produced the maximum
+        lg, lmax, z = kernels.logits_stats(logits.detach().to(env.device), B)
+        return logits, alpha, lg, lmax, z
+
+    # The throughput step in three phases, so a caller can capture the collective-free ones in
+    # HIP graphs (bench.py): begin = policy, select, sort, fill of this rank's lines; exchange =
+    # the split's one all_reduce (nothing on one GPU); end = fwd_probs, rewards, the Log.  No
+    # phase synchronises with the host; the Philox stream id lives on the device and the select
+    # phase advances it, so a replayed graph draws a fresh rollout.
+    def rollout_begin(self, s0) -> dict:
+        env = self.env
+        B = len(s0)
+        E = env.num_actions - 1
+        logits, alpha, lg, lmax, _ = self._logits(s0)
+        if self._ctr is None or self._ctr.device != lg.device:
+            self._ctr = torch.tensor([self.rollouts], dtype=torch.int64, device=lg.device)
+        self.rollouts += 1
+        rank, world, group = self.shard if self.shard is not None else (0, 1, None)
+        removed, counts, ws = kernels.rollout_select(lg, B, lmax, self.seed, 0, self.sample_base, self._ctr, rank,
+                                                     world)
+        actions = kernels.rollout_sort(lg, B, lmax, ws, rank, world)
+        lines = self.lines if self.shard is not None else (0, None)
+        res2 = env.fill_partial(removed, *lines)
+        return dict(s0=s0, B=B, E=E, logits=logits, alpha=alpha, lg=lg, lmax=lmax, removed=removed, counts=counts,
+                    ws=ws, actions=actions, res2_part=res2, part=(rank, world, group))
+
+    def rollout_exchange(self, st: dict) -> None:
+        """ONE all_reduce over the split: the parts' bucket weight sums (disjoint supports: the
+        sum is exact and equals the one-GPU array) and the lines' squared residual partials.
+        The summed residuals land in the same buffer on every call with the same ``st`` (a
+        captured ``rollout_end`` graph keeps reading it)."""
+        rank, world, group = st["part"]
+        if world == 1:
+            st["res2"] = st["res2_part"]
+            return
+        from .distributed import exchange_parts
+        bs = kernels.bucket_sums(st["ws"], st["E"], st["B"])
+        if "packed" not in st:
+            st["packed"] = torch.empty(bs.numel() + st["B"], dtype=torch.float64, device=bs.device)
+        st["res2"] = exchange_parts(bs, st["res2_part"], group, st["packed"])
+
+    def rollout_end(self, st: dict) -> Log:
+        env = self.env
+        rank, world, group = st["part"]
+        B, E, lg, lmax, counts, ws = st["B"], st["E"], st["lg"], st["lmax"], st["counts"], st["ws"]
+        fwd, t_dev = kernels.rollout_finish(lg, B, lmax, counts, ws, st["actions"], rank, world)
+        rewards = env.rewards_from_res2(st["res2"], counts, st["alpha"])
+        log = Log(st["s0"], self.backward_policy, self.total_flow, env)
+        log._set_rollout(st["logits"], st["actions"], fwd, t_dev, lmax=lmax)
+        if world > 1:
+            log._set_part(rank, world, group, kernels.part_bounds(ws, E, B, rank, world))
+        log.removed, log.counts = st["removed"], counts
         log.rewards = rewards.detach().to(torch.float32)
-        return log if return_log else None
+        return log
 
     def _parity_rollout(self, lg: Tensor, B: int, lmax: Tensor, z: Tensor):
         E1 = lg.shape[-1]

@@ -73,8 +73,13 @@ def parity_step(lg: torch.Tensor, B: int, noise: torch.Tensor, lmax, chosen, act
     return out_a, out_p
 
 
-def rollout_select(lg: torch.Tensor, B: int, lmax: torch.Tensor, seed: int, stream_id: int, sample_base: int = 0):
-    """Phase 1 of the throughput rollout: removal bitmaps [B, ceil(E/32)] and counts [B]."""
+def rollout_select(lg: torch.Tensor, B: int, lmax: torch.Tensor, seed: int, stream_id: int, sample_base: int = 0,
+                   stream_ctr: torch.Tensor | None = None, part: int = 0, nparts: int = 1, ws_tag: str = "rollout"):
+    """Phase 1 of the throughput rollout: removal bitmaps [B, ceil(E/32)] and counts [B].
+
+    stream_ctr: optional device uint64 (int64 tensor) holding the Philox stream id, advanced
+    by one on the device (graph replays draw fresh rollouts); part/nparts: this process orders
+    buckets [nb*part/nparts, nb*(part+1)/nparts) of every sample (the multi-GPU split)."""
     _lib.require_device(lg)
     E = lg.shape[-1] - 1
     words = (E + 31) // 32
@@ -83,12 +88,15 @@ def rollout_select(lg: torch.Tensor, B: int, lmax: torch.Tensor, seed: int, stre
     nb = _l().spai_rollout_workspace_bytes(E, B)
     if nb == 0:
         raise RuntimeError("spai_rollout_workspace_bytes failed: " + _l().spai_last_error().decode())
-    ws = _lib.workspace(nb, lg.device, "rollout")
+    ws = _lib.workspace(nb, lg.device, ws_tag)
+    if stream_ctr is not None and (stream_ctr.dtype != torch.int64 or stream_ctr.numel() != 1 or
+                                   stream_ctr.device != lg.device):
+        raise ValueError("stream_ctr must be a 1-element int64 tensor on the logits' device")
     with _timed("rollout_select"):
         st = _l().spai_rollout_select(_lib.ptr(lg), 0 if lg.dim() == 1 else E + 1, E, B, _lib.ptr(lmax),
-                                      seed & (2**64 - 1),
-                                        stream_id & (2**64 - 1), sample_base, _lib.ptr(removed), words,
-                                        _lib.ptr(counts), _lib.ptr(ws), ws.numel(), _lib.stream_ptr(lg.device))
+                                      seed & (2**64 - 1), stream_id & (2**64 - 1), _lib.ptr(stream_ctr),
+                                      sample_base, part, nparts, _lib.ptr(removed), words, _lib.ptr(counts),
+                                      _lib.ptr(ws), ws.numel(), _lib.stream_ptr(lg.device))
     _lib.check(st, "spai_rollout_select")
     return removed, counts, ws
 
@@ -108,6 +116,56 @@ def rollout_order(lg, B, lmax, counts, ws):
                                      _lib.ptr(ws), ws.numel(), _lib.stream_ptr(lg.device))
     _lib.check(st, "spai_rollout_order")
     return actions, fwd, t_dev
+
+
+def bucket_sums(ws: torch.Tensor, E: int, B: int) -> torch.Tensor:
+    """fp64 [B, kMaxB] view of the bucket weight sums inside a rollout workspace (the array the
+    parts of a split rollout sum before spai_rollout_finish)."""
+    off = _l().spai_rollout_ws_offset(E, B, 2)
+    kmax = _l().spai_rollout_ws_offset(E, B, 3)
+    if off < 0 or kmax <= 0:
+        raise ValueError("spai_rollout_ws_offset failed")
+    return ws[off:off + B * kmax * 8].view(torch.float64).view(B, kmax)
+
+
+def part_bounds(ws: torch.Tensor, E: int, B: int, part: int, nparts: int) -> torch.Tensor:
+    """[B, 2] int64 trajectory slice [start, end) a part orders (device tensor, no sync; the last
+    part's end is E + 1: it also writes the terminal step and the padding)."""
+    lib = _l()
+    kmax = lib.spai_rollout_ws_offset(E, B, 3)
+    o_bs, o_nb = lib.spai_rollout_ws_offset(E, B, 4), lib.spai_rollout_ws_offset(E, B, 5)
+    bstart = ws[o_bs:o_bs + B * (kmax + 1) * 4].view(torch.int32).view(B, kmax + 1).long()
+    nb = ws[o_nb:o_nb + B * 4].view(torch.int32).long()
+    k0, k1 = (nb * part) // nparts, (nb * (part + 1)) // nparts
+    start = bstart.gather(1, k0.view(B, 1))
+    end = bstart.gather(1, k1.view(B, 1)) if part < nparts - 1 else torch.full_like(start, E + 1)
+    return torch.cat([start, end], 1)
+
+
+def rollout_sort(lg, B, lmax, ws, part: int, nparts: int):
+    """Split order phase, step 1: sorts this part's buckets; returns the actions buffer
+    [B, E+1] (the part's trajectory slice written) — then sum bucket_sums(ws) over the parts."""
+    E = lg.shape[-1] - 1
+    actions = torch.empty(B, E + 1, dtype=torch.int64, device=lg.device)
+    with _timed("rollout_sort"):
+        st = _l().spai_rollout_sort(_lib.ptr(lg), 0 if lg.dim() == 1 else E + 1, E, B, _lib.ptr(lmax), part, nparts,
+                                    E + 1, _lib.ptr(actions), _lib.ptr(ws), ws.numel(), _lib.stream_ptr(lg.device))
+    _lib.check(st, "spai_rollout_sort")
+    return actions
+
+
+def rollout_finish(lg, B, lmax, counts, ws, actions, part: int, nparts: int):
+    """Split order phase, step 2 (after the bucket sums are complete): fwd_probs of the part's
+    slice, the terminal step and padding on the last part.  Returns (fwd [B, E+1], T)."""
+    E = lg.shape[-1] - 1
+    fwd = torch.empty(B, E + 1, dtype=torch.float32, device=lg.device)
+    t_dev = torch.empty(1, dtype=torch.int32, device=lg.device)
+    with _timed("rollout_finish"):
+        st = _l().spai_rollout_finish(_lib.ptr(lg), 0 if lg.dim() == 1 else E + 1, E, B, _lib.ptr(lmax),
+                                      _lib.ptr(counts), part, nparts, E + 1, _lib.ptr(actions), _lib.ptr(fwd),
+                                      _lib.ptr(t_dev), _lib.ptr(ws), ws.numel(), _lib.stream_ptr(lg.device))
+    _lib.check(st, "spai_rollout_finish")
+    return fwd, t_dev
 
 
 def actions_to_removed(actions_bt: torch.Tensor, E: int):

@@ -101,10 +101,26 @@ class Log:
         else:
             self._full = (actions_bt, fwd_bt, t_dev)
 
+    def _set_part(self, rank: int, world: int, group, bounds: Tensor):
+        """The rollout was split over ``world`` processes: this rank's buffers hold
+        only the trajectory slice [bounds[b, 0], bounds[b, 1]) of each sample.  The full log is
+        assembled on first use (one all_reduce of the zero-masked slices: the slices are
+        disjoint, so the sum is exact); ``local_slice`` reads the rank's part without it."""
+        self._part = (rank, world, group, bounds)
+
+    def local_slice(self):
+        """(actions [B, cap], fwd [B, cap], bounds [B, 2]) of this rank's part (split rollouts)."""
+        a, f, _ = self._full
+        return a, f, self._part[3]
+
     def _materialize(self):
         if self._full is not None:
             a, f, t = self._full
             T = int(t)
+            part = getattr(self, "_part", None)
+            if part is not None and part[1] > 1:
+                from .distributed import gather_slices
+                a, f = gather_slices(a, f, part[3], T, part[2])
             self._actions_bt, self._fwd_probs = a[:, :T], f[:, :T]
             self._act_tb = self._actions_bt.t()
             self._full = None

@@ -108,18 +108,28 @@ class PreconditionerEnv(Env):
                              line_end: int | None = None, group=None) -> Tensor:
         """[B] fp64 rewards from removal bitmaps; with ``group`` the lines are a shard and the
         per-sample squared norms are summed across the process group (one all_reduce)."""
+        res2 = self.fill_partial(removed, line_begin, line_end)
+        if group is not None:
+            import torch.distributed as dist
+            dist.all_reduce(res2, group=group)
+        return self.rewards_from_res2(res2, counts, alpha)
+
+    def fill_partial(self, removed: Tensor, line_begin: int = 0, line_end: int | None = None) -> Tensor:
+        """Fill lines [line_begin, line_end) of M for every sample and return the per-sample
+        squared residual norms of those lines, [B] fp64 (kept in ``last_m`` / ``last_removed``)."""
         if self.gram is not None:
             res2, m = kernels.fill_residual_gram(self.pattern, self.gram, removed, self.fill == "lsq", line_begin,
                                                  line_end, store_m=self.keep_m, m_dtype=self.a_lines.val.dtype)
         else:
             res2, m = kernels.fill_residual(self.pattern, self.a_lines, removed, self.fill == "lsq", line_begin,
                                             line_end, store_m=self.keep_m, m_dtype=self.a_lines.val.dtype)
-        if group is not None:
-            import torch.distributed as dist
-            dist.all_reduce(res2, group=group)
         if self.keep_m:
             self.last_m = m
         self.last_removed = removed
+        return res2
+
+    def rewards_from_res2(self, res2: Tensor, counts: Tensor, alpha) -> Tensor:
+        """Residuals (``last_residual``) and rewards [B] fp64 from the summed squared norms."""
         if not torch.is_tensor(alpha):
             alpha = torch.tensor(float(alpha), dtype=torch.float32)
         self.last_residual, reward = kernels.rewards(res2, counts, self.init_nnz, self.matrix_size, self._r0,

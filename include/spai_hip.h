@@ -95,18 +95,45 @@ int spai_parity_step(const float* logits, int64_t bstride, int32_t E1, int32_t B
  *   mass of the actions never removed (terminal included) = the masked-softmax probability
  *   of step t (policy.py:65-73, log.py:70), 1.0 after the terminal;
  * (log.py:67-87 semantics: the Log's actions [T,B] is the transpose).  lmax comes from
- * spai_logits_stats.  One workspace serves both phases of one rollout. */
+ * spai_logits_stats.  One workspace serves both phases of one rollout; the order phase may be
+ * repeated on the same select (it is idempotent).
+ *
+ * stream_ctr (optional, device uint64): when non-null the Philox stream id is read from it
+ * instead of `stream_id`, and the select phase adds 1 to it (a captured HIP graph of the
+ * rollout then draws a fresh rollout on every replay).
+ *
+ * Parts (the multi-GPU split): the presampled splitters cut every sample's
+ * winners into nb buckets in trajectory order; part p of nparts orders buckets
+ * [nb*p/nparts, nb*(p+1)/nparts), i.e. one contiguous slice of every trajectory.  Every part
+ * scans all E actions (removed, counts, T, the untouched mass and the bucket totals are
+ * complete on every part); only its own winners are staged and sorted.  After
+ * spai_rollout_sort the part has filled its buckets' weight sums in the workspace array
+ * spai_rollout_ws_offset(E, B, 2) ([B][kMaxB] fp64, zero elsewhere); summing that array over
+ * the parts (an all-reduce: x + 0 is exact, so the sum equals the one-part array bit for
+ * bit) before spai_rollout_finish makes the part's fwd_probs identical to a one-part run.
+ * spai_rollout_finish writes actions/fwd_probs of the part's slice only; the last part also
+ * writes the terminal step and the padding; t_out is written by every part.
+ * spai_rollout_order = sort + finish with nparts = 1. */
 size_t spai_rollout_workspace_bytes(int32_t E, int32_t B);
 int spai_rollout_select(const float* logits, int64_t bstride, int32_t E, int32_t B, const float* lmax,
-                        uint64_t seed, uint64_t stream_id, int32_t sample_base, uint32_t* removed,
-                        int32_t words, int32_t* counts, void* workspace, size_t workspace_bytes,
-                        void* stream);
+                        uint64_t seed, uint64_t stream_id, uint64_t* stream_ctr, int32_t sample_base,
+                        int32_t part, int32_t nparts, uint32_t* removed, int32_t words, int32_t* counts,
+                        void* workspace, size_t workspace_bytes, void* stream);
+int spai_rollout_sort(const float* logits, int64_t bstride, int32_t E, int32_t B, const float* lmax,
+                      int32_t part, int32_t nparts, int64_t t_cap, int64_t* actions, void* workspace,
+                      size_t workspace_bytes, void* stream);
+int spai_rollout_finish(const float* logits, int64_t bstride, int32_t E, int32_t B, const float* lmax,
+                        const int32_t* counts, int32_t part, int32_t nparts, int64_t t_cap, int64_t* actions,
+                        float* fwd_probs, int32_t* t_out, void* workspace, size_t workspace_bytes, void* stream);
 int spai_rollout_order(const float* logits, int64_t bstride, int32_t E, int32_t B, const float* lmax,
                        const int32_t* counts, int64_t t_cap, int64_t* actions, float* fwd_probs,
                        int32_t* t_out, void* workspace, size_t workspace_bytes, void* stream);
-/* Byte offset inside the rollout workspace of a diagnostic int32 (tests/diagnostics):
- * field 0 = oversized buckets the last order phase handed to the global-memory sort,
- * field 1 = T of the last rollout.  -1 for an unknown field or bad shape. */
+/* Byte offset inside the rollout workspace (tests, the multi-part exchange): field 0 = int32
+ * oversized buckets the last order phase handed to the global-memory sort, 1 = int32 T of the
+ * last rollout, 2 = fp64 [B][kMaxB] bucket weight sums, 4 = int32 [B][kMaxB + 1] trajectory
+ * position of each bucket's first winner, 5 = int32 [B] buckets per sample (a part's slice of
+ * sample b is [pos[b][nb*p/np], pos[b][nb*(p+1)/np])); field 3 returns kMaxB itself.
+ * -1 for an unknown field or bad shape. */
 int64_t spai_rollout_ws_offset(int32_t E, int32_t B, int32_t field);
 
 /* ---------------------------------------------------------------- actions -> removal sets

@@ -109,25 +109,7 @@ def parity_rollout(logits, B, generator=None):
     hist = []  # list of [B] int64 (log._actions)
     fwd = []
     while not bool(done.all()):
-        acts = torch.stack(hist, 1) if hist else torch.empty(B, 0, dtype=torch.long)
-        probs = []
-        for b in range(B):
-            x = logits
-            if acts.shape[1] > 0:
-                mask = torch.ones_like(x, dtype=torch.bool)
-                mask[:, acts[b]] = 0
-                x = x.masked_fill(~mask, float("-inf"))
-            probs.append(torch.softmax(x, dim=1))
-        probs_all = torch.stack(probs, 0)  # [B,1,E+1]
-        if B > 1:
-            s = probs_all.sum(2)
-            s[s == 0] = 1
-            probs_all = probs_all / s.unsqueeze(1)
-        # torch.distributions.Categorical(probs).sample() == multinomial(p/sum, 1, True)
-        p2 = probs_all.reshape(-1, A1)
-        p2 = p2 / p2.sum(-1, keepdim=True)
-        q = torch.empty_like(p2).exponential_(1, generator=generator)
-        a_all = torch.argmax(p2 / q, dim=-1).view(B, 1)
+        a_all, probs_all = reference_step(logits, B, hist, generator)
         mask_active = ~done
         fp = torch.ones(B)
         gathered = probs_all.gather(2, a_all.unsqueeze(1)).view(B)
@@ -139,6 +121,47 @@ def parity_rollout(logits, B, generator=None):
         term = (a_all.view(B) == E)
         done[mask_active] = term[mask_active]
     return torch.stack(hist, 0), torch.stack(fwd, 0).t().contiguous()
+
+
+def reference_step(logits, B, hist, generator=None):
+    """One step of the reference's sampler with its torch-CPU ops: per sample the policy's
+    masked softmax over the action history (policy.py:65-73), stacked [B,1,E+1], renormalised
+    when B > 1 (gflownet.py:116-120), then Categorical(probs).sample() (gflownet.py:148), i.e.
+    multinomial's fast path argmax(p / q), q ~ Exp(1) of shape [B, E+1] from the generator.
+    Returns (actions [B,1], probs_all [B,1,E+1])."""
+    A1 = logits.shape[1]
+    acts = torch.stack(hist, 1) if hist else torch.empty(B, 0, dtype=torch.long)
+    probs = []
+    for b in range(B):
+        x = logits
+        if acts.shape[1] > 0:
+            mask = torch.ones_like(x, dtype=torch.bool)
+            mask[:, acts[b]] = 0
+            x = x.masked_fill(~mask, float("-inf"))
+        probs.append(torch.softmax(x, dim=1))
+    probs_all = torch.stack(probs, 0)  # [B,1,E+1]
+    if B > 1:
+        s = probs_all.sum(2)
+        s[s == 0] = 1
+        probs_all = probs_all / s.unsqueeze(1)
+    # torch.distributions.Categorical(probs).sample() == multinomial(p/sum, 1, True)
+    p2 = probs_all.reshape(-1, A1)
+    p2 = p2 / p2.sum(-1, keepdim=True)
+    q = torch.empty_like(p2).exponential_(1, generator=generator)
+    return torch.argmax(p2 / q, dim=-1).view(B, 1), probs_all
+
+
+def reference_update_residual(rows, cols, vals, removed_b, n, A_t):
+    """One sample of env.update with the reference's torch-CPU ops: the kept edges as a fresh
+    COO M (utils.py:315-353: keep mask over E, coalesce), ||M A - I||_F by sparse torch.mm,
+    the fp64 identity subtraction and torch.norm (preconditioner.py:79-93).  A_t: A as a torch
+    sparse COO tensor (fp32)."""
+    keep = ~torch.as_tensor(removed_b)
+    ind = torch.stack([torch.as_tensor(rows)[keep], torch.as_tensor(cols)[keep]])
+    M = torch.sparse_coo_tensor(ind, torch.as_tensor(vals)[keep].float(), (n, n)).coalesce()
+    i = torch.arange(n)
+    eye = torch.sparse_coo_tensor(torch.stack([i, i]), torch.ones(n, dtype=torch.float64), (n, n))
+    return float(torch.norm(torch.mm(M, A_t) - eye))
 
 
 # --------------------------------------------------------------------------------------

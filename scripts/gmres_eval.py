@@ -85,7 +85,7 @@ def main():
     fwd = bench.make_policy(env, A32, dev)
     torch.manual_seed(0)
     bwd = BackwardPolicy(1, 4, env.num_actions).to(dev)
-    g = GFlowNet(fwd, bwd, env, mode="throughput", seed=1234, overlap=False)
+    g = GFlowNet(fwd, bwd, env, mode="throughput", seed=1234)
     with torch.no_grad():
         log = g.sample_states([A32] * args.samples, return_log=True)
     for s in range(args.samples):

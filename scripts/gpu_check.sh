@@ -12,7 +12,7 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_ou
 rc=$?; echo "smoke rc=$rc"; tail -3 gpurun_out/smoke.log
 [ $rc -ne 0 ] && exit $rc
 for cfg in ${BENCH_CONFIGS:-c4 c3}; do
-  timeout -k 10 400 python bench.py --config $cfg --steps $STEPS --warmup 2 ${BENCH_ARGS:---no-cpu-baseline} > gpurun_out/bench_$cfg.log 2>&1
+  timeout -k 10 400 python bench.py --config $cfg --steps $STEPS --warmup 2 ${BENCH_ARGS:-} > gpurun_out/bench_$cfg.log 2>&1
   rc=$?; echo "bench $cfg rc=$rc"; tail -2 gpurun_out/bench_$cfg.log
   [ $rc -ne 0 ] && exit $rc
 done

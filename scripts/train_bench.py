@@ -33,7 +33,7 @@ def main():
     fwd.requires_grad_(True)
     torch.manual_seed(0)
     bwd = BackwardPolicy(1, 4, E + 1).to(dev)
-    model = GFlowNet(fwd, bwd, env, mode="throughput", seed=1234, overlap=False)
+    model = GFlowNet(fwd, bwd, env, mode="throughput", seed=1234)
     opt = torch.optim.Adam(model.parameters(), lr=1e-3)
     s0 = [A] * args.batch
     rec = []

@@ -39,8 +39,12 @@ def test_argument_validation_without_gpu():
                                 None, None, 0, None)
     assert rc == _lib.SPAI_ERR_INVALID
     assert b"fill_mode" in lib.spai_last_error()
-    rc = lib.spai_rollout_select(None, 0, 10, 1, None, 0, 0, 0, None, 1, None, None, 0, None)
+    rc = lib.spai_rollout_select(None, 0, 10, 1, None, 0, 0, None, 0, 0, 1, None, 1, None, None, 0, None)
     assert rc == _lib.SPAI_ERR_INVALID
+    rc = lib.spai_rollout_sort(None, 0, 10, 1, None, 2, 2, 11, None, None, 0, None)
+    assert rc == _lib.SPAI_ERR_INVALID and b"null pointer" in lib.spai_last_error()
+    assert lib.spai_rollout_ws_offset(1000, 2, 3) == 2048 and lib.spai_rollout_ws_offset(1000, 2, 9) == -1
+    assert 0 < lib.spai_rollout_ws_offset(1000, 2, 2) < lib.spai_rollout_workspace_bytes(1000, 2)
     with pytest.raises(ValueError):
         _lib.check(rc, "spai_rollout_select")
     assert lib.spai_fill_workspace_bytes(1000, 4) >= 1000 * 4 * 8

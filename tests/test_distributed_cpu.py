@@ -13,7 +13,8 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from gflownet_spai_amd.distributed import allgather_lines, allreduce_res2, gather_rewards, shard_lines
+from gflownet_spai_amd.distributed import (allgather_lines, allreduce_res2, exchange_parts, gather_rewards, gather_slices,
+                                          shard_lines)
 from oracle import spai_oracle as O
 
 
@@ -59,9 +60,44 @@ def _worker(rank, world, port, q):
         out["res2"] = res2.numpy()
         out["m"] = full_m.numpy()
         out["rewards"] = gather_rewards(torch.arange(B, dtype=torch.float64) + 10 * rank).numpy()
+        # the split rollout's exchange: each part fills the bucket weight sums of its own bucket
+        # range (zero elsewhere) and its lines' residual partials; one packed all_reduce
+        full_bs, full_r2 = _split_fixture()
+        nb = full_bs.shape[1]
+        k0, k1 = nb * rank // world, nb * (rank + 1) // world
+        bs = torch.zeros_like(full_bs)
+        bs[:, k0:k1] = full_bs[:, k0:k1]
+        r2 = full_r2 * (0.25 if rank == 0 else 0.75)
+        out["r2"] = exchange_parts(bs, r2).numpy()
+        out["bs"] = bs.numpy()
+        # the split log: rank q holds slice [bounds[b,0], bounds[b,1]) of each trajectory
+        acts, fwd, cuts, T = _slices_fixture()
+        bounds = torch.stack([cuts[:, rank], cuts[:, rank + 1]], 1)
+        mine_a = torch.full_like(acts, -99)
+        mine_f = torch.full_like(fwd, -99.0)
+        for b in range(acts.shape[0]):
+            s0, e0 = int(bounds[b, 0]), int(bounds[b, 1])
+            mine_a[b, s0:e0] = acts[b, s0:e0]
+            mine_f[b, s0:e0] = fwd[b, s0:e0]
+        ga, gf = gather_slices(mine_a, mine_f, bounds, T)
+        out["slices"] = (ga.numpy(), gf.numpy())
         q.put((rank, out))
     finally:
         dist.destroy_process_group()
+
+
+def _split_fixture():
+    g = torch.Generator().manual_seed(3)
+    return torch.rand(3, 37, generator=g, dtype=torch.float64) * 1e3, torch.rand(3, generator=g, dtype=torch.float64)
+
+
+def _slices_fixture():
+    g = torch.Generator().manual_seed(4)
+    B, T = 3, 50
+    acts = torch.randint(0, 1000, (B, T), generator=g)
+    fwd = torch.rand(B, T, generator=g)
+    cuts = torch.tensor([[0, 20, T], [0, 0, T], [0, 50, T]])  # empty slices at either end too
+    return acts, fwd, cuts, T
 
 
 def test_shard_lines_partition():
@@ -99,3 +135,10 @@ def test_world2_column_sharded_reward_and_assembly():
             assert res[rank]["res2"][b] == pytest.approx(full, rel=1e-12)
             np.testing.assert_allclose(res[rank]["m"][b], m, rtol=1e-12, atol=1e-15)
     np.testing.assert_array_equal(res[0]["rewards"], [0, 1, 2, 10, 11, 12])
+    full_bs, full_r2 = _split_fixture()
+    acts, fwd, _, _ = _slices_fixture()
+    for rank in (0, 1):
+        assert np.array_equal(res[rank]["bs"], full_bs.numpy())  # bit-exact: one non-zero term each
+        np.testing.assert_allclose(res[rank]["r2"], full_r2.numpy(), rtol=1e-15)
+        assert np.array_equal(res[rank]["slices"][0], acts.numpy())
+        assert np.array_equal(res[rank]["slices"][1], fwd.numpy())

@@ -285,26 +285,6 @@ def test_throughput_sample_states_end_to_end():
         assert float(env.last_residual[b]) == pytest.approx(res, rel=1e-10)
 
 
-def test_overlapped_and_serial_fill_agree():
-    """GFlowNet(overlap=True) (fill/reward on a side stream during the sort) and the default
-    serial order give identical trajectories, probabilities, M and rewards."""
-    from gflownet_spai_amd import GFlowNet, PreconditionerEnv, poisson_2d
-    A = poisson_2d(40)
-    n = 40 * 40
-    outs = []
-    for overlap in (False, True):
-        env = PreconditionerEnv(n, A, A, side="AM", fill="lsq", keep_m=True)
-        E = env.num_actions - 1
-        logits = torch.randn(E + 1, generator=torch.Generator().manual_seed(7))
-        logits[E] = 7.0
-        g = GFlowNet(FixedLogits(logits), None, env, mode="throughput", seed=5, overlap=overlap)
-        log = g.sample_states([A] * 3, return_log=True)
-        torch.cuda.synchronize()
-        outs.append((log.actions.cpu(), log.fwd_probs.detach().cpu(), env.last_m.cpu(), log.rewards.cpu()))
-    for x, y in zip(*outs):
-        assert torch.equal(x, y)
-
-
 def test_lsq_fp64_3d_vs_oracle():
     """64^3 is the C3 config; a 12^3 7-pt fp64 lattice checks the fp64 LSQ kernel exactly."""
     from gflownet_spai_amd import GFlowNet, PreconditionerEnv, poisson_3d
@@ -561,3 +541,97 @@ def test_sample_states_distinct_initial_states():
     A3 = torch.sparse_coo_tensor(A._indices().clone(), A._values().clone(), A.shape)
     g.sample_states([A, A3, A], return_log=True)  # equal content, other storage: one call
     assert EdgeLogits.calls == 1
+
+
+@pytest.mark.parametrize("P", [2, 3, 5])
+def test_split_rollout_parts_reassemble_bit_exact(P):
+    """The multi-GPU split played by P parts in one process: every part's select
+    gives the complete removed sets and counts; each part sorts its bucket range; the parts'
+    bucket weight sums are summed (what the all_reduce does); each part's finish then writes
+    its trajectory slice.  The slices tile [0, T) and reassemble the one-part rollout bit for
+    bit (actions and fwd_probs)."""
+    from gflownet_spai_amd import kernels
+    E, B = 300000, 3
+    rng = np.random.default_rng(P)
+    logits = rng.standard_normal(E + 1).astype(np.float32)
+    logits[E] = 1.2
+    lg, lmax, _ = kernels.logits_stats(torch.from_numpy(logits).to(DEV), B)
+    removed1, counts1, ws1 = kernels.rollout_select(lg, B, lmax, 17, 4)
+    a1, f1, t1 = kernels.rollout_order(lg, B, lmax, counts1, ws1)
+    T = int(t1)
+    parts = []
+    for q in range(P):
+        rq, cq, wq = kernels.rollout_select(lg, B, lmax, 17, 4, 0, None, q, P, ws_tag=f"part{q}")
+        assert torch.equal(rq, removed1) and torch.equal(cq, counts1)
+        aq = kernels.rollout_sort(lg, B, lmax, wq, q, P)
+        parts.append((wq, aq))
+    total = sum(kernels.bucket_sums(wq, E, B).clone() for wq, _ in parts)
+    nb = kernels.part_bounds(parts[0][0], E, B, 0, 1)  # sanity: one part spans everything
+    assert int(nb[0, 0]) == 0
+    acts = torch.full((B, T), -7, dtype=torch.int64, device=DEV)
+    fwds = torch.full((B, T), -7.0, device=DEV)
+    covered = torch.zeros((B, T), dtype=torch.int32, device=DEV)
+    for q, (wq, aq) in enumerate(parts):
+        kernels.bucket_sums(wq, E, B).copy_(total)
+        fq, tq = kernels.rollout_finish(lg, B, lmax, counts1, wq, aq, q, P)
+        assert int(tq) == T
+        bd = kernels.part_bounds(wq, E, B, q, P).cpu()
+        for b in range(B):
+            s0, e0 = int(bd[b, 0]), min(int(bd[b, 1]), T)
+            acts[b, s0:e0] = aq[b, s0:e0]
+            fwds[b, s0:e0] = fq[b, s0:e0]
+            covered[b, s0:e0] += 1
+    assert bool((covered == 1).all())
+    assert torch.equal(acts, a1[:, :T])
+    assert torch.equal(fwds, f1[:, :T])
+    r_o, a_o, f_o, c_o = O.throughput_rollout(logits, B, 17, 4)
+    assert np.array_equal(acts.cpu().numpy(), a_o.T)
+
+
+def test_stream_counter_and_graph_replay():
+    """The Philox stream id read from the device counter equals the host argument and advances
+    by one per select; a HIP graph of GFlowNet.sample_states replays fresh rollouts (streams
+    1, 2, ...) identical to the oracle's, with M and rewards recomputed each replay."""
+    from gflownet_spai_amd import GFlowNet, PreconditionerEnv, kernels, poisson_2d
+    E, B = 5000, 2
+    logits = np.random.default_rng(3).standard_normal(E + 1).astype(np.float32)
+    logits[E] = 2.0
+    lg, lmax, _ = kernels.logits_stats(torch.from_numpy(logits).to(DEV), B)
+    ctr = torch.tensor([41], dtype=torch.int64, device=DEV)
+    r_a, c_a, _ = kernels.rollout_select(lg, B, lmax, 9, 0, 0, ctr)
+    assert int(ctr) == 42
+    r_b, c_b, _ = kernels.rollout_select(lg, B, lmax, 9, 41)
+    assert torch.equal(r_a, r_b) and torch.equal(c_a, c_b)
+
+    A = poisson_2d(24)
+    n = 24 * 24
+    env = PreconditionerEnv(n, A, A, side="AM", fill="lsq", keep_m=True)
+    El = env.num_actions - 1
+    lgt = torch.randn(El + 1, generator=torch.Generator().manual_seed(5))
+    lgt[El] = 4.0
+    g = GFlowNet(FixedLogits(lgt).to(DEV), None, env, mode="throughput", seed=11)  # no H2D copy in capture
+    s0 = [A] * 3
+    with torch.no_grad():
+        log0 = g.sample_states(s0, return_log=True)  # stream 0, eager (also warms every cache)
+        torch.cuda.synchronize()
+        graph = torch.cuda.CUDAGraph()
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            g.sample_states(s0, return_log=True)  # stream 1 (warm-up on the capture stream)
+        torch.cuda.current_stream().wait_stream(side)
+        with torch.cuda.graph(graph):
+            logc = g.sample_states(s0, return_log=True)  # captured: not executed
+        outs = []
+        for _ in range(2):
+            graph.replay()
+            torch.cuda.synchronize()
+            outs.append((logc._full[0].clone(), logc._full[2].clone(), env.last_m.clone(), logc.rewards.clone()))
+    _, a_0, _, _ = O.throughput_rollout(lgt.numpy(), 3, 11, 0)
+    assert np.array_equal(log0.actions.cpu().numpy(), a_0)
+    for k, (acts, t, m, rw) in enumerate(outs):
+        _, a_o, _, c_o = O.throughput_rollout(lgt.numpy(), 3, 11, 2 + k)
+        T = int(t)
+        assert T == a_o.shape[0]
+        assert np.array_equal(acts[:, :T].cpu().numpy(), a_o.T)
+    assert not torch.equal(outs[0][2], outs[1][2])  # the fill ran again on the new removal sets

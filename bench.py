@@ -185,6 +185,23 @@ def roofline_obj(kernel, nbytes, ms, traffic=None):
             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "bytes_per_launch": nbytes, "avg_launch_ms": ms}
 
 
+def launch_ranks(n: int) -> int:
+    """`bench.py --gpus N` run directly: start the N ranks (one process per GPU) under
+    torch.distributed.run on 127.0.0.1 as child processes and return their exit status.
+    The parent has not initialised the GPU (no HIP call before this point)."""
+    import socket
+    import subprocess
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.run(cmd, env=env).returncode
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)

@@ -113,7 +113,10 @@ def measured_traffic(cfg: str, B: int):
         rec = json.load(open(path))
     except (OSError, ValueError):
         return None
-    if rec.get("config") == cfg and rec.get("batch") == B:
+    if "config" in rec:  # single-record form
+        rec = {rec["config"]: rec}
+    rec = rec.get(cfg, {})
+    if rec.get("batch") == B:
         return float(rec["hbm_bytes_per_launch"])
     return None
 

@@ -14,7 +14,7 @@ import os
 import shutil
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-ROOF_KERNEL = "k_gram_fill<5, float, true"  # any Gram storage type (fp32 exact or fp64)
+ROOF_KERNELS = {"c4": "k_gram_fill<5, ", "c2": "k_gram_fill<5, ", "c3": "k_gram_fill_wide<13, "}  # LSQ fill, any Gram type
 
 
 def short(name):
@@ -55,14 +55,23 @@ def main():
         dst.update(e)
     with open(os.path.join(args.out, f"pmc_{args.tag}.json"), "w") as f:
         json.dump(summary, f, indent=1)
-    roof = [(k, v) for k, v in summary["kernels"].items() if ROOF_KERNEL in k and "hbm_bytes_per_launch" in v]
+    roof = [(k, v) for k, v in summary["kernels"].items()
+            if ROOF_KERNELS[args.config] in k and "true" in k and "hbm_bytes_per_launch" in v]
     if roof:
         k, v = roof[0]
         rec = {"config": args.config, "batch": args.batch, "kernel": k, "avg_us": v.get("avg_us"),
                "hbm_bytes_per_launch": v["hbm_bytes_per_launch"], "FETCH_SIZE_KB": v["pmc"].get("FETCH_SIZE"),
                "WRITE_SIZE_KB": v["pmc"].get("WRITE_SIZE"), "source": f"profiles/pmc_{args.tag}.json",
                "command": args.cmd}
-        json.dump(rec, open(os.path.join(args.out, "fill_traffic.json"), "w"), indent=1)
+        path = os.path.join(args.out, "fill_traffic.json")
+        try:
+            allrec = json.load(open(path))
+        except (OSError, ValueError):
+            allrec = {}
+        if "config" in allrec:  # older single-record form
+            allrec = {allrec["config"]: allrec}
+        allrec[args.config] = rec
+        json.dump(allrec, open(path, "w"), indent=1)
         print(json.dumps(rec))
 
 

@@ -21,7 +21,7 @@ if os.environ.get("SPAI_LIB_VARIANT"):  # A/B timing of kernel variants built un
 SPAI_OK, SPAI_ERR_INVALID, SPAI_ERR_HIP, SPAI_ERR_UNSUPPORTED = 0, 1, 2, 3
 FILL_COPY, FILL_LSQ = 0, 1
 DTYPE_F32, DTYPE_F64 = 0, 1
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 _c_i32, _c_i64, _c_u64, _c_sz, _c_p = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_size_t, ctypes.c_void_p
 
@@ -37,8 +37,10 @@ SIGNATURES = {
     "spai_rollout_workspace_bytes": (_c_sz, [_c_i32, _c_i32]),
     "spai_rollout_select": (ctypes.c_int, [_c_p, _c_i64, _c_i32, _c_i32, _c_p, _c_u64, _c_u64, _c_p, _c_i32, _c_i32,
                                            _c_i32, _c_p, _c_i32, _c_p, _c_p, _c_sz, _c_p]),
+    "spai_rollout_merge": (ctypes.c_int, [_c_p, _c_i64, _c_i32, _c_i32, _c_p, _c_i32, _c_i32, _c_p, _c_p, _c_sz,
+                                          _c_p]),
     "spai_rollout_sort": (ctypes.c_int, [_c_p, _c_i64, _c_i32, _c_i32, _c_p, _c_i32, _c_i32, _c_i64, _c_p, _c_p,
-                                         _c_sz, _c_p]),
+                                         _c_p, _c_sz, _c_p]),
     "spai_rollout_finish": (ctypes.c_int, [_c_p, _c_i64, _c_i32, _c_i32, _c_p, _c_p, _c_i32, _c_i32, _c_i64, _c_p,
                                            _c_p, _c_p, _c_p, _c_sz, _c_p]),
     "spai_rollout_order": (ctypes.c_int, [_c_p, _c_i64, _c_i32, _c_i32, _c_p, _c_p, _c_i64, _c_p, _c_p, _c_p, _c_p,

@@ -96,6 +96,35 @@ __device__ __forceinline__ spai_f2 gumbel_key2(spai_f2 logit, uint32_t w0, uint3
   return key + (spai_f2){0.0f, 0.0f};
 }
 
+// Deterministic e^x in fp32, bit-exact with oracle.det_expf: k = rint(x * log2 e) (fp32),
+// Cody-Waite r = x - k ln2 in two single-rounded FMAs, degree-7 Taylor Horner in fp32 FMAs,
+// 2^k by ldexp (exact: results stay normal).  x > 88.72 -> +inf, x < -87.33 -> 0.
+constexpr uint32_t kExpC[8] = {0x3f800000u, 0x3f800000u, 0x3f000000u, 0x3e2aaaabu,
+                               0x3d2aaaabu, 0x3c088889u, 0x3ab60b61u, 0x39500d01u};
+__device__ __forceinline__ float det_expf(float x) {
+#pragma clang fp contract(off)
+  if (x > 88.72f) return __uint_as_float(0x7f800000u);
+  if (x < -87.33f) return 0.0f;
+  const float k = __builtin_rintf(x * __uint_as_float(0x3fb8aa3bu));  // log2(e)
+  float r = __builtin_fmaf(-k, __uint_as_float(0x3f317200u), x);      // ln2 head (exact k * head)
+  r = __builtin_fmaf(-k, __uint_as_float(0x35bfbe8eu), r);            // ln2 tail
+  float p = __uint_as_float(kExpC[7]);
+#pragma unroll
+  for (int i = 6; i >= 0; --i) p = __builtin_fmaf(p, r, __uint_as_float(kExpC[i]));
+  return __builtin_ldexpf(p, (int)k);
+}
+
+// Exponential race (throughput sampler): action a arrives at t_a = q_a * r_a with
+// q_a = -ln u_a ~ Exp(1) and r_a = e^(l_E - l_a) (the inverse rate relative to the terminal
+// E, whose r is exactly 1), so t_a < t_E <=> key_a > key_E of the Gumbel keys l - ln q and
+// the arrival order is the Plackett-Luce (sequential sampling) order.
+__device__ __forceinline__ float arrival_q(uint32_t word) { return -det_logf(gumbel_u(word)); }
+__device__ __forceinline__ spai_f2 arrival_q2(uint32_t w0, uint32_t w1) {
+  return -det_logf2((spai_f2){gumbel_u(w0), gumbel_u(w1)});
+}
+// Trajectory-order key of an arrival time t >= 0: larger = earlier (ties: action ascending).
+__device__ __forceinline__ uint32_t arrival_ord(float t) { return ~__float_as_uint(t); }
+
 // Monotone map float -> uint32 (larger float => larger uint).
 __device__ __forceinline__ uint32_t orderable(float f) {
   const uint32_t u = __float_as_uint(f);

@@ -1,27 +1,31 @@
 // One-pass trajectory sampler for gfx950 (throughput mode) — replaces the T-step loop of
 // GFlowNet.sample_states (gflownet/gflownet.py:135-179) and Log.log (gflownet/log.py:24-89).
 //
-// Sampling without replacement until the terminal id E is drawn == the Plackett-Luce order
-// of the Gumbel keys key_a = l_a - ln(-ln u_a); the removed set is {a < E : key_a > key_E}
-// and the trajectory lists it by key descending (ties: action ascending), then E.
+// Sampling without replacement until the terminal id E is drawn == an exponential race:
+// action a arrives at t_a = q_a * r_a (q_a = -ln u_a ~ Exp(1), r_a = e^(l_E - l_a), r_E = 1);
+// the removed set is {a < E : t_a < t_E} and the trajectory lists it by t ascending (ties:
+// action ascending), then E.  (Equivalently the Gumbel keys l - ln q, ordered descending.)
 //
 // Ordering ~1e6 winners per sample is a SAMPLE SORT whose only global data movement is
 // one coalesced staging write and one gather of contiguous runs:
-//   k_presample  keys of a pseudo-random stratified subset of <= 65536 actions per sample
-//                (1.2 % of the Philox work at C4); winners kept in subset order.
+//   k_presample  arrival times of a pseudo-random stratified subset of <= 65536 actions per
+//                sample (1.2 % of the Philox work at C4); winners kept in subset order.  Its
+//                extra blocks precompute the per-action inverse rates r and weights
+//                w = e^(l - lmax) once per logits row (shared by every sample of the row).
 //   k_splitters  per sample: value-linear histogram quantiles of the sampled winner keys
 //                -> nb ~ est/4096 bucket splitters and a 4096-bin bucket lookup table.
-//   k_tile       one kTile (16384)-action tile of one sample per block: Philox4x32-10 +
-//                deterministic fp32 keys (in registers), removal bitmap words, the fp64
-//                mass of the untouched actions, bucket histogram with in-bucket ranks, and
-//                the tile's winners written grouped by bucket through LDS windows as one
-//                contiguous 8 B record stream + 4 B logit stream; per-(bucket, tile) runs
-//                in a bucket-major table (one contiguous row per bucket).
+//   k_tile       one kTile (16384)-action tile of one sample per block (the samples of a
+//                tile share an XCD and its L2): Philox4x32-10 + deterministic fp32 arrival
+//                times (in registers), removal bitmap words, the fp64 mass of the untouched
+//                actions, bucket histogram with in-bucket ranks, and the tile's winners
+//                written grouped by bucket through LDS windows as one contiguous 8 B record
+//                stream + 4 B weight stream; per-(bucket, tile) runs in a bucket-major table
+//                (one contiguous row per bucket).
 //   k_bscan      per sample: bucket starts, winner count, untouched mass, T.
 //   k_sort2      persistent; per bucket: one-round-trip gather of its runs (one per tile)
-//                into registers, value-linear sub-buckets + rank counting in LDS, fp32
-//                weights w = exp(l - lmax), fp64 in-bucket suffix sums.  Outputs stored
-//                during the next bucket.  Buckets above the LDS capacity: k_sort2_big.
+//                into registers, value-linear sub-buckets + rank counting in LDS, fp64
+//                in-bucket suffix sums of the weights.  Outputs stored during the next
+//                bucket.  Buckets above the LDS capacity: k_sort2_big.
 //   k_wscan      per sample suffix over the bucket weight sums (fixed order).
 //   k_final      fwd_probs = w / (W_rest + later buckets + in-bucket suffix).
 //   k_pad        terminal step, -1 / 1.0 padding up to T = max_b k_b + 1.
@@ -50,6 +54,7 @@ constexpr int kWin = KWIN;                 // records per LDS output window of k
 constexpr int kSampM = 65536;              // subset size (power of two, capped by E)
 constexpr int kSampNT = 256;
 constexpr int kSampCap = 32768;            // sampled winners behind the splitters
+constexpr int kMaxNsb = kSampM / kSampNT;  // presample blocks per sample (256)
 constexpr int kTarget = 4096;              // winners per bucket (target)
 constexpr int kMaxB = 2048;                // buckets per sample (11 bits in the LDS record)
 constexpr int kCap2 = 8192;               // LDS capacity of k_sort2 (records per bucket)
@@ -62,12 +67,13 @@ constexpr int kBins = 4096;                // splitter histogram / bucket lookup
 
 struct TrajWs {
   int32_t ntiles, M;
-  int32_t* ctl;           // zeroed per rollout: btot [B][kMaxB] | bigcnt, reserved [B] | tdev | lastbig
-  int32_t* bigcnt;        // number of oversized buckets (k_sort2 -> k_sort2_big); back to 0 after each order
-  int32_t* lastbig;       // bigcnt of the last order phase (kept for tests / diagnostics)
-  int32_t* biglist;       // [B][kMaxB] their flattened (sample, bucket) indices
-  int32_t* btot;          // [B][kMaxB] winners per bucket (atomic sums over tiles)
+  int32_t* ctl;           // zeroed per rollout: bigcnt | tdev | lastbig | pad
+  int32_t* bigcnt;        // number of oversized buckets (k_sort2 -> k_sort2_big); back to 0 after each sort
   int32_t* tdev;
+  int32_t* lastbig;       // bigcnt of the last sort (kept for tests / diagnostics)
+  int32_t* biglist;       // [B][kMaxB] their flattened (sample, bucket) indices
+  double* xch;            // exchange array: [B][2][kMaxB] bucket weight sums | winner counts, then [B]
+                          // residual partials (the caller's slot); a part fills its own buckets
   int32_t* samp_cnt;      // [B][M / kSampNT] winners per presample block
   uint32_t* samp;         // [B][M] winner keys (orderable), block-compacted
   int32_t* nb;            // [B] buckets
@@ -75,18 +81,21 @@ struct TrajWs {
   uint16_t* lut;          // [B][kBins] bucket lookup table
   uint32_t* lut_base;     // [B][2] (min key, shift) of the table
   uint64_t* staging;      // [B][ntiles][kTile] (~ord << 32 | action), grouped by bucket per tile
-  float* stlog;           // [B][ntiles][kTile] logit of each staged record
+  float* stw;             // [B][ntiles][kTile] weight w of each staged record
+  int64_t wstride;        // row stride of rr / ww: E + 1 rounded up to 4 (16-byte aligned rows)
+  float* rr;              // [B][wstride] inverse rates r_a = e^(l_E - l_a) (row 0 only: shared logits)
+  float* ww;              // [B][wstride] weights w_a = e^(l_a - lmax)
   uint32_t* runs;         // [B][kMaxB][ntiles] run of bucket k in tile t: offset << 16 | count (k_tile)
+  double* tbw;            // [B][kMaxB][ntiles] weight sum of that run
   double* tile_wrest;     // [B][ntiles]
   int32_t* bstart;        // [B][kMaxB + 1]
   double* wrest;          // [B]
-  double* bwsum;          // [B][kMaxB]
   double* bwsuf;          // [B][kMaxB]
-  float* out_w;           // [B][E]
-  float* out_suf;         // [B][E] in-bucket suffix sums (one rounding of an fp64 sum of positives)
   uint64_t* scratch;      // [B][E] oversized-bucket radix scratch
   size_t total_bytes;
 };
+
+static size_t xch_doubles(int32_t B) { return (size_t)B * 2 * kMaxB + B; }
 
 static void traj_ws(void* base, int32_t E, int32_t B, TrajWs* w) {
   Carve c(base);
@@ -95,12 +104,12 @@ static void traj_ws(void* base, int32_t E, int32_t B, TrajWs* w) {
   while (M * 2 <= E && M * 2 <= kSampM) M *= 2;
   w->M = M;
   const int nsb = (M + kSampNT - 1) / kSampNT;
-  w->ctl = c.take<int32_t>((size_t)B * kMaxB + B + 2);
-  w->btot = w->ctl;
-  w->tdev = w->ctl + (size_t)B * kMaxB + B;
-  w->lastbig = w->tdev + 1;
-  w->bigcnt = w->ctl + (size_t)B * kMaxB;  // first reserved slot: oversized buckets found by k_sort2
+  w->ctl = c.take<int32_t>(4);
+  w->bigcnt = w->ctl;
+  w->tdev = w->ctl + 1;
+  w->lastbig = w->ctl + 2;
   w->biglist = c.take<int32_t>((size_t)B * kMaxB);
+  w->xch = c.take<double>(xch_doubles(B));
   w->samp_cnt = c.take<int32_t>((size_t)B * nsb);
   w->samp = c.take<uint32_t>((size_t)B * M);
   w->nb = c.take<int32_t>(B);
@@ -108,15 +117,16 @@ static void traj_ws(void* base, int32_t E, int32_t B, TrajWs* w) {
   w->lut = c.take<uint16_t>((size_t)B * kBins);
   w->lut_base = c.take<uint32_t>((size_t)B * 2);
   w->staging = c.take<uint64_t>((size_t)B * w->ntiles * kTile);
-  w->stlog = c.take<float>((size_t)B * w->ntiles * kTile);
-  w->runs =c.take<uint32_t>((size_t)B * kMaxB * w->ntiles);
+  w->stw = c.take<float>((size_t)B * w->ntiles * kTile);
+  w->wstride = ((int64_t)E + 1 + 3) & ~(int64_t)3;
+  w->rr = c.take<float>((size_t)B * w->wstride);
+  w->ww = c.take<float>((size_t)B * w->wstride);
+  w->runs = c.take<uint32_t>((size_t)B * kMaxB * w->ntiles);
+  w->tbw = c.take<double>((size_t)B * kMaxB * w->ntiles);
   w->tile_wrest = c.take<double>((size_t)B * w->ntiles);
   w->bstart = c.take<int32_t>((size_t)B * (kMaxB + 1));
   w->wrest = c.take<double>(B);
-  w->bwsum = c.take<double>((size_t)B * kMaxB);
   w->bwsuf = c.take<double>((size_t)B * kMaxB);
-  w->out_w = c.take<float>((size_t)B * E);
-  w->out_suf = c.take<float>((size_t)B * E);
   w->scratch = c.take<uint64_t>((size_t)B * E);
   w->total_bytes = c.off;
 }
@@ -194,10 +204,20 @@ __device__ __forceinline__ uint32_t wave_or_u32(uint32_t v) {
   return v;
 }
 
-__device__ __forceinline__ float terminal_key(const float* lg, int32_t E, uint32_t bg, uint32_t st0, uint32_t st1,
-                                              uint32_t seed0, uint32_t seed1) {
+// Arrival time of the terminal: t_E = q_E (its inverse rate is exactly 1).
+__device__ __forceinline__ float terminal_t(int32_t E, uint32_t bg, uint32_t st0, uint32_t st1, uint32_t seed0,
+                                            uint32_t seed1) {
   const uint4 r = philox4x32_10((uint32_t)E >> 2, bg, st0, st1, seed0, seed1);
-  return gumbel_key(lg[E], pick_word(r, E & 3));
+  return arrival_q(pick_word(r, E & 3));
+}
+
+// w = e^(l - lmax) in fp32 to within ~1 ulp: l - lmax is exact in fp64, split into a float
+// head and a tiny tail, e^(hi + lo) = e^hi (1 + lo).
+__device__ __forceinline__ float action_weight(float l, float lm) {
+  const double d = (double)l - (double)lm;
+  const float hi = (float)d, lo = (float)(d - (double)hi);
+  const float e = det_expf(hi);
+  return fmaf(e, lo, e);
 }
 
 // Stratified pseudo-random subset: subset index i -> stratum (i * odd) mod M -> one action
@@ -249,42 +269,75 @@ __device__ __forceinline__ void stream_words(const uint64_t* sctr, uint32_t& st0
   }
 }
 
+constexpr int kWChunk = 1024;  // actions per rate/weight block of k_presample
 __global__ __launch_bounds__(kSampNT) void k_presample(const float* __restrict__ logits, int64_t bstride, int32_t E,
-                                                       int32_t M, uint32_t seed0, uint32_t seed1, uint32_t st0,
-                                                       uint32_t st1, const uint64_t* __restrict__ sctr,
+                                                       int32_t M, int32_t nsb, int32_t nsmp, uint32_t seed0,
+                                                       uint32_t seed1,
+                                                       uint32_t st0, uint32_t st1, const uint64_t* __restrict__ sctr,
                                                        int32_t sample_base,
                                                        uint32_t* __restrict__ samp, int32_t* __restrict__ samp_cnt,
-                                                       int32_t* __restrict__ ctl, int32_t nctl) {
-  const int b = blockIdx.y, tid = threadIdx.x;
+                                                       int32_t* __restrict__ ctl, int32_t nctl,
+                                                       const float* __restrict__ lmax, float* __restrict__ rr,
+                                                       float* __restrict__ ww, int64_t wstride) {
+  const int tid = threadIdx.x;
   stream_words(sctr, st0, st1);
   {  // the rollout's control block (bucket totals, oversized-bucket list count, tdev) starts at 0;
      // its first users (k_tile, k_sort2, k_bscan) run after this launch on the same stream
-    const int nthr = gridDim.x * gridDim.y * kSampNT;
-    for (int q = (blockIdx.y * gridDim.x + blockIdx.x) * kSampNT + tid; q < nctl; q += nthr) ctl[q] = 0;
+    const int nthr = gridDim.x * kSampNT;
+    for (int q = blockIdx.x * kSampNT + tid; q < nctl; q += nthr) ctl[q] = 0;
   }
+  const int B = nsmp;  // blocks [0, nsb * B): presample; then nwb blocks per logits row: rates and weights
+  if (blockIdx.x >= nsb * B) {  // inverse rates and weights of one chunk of a row (k_tile reads them)
+    const int q = blockIdx.x - nsb * B, nwb = (int)((wstride + kWChunk - 1) / kWChunk);
+    const int row = q / nwb;
+    const float* lg = logits + (int64_t)row * bstride;
+    constexpr int kPer = kWChunk / kSampNT;
+    const int64_t beg = (int64_t)(q % nwb) * kWChunk + tid;
+    const float lE = lg[E], lm = lmax[row];
+    float* r = rr + (int64_t)row * wstride;
+    float* w = ww + (int64_t)row * wstride;
+    float l[kPer];
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {  // every load in flight before the math
+      const int64_t i = beg + j * kSampNT;
+      l[j] = i <= E ? lg[i] : 0.0f;
+    }
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      const int64_t i = beg + j * kSampNT;
+      if (i <= E) {
+        r[i] = det_expf(lE - l[j]);
+        w[i] = action_weight(l[j], lm);
+      } else if (i < wstride) {  // row padding: never a winner, no mass
+        r[i] = __uint_as_float(0x7f800000u);
+        w[i] = 0.0f;
+      }
+    }
+    return;
+  }
+  const int b = blockIdx.x / nsb, blk = blockIdx.x % nsb;
   const float* lg = logits + (int64_t)b * bstride;
   const uint32_t bg = (uint32_t)(sample_base + b);
   __shared__ float s_tk;
   __shared__ int s_wc[kSampNT / 64];
-  if (tid == 0) s_tk = terminal_key(lg, E, bg, st0, st1, seed0, seed1);
+  if (tid == 0) s_tk = terminal_t(E, bg, st0, st1, seed0, seed1);
   __syncthreads();
-  const int i = blockIdx.x * kSampNT + tid;
+  const int i = blk * kSampNT + tid;
   int win = 0;
   uint32_t o = 0;
   if (i < M) {
     const int32_t a = subset_action(i, M, E);
     const uint4 r = philox4x32_10((uint32_t)a >> 2, bg, st0, st1, seed0, seed1);
-    const float key = gumbel_key(lg[a], pick_word(r, a & 3));
-    if (key > s_tk) {
+    const float t = arrival_q(pick_word(r, a & 3)) * det_expf(lg[E] - lg[a]);
+    if (t < s_tk) {
       win = 1;
-      o = orderable(key);
+      o = arrival_ord(t);
     }
   }
   int tot;
   const int pos = block_excl_scan<kSampNT>(win, s_wc, &tot);
-  const int nsb = gridDim.x;
-  if (win) samp[(int64_t)b * M + blockIdx.x * kSampNT + pos] = o;
-  if (tid == 0) samp_cnt[b * nsb + blockIdx.x] = tot;
+  if (win) samp[(int64_t)b * M + blk * kSampNT + pos] = o;
+  if (tid == 0) samp_cnt[b * nsb + blk] = tot;
 }
 
 // ------------------------------------------------------------------ k_splitters
@@ -297,8 +350,9 @@ __global__ __launch_bounds__(kSortNT) void k_splitters(int32_t E, int32_t M, int
                                                        int32_t* __restrict__ nb_out, uint32_t* __restrict__ spl,
                                                        uint16_t* __restrict__ lut, uint32_t* __restrict__ lut_base) {
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  __shared__ uint32_t s_smp[kSampCap];  // the sampled winner keys, compacted
   __shared__ int hist[kBins + 1];
-  __shared__ int sblk[1024 + 1];
+  __shared__ int sblk[kMaxNsb + 1];
   __shared__ int s_wc[kSortNT / 64];
   __shared__ uint32_t s_mn[kSortNT / 64], s_mx[kSortNT / 64];
   const int c = tid < nsb ? samp_cnt[b * nsb + tid] : 0;
@@ -310,15 +364,40 @@ __global__ __launch_bounds__(kSortNT) void k_splitters(int32_t E, int32_t M, int
   __syncthreads();
   const int ns = min(total, kSampCap);
   const uint32_t* sb = samp + (int64_t)b * M;
-  // pass 1: key range of the first ns sampled winners (wave per presample block)
+  // the first ns sampled winners, compacted into LDS in two halves with every load of a half in
+  // flight at once: wave w reads presample blocks w*kBPW .. w*kBPW + kBPW - 1 (kSampNT keys
+  // each, kLPB per lane); the key range comes from the registers
+  constexpr int kBPW = kMaxNsb / (kSortNT / 64), kLPB = kSampNT / 64, kHalf = kBPW / 2;
+  static_assert(kMaxNsb % (kSortNT / 64) == 0 && kSampNT % 64 == 0 && kBPW % 2 == 0, "k_splitters staging");
   uint32_t mn = 0xFFFFFFFFu, mx = 0u;
-  for (int k = wave; k < nsb && sblk[k] < ns; k += kSortNT / 64) {
-    const int cnt = min(sblk[k + 1], ns) - sblk[k];
-    for (int i = lane; i < cnt; i += 64) {
-      const uint32_t v = sb[k * kSampNT + i];
-      mn = min(mn, v);
-      mx = max(mx, v);
+#pragma unroll 1
+  for (int h = 0; h < 2; ++h) {
+    uint32_t v[kHalf * kLPB];
+    int pos[kHalf];
+    uint32_t ok = 0;
+#pragma unroll
+    for (int j = 0; j < kHalf; ++j) {
+      const int k = wave * kBPW + h * kHalf + j;
+      const int beg = k < nsb ? sblk[k] : ns, cnt = k < nsb ? min(sblk[k + 1], ns) - beg : 0;
+      pos[j] = beg;
+#pragma unroll
+      for (int q = 0; q < kLPB; ++q) {
+        const int i = lane + 64 * q;
+        const bool in = i < cnt;
+        v[j * kLPB + q] = in ? sb[k * kSampNT + i] : 0u;
+        ok |= (uint32_t)in << (j * kLPB + q);
+      }
     }
+#pragma unroll
+    for (int j = 0; j < kHalf; ++j)
+#pragma unroll
+      for (int q = 0; q < kLPB; ++q)
+        if ((ok >> (j * kLPB + q)) & 1u) {
+          const uint32_t x = v[j * kLPB + q];
+          mn = min(mn, x);
+          mx = max(mx, x);
+          s_smp[pos[j] + lane + 64 * q] = x;
+        }
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -339,11 +418,8 @@ __global__ __launch_bounds__(kSortNT) void k_splitters(int32_t E, int32_t M, int
   }
   const uint32_t range = ns > 0 ? mx - mn : 0u;
   const int shift = range >= (uint32_t)kBins ? 32 - __clz((int)(range >> 12)) : 0;  // (range >> shift) < kBins
-  // pass 2: histogram
-  for (int k = wave; k < nsb && sblk[k] < ns; k += kSortNT / 64) {
-    const int cnt = min(sblk[k + 1], ns) - sblk[k];
-    for (int i = lane; i < cnt; i += 64) atomicAdd(&hist[(sb[k * kSampNT + i] - mn) >> shift], 1);
-  }
+  // histogram of the staged keys
+  for (int p = tid; p < ns; p += kSortNT) atomicAdd(&hist[(s_smp[p] - mn) >> shift], 1);
   __syncthreads();
   // exclusive scan of the bins (4 per thread), in place
   {
@@ -403,16 +479,6 @@ __global__ __launch_bounds__(kSortNT) void k_splitters(int32_t E, int32_t M, int
   }
 }
 
-// w = exp(l - lmax) in fp32 to within ~1 ulp of the correctly rounded value: l - lmax is
-// exact in fp64, split into a float head and a tiny tail, exp(hi + lo) = exp(hi) (1 + lo).
-// (An fp64 exp costs ~30 us per rollout wherever it is placed.)
-__device__ __forceinline__ float winner_weight(float l, float lm) {
-  const double d = (double)l - (double)lm;
-  const float hi = (float)d, lo = (float)(d - (double)hi);
-  const float e = expf(hi);
-  return fmaf(e, lo, e);
-}
-
 #ifdef SPAI_PROF  // phase timing (variant builds only: make EXTRA=-DSPAI_PROF); slots 16*kernel + phase
 __device__ unsigned long long g_prof[64];
 __device__ __forceinline__ uint64_t prof_stamp() {
@@ -447,26 +513,29 @@ extern "C" int spai_debug_prof(unsigned long long* out, int reset) {
 #endif
 
 // ------------------------------------------------------------------ k_tile
-// Selection and grouping fused, one 16384-action tile of one sample per block: Gumbel keys
-// of the tile (16 actions per thread; keys and logits kept in registers), the removed bitmap, the rest mass
-// of the tile's non-winners, then the grouping steps on the register-resident winners:
-// bucket histogram, per-(bucket, tile) runs, and the winners re-written grouped by bucket
-// through LDS windows (whole cache lines out).  The splitter tables load while the keys are
-// computed, so the only exposed global trip is the logits read.
-constexpr int kTileG = kTile / (kGrpNT * 4);  // Philox groups (of 4 actions) per thread: 8
+// Selection and grouping fused, one 16384-action tile of one sample per block: arrival times
+// of the tile (16 actions per thread; times and weights kept in registers), the removed
+// bitmap, the rest mass of the tile's non-winners, then the grouping steps on the
+// register-resident winners: bucket histogram, per-(bucket, tile) runs, and the winners
+// re-written grouped by bucket through LDS windows (whole cache lines out).  The splitter
+// tables load while the times are computed, so the only exposed global trip is the read of
+// the tile's inverse rates and weights.  Block -> (tile, sample): the samples of one tile are
+// consecutive blocks of one XCD (bijective XCD remap), so the rate/weight rows are read from
+// HBM once per tile and served to the other samples by that XCD's L2.
+constexpr int kTileG = kTile / (kGrpNT * 4);  // Philox groups (of 4 actions) per thread: 4
+constexpr int kXcd = 8;
+__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
+  const int x = orig % kXcd, q = nwg / kXcd, r = nwg % kXcd;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + orig / kXcd;
+}
 __global__ __launch_bounds__(kGrpNT)
-void k_tile(const float* __restrict__ logits, int64_t bstride, int32_t E,
-                                                 int32_t ntiles, uint32_t seed0, uint32_t seed1, uint32_t st0,
-                                                 uint32_t st1, const uint64_t* __restrict__ sctr,
-                                                 int32_t sample_base, int32_t part, int32_t nparts,
-                                                 uint32_t* __restrict__ removed,
-                                                 int32_t words, const float* __restrict__ lmax,
-                                                 const int32_t* __restrict__ nb_, const uint32_t* __restrict__ spl_,
-                                                 const uint16_t* __restrict__ lut_,
-                                                 const uint32_t* __restrict__ lut_base,
-                                                 uint64_t* __restrict__ staging, float* __restrict__ stlog,
-                                                 uint32_t* __restrict__ runs, int32_t* __restrict__ btot,
-                                                 double* __restrict__ tile_wrest) {
+void k_tile(const float* __restrict__ rr, const float* __restrict__ ww, int64_t wstride, int64_t rowsel,
+            int32_t E, int32_t B, int32_t ntiles, uint32_t seed0, uint32_t seed1, uint32_t st0, uint32_t st1,
+            const uint64_t* __restrict__ sctr, int32_t sample_base, int32_t part, int32_t nparts,
+            uint32_t* __restrict__ removed, int32_t words, const int32_t* __restrict__ nb_,
+            const uint32_t* __restrict__ spl_, const uint16_t* __restrict__ lut_,
+            const uint32_t* __restrict__ lut_base, uint64_t* __restrict__ staging, float* __restrict__ stw,
+            uint32_t* __restrict__ runs, double* __restrict__ tbw, double* __restrict__ tile_wrest) {
   __shared__ uint64_t w_rec[kWin];  // one window of the grouped output
   __shared__ float w_log[kWin];
   __shared__ __attribute__((aligned(16))) uint32_t s_spl[kMaxB];
@@ -474,16 +543,22 @@ void k_tile(const float* __restrict__ logits, int64_t bstride, int32_t E,
   __shared__ __attribute__((aligned(16))) uint16_t s_lut[kBins];
   __shared__ int s_wc[kGrpNT / 64];
   __shared__ double s_wr[kGrpNT / 64];
-  const int b = blockIdx.y, tile = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+#ifdef KTILE_NOREMAP
+  const int wg = (blockIdx.x % (gridDim.x / B)) * B + blockIdx.x / (gridDim.x / B);  // sample-major order
+#else
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+#endif
+  const int b = wg % B, tile = wg / B, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   PROF_INIT
   stream_words(sctr, st0, st1);
-  const float* lg = logits + (int64_t)b * bstride;
+  const float* rrow = rr + (int64_t)b * rowsel * wstride;  // rowsel 0: one shared row
+  const float* wrow = ww + (int64_t)b * rowsel * wstride;
   const uint32_t bg = (uint32_t)(sample_base + b);
   const int nb = nb_[b];
   // buckets [k0, k1) are ordered by this part (the others only counted: the removal bitmap,
   // the bucket totals and the untouched mass cover every action in every part)
   const int k0 = part_lo(nb, part, nparts), k1 = part_lo(nb, part + 1, nparts);
-  // splitter tables (consumed only after the keys; their latency hides behind the Philox work)
+  // splitter tables (consumed only after the times; their latency hides behind the Philox work)
   static_assert((kBins * 2 == 512 * 16 && kMaxB * 4 == 512 * 16 && kGrpNT % 512 == 0) || kGrpNT == 512,
                 "prologue vector widths");
   for (int i = tid; i < 1024; i += kGrpNT) {
@@ -493,31 +568,36 @@ void k_tile(const float* __restrict__ logits, int64_t bstride, int32_t E,
       reinterpret_cast<uint4*>(s_spl)[i - 512] = reinterpret_cast<const uint4*>(spl_ + (int64_t)b * kMaxB)[i - 512];
   }
   for (int k = tid; k < nb; k += kGrpNT) s_off[k] = 0;
+  // per-bucket weight sums of the tile's winners as exact fixed point (integer LDS atomics: the
+  // result is independent of their order): w >= 2^-20 in units of 2^-47, smaller w in units of
+  // 2^-69 (a tile adds <= 2^14 terms, so neither overflows 64 bits; every w >= 2^-45 is exact).
+  // The two [kMaxB] u64 arrays live in the record window, unused until the placement.
+  static_assert(kWin * 8 >= 2 * kMaxB * 8, "fixed-point accumulators alias the record window");
+  uint64_t* s_fx = w_rec;
+  for (int k = tid; k < 2 * kMaxB; k += kGrpNT) s_fx[k] = 0ull;
   const uint32_t lmn = lut_base[2 * b];
   const int lsh = (int)lut_base[2 * b + 1];
-  const float lm = lmax[b];
   const int a_t = tile * kTile;  // first action of the tile
-  const bool al16 = (reinterpret_cast<uintptr_t>(lg) & 15u) == 0;  // rows of E+1 floats need not be
-  // all logits of the thread in flight at once (group g: actions a_t + g * (4 * kGrpNT) +
-  // 4 * tid + 0..3, coalesced float4); no barrier before the keys
-  float lvk[4 * kTileG];  // the logits stay in registers for the grouped logit stream
+  // all rates and weights of the thread in flight at once (group g: actions a_t + g * (4 *
+  // kGrpNT) + 4 * tid + 0..3, coalesced float4 from the 16-byte aligned rows; the padding
+  // past E reads r = inf, w = 0); no barrier before the times
+  float lvk[4 * kTileG];  // the weights stay in registers for the grouped weight stream
+  float rvk[4 * kTileG];
 #pragma unroll
   for (int g = 0; g < kTileG; ++g) {
     const int a0 = a_t + g * 4 * kGrpNT + 4 * tid;
-    float* lv = lvk + 4 * g;
-    if (al16 && a0 + 3 < E) {
-      const float4 v = *reinterpret_cast<const float4*>(lg + a0);
-      lv[0] = v.x;
-      lv[1] = v.y;
-      lv[2] = v.z;
-      lv[3] = v.w;
+    if (a0 < wstride) {
+      const float4 r4 = *reinterpret_cast<const float4*>(rrow + a0);
+      const float4 w4 = *reinterpret_cast<const float4*>(wrow + a0);
+      rvk[4 * g] = r4.x, rvk[4 * g + 1] = r4.y, rvk[4 * g + 2] = r4.z, rvk[4 * g + 3] = r4.w;
+      lvk[4 * g] = w4.x, lvk[4 * g + 1] = w4.y, lvk[4 * g + 2] = w4.z, lvk[4 * g + 3] = w4.w;
     } else {
 #pragma unroll
-      for (int s = 0; s < 4; ++s) lv[s] = a0 + s < E ? lg[a0 + s] : 0.0f;
+      for (int s = 0; s < 4; ++s) rvk[4 * g + s] = lvk[4 * g + s] = 0.0f;
     }
   }
-  // the terminal's key, redundantly per thread (one Philox call) instead of a barrier
-  const float tk = terminal_key(lg, E, bg, st0, st1, seed0, seed1);
+  // the terminal's arrival time, redundantly per thread (one Philox call) instead of a barrier
+  const float tE = terminal_t(E, bg, st0, st1, seed0, seed1);
   PROF(0)
   uint32_t ord[4 * kTileG];
   uint32_t win = 0;  // bit 4g + s: action a_t + g * 4 * kGrpNT + 4 * tid + s is a winner
@@ -525,22 +605,20 @@ void k_tile(const float* __restrict__ logits, int64_t bstride, int32_t E,
 #pragma unroll
   for (int g = 0; g < kTileG; ++g) {
     const int a0 = a_t + g * 4 * kGrpNT + 4 * tid;
-    const float* lv = lvk + 4 * g;
-    const uint4 rr = philox4x32_10((uint32_t)a0 >> 2, bg, st0, st1, seed0, seed1);
-    const spai_f2 k01 = gumbel_key2((spai_f2){lv[0], lv[1]}, rr.x, rr.y);
-    const spai_f2 k23 = gumbel_key2((spai_f2){lv[2], lv[3]}, rr.z, rr.w);
-    const float keys[4] = {k01.x, k01.y, k23.x, k23.y};
+    const uint4 ph = philox4x32_10((uint32_t)a0 >> 2, bg, st0, st1, seed0, seed1);
+    const spai_f2 t01 = arrival_q2(ph.x, ph.y) * (spai_f2){rvk[4 * g], rvk[4 * g + 1]};
+    const spai_f2 t23 = arrival_q2(ph.z, ph.w) * (spai_f2){rvk[4 * g + 2], rvk[4 * g + 3]};
+    const float ts[4] = {t01.x, t01.y, t23.x, t23.y};
     uint32_t nib = 0;
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       ord[4 * g + s] = 0u;
       if (a0 + s < E) {
-        const float key = keys[s];
-        if (key > tk) {
+        if (ts[s] < tE) {
           nib |= 1u << s;
-          ord[4 * g + s] = orderable(key);
+          ord[4 * g + s] = arrival_ord(ts[s]);
         } else {
-          wr += (double)__expf(lv[s] - lm);
+          wr += (double)lvk[4 * g + s];
         }
       }
     }
@@ -557,13 +635,34 @@ void k_tile(const float* __restrict__ logits, int64_t bstride, int32_t E,
   if (lane == 0) s_wr[wave] = wr;
   __syncthreads();  // splitter tables, zeroed histogram
   PROF(1)
-  // bucket histogram of the winners; each winner keeps its bucket and its rank inside the
-  // bucket (the histogram atomic's return; any order: the level-2 sort orders buckets fully)
+  if (tid == 0) {
+    double t = 0.0;
+#pragma unroll
+    for (int w = 0; w < kGrpNT / 64; ++w) t += s_wr[w];
+    tile_wrest[(int64_t)b * ntiles + tile] = t;
+  }
+  const int nbl = nb - 1;
+  // this part's winners: bucket k = nbl - #(splitters <= key) in [k0, k1) <=> spl[nbl - k1] <= key
+  // (when nbl - k1 >= 0) and key < spl[nbl - k0] (when nbl - k0 <= nb - 2); the other winners
+  // are only in the bitmap and the counts their own part stages
+  {
+    const int jlo = nbl - k1, jhi = nbl - k0;
+    const uint32_t slo = jlo >= 0 ? s_spl[jlo] : 0u, shi = jhi <= nb - 2 ? s_spl[jhi] : 0u;
+    const bool clo = jlo >= 0, chi = jhi <= nb - 2;
+    uint32_t mine = 0;
+#pragma unroll
+    for (int q = 0; q < 4 * kTileG; ++q)
+      mine |= (((win >> q) & 1u) && (!clo || slo <= ord[q]) && (!chi || ord[q] < shi)) ? 1u << q : 0u;
+    win = mine;
+  }
+  // bucket histogram of the part's winners; each winner keeps its bucket and its rank inside
+  // the bucket (the histogram atomic's return; any order: the level-2 sort orders buckets fully)
   static_assert(kMaxB <= (1 << 11) && kTile <= (1 << 21), "bucket | rank << 11 packing");
   // bucket of a winner's orderable key (buckets numbered in trajectory order, descending key):
-  // value-linear lookup table, then the splitters, for all the thread's slots at once: the table guesses of every slot are read
-  // together, then wave-uniform correction rounds over the splitters (usually one step and one
-  // check), so the LDS reads of the slots overlap instead of forming one dependent chain each
+  // value-linear lookup table, then the splitters, for all the thread's slots at once: the table
+  // guesses of every slot are read together, then wave-uniform correction rounds over the
+  // splitters (usually one step and one check), so the LDS reads of the slots overlap instead of
+  // forming one dependent chain each
   int bc[4 * kTileG];
 #pragma unroll
   for (int q = 0; q < 4 * kTileG; ++q) {
@@ -571,7 +670,6 @@ void k_tile(const float* __restrict__ logits, int64_t bstride, int32_t E,
     const uint32_t bin = o < lmn ? 0u : min((uint32_t)(kBins - 1), (o - lmn) >> lsh);
     bc[q] = s_lut[bin];
   }
-  const int nbl = nb - 1;
   bool more;
   do {
     more = false;
@@ -590,24 +688,23 @@ void k_tile(const float* __restrict__ logits, int64_t bstride, int32_t E,
     if ((win >> q) & 1u) {
       const int bk = nbl - bc[q];
       br[q] = (uint32_t)bk | ((uint32_t)atomicAdd(&s_off[bk], 1) << 11);
+      const float wq = lvk[q];
+      const bool big = wq >= 9.5367431640625e-07f;  // 2^-20
+      const uint64_t fx = (uint64_t)((double)wq * (big ? 140737488355328.0 : 590295810358705651712.0));
+      atomicAdd((unsigned long long*)&s_fx[bk + (big ? 0 : kMaxB)], (unsigned long long)fx);
     }
   }
   __syncthreads();
   PROF(2)
-  if (tid == 0) {
-    double t = 0.0;
-#pragma unroll
-    for (int w = 0; w < kGrpNT / 64; ++w) t += s_wr[w];
-    tile_wrest[(int64_t)b * ntiles + tile] = t;
-  }
-  // bucket offsets inside the tile (exclusive scan, kMaxB / kGrpNT buckets per thread)
+  // bucket offsets inside the tile (exclusive scan, kMaxB / kGrpNT buckets per thread; buckets
+  // of other parts count 0)
   constexpr int kQ = kMaxB / kGrpNT;
   int hv[kQ], loc = 0;
 #pragma unroll
   for (int q = 0; q < kQ; ++q) {
     const int k = tid * kQ + q;
     hv[q] = k < nb ? s_off[k] : 0;
-    loc += (k >= k0 && k < k1) ? hv[q] : 0;
+    loc += hv[q];
   }
   int tot;
   int run = block_excl_scan<kGrpNT>(loc, s_wc, &tot);
@@ -618,15 +715,15 @@ void k_tile(const float* __restrict__ logits, int64_t bstride, int32_t E,
 #pragma unroll
   for (int q = 0; q < kQ; ++q) {
     const int k = tid * kQ + q;
-    const bool mine = k >= k0 && k < k1;
-    if (k < nb) {
-      s_off[k] = mine ? run : 0xFFFF;  // other parts' winners are not staged (beyond every window)
-      if (mine) rcol[(int64_t)k * ntiles] = ((uint32_t)run << 16) | (uint32_t)hv[q];
-      if (hv[q]) atomicAdd(&btot[(int64_t)b * kMaxB + k], hv[q]);
+    if (k >= k0 && k < k1) {
+      s_off[k] = run;
+      rcol[(int64_t)k * ntiles] = ((uint32_t)run << 16) | (uint32_t)hv[q];
     }
-    run += mine ? hv[q] : 0;
+    run += hv[q];
+    if (k >= k0 && k < k1)  // the run's weight sum (k_bsum adds them over the tiles)
+      tbw[((int64_t)b * kMaxB + k) * ntiles + tile] =
+          (double)s_fx[k] * 7.105427357601002e-15 + (double)s_fx[kMaxB + k] * 1.6940658945086007e-21;
   }
-  if (tid == 0) s_off[nb] = tot;
   __syncthreads();
   PROF(3)
   // final tile-local position of every winner, two per VGPR
@@ -638,7 +735,7 @@ void k_tile(const float* __restrict__ logits, int64_t bstride, int32_t E,
     else pp[q >> 1] = pos;
   }
   uint64_t* st = staging + ((int64_t)b * ntiles + tile) * kTile;
-  float* sl = stlog + ((int64_t)b * ntiles + tile) * kTile;
+  float* sl = stw + ((int64_t)b * ntiles + tile) * kTile;
   // positional windows of kWin records staged in LDS, written out as whole cache lines
 #pragma unroll 1
   for (int w0 = 0; w0 < tot; w0 += kWin) {
@@ -666,30 +763,82 @@ void k_tile(const float* __restrict__ logits, int64_t bstride, int32_t E,
   PROF_END(32)
 }
 
+// ------------------------------------------------------------------ k_bsum
+// Per (sample, bucket) of this part, one block: the winner count and the weight sum over the
+// tiles (thread t adds tiles t, t + kBsumNT, ... in order, then a fixed butterfly per wave and
+// the waves in order) of the per-(bucket, tile) runs and run sums k_tile left, into the exchange
+// array xch[b][0][k] (weights) / xch[b][1][k] (counts); the other buckets are zeroed, so the
+// sum of the parts' arrays is the one-part array.  Also advances the device stream counter:
+// every k_presample / k_tile block has read it.
+constexpr int kBsumNT = 256;
+__global__ __launch_bounds__(kBsumNT) void k_bsum(int32_t ntiles, const int32_t* __restrict__ nb_,
+                                                  const uint32_t* __restrict__ runs, const double* __restrict__ tbw,
+                                                  double* __restrict__ xch, uint64_t* __restrict__ sctr,
+                                                  int32_t part, int32_t nparts) {
+  const int b = blockIdx.y, k = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (sctr && b == 0 && k == 0 && tid == 0) *sctr += 1;
+  const int nb = nb_[b];
+  double* xw = xch + (int64_t)b * 2 * kMaxB;
+  if (k >= nb) {  // beyond this sample's buckets: zero the rest of its rows (one block does it)
+    if (k == nb)
+      for (int j = nb + tid; j < kMaxB; j += kBsumNT) xw[j] = xw[kMaxB + j] = 0.0;
+    return;
+  }
+  if (k < part_lo(nb, part, nparts) || k >= part_lo(nb, part + 1, nparts)) {
+    if (tid == 0) xw[k] = xw[kMaxB + k] = 0.0;
+    return;
+  }
+  __shared__ double s_d[kBsumNT / 64];
+  __shared__ int s_c[kBsumNT / 64];
+  const int64_t row = ((int64_t)b * kMaxB + k) * ntiles;
+  double s = 0.0;
+  int c = 0;
+  for (int t = tid; t < ntiles; t += kBsumNT) {  // coalesced over the tiles, in order per thread
+    s += tbw[row + t];
+    c += (int)(runs[row + t] & 0xFFFFu);
+  }
+  s = wave_sum(s);
+  c = wave_sum(c);
+  if (lane == 0) {
+    s_d[wave] = s;
+    s_c[wave] = c;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    double t = 0.0;
+    int ct = 0;
+#pragma unroll
+    for (int w = 0; w < kBsumNT / 64; ++w) {
+      t += s_d[w];
+      ct += s_c[w];
+    }
+    xw[k] = t;
+    xw[kMaxB + k] = (double)ct;
+  }
+}
+
 // ------------------------------------------------------------------ k_bscan
-__global__ __launch_bounds__(1024) void k_bscan(int32_t E, int32_t ntiles, const float* __restrict__ logits,
-                                                int64_t bstride, const float* __restrict__ lmax,
-                                                const int32_t* __restrict__ nb_, const int32_t* __restrict__ btot,
-                                                const double* __restrict__ tile_wrest, int32_t* __restrict__ bstart,
-                                                int32_t* __restrict__ counts, double* __restrict__ wrest,
-                                                int32_t* __restrict__ tdev, uint64_t* __restrict__ sctr,
-                                                double* __restrict__ bwsum) {
+// Per sample, once the exchange array holds every part's buckets: bucket starts (trajectory
+// positions), winner count, T, the untouched mass W_rest (terminal included) and the mass of
+// all later buckets per bucket (fixed-order suffix).
+__global__ __launch_bounds__(1024) void k_bscan(int32_t E, int32_t ntiles, const float* __restrict__ ww,
+                                                int64_t wrow_stride, const int32_t* __restrict__ nb_,
+                                                const double* __restrict__ xch, const double* __restrict__ tile_wrest,
+                                                int32_t* __restrict__ bstart, int32_t* __restrict__ counts,
+                                                double* __restrict__ wrest, int32_t* __restrict__ tdev,
+                                                double* __restrict__ bwsuf) {
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  // every k_presample / k_tile block has read the stream id: the next rollout draws the next one
-  if (sctr && b == 0 && tid == 0) *sctr += 1;
-  // bucket weight sums start at 0: the order phase fills its part's buckets (the other parts'
-  // stay 0, so a sum over the parts reproduces the single-part array exactly)
-  for (int k = tid; k < kMaxB; k += 1024) bwsum[(int64_t)b * kMaxB + k] = 0.0;
   __shared__ int s_wc[16];
-  __shared__ double s_wr[16];
+  __shared__ double s_wr[16], s_wd[16];
   const int nb = nb_[b];
   double wr = 0.0;
   for (int t = tid; t < ntiles; t += 1024) wr += tile_wrest[(int64_t)b * ntiles + t];
   wr = wave_sum(wr);
   if (lane == 0) s_wr[wave] = wr;
-  const int32_t* bt = btot + (int64_t)b * kMaxB;
+  const double* xw = xch + (int64_t)b * 2 * kMaxB;
+  const double* xc = xw + kMaxB;
   const int k0 = 2 * tid, k1 = 2 * tid + 1;
-  const int h0 = k0 < nb ? bt[k0] : 0, h1 = k1 < nb ? bt[k1] : 0;
+  const int h0 = k0 < nb ? (int)xc[k0] : 0, h1 = k1 < nb ? (int)xc[k1] : 0;
   int tot;
   const int ex = block_excl_scan<1024>(h0 + h1, s_wc, &tot);
   int32_t* bs = bstart + (int64_t)b * (kMaxB + 1);
@@ -697,12 +846,25 @@ __global__ __launch_bounds__(1024) void k_bscan(int32_t E, int32_t ntiles, const
   if (k1 < nb) bs[k1] = ex + h0;
   if (tid == 0) {
     bs[nb] = tot;
-    double t = exp((double)logits[(int64_t)b * bstride + E] - (double)lmax[b]);  // the terminal stays available
+    double t = (double)ww[(int64_t)b * wrow_stride + E];  // the terminal stays available
 #pragma unroll
     for (int w = 0; w < 16; ++w) t += s_wr[w];
     wrest[b] = t;
     counts[b] = tot;
     atomicMax(tdev, tot + 1);
+  }
+  // bwsuf[k] = sum of the weights of all buckets after k: thread t owns the t-th chunk counted
+  // from the end (contiguous, fixed order)
+  const int per = (nb + 1023) / 1024;
+  const int hi_ = nb - min(tid * per, nb), lo_ = max(hi_ - per, 0);
+  double loc = 0.0;
+  for (int k = hi_ - 1; k >= lo_; --k) loc += xw[k];
+  double total;
+  double run = block_excl_scan_d<1024>(loc, s_wd, &total);
+  double* wp = bwsuf + (int64_t)b * kMaxB;
+  for (int k = hi_ - 1; k >= lo_; --k) {
+    wp[k] = run;
+    run += xw[k];
   }
 }
 
@@ -777,9 +939,9 @@ __device__ void big_bucket_sort(uint64_t* __restrict__ s0, uint64_t* __restrict_
 // Oversized bucket (the sampled splitters missed; rare): gather into scratch, exact
 // in-block radix in global memory, then the same outputs as the LDS path.
 __device__ __forceinline__ void big_bucket(const int n, const int ntiles, const int* s_pre, const int* s_loc,
-                                           const uint64_t* stb, const float* lg, const double lmax, int64_t* act_out,
-                                           float* w_out, float* suf_out, uint64_t* s0, uint64_t* s1,
-                                           double* wsum_out, int* s_wc, double* s_wd, uint32_t* s_red) {
+                                           const uint64_t* stb, const float* wrow, int64_t* act_out,
+                                           float* fwd_out, uint64_t* s0, uint64_t* s1, const double later,
+                                           int* s_wc, double* s_wd, uint32_t* s_red) {
   const int tid = threadIdx.x;
   for (int i = tid; i < n; i += kSortNT) {
     int lo = 0, hi = ntiles - 1;
@@ -796,17 +958,15 @@ __device__ __forceinline__ void big_bucket(const int n, const int ntiles, const 
   for (int c1e = n; c1e > 0; c1e -= kSortNT) {
     const int i = c1e - 1 - tid;
     const uint32_t a = i >= 0 ? (uint32_t)s0[i] : 0u;
-    const double w = i >= 0 ? exp((double)lg[a] - lmax) : 0.0;
+    const double w = i >= 0 ? (double)wrow[a] : 0.0;
     double t;
     const double exs = block_excl_scan_d<kSortNT>(w, s_wd, &t);
     if (i >= 0) {
       act_out[i] = (int64_t)a;
-      w_out[i] = (float)w;
-      suf_out[i] = (float)(carry + exs + w);
+      fwd_out[i] = (float)(w / (later + (carry + exs + w)));
     }
     carry += t;
   }
-  if (tid == 0) *wsum_out = carry;
 }
 
 // Level-2 sort, persistent: one resident block per CU walks the FLATTENED (sample, bucket)
@@ -815,8 +975,9 @@ __device__ __forceinline__ void big_bucket(const int n, const int ntiles, const 
 // the runs (one per select tile) are mapped into an LDS gather table and every record is
 // loaded into registers in one round trip; records are ranked inside value-linear
 // sub-buckets of ~0.5 record (almost always a direct placement) and re-laid in trajectory
-// order in LDS together with their weights; then fp64 in-bucket suffix sums and coalesced
-// stores.  The next bucket's run
+// order in LDS together with their weights; then fp64 in-bucket suffix sums, the step
+// probabilities fwd = w / (W_rest + later buckets + in-bucket suffix) and coalesced stores.
+// The next bucket's run
 // table is prefetched while the current one is processed (LDS-only barriers keep it in
 // flight).  Oversized buckets are left to k_sort2_big.
 __global__ __launch_bounds__(kSortNT) void k_sort2(int32_t E, int32_t B, int32_t ntiles,
@@ -824,16 +985,15 @@ __global__ __launch_bounds__(kSortNT) void k_sort2(int32_t E, int32_t B, int32_t
                                                    const int32_t* __restrict__ bstart,
                                                    const uint32_t* __restrict__ runs,
                                                    const uint64_t* __restrict__ staging,
-                                                   const float* __restrict__ stlog, const float* __restrict__ lmax_,
+                                                   const float* __restrict__ stw,
                                                    int64_t t_cap, int64_t* __restrict__ actions,
-                                                   float* __restrict__ out_w, float* __restrict__ out_suf,
-                                                   double* __restrict__ bwsum, int32_t* __restrict__ bigcnt,
+                                                   float* __restrict__ fwd, const double* __restrict__ wrest,
+                                                   const double* __restrict__ bwsuf, int32_t* __restrict__ bigcnt,
                                                    int32_t* __restrict__ biglist, int32_t part, int32_t nparts) {
   __shared__ uint64_t A[kCap2];  // low half: gather map; high half: actions awaiting store
   __shared__ float L[kCap2];     // weights in trajectory order
-  __shared__ float S[kCap2];     // suffix sums awaiting store
+  __shared__ float S[kCap2];     // step probabilities awaiting store
   __shared__ int s_sub[kMaxSub + 1];
-  __shared__ float s_lm[kMaxSamples];
   __shared__ int s_nbp[kMaxSamples + 1];
   __shared__ int s_wc[kSortNT / 64];
   __shared__ double s_wd[kSortNT / 64];
@@ -844,7 +1004,6 @@ __global__ __launch_bounds__(kSortNT) void k_sort2(int32_t E, int32_t B, int32_t
     const int v = part_lo(nbb, part + 1, nparts) - part_lo(nbb, part, nparts);
     int tot;
     const int ex = block_excl_scan<kSortNT>(v, s_wc, &tot);
-    if (tid < B) s_lm[tid] = lmax_[tid];
     if (tid < B) s_nbp[tid] = ex;
     if (tid == 0) s_nbp[B] = tot;
   }
@@ -853,21 +1012,24 @@ __global__ __launch_bounds__(kSortNT) void k_sort2(int32_t E, int32_t B, int32_t
   const int t0 = 2 * tid, t1 = 2 * tid + 1;
   // bucket f: sample, bucket index, start/size, and the count and tile-local offset of its
   // runs in tiles t0, t1
-  auto fetch = [&](int f, int& bb, int& kk, int& s0, int& s1, uint32_t& r0, uint32_t& r1) {
+  auto fetch = [&](int f, int& bb, int& kk, int& s0, int& s1, uint32_t& r0, uint32_t& r1, double& lt) {
     r0 = r1 = 0u;
     bb = kk = s0 = s1 = 0;
+    lt = 0.0;
     if (f < total) {
       while (s_nbp[bb + 1] <= f) ++bb;
       kk = f - s_nbp[bb] + part_lo(nb_[bb], part, nparts);
       const int32_t* bs = bstart + (int64_t)bb * (kMaxB + 1);
       s0 = bs[kk];
       s1 = bs[kk + 1];
+      lt = wrest[bb] + bwsuf[(int64_t)bb * kMaxB + kk];  // mass of the untouched actions + later buckets
       const uint32_t* rr = runs + ((int64_t)bb * kMaxB + kk) * ntiles;  // [b][bucket][tile]
       if (t0 < ntiles) r0 = rr[t0];
       if (t1 < ntiles) r1 = rr[t1];
     }
   };
   int nxb, nxk, nxs0, nxs1;
+  double nxl;
   uint32_t r0, r1;  // packed runs (offset << 16 | count) of the next bucket in tiles t0, t1
   int* dlt = reinterpret_cast<int*>(A);
   uint32_t* a_out = reinterpret_cast<uint32_t*>(A) + kCap2;
@@ -876,20 +1038,16 @@ __global__ __launch_bounds__(kSortNT) void k_sort2(int32_t E, int32_t B, int32_t
   // in the (in-order) vmcnt, and every wait on those loads would wait for them.
   int pv_n = 0;
   int64_t* pv_act = nullptr;
-  float *pv_w = nullptr, *pv_suf = nullptr;
-  double* pv_bw = nullptr;
-  double pv_wsum = 0.0;
+  float* pv_fwd = nullptr;
   auto flush = [&]() {
 #pragma unroll
     for (int j = 0; j < kCap2 / kSortNT; ++j) {
       const int i = j * kSortNT + tid;
       if (i < pv_n) {
         pv_act[i] = (int64_t)a_out[i];
-        pv_w[i] = L[i];
-        pv_suf[i] = S[i];
+        pv_fwd[i] = S[i];
       }
     }
-    if (tid == 0 && pv_n) *pv_bw = pv_wsum;
     pv_n = 0;
   };
   // gather map of a bucket (in A, free until the scatter): record i sits at staging offset
@@ -906,7 +1064,7 @@ __global__ __launch_bounds__(kSortNT) void k_sort2(int32_t E, int32_t B, int32_t
       for (int i = 0; i < c1; ++i) dlt[ex + c0 + i] = d1;
     }
   };
-  fetch(blockIdx.x, nxb, nxk, nxs0, nxs1, r0, r1);
+  fetch(blockIdx.x, nxb, nxk, nxs0, nxs1, r0, r1, nxl);
   // retire the first fetch here: the loop header then has no load pending on either path,
   // so the map build below never waits behind the previous bucket's stores
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
@@ -914,19 +1072,19 @@ __global__ __launch_bounds__(kSortNT) void k_sort2(int32_t E, int32_t B, int32_t
 #pragma unroll 1
   for (int f = blockIdx.x; f < total; f += gridDim.x) {
     const int b = nxb, k = nxk, s = nxs0, n = nxs1 - nxs0;
+    const double later = nxl;
     build_map();
     // the next bucket's run table is in flight during the gather (whose wait retires it)
-    fetch(f + gridDim.x, nxb, nxk, nxs0, nxs1, r0, r1);
+    fetch(f + gridDim.x, nxb, nxk, nxs0, nxs1, r0, r1, nxl);
     lds_barrier();
     PROF(0)
     if (n == 0 || n > kCap2) {
-      if (n == 0 && tid == 0) bwsum[(int64_t)b * kMaxB + k] = 0.0;
       if (n > kCap2 && tid == 0) biglist[atomicAdd(bigcnt, 1)] = (b << 16) | k;  // for k_sort2_big (rare)
       __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): retire the fetch (see above)
       continue;
     }
     const uint64_t* stb = staging + (int64_t)b * ntiles * kTile;
-    const float* slb = stlog + (int64_t)b * ntiles * kTile;
+    const float* slb = stw + (int64_t)b * ntiles * kTile;
     constexpr int kPer = kCap2 / kSortNT;
     // flat gather: every record of the bucket in flight at once (one round trip)
     int dv[kPer];
@@ -948,11 +1106,6 @@ __global__ __launch_bounds__(kSortNT) void k_sort2(int32_t E, int32_t B, int32_t
     // the loop header does not wait behind this bucket's stores
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
     flush();  // the previous bucket's outputs (drain during this bucket's LDS phases)
-    {
-      const float lm = s_lm[b];
-#pragma unroll
-      for (int j = 0; j < kPer; ++j) lw[j] = winner_weight(lw[j], lm);  // logit -> weight
-    }
     uint32_t mn = 0xFFFFFFFFu, mx = 0u;
 #pragma unroll
     for (int j = 0; j < kPer; ++j) {
@@ -1065,7 +1218,7 @@ __global__ __launch_bounds__(kSortNT) void k_sort2(int32_t E, int32_t B, int32_t
       const int i = hi_ - 1 - j;
       if (i >= lo_) {
         run += (double)L[i];
-        S[i] = (float)run;
+        S[i] = (float)((double)L[i] / (later + run));
       }
     }
 #pragma unroll
@@ -1075,10 +1228,7 @@ __global__ __launch_bounds__(kSortNT) void k_sort2(int32_t E, int32_t B, int32_t
     }
     pv_n = n;
     pv_act = actions + (int64_t)b * t_cap + s;
-    pv_w = out_w + (int64_t)b * E + s;
-    pv_suf = out_suf + (int64_t)b * E + s;
-    pv_bw = bwsum + (int64_t)b * kMaxB + k;
-    pv_wsum = wsum;
+    pv_fwd = fwd + (int64_t)b * t_cap + s;
     lds_barrier();  // LDS reuse by the next bucket
     PROF(9)
   }
@@ -1092,11 +1242,12 @@ __global__ __launch_bounds__(kSortNT) void k_sort2_big(int32_t E, int32_t B, int
                                                        const int32_t* __restrict__ bstart,
                                                        const uint32_t* __restrict__ runs,
                                                        const uint64_t* __restrict__ staging,
-                                                       const float* __restrict__ logits, int64_t bstride,
-                                                       const float* __restrict__ lmax_, int64_t t_cap,
-                                                       int64_t* __restrict__ actions, float* __restrict__ out_w,
-                                                       float* __restrict__ out_suf, uint64_t* __restrict__ scratch,
-                                                       double* __restrict__ bwsum, const int32_t* __restrict__ bigcnt,
+                                                       const float* __restrict__ ww, int64_t wrow_stride,
+                                                       int64_t t_cap,
+                                                       int64_t* __restrict__ actions, float* __restrict__ fwd,
+                                                       const double* __restrict__ wrest,
+                                                       const double* __restrict__ bwsuf, uint64_t* __restrict__ scratch,
+                                                       const int32_t* __restrict__ bigcnt,
                                                        const int32_t* __restrict__ biglist) {
   __shared__ int s_pre[kMaxTiles + 1];
   __shared__ int s_loc[kMaxTiles];
@@ -1130,78 +1281,36 @@ __global__ __launch_bounds__(kSortNT) void k_sort2_big(int32_t E, int32_t B, int
     if (tid == 0) s_pre[ntiles] = tot;
     __syncthreads();
     int64_t* act_out = actions + (int64_t)b * t_cap + s;
-    big_bucket(n, ntiles, s_pre, s_loc, staging + (int64_t)b * ntiles * kTile, logits + (int64_t)b * bstride,
-               (double)lmax_[b], act_out, out_w + (int64_t)b * E + s, out_suf + (int64_t)b * E + s,
-               scratch + (int64_t)b * E + s, reinterpret_cast<uint64_t*>(act_out), bwsum + (int64_t)b * kMaxB + k,
-               s_wc, s_wd, s_red);
+    big_bucket(n, ntiles, s_pre, s_loc, staging + (int64_t)b * ntiles * kTile, ww + (int64_t)b * wrow_stride,
+               act_out, fwd + (int64_t)b * t_cap + s, scratch + (int64_t)b * E + s, reinterpret_cast<uint64_t*>(act_out),
+               wrest[b] + bwsuf[(int64_t)b * kMaxB + k], s_wc, s_wd, s_red);
     __syncthreads();
   }
-}
-
-// bwsuf[k] = sum of the weights of all buckets after k (exclusive suffix, fixed order).
-// Also retires the oversized-bucket list of this order phase: k_sort2_big (the only reader)
-// ran before this launch on the same stream, so the count goes back to 0 and a second order
-// call on the same select (k_sort2 appends to the list) starts from an empty list.
-__global__ __launch_bounds__(1024) void k_wscan(const int32_t* __restrict__ nb_, const double* __restrict__ bwsum,
-                                                double* __restrict__ bwsuf, int32_t* __restrict__ bigcnt,
-                                                int32_t* __restrict__ lastbig) {
-  const int b = blockIdx.x, tid = threadIdx.x;
-  if (b == 0 && tid == 0) {
-    *lastbig = *bigcnt;
-    *bigcnt = 0;
-  }
-  __shared__ double sd[16];
-  const int nb = nb_[b];
-  const int per = (nb + 1023) / 1024;
-  const int hi_ = nb - min(tid * per, nb), lo_ = max(hi_ - per, 0);
-  const double* ws = bwsum + (int64_t)b * kMaxB;
-  double* wp = bwsuf + (int64_t)b * kMaxB;
-  double loc = 0.0;
-  for (int k = hi_ - 1; k >= lo_; --k) loc += ws[k];
-  double total;
-  double run = block_excl_scan_d<1024>(loc, sd, &total);
-  for (int k = hi_ - 1; k >= lo_; --k) {
-    wp[k] = run;
-    run += ws[k];
-  }
-}
-
-// fwd_probs = w / (W_rest + later buckets + in-bucket suffix), one block per bucket.
-__global__ __launch_bounds__(kFinNT) void k_final(int32_t E, const int32_t* __restrict__ nb_,
-                                                  const int32_t* __restrict__ bstart,
-                                                  const double* __restrict__ bwsuf, const float* __restrict__ out_w,
-                                                  const float* __restrict__ out_suf,
-                                                  const double* __restrict__ wrest, int64_t t_cap,
-                                                  float* __restrict__ fwd, int32_t part, int32_t nparts) {
-  const int k = blockIdx.x, b = blockIdx.y;
-  const int nb = nb_[b];
-  if (k < part_lo(nb, part, nparts) || k >= part_lo(nb, part + 1, nparts)) return;
-  const int32_t* bs = bstart + (int64_t)b * (kMaxB + 1);
-  const int s = bs[k], e = bs[k + 1];
-  const double later = wrest[b] + bwsuf[(int64_t)b * kMaxB + k];
-  const float* wb = out_w + (int64_t)b * E;
-  const float* sb = out_suf + (int64_t)b * E;
-  float* fb = fwd + (int64_t)b * t_cap;
-  for (int t = s + threadIdx.x; t < e; t += kFinNT) fb[t] = (float)((double)wb[t] / (later + (double)sb[t]));
 }
 
 // Terminal step and the -1 / 1.0 padding up to T (grid-stride: the padding of a sample
 // with few removals can be millions of steps).
 __global__ __launch_bounds__(kFinNT) void k_pad(int32_t E, const int32_t* __restrict__ counts,
                                                 const int32_t* __restrict__ tdev, const double* __restrict__ wrest,
-                                                const float* __restrict__ logits, int64_t bstride,
-                                                const float* __restrict__ lmax, int64_t t_cap,
+                                                const float* __restrict__ ww, int64_t wrow_stride, int64_t t_cap,
                                                 int64_t* __restrict__ actions, float* __restrict__ fwd,
-                                                int32_t* __restrict__ t_out, int32_t do_pad) {
+                                                int32_t* __restrict__ t_out, int32_t* __restrict__ bigcnt,
+                                                int32_t* __restrict__ lastbig, int32_t do_pad) {
   const int b = blockIdx.y;
   const int k = counts[b], T = *tdev;
-  if (t_out && b == 0 && blockIdx.x == 0 && threadIdx.x == 0) *t_out = T;
+  if (b == 0 && blockIdx.x == 0 && threadIdx.x == 0) {
+    if (t_out) *t_out = T;
+    // retire the oversized-bucket list of this sort (k_sort2_big, its only reader, ran before
+    // this launch on the same stream): a second sort on the same select starts from 0
+    *lastbig = *bigcnt;
+    *bigcnt = 0;
+  }
   if (!do_pad) return;  // the terminal step and the padding belong to the last part
   int64_t* ab = actions + (int64_t)b * t_cap;
   float* fb = fwd + (int64_t)b * t_cap;
   for (int t = k + blockIdx.x * kFinNT + threadIdx.x; t < T; t += gridDim.x * kFinNT) {
     if (t == k) {
-      const double wE = exp((double)logits[(int64_t)b * bstride + E] - (double)lmax[b]);
+      const double wE = (double)ww[(int64_t)b * wrow_stride + E];
       ab[t] = E;
       fb[t] = (float)(wE / wrest[b]);
     } else {
@@ -1243,12 +1352,14 @@ extern "C" size_t spai_rollout_workspace_bytes(int32_t E, int32_t B) {
 
 // Byte offset of a diagnostic / exchange array inside the rollout workspace (tests and the
 // multi-part exchange address it in the caller-owned buffer instead of hard-coding the carve):
-//   0 = int32 oversized buckets of the last order phase (k_sort2 -> k_sort2_big)
+//   0 = int32 oversized buckets of the last sort (k_sort2 -> k_sort2_big)
 //   1 = int32 T of the last rollout
-//   2 = fp64 [B][kMaxB] bucket weight sums (a part fills its own buckets, the rest stay 0)
+//   2 = fp64 exchange array: [B][2][kMaxB] bucket weight sums | bucket winner counts (a part
+//       fills its own buckets, the rest are 0), then [B] slots for the caller's residual partials
 //   3 = kMaxB (the row length of field 2), as a value, not an offset
 //   4 = int32 [B][kMaxB + 1] trajectory position of each bucket's first winner (bucket nb: count)
 //   5 = int32 [B] buckets of each sample
+//   6 = the number of fp64 values of field 2, as a value
 // -1 for a bad field or shape.
 extern "C" int64_t spai_rollout_ws_offset(int32_t E, int32_t B, int32_t field) {
   if (E <= 0 || B <= 0) return -1;
@@ -1258,51 +1369,87 @@ extern "C" int64_t spai_rollout_ws_offset(int32_t E, int32_t B, int32_t field) {
   switch (field) {
     case 0: return reinterpret_cast<char*>(w.lastbig) - base;
     case 1: return reinterpret_cast<char*>(w.tdev) - base;
-    case 2: return reinterpret_cast<char*>(w.bwsum) - base;
+    case 2: return reinterpret_cast<char*>(w.xch) - base;
     case 3: return kMaxB;
     case 4: return reinterpret_cast<char*>(w.bstart) - base;
     case 5: return reinterpret_cast<char*>(w.nb) - base;
+    case 6: return (int64_t)xch_doubles(B);
     default: return -1;
   }
+}
+
+static int select_args(const float* logits, const float* lmax, int32_t E, int32_t B, int64_t bstride,
+                       int32_t sample_base, int32_t part, int32_t nparts, const void* workspace,
+                       size_t workspace_bytes, TrajWs* w, const char* who) {
+  SPAI_CHECK_ARG(logits && lmax && workspace, "%s: null pointer", who);
+  SPAI_CHECK_ARG(E > 0 && B > 0 && bstride >= 0 && sample_base >= 0, "%s: bad shape", who);
+  SPAI_CHECK_ARG((int64_t)E <= (int64_t)kMaxTiles * kTile, "%s: E=%d too large", who, E);
+  SPAI_CHECK_ARG(B <= kMaxSamples, "%s: B=%d above %d", who, B, kMaxSamples);
+  SPAI_CHECK_ARG(nparts >= 1 && part >= 0 && part < nparts, "%s: part %d of %d", who, part, nparts);
+  traj_ws(const_cast<void*>(workspace), E, B, w);
+  SPAI_CHECK_ARG(workspace_bytes >= w->total_bytes, "%s: workspace too small (%zu < %zu)", who, workspace_bytes,
+                 w->total_bytes);
+  return SPAI_OK;
+}
+
+static void launch_merge(const TrajWs& w, int32_t E, int32_t B, int64_t bstride, int32_t* counts, hipStream_t s) {
+  k_bscan<<<B, 1024, 0, s>>>(E, w.ntiles, w.ww, bstride ? w.wstride : 0, w.nb, w.xch, w.tile_wrest, w.bstart,
+                             counts, w.wrest, w.tdev, w.bwsuf);
 }
 
 extern "C" int spai_rollout_select(const float* logits, int64_t bstride, int32_t E, int32_t B, const float* lmax,
                                    uint64_t seed, uint64_t stream_id, uint64_t* stream_ctr, int32_t sample_base,
                                    int32_t part, int32_t nparts, uint32_t* removed, int32_t words, int32_t* counts,
                                    void* workspace, size_t workspace_bytes, void* stream) {
-  SPAI_CHECK_ARG(logits && lmax && removed && counts && workspace, "spai_rollout_select: null pointer");
-  SPAI_CHECK_ARG(E > 0 && B > 0 && bstride >= 0 && sample_base >= 0, "spai_rollout_select: bad shape");
-  SPAI_CHECK_ARG((int64_t)E <= (int64_t)kMaxTiles * kTile, "spai_rollout_select: E=%d too large", E);
-  SPAI_CHECK_ARG(B <= kMaxSamples, "spai_rollout_select: B=%d above %d", B, kMaxSamples);
-  SPAI_CHECK_ARG(nparts >= 1 && part >= 0 && part < nparts, "spai_rollout_select: part %d of %d", part, nparts);
-  SPAI_CHECK_ARG(words == (E + 31) / 32, "spai_rollout_select: words must be ceil(E/32)");
   TrajWs w;
-  traj_ws(workspace, E, B, &w);
-  SPAI_CHECK_ARG(workspace_bytes >= w.total_bytes, "spai_rollout_select: workspace too small (%zu < %zu)",
-                 workspace_bytes, w.total_bytes);
+  const int st = select_args(logits, lmax, E, B, bstride, sample_base, part, nparts, workspace, workspace_bytes, &w,
+                             "spai_rollout_select");
+  if (st != SPAI_OK) return st;
+  SPAI_CHECK_ARG(removed && counts, "spai_rollout_select: null pointer");
+  SPAI_CHECK_ARG(words == (E + 31) / 32, "spai_rollout_select: words must be ceil(E/32)");
   hipStream_t s = (hipStream_t)stream;
   const uint32_t s0 = (uint32_t)seed, s1 = (uint32_t)(seed >> 32);
   const uint32_t t0 = (uint32_t)stream_id, t1 = (uint32_t)(stream_id >> 32);
   const int nsb = (w.M + kSampNT - 1) / kSampNT;
-  k_presample<<<dim3(nsb, B), kSampNT, 0, s>>>(logits, bstride, E, w.M, s0, s1, t0, t1, stream_ctr, sample_base,
-                                              w.samp, w.samp_cnt, w.ctl, B * kMaxB + B + 2);
+  const int nwb = (int)((w.wstride + kWChunk - 1) / kWChunk);  // rate/weight blocks per logits row
+  const int64_t rowsel = bstride ? 1 : 0;
+  k_presample<<<nsb * B + nwb * (bstride ? B : 1), kSampNT, 0, s>>>(
+      logits, bstride, E, w.M, nsb, B, s0, s1, t0, t1, stream_ctr, sample_base, w.samp, w.samp_cnt, w.ctl, 4, lmax,
+      w.rr, w.ww, w.wstride);
   SPAI_CHECK_LAUNCH();
   k_splitters<<<B, kSortNT, 0, s>>>(E, w.M, nsb, w.samp, w.samp_cnt, w.nb, w.spl, w.lut, w.lut_base);
   SPAI_CHECK_LAUNCH();
-  k_tile<<<dim3(w.ntiles, B), kGrpNT, 0, s>>>(logits, bstride, E, w.ntiles, s0, s1, t0, t1, stream_ctr,
-                                              sample_base, part, nparts, removed, words, lmax, w.nb, w.spl, w.lut,
-                                              w.lut_base, w.staging, w.stlog, w.runs, w.btot, w.tile_wrest);
+  k_tile<<<w.ntiles * B, kGrpNT, 0, s>>>(w.rr, w.ww, w.wstride, rowsel, E, B, w.ntiles, s0, s1, t0, t1, stream_ctr,
+                                         sample_base, part, nparts, removed, words, w.nb, w.spl, w.lut, w.lut_base,
+                                         w.staging, w.stw, w.runs, w.tbw, w.tile_wrest);
   SPAI_CHECK_LAUNCH();
-  k_bscan<<<B, 1024, 0, s>>>(E, w.ntiles, logits, bstride, lmax, w.nb, w.btot, w.tile_wrest, w.bstart,
-                             counts, w.wrest, w.tdev, stream_ctr, w.bwsum);
+  k_bsum<<<dim3(max_buckets(E) + 1, B), kBsumNT, 0, s>>>(w.ntiles, w.nb, w.runs, w.tbw, w.xch, stream_ctr, part,
+                                                         nparts);
+  SPAI_CHECK_LAUNCH();
+  if (nparts == 1) {
+    launch_merge(w, E, B, bstride, counts, s);
+    SPAI_CHECK_LAUNCH();
+  }
+  return SPAI_OK;
+}
+
+extern "C" int spai_rollout_merge(const float* logits, int64_t bstride, int32_t E, int32_t B, const float* lmax,
+                                  int32_t part, int32_t nparts, int32_t* counts, void* workspace,
+                                  size_t workspace_bytes, void* stream) {
+  TrajWs w;
+  const int st = select_args(logits, lmax, E, B, bstride, 0, part, nparts, workspace, workspace_bytes, &w,
+                             "spai_rollout_merge");
+  if (st != SPAI_OK) return st;
+  SPAI_CHECK_ARG(counts, "spai_rollout_merge: null pointer");
+  launch_merge(w, E, B, bstride, counts, (hipStream_t)stream);
   SPAI_CHECK_LAUNCH();
   return SPAI_OK;
 }
 
-static int order_args(const float* logits, const float* lmax, const void* actions, const void* workspace, int32_t E,
-                      int32_t B, int64_t t_cap, int32_t part, int32_t nparts, size_t workspace_bytes, TrajWs* w,
-                      const char* who) {
-  SPAI_CHECK_ARG(logits && lmax && actions && workspace, "%s: null pointer", who);
+static int order_args(const float* logits, const float* lmax, const void* actions, const void* fwd,
+                      const void* workspace, int32_t E, int32_t B, int64_t t_cap, int32_t part, int32_t nparts,
+                      size_t workspace_bytes, TrajWs* w, const char* who) {
+  SPAI_CHECK_ARG(logits && lmax && actions && fwd && workspace, "%s: null pointer", who);
   SPAI_CHECK_ARG(E > 0 && B > 0 && t_cap >= (int64_t)E + 1, "%s: bad shape (E=%d B=%d t_cap=%lld)", who, E, B,
                  (long long)t_cap);
   SPAI_CHECK_ARG((int64_t)E <= (int64_t)kMaxTiles * kTile, "%s: E=%d too large", who, E);
@@ -1314,21 +1461,21 @@ static int order_args(const float* logits, const float* lmax, const void* action
 }
 
 extern "C" int spai_rollout_sort(const float* logits, int64_t bstride, int32_t E, int32_t B, const float* lmax,
-                                 int32_t part, int32_t nparts, int64_t t_cap, int64_t* actions, void* workspace,
-                                 size_t workspace_bytes, void* stream) {
+                                 int32_t part, int32_t nparts, int64_t t_cap, int64_t* actions, float* fwd_probs,
+                                 void* workspace, size_t workspace_bytes, void* stream) {
   TrajWs w;
-  const int st = order_args(logits, lmax, actions, workspace, E, B, t_cap, part, nparts, workspace_bytes, &w,
-                            "spai_rollout_sort");
+  const int st = order_args(logits, lmax, actions, fwd_probs, workspace, E, B, t_cap, part, nparts, workspace_bytes,
+                            &w, "spai_rollout_sort");
   if (st != SPAI_OK) return st;
   hipStream_t s = (hipStream_t)stream;
   const int nbm = max_buckets(E);
   const int g2 = std::max(1, std::min((nbm + nparts - 1) / nparts * B, num_cus()));
-  k_sort2<<<g2, kSortNT, 0, s>>>(E, B, w.ntiles, w.nb, w.bstart, w.runs, w.staging, w.stlog, lmax, t_cap,
-                                 actions, w.out_w, w.out_suf, w.bwsum, w.bigcnt, w.biglist, part, nparts);
+  const int64_t wrs = bstride ? w.wstride : 0;
+  k_sort2<<<g2, kSortNT, 0, s>>>(E, B, w.ntiles, w.nb, w.bstart, w.runs, w.staging, w.stw, t_cap, actions, fwd_probs,
+                                 w.wrest, w.bwsuf, w.bigcnt, w.biglist, part, nparts);
   SPAI_CHECK_LAUNCH();
-  k_sort2_big<<<g2, kSortNT, 0, s>>>(E, B, w.ntiles, w.nb, w.bstart, w.runs, w.staging, logits, bstride,
-                                     lmax, t_cap, actions, w.out_w, w.out_suf, w.scratch, w.bwsum, w.bigcnt,
-                                     w.biglist);
+  k_sort2_big<<<g2, kSortNT, 0, s>>>(E, B, w.ntiles, w.nb, w.bstart, w.runs, w.staging, w.ww, wrs, t_cap, actions,
+                                     fwd_probs, w.wrest, w.bwsuf, w.scratch, w.bigcnt, w.biglist);
   SPAI_CHECK_LAUNCH();
   return SPAI_OK;
 }
@@ -1338,20 +1485,15 @@ extern "C" int spai_rollout_finish(const float* logits, int64_t bstride, int32_t
                                    int64_t* actions, float* fwd_probs, int32_t* t_out, void* workspace,
                                    size_t workspace_bytes, void* stream) {
   TrajWs w;
-  const int st = order_args(logits, lmax, actions, workspace, E, B, t_cap, part, nparts, workspace_bytes, &w,
-                            "spai_rollout_finish");
+  const int st = order_args(logits, lmax, actions, fwd_probs, workspace, E, B, t_cap, part, nparts, workspace_bytes,
+                            &w, "spai_rollout_finish");
   if (st != SPAI_OK) return st;
-  SPAI_CHECK_ARG(counts && fwd_probs, "spai_rollout_finish: null pointer");
+  SPAI_CHECK_ARG(counts, "spai_rollout_finish: null pointer");
   hipStream_t s = (hipStream_t)stream;
-  const int nbm = max_buckets(E);
-  k_wscan<<<B, 1024, 0, s>>>(w.nb, w.bwsum, w.bwsuf, w.bigcnt, w.lastbig);
-  SPAI_CHECK_LAUNCH();
-  k_final<<<dim3(nbm, B), kFinNT, 0, s>>>(E, w.nb, w.bstart, w.bwsuf, w.out_w, w.out_suf, w.wrest, t_cap, fwd_probs,
-                                          part, nparts);
-  SPAI_CHECK_LAUNCH();
   const int last = part == nparts - 1;
-  k_pad<<<dim3(last ? std::max(1, 1024 / B) : 1, B), kFinNT, 0, s>>>(E, counts, w.tdev, w.wrest, logits, bstride,
-                                                                     lmax, t_cap, actions, fwd_probs, t_out, last);
+  k_pad<<<dim3(last ? std::max(1, 1024 / B) : 1, B), kFinNT, 0, s>>>(E, counts, w.tdev, w.wrest, w.ww,
+                                                                     bstride ? w.wstride : 0, t_cap, actions,
+                                                                     fwd_probs, t_out, w.bigcnt, w.lastbig, last);
   SPAI_CHECK_LAUNCH();
   return SPAI_OK;
 }
@@ -1359,8 +1501,8 @@ extern "C" int spai_rollout_finish(const float* logits, int64_t bstride, int32_t
 extern "C" int spai_rollout_order(const float* logits, int64_t bstride, int32_t E, int32_t B, const float* lmax,
                                   const int32_t* counts, int64_t t_cap, int64_t* actions, float* fwd_probs,
                                   int32_t* t_out, void* workspace, size_t workspace_bytes, void* stream) {
-  const int st = spai_rollout_sort(logits, bstride, E, B, lmax, 0, 1, t_cap, actions, workspace, workspace_bytes,
-                                   stream);
+  const int st = spai_rollout_sort(logits, bstride, E, B, lmax, 0, 1, t_cap, actions, fwd_probs, workspace,
+                                   workspace_bytes, stream);
   if (st != SPAI_OK) return st;
   return spai_rollout_finish(logits, bstride, E, B, lmax, counts, 0, 1, t_cap, actions, fwd_probs, t_out, workspace,
                              workspace_bytes, stream);

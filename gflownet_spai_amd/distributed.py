@@ -5,8 +5,9 @@ Two ways to spread work:
   * columns (default of bench.py, the north star's split, strong scaling): every rank draws
     the same B candidates; rank r orders the r-th slice of every trajectory (rollout parts:
     a contiguous range of the presampled key buckets) and fills lines shard_lines(n, r, P) of
-    every candidate's M.  ONE all_reduce per step carries the parts' bucket weight sums and the
-    squared residual partials (``exchange_parts``); the chosen M is assembled with ONE
+    every candidate's M.  ONE all_reduce per step carries the parts' bucket weight sums and
+    winner counts and the squared residual partials (``exchange_parts``); the chosen M is
+    assembled with ONE
     all_gather of equal-size ELL blocks (``allgather_lines``).
   * candidates (weak scaling): rank r samples candidates with Philox sample ids
     r*B .. r*B+B-1 (``GFlowNet(sample_base=r*B)``); every candidate's trajectory, fill and
@@ -61,21 +62,17 @@ def gather_rewards(rewards: torch.Tensor, group=None) -> torch.Tensor:
     return out
 
 
-def exchange_parts(bucket_sums: torch.Tensor, res2: torch.Tensor, group=None,
-                   packed: torch.Tensor | None = None) -> torch.Tensor:
-    """The split rollout's one collective: sum the parts' bucket weight sums ([B, kMaxB] fp64,
-    each part non-zero on its own buckets only, so the sum is exact and equals the one-GPU
-    array) into ``bucket_sums`` in place, and the lines' squared residual partials [B]; returns
-    the summed residuals (a view of ``packed``, reused when given).  Packed into one buffer:
-    one all_reduce instead of two."""
-    nb = bucket_sums.numel()
-    if packed is None:
-        packed = torch.empty(nb + res2.numel(), dtype=torch.float64, device=bucket_sums.device)
-    packed[:nb].copy_(bucket_sums.reshape(-1))
-    packed[nb:].copy_(res2.reshape(-1))
-    dist.all_reduce(packed, op=dist.ReduceOp.SUM, group=group)
-    bucket_sums.copy_(packed[:bucket_sums.numel()].view_as(bucket_sums))
-    return packed[bucket_sums.numel():]
+def exchange_parts(xch: torch.Tensor, res2: torch.Tensor, group=None) -> torch.Tensor:
+    """The split rollout's one collective, in place on the rollout workspace's exchange array
+    (kernels.exchange_array: per-bucket weight sums and winner counts, each part non-zero on
+    its own buckets only, so the sum is exact and equals the one-GPU array; then B slots):
+    the lines' squared residual partials [B] go into the slots, one all_reduce sums
+    everything, and the summed residuals (a view of the slots) are returned."""
+    B = res2.numel()
+    slots = xch[xch.numel() - B:]
+    slots.copy_(res2.reshape(-1))
+    dist.all_reduce(xch, op=dist.ReduceOp.SUM, group=group)
+    return slots
 
 
 def gather_slices(actions: torch.Tensor, fwd: torch.Tensor, bounds: torch.Tensor, T: int, group=None):

@@ -188,8 +188,9 @@ class GFlowNet(nn.Module):
         return logits, alpha, lg, lmax, z
 
     # The throughput step in three phases, so a caller can capture the collective-free ones in
-    # HIP graphs (bench.py): begin = policy, select, sort, fill of this rank's lines; exchange =
-    # the split's one all_reduce (nothing on one GPU); end = fwd_probs, rewards, the Log.  No
+    # HIP graphs (bench.py): begin = policy, select, fill of this rank's lines; exchange = the
+    # split's one all_reduce (nothing on one GPU); end = merge (split only), sort of this rank's
+    # trajectory slice with its fwd_probs, terminal step / padding, rewards, the Log.  No
     # phase synchronises with the host; the Philox stream id lives on the device and the select
     # phase advances it, so a replayed graph draws a fresh rollout.
     def rollout_begin(self, s0) -> dict:
@@ -203,35 +204,34 @@ class GFlowNet(nn.Module):
         rank, world, group = self.shard if self.shard is not None else (0, 1, None)
         removed, counts, ws = kernels.rollout_select(lg, B, lmax, self.seed, 0, self.sample_base, self._ctr, rank,
                                                      world)
-        actions = kernels.rollout_sort(lg, B, lmax, ws, rank, world)
         lines = self.lines if self.shard is not None else (0, None)
         res2 = env.fill_partial(removed, *lines)
         return dict(s0=s0, B=B, E=E, logits=logits, alpha=alpha, lg=lg, lmax=lmax, removed=removed, counts=counts,
-                    ws=ws, actions=actions, res2_part=res2, part=(rank, world, group))
+                    ws=ws, res2_part=res2, part=(rank, world, group))
 
     def rollout_exchange(self, st: dict) -> None:
-        """ONE all_reduce over the split: the parts' bucket weight sums (disjoint supports: the
-        sum is exact and equals the one-GPU array) and the lines' squared residual partials.
-        The summed residuals land in the same buffer on every call with the same ``st`` (a
-        captured ``rollout_end`` graph keeps reading it)."""
+        """ONE all_reduce over the split, in place on the rollout workspace's exchange array:
+        the parts' bucket weight sums and winner counts (disjoint supports: the sum is exact and
+        equals the one-GPU array) and the lines' squared residual partials.  The summed
+        residuals are a view of that array (a captured ``rollout_end`` graph keeps reading it)."""
         rank, world, group = st["part"]
         if world == 1:
             st["res2"] = st["res2_part"]
             return
         from .distributed import exchange_parts
-        bs = kernels.bucket_sums(st["ws"], st["E"], st["B"])
-        if "packed" not in st:
-            st["packed"] = torch.empty(bs.numel() + st["B"], dtype=torch.float64, device=bs.device)
-        st["res2"] = exchange_parts(bs, st["res2_part"], group, st["packed"])
+        st["res2"] = exchange_parts(kernels.exchange_array(st["ws"], st["E"], st["B"]), st["res2_part"], group)
 
     def rollout_end(self, st: dict) -> Log:
         env = self.env
         rank, world, group = st["part"]
         B, E, lg, lmax, counts, ws = st["B"], st["E"], st["lg"], st["lmax"], st["counts"], st["ws"]
-        fwd, t_dev = kernels.rollout_finish(lg, B, lmax, counts, ws, st["actions"], rank, world)
+        if world > 1:  # counts, T and the bucket positions need every part's buckets
+            kernels.rollout_merge(lg, B, lmax, ws, rank, world, counts)
+        actions, fwd = kernels.rollout_sort(lg, B, lmax, ws, rank, world)
+        t_dev = kernels.rollout_finish(lg, B, lmax, counts, ws, actions, fwd, rank, world)
         rewards = env.rewards_from_res2(st["res2"], counts, st["alpha"])
         log = Log(st["s0"], self.backward_policy, self.total_flow, env)
-        log._set_rollout(st["logits"], st["actions"], fwd, t_dev, lmax=lmax)
+        log._set_rollout(st["logits"], actions, fwd, t_dev, lmax=lmax)
         if world > 1:
             log._set_part(rank, world, group, kernels.part_bounds(ws, E, B, rank, world))
         log.removed, log.counts = st["removed"], counts

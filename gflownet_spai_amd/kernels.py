@@ -75,7 +75,8 @@ def parity_step(lg: torch.Tensor, B: int, noise: torch.Tensor, lmax, chosen, act
 
 def rollout_select(lg: torch.Tensor, B: int, lmax: torch.Tensor, seed: int, stream_id: int, sample_base: int = 0,
                    stream_ctr: torch.Tensor | None = None, part: int = 0, nparts: int = 1, ws_tag: str = "rollout"):
-    """Phase 1 of the throughput rollout: removal bitmaps [B, ceil(E/32)] and counts [B].
+    """Phase 1 of the throughput rollout: removal bitmaps [B, ceil(E/32)] and counts [B] (for
+    nparts > 1 the counts are written by rollout_merge, after the exchange).
 
     stream_ctr: optional device uint64 (int64 tensor) holding the Philox stream id, advanced
     by one on the device (graph replays draw fresh rollouts); part/nparts: this process orders
@@ -118,19 +119,22 @@ def rollout_order(lg, B, lmax, counts, ws):
     return actions, fwd, t_dev
 
 
-def bucket_sums(ws: torch.Tensor, E: int, B: int) -> torch.Tensor:
-    """fp64 [B, kMaxB] view of the bucket weight sums inside a rollout workspace (the array the
-    parts of a split rollout sum before spai_rollout_finish)."""
-    off = _l().spai_rollout_ws_offset(E, B, 2)
-    kmax = _l().spai_rollout_ws_offset(E, B, 3)
-    if off < 0 or kmax <= 0:
+def exchange_array(ws: torch.Tensor, E: int, B: int) -> torch.Tensor:
+    """fp64 view of the exchange array inside a rollout workspace: [B][2][kMaxB] bucket weight
+    sums | winner counts (a part fills its own buckets, the rest are 0), then B slots the caller
+    uses for the residual partials.  The parts of a split rollout sum it (one all_reduce)
+    before rollout_merge."""
+    lib = _l()
+    off, n = lib.spai_rollout_ws_offset(E, B, 2), lib.spai_rollout_ws_offset(E, B, 6)
+    if off < 0 or n <= 0:
         raise ValueError("spai_rollout_ws_offset failed")
-    return ws[off:off + B * kmax * 8].view(torch.float64).view(B, kmax)
+    return ws[off:off + n * 8].view(torch.float64)
 
 
 def part_bounds(ws: torch.Tensor, E: int, B: int, part: int, nparts: int) -> torch.Tensor:
     """[B, 2] int64 trajectory slice [start, end) a part orders (device tensor, no sync; the last
-    part's end is E + 1: it also writes the terminal step and the padding)."""
+    part's end is E + 1: it also writes the terminal step and the padding).  Valid after
+    rollout_merge (or a one-part select)."""
     lib = _l()
     kmax = lib.spai_rollout_ws_offset(E, B, 3)
     o_bs, o_nb = lib.spai_rollout_ws_offset(E, B, 4), lib.spai_rollout_ws_offset(E, B, 5)
@@ -142,30 +146,47 @@ def part_bounds(ws: torch.Tensor, E: int, B: int, part: int, nparts: int) -> tor
     return torch.cat([start, end], 1)
 
 
+def _bstride(lg, E):
+    return 0 if lg.dim() == 1 else E + 1
+
+
+def rollout_merge(lg, B, lmax, ws, part: int, nparts: int, counts: torch.Tensor | None = None):
+    """Split rollout, after the parts' exchange arrays are summed: counts [B], T, the bucket
+    positions and the later-bucket masses.  Returns counts (int32 [B])."""
+    E = lg.shape[-1] - 1
+    if counts is None:
+        counts = torch.empty(B, dtype=torch.int32, device=lg.device)
+    with _timed("rollout_merge"):
+        st = _l().spai_rollout_merge(_lib.ptr(lg), _bstride(lg, E), E, B, _lib.ptr(lmax), part, nparts,
+                                     _lib.ptr(counts), _lib.ptr(ws), ws.numel(), _lib.stream_ptr(lg.device))
+    _lib.check(st, "spai_rollout_merge")
+    return counts
+
+
 def rollout_sort(lg, B, lmax, ws, part: int, nparts: int):
-    """Split order phase, step 1: sorts this part's buckets; returns the actions buffer
-    [B, E+1] (the part's trajectory slice written) — then sum bucket_sums(ws) over the parts."""
+    """Sorts this part's buckets: actions [B, E+1] and fwd_probs [B, E+1] with the part's
+    trajectory slice written (one-part select, or after rollout_merge)."""
     E = lg.shape[-1] - 1
     actions = torch.empty(B, E + 1, dtype=torch.int64, device=lg.device)
-    with _timed("rollout_sort"):
-        st = _l().spai_rollout_sort(_lib.ptr(lg), 0 if lg.dim() == 1 else E + 1, E, B, _lib.ptr(lmax), part, nparts,
-                                    E + 1, _lib.ptr(actions), _lib.ptr(ws), ws.numel(), _lib.stream_ptr(lg.device))
-    _lib.check(st, "spai_rollout_sort")
-    return actions
-
-
-def rollout_finish(lg, B, lmax, counts, ws, actions, part: int, nparts: int):
-    """Split order phase, step 2 (after the bucket sums are complete): fwd_probs of the part's
-    slice, the terminal step and padding on the last part.  Returns (fwd [B, E+1], T)."""
-    E = lg.shape[-1] - 1
     fwd = torch.empty(B, E + 1, dtype=torch.float32, device=lg.device)
+    with _timed("rollout_sort"):
+        st = _l().spai_rollout_sort(_lib.ptr(lg), _bstride(lg, E), E, B, _lib.ptr(lmax), part, nparts, E + 1,
+                                    _lib.ptr(actions), _lib.ptr(fwd), _lib.ptr(ws), ws.numel(),
+                                    _lib.stream_ptr(lg.device))
+    _lib.check(st, "spai_rollout_sort")
+    return actions, fwd
+
+
+def rollout_finish(lg, B, lmax, counts, ws, actions, fwd, part: int, nparts: int):
+    """Terminal step and padding (last part) and T (int32 [1] device tensor)."""
+    E = lg.shape[-1] - 1
     t_dev = torch.empty(1, dtype=torch.int32, device=lg.device)
     with _timed("rollout_finish"):
-        st = _l().spai_rollout_finish(_lib.ptr(lg), 0 if lg.dim() == 1 else E + 1, E, B, _lib.ptr(lmax),
-                                      _lib.ptr(counts), part, nparts, E + 1, _lib.ptr(actions), _lib.ptr(fwd),
-                                      _lib.ptr(t_dev), _lib.ptr(ws), ws.numel(), _lib.stream_ptr(lg.device))
+        st = _l().spai_rollout_finish(_lib.ptr(lg), _bstride(lg, E), E, B, _lib.ptr(lmax), _lib.ptr(counts), part,
+                                      nparts, E + 1, _lib.ptr(actions), _lib.ptr(fwd), _lib.ptr(t_dev),
+                                      _lib.ptr(ws), ws.numel(), _lib.stream_ptr(lg.device))
     _lib.check(st, "spai_rollout_finish")
-    return fwd, t_dev
+    return t_dev
 
 
 def actions_to_removed(actions_bt: torch.Tensor, E: int):

@@ -77,51 +77,54 @@ int spai_parity_step(const float* logits, int64_t bstride, int32_t E1, int32_t B
                      void* stream);
 
 /* ---------------------------------------------------------------- throughput rollout
- * Whole trajectories in one pass (replaces the T-step loop of gflownet.py:135-179):
- * Gumbel-top-k over key_a = l_a - ln(-ln u_a), u from Philox4x32-10 with counter
- * (a >> 2, sample_base + b, stream_lo, stream_hi) and key (seed_lo, seed_hi); the
- * removed set of sample b is {a < E : key_a > key_E}.  Distributionally identical to
- * the reference's sequential sampling without replacement; bit-exact to oracle/.
+ * Whole trajectories in one pass (replaces the T-step loop of gflownet.py:135-179) as an
+ * exponential race: action a arrives at t_a = q_a * r_a, q_a = -ln u_a (u from Philox4x32-10
+ * with counter (a >> 2, sample_base + b, stream_lo, stream_hi) and key (seed_lo, seed_hi)),
+ * r_a = e^(l_E - l_a) (r_E = 1); the removed set of sample b is {a < E : t_a < t_E} and the
+ * trajectory lists it by t ascending (ties: action ascending), i.e. the Gumbel keys
+ * l_a - ln q_a in descending order.  Distributionally identical to the reference's sequential
+ * sampling without replacement; bit-exact to oracle/ (arrival_times, throughput_rollout).
  *
- * Phase 1 (spai_rollout_select): writes removed[B][words] (words = ceil(E/32)),
- * counts[B] (= k_b, the number removed) and stages the winners in the workspace.
- * Phase 2 (spai_rollout_order): sorts each sample's winners by key descending (ties:
- * action ascending; a sample sort: phase 1 groups the winners of every 16384-action tile
- * by presampled key buckets, phase 2 sorts each bucket in LDS; no host round trip) and writes the
- * trajectory log in [B][t_cap] layout (t_cap >= E + 1, only the first T columns are
- * written, T = max_b k_b + 1 is stored to *t_out):
+ * Phase 1 (spai_rollout_select): writes removed[B][words] (words = ceil(E/32)), stages the
+ * winners in the workspace grouped by presampled time buckets, and (nparts = 1) counts[B]
+ * (= k_b, the number removed).
+ * Phase 2 (spai_rollout_sort, then spai_rollout_finish; spai_rollout_order = both): sorts
+ * each bucket in LDS and writes the trajectory log in [B][t_cap] layout (t_cap >= E + 1, only
+ * the first T columns are written, T = max_b k_b + 1 is stored to *t_out):
  *   actions[b][t] = t-th removed action, actions[b][k_b] = E, -1 up to T;
  *   fwd_probs[b][t] = w_{a_t} / (W_rest + sum_{s>=t} w_{a_s}), w = exp(l - lmax), W_rest =
  *   mass of the actions never removed (terminal included) = the masked-softmax probability
  *   of step t (policy.py:65-73, log.py:70), 1.0 after the terminal;
  * (log.py:67-87 semantics: the Log's actions [T,B] is the transpose).  lmax comes from
- * spai_logits_stats.  One workspace serves both phases of one rollout; the order phase may be
- * repeated on the same select (it is idempotent).
+ * spai_logits_stats (or the policy's k_max).  One workspace serves both phases of one rollout;
+ * phase 2 may be repeated on the same select (it is idempotent).
  *
  * stream_ctr (optional, device uint64): when non-null the Philox stream id is read from it
  * instead of `stream_id`, and the select phase adds 1 to it (a captured HIP graph of the
  * rollout then draws a fresh rollout on every replay).
  *
  * Parts (the multi-GPU split): the presampled splitters cut every sample's
- * winners into nb buckets in trajectory order; part p of nparts orders buckets
+ * winners into nb buckets in trajectory order; part p of nparts owns buckets
  * [nb*p/nparts, nb*(p+1)/nparts), i.e. one contiguous slice of every trajectory.  Every part
- * scans all E actions (removed, counts, T, the untouched mass and the bucket totals are
- * complete on every part); only its own winners are staged and sorted.  After
- * spai_rollout_sort the part has filled its buckets' weight sums in the workspace array
- * spai_rollout_ws_offset(E, B, 2) ([B][kMaxB] fp64, zero elsewhere); summing that array over
- * the parts (an all-reduce: x + 0 is exact, so the sum equals the one-part array bit for
- * bit) before spai_rollout_finish makes the part's fwd_probs identical to a one-part run.
- * spai_rollout_finish writes actions/fwd_probs of the part's slice only; the last part also
- * writes the terminal step and the padding; t_out is written by every part.
- * spai_rollout_order = sort + finish with nparts = 1. */
+ * draws all E actions (removed and the untouched mass are complete on every part), but only
+ * its own winners are bucketed, staged and sorted.  Its select fills the exchange array
+ * (spai_rollout_ws_offset fields 2/6: per-bucket weight sums and winner counts of its own
+ * buckets, 0 elsewhere, and B caller slots); the caller sums that array over the parts (an
+ * all-reduce: x + 0 is exact, so the sum equals the one-part array bit for bit), then calls
+ * spai_rollout_merge (counts, T, bucket positions and masses), spai_rollout_sort (actions and
+ * fwd_probs of its slice) and spai_rollout_finish (the last part writes the terminal step and
+ * the padding; t_out is written by every part). */
 size_t spai_rollout_workspace_bytes(int32_t E, int32_t B);
 int spai_rollout_select(const float* logits, int64_t bstride, int32_t E, int32_t B, const float* lmax,
                         uint64_t seed, uint64_t stream_id, uint64_t* stream_ctr, int32_t sample_base,
                         int32_t part, int32_t nparts, uint32_t* removed, int32_t words, int32_t* counts,
                         void* workspace, size_t workspace_bytes, void* stream);
+int spai_rollout_merge(const float* logits, int64_t bstride, int32_t E, int32_t B, const float* lmax,
+                       int32_t part, int32_t nparts, int32_t* counts, void* workspace, size_t workspace_bytes,
+                       void* stream);
 int spai_rollout_sort(const float* logits, int64_t bstride, int32_t E, int32_t B, const float* lmax,
-                      int32_t part, int32_t nparts, int64_t t_cap, int64_t* actions, void* workspace,
-                      size_t workspace_bytes, void* stream);
+                      int32_t part, int32_t nparts, int64_t t_cap, int64_t* actions, float* fwd_probs,
+                      void* workspace, size_t workspace_bytes, void* stream);
 int spai_rollout_finish(const float* logits, int64_t bstride, int32_t E, int32_t B, const float* lmax,
                         const int32_t* counts, int32_t part, int32_t nparts, int64_t t_cap, int64_t* actions,
                         float* fwd_probs, int32_t* t_out, void* workspace, size_t workspace_bytes, void* stream);
@@ -129,11 +132,12 @@ int spai_rollout_order(const float* logits, int64_t bstride, int32_t E, int32_t 
                        const int32_t* counts, int64_t t_cap, int64_t* actions, float* fwd_probs,
                        int32_t* t_out, void* workspace, size_t workspace_bytes, void* stream);
 /* Byte offset inside the rollout workspace (tests, the multi-part exchange): field 0 = int32
- * oversized buckets the last order phase handed to the global-memory sort, 1 = int32 T of the
- * last rollout, 2 = fp64 [B][kMaxB] bucket weight sums, 4 = int32 [B][kMaxB + 1] trajectory
- * position of each bucket's first winner, 5 = int32 [B] buckets per sample (a part's slice of
- * sample b is [pos[b][nb*p/np], pos[b][nb*(p+1)/np])); field 3 returns kMaxB itself.
- * -1 for an unknown field or bad shape. */
+ * oversized buckets the last sort handed to the global-memory sort, 1 = int32 T of the last
+ * rollout, 2 = fp64 exchange array ([B][2][kMaxB] bucket weight sums | bucket winner counts,
+ * then [B] caller slots), 4 = int32 [B][kMaxB + 1] trajectory position of each bucket's first
+ * winner, 5 = int32 [B] buckets per sample (a part's slice of sample b is
+ * [pos[b][nb*p/np], pos[b][nb*(p+1)/np])); field 3 returns kMaxB itself, field 6 the length of
+ * the exchange array in fp64 values.  -1 for an unknown field or bad shape. */
 int64_t spai_rollout_ws_offset(int32_t E, int32_t B, int32_t field);
 
 /* ---------------------------------------------------------------- actions -> removal sets

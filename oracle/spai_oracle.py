@@ -244,30 +244,67 @@ def det_logf(x):
     return fma32(e.astype(np.float32), _LN2F, p)
 
 
-def gumbel_keys(logits, b_global, seed, stream):
-    """key_a = l_a - ln(-ln u_a) in fp32 for a = 0..E (E = terminal).
+_EXP_C = np.array([0x3f800000, 0x3f800000, 0x3f000000, 0x3e2aaaab, 0x3d2aaaab, 0x3c088889, 0x3ab60b61,
+                   0x39500d01], np.uint32).view(np.float32)  # 1/i! for i = 0..7
+_LOG2EF = np.array([0x3fb8aa3b], np.uint32).view(np.float32)[0]
+_LN2_HI = np.array([0x3f317200], np.uint32).view(np.float32)[0]
+_LN2_LO = np.array([0x35bfbe8e], np.uint32).view(np.float32)[0]
 
-    Counter = (a >> 2, b_global, stream_lo, stream_hi), key = (seed_lo, seed_hi),
-    output word a & 3; u = (2*(w >> 9) + 1) * 2^-24 in (0, 1), exact in fp32.
+
+def det_expf(x):
+    """Deterministic e^x of float32 values (spai_device.h det_expf, op for op).
+
+    k = rint(x * log2 e) in fp32, r = x - k ln2 by two single-rounded FMAs (ln2 split in a
+    head and a tail), e^r by a degree-7 Taylor Horner in fp32 FMAs, times 2^k (ldexp, exact:
+    the results stay normal).  x > 88.72 gives +inf, x < -87.33 gives 0.
     """
-    logits = np.asarray(logits, np.float32)
-    a = np.arange(logits.size, dtype=np.uint64)
+    x = np.asarray(x, np.float32)
+    xc = np.clip(x, np.float32(-87.33), np.float32(88.72))
+    k = np.rint(xc * _LOG2EF).astype(np.float32)
+    r = fma32(-k, _LN2_HI, xc)
+    r = fma32(-k, _LN2_LO, r)
+    p = np.full_like(r, _EXP_C[7])
+    for c in _EXP_C[6::-1]:
+        p = fma32(p, r, c)
+    out = np.ldexp(p, k.astype(np.int32)).astype(np.float32)
+    out = np.where(x > np.float32(88.72), np.float32(np.inf), out)
+    return np.where(x < np.float32(-87.33), np.float32(0.0), out).astype(np.float32)
+
+
+def philox_u(n, b_global, seed, stream):
+    """u_a for a = 0..n-1: counter = (a >> 2, b_global, stream_lo, stream_hi), key = (seed_lo,
+    seed_hi), output word a & 3; u = (2*(w >> 9) + 1) * 2^-24 in (0, 1), exact in fp32."""
+    a = np.arange(n, dtype=np.uint64)
     w = philox4x32_10(a >> np.uint64(2), np.full_like(a, b_global), np.full_like(a, stream & 0xFFFFFFFF),
                       np.full_like(a, (stream >> 32) & 0xFFFFFFFF), seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF)
     sel = (a & np.uint64(3)).astype(np.int64)
     word = np.choose(sel, w).astype(np.uint64)
     k = (word >> np.uint64(9)).astype(np.uint32)
-    u = (np.float32(2.0) * k.astype(np.float32) + np.float32(1.0)) * np.float32(2.0 ** -24)
-    q = -det_logf(u)
-    key = logits - det_logf(q)
-    return key + np.float32(0.0)  # -0 -> +0
+    return (np.float32(2.0) * k.astype(np.float32) + np.float32(1.0)) * np.float32(2.0 ** -24)
+
+
+def inverse_rates(logits):
+    """r_a = e^(l_E - l_a) (det_expf of the fp32 difference), r_E = 1 exactly."""
+    logits = np.asarray(logits, np.float32)
+    return det_expf(logits[-1] - logits)
+
+
+def arrival_times(logits, b_global, seed, stream):
+    """Exponential race of sample b_global: t_a = q_a * r_a in fp32 for a = 0..E (E = terminal),
+    q_a = -ln u_a (det_logf) ~ Exp(1), r_a = inverse_rates.  t_a < t_E <=> the Gumbel key
+    l_a - ln q_a exceeds the terminal's, and ascending t is the Plackett-Luce order of
+    sequential sampling without replacement (gflownet.py:135-179)."""
+    logits = np.asarray(logits, np.float32)
+    q = -det_logf(philox_u(logits.size, b_global, seed, stream))
+    return (q * inverse_rates(logits)).astype(np.float32)
 
 
 def throughput_rollout(logits, B, seed, stream, sample_base=0):
     """Removed sets, ordered trajectories and forward probabilities for B samples.
 
     Returns (removed [B,E] bool, actions [T,B] int64, fwd_probs [B,T] fp32, counts [B]).
-    Order: key descending, ties by action id ascending; trajectory = winners then E.
+    Removed: t_a < t_E (arrival_times); order: t ascending, ties by action id ascending;
+    trajectory = winners then E.
     fwd_probs[t] = w_{a_t} / (W_rest + sum_{s>=t} w_{a_s}), w = exp(l - lmax) in fp64 and
     W_rest the mass of the actions never removed (terminal included): the masked-softmax
     probability the sequential reference assigns to that step (policy.py:65-73, log.py:70),
@@ -280,10 +317,10 @@ def throughput_rollout(logits, B, seed, stream, sample_base=0):
     removed = np.zeros((B, E), np.bool_)
     orders, probs = [], []
     for b in range(B):
-        key = gumbel_keys(logits, sample_base + b, seed, stream)
-        win = np.flatnonzero(key[:E] > key[E])
+        t = arrival_times(logits, sample_base + b, seed, stream)
+        win = np.flatnonzero(t[:E] < t[E])
         removed[b, win] = True
-        o = win[np.lexsort((win, -key[win]))]
+        o = win[np.lexsort((win, t[win]))]
         ww = w[o]
         rest = w[E] + w[:E][~removed[b]].sum()
         suffix = np.cumsum(ww[::-1])[::-1]

@@ -41,8 +41,11 @@ def test_argument_validation_without_gpu():
     assert b"fill_mode" in lib.spai_last_error()
     rc = lib.spai_rollout_select(None, 0, 10, 1, None, 0, 0, None, 0, 0, 1, None, 1, None, None, 0, None)
     assert rc == _lib.SPAI_ERR_INVALID
-    rc = lib.spai_rollout_sort(None, 0, 10, 1, None, 2, 2, 11, None, None, 0, None)
+    rc = lib.spai_rollout_sort(None, 0, 10, 1, None, 2, 2, 11, None, None, None, 0, None)
     assert rc == _lib.SPAI_ERR_INVALID and b"null pointer" in lib.spai_last_error()
+    rc = lib.spai_rollout_merge(None, 0, 10, 1, None, 0, 2, None, None, 0, None)
+    assert rc == _lib.SPAI_ERR_INVALID and b"null pointer" in lib.spai_last_error()
+    assert lib.spai_rollout_ws_offset(1000, 2, 6) == 2 * 2 * 2048 + 2
     assert lib.spai_rollout_ws_offset(1000, 2, 3) == 2048 and lib.spai_rollout_ws_offset(1000, 2, 9) == -1
     assert 0 < lib.spai_rollout_ws_offset(1000, 2, 2) < lib.spai_rollout_workspace_bytes(1000, 2)
     with pytest.raises(ValueError):

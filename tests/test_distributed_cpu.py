@@ -60,15 +60,17 @@ def _worker(rank, world, port, q):
         out["res2"] = res2.numpy()
         out["m"] = full_m.numpy()
         out["rewards"] = gather_rewards(torch.arange(B, dtype=torch.float64) + 10 * rank).numpy()
-        # the split rollout's exchange: each part fills the bucket weight sums of its own bucket
-        # range (zero elsewhere) and its lines' residual partials; one packed all_reduce
+        # the split rollout's exchange: each part fills the bucket weight sums and winner counts
+        # of its own bucket range (zero elsewhere, the exchange array's [B][2][kMaxB] layout)
+        # and its lines' residual partials go into the B trailing slots; one all_reduce in place
         full_bs, full_r2 = _split_fixture()
-        nb = full_bs.shape[1]
+        B3, nb = full_bs.shape[0], full_bs.shape[2]
         k0, k1 = nb * rank // world, nb * (rank + 1) // world
-        bs = torch.zeros_like(full_bs)
-        bs[:, k0:k1] = full_bs[:, k0:k1]
+        xch = torch.zeros(full_bs.numel() + B3, dtype=torch.float64)
+        bs = xch[:full_bs.numel()].view_as(full_bs)
+        bs[:, :, k0:k1] = full_bs[:, :, k0:k1]
         r2 = full_r2 * (0.25 if rank == 0 else 0.75)
-        out["r2"] = exchange_parts(bs, r2).numpy()
+        out["r2"] = exchange_parts(xch, r2).clone().numpy()
         out["bs"] = bs.numpy()
         # the split log: rank q holds slice [bounds[b,0], bounds[b,1]) of each trajectory
         acts, fwd, cuts, T = _slices_fixture()
@@ -88,7 +90,9 @@ def _worker(rank, world, port, q):
 
 def _split_fixture():
     g = torch.Generator().manual_seed(3)
-    return torch.rand(3, 37, generator=g, dtype=torch.float64) * 1e3, torch.rand(3, generator=g, dtype=torch.float64)
+    sums = torch.rand(3, 1, 37, generator=g, dtype=torch.float64) * 1e3
+    counts = torch.randint(0, 5000, (3, 1, 37), generator=g).double()
+    return torch.cat([sums, counts], 1), torch.rand(3, generator=g, dtype=torch.float64)
 
 
 def _slices_fixture():

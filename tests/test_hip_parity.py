@@ -546,10 +546,10 @@ def test_sample_states_distinct_initial_states():
 @pytest.mark.parametrize("P", [2, 3, 5])
 def test_split_rollout_parts_reassemble_bit_exact(P):
     """The multi-GPU split played by P parts in one process: every part's select
-    gives the complete removed sets and counts; each part sorts its bucket range; the parts'
-    bucket weight sums are summed (what the all_reduce does); each part's finish then writes
-    its trajectory slice.  The slices tile [0, T) and reassemble the one-part rollout bit for
-    bit (actions and fwd_probs)."""
+    gives the complete removed sets and fills the exchange array for its own buckets only; the
+    parts' arrays are summed (what the all_reduce does); each part's merge then reproduces the
+    one-part counts, and its sort + finish write its trajectory slice.  The slices tile [0, T)
+    and reassemble the one-part rollout bit for bit (actions and fwd_probs)."""
     from gflownet_spai_amd import kernels
     E, B = 300000, 3
     rng = np.random.default_rng(P)
@@ -561,19 +561,27 @@ def test_split_rollout_parts_reassemble_bit_exact(P):
     T = int(t1)
     parts = []
     for q in range(P):
-        rq, cq, wq = kernels.rollout_select(lg, B, lmax, 17, 4, 0, None, q, P, ws_tag=f"part{q}")
-        assert torch.equal(rq, removed1) and torch.equal(cq, counts1)
-        aq = kernels.rollout_sort(lg, B, lmax, wq, q, P)
-        parts.append((wq, aq))
-    total = sum(kernels.bucket_sums(wq, E, B).clone() for wq, _ in parts)
-    nb = kernels.part_bounds(parts[0][0], E, B, 0, 1)  # sanity: one part spans everything
-    assert int(nb[0, 0]) == 0
+        rq, _, wq = kernels.rollout_select(lg, B, lmax, 17, 4, 0, None, q, P, ws_tag=f"part{q}")
+        assert torch.equal(rq, removed1)
+        parts.append(wq)
+    from gflownet_spai_amd import _lib
+    nbk = B * 2 * _lib.load().spai_rollout_ws_offset(E, B, 3)  # the bucket part (then B caller slots)
+    xs = [kernels.exchange_array(wq, E, B)[:nbk] for wq in parts]
+    # disjoint supports: each bucket's entries come from exactly one part
+    nz = sum((x != 0).int() for x in xs)
+    assert int(nz.max()) <= 1
+    total = sum(x.clone() for x in xs)
+    one = kernels.exchange_array(ws1, E, B)[:nbk]
+    assert torch.equal(total, one)
     acts = torch.full((B, T), -7, dtype=torch.int64, device=DEV)
     fwds = torch.full((B, T), -7.0, device=DEV)
     covered = torch.zeros((B, T), dtype=torch.int32, device=DEV)
-    for q, (wq, aq) in enumerate(parts):
-        kernels.bucket_sums(wq, E, B).copy_(total)
-        fq, tq = kernels.rollout_finish(lg, B, lmax, counts1, wq, aq, q, P)
+    for q, wq in enumerate(parts):
+        kernels.exchange_array(wq, E, B)[:nbk].copy_(total)
+        cq = kernels.rollout_merge(lg, B, lmax, wq, q, P)
+        assert torch.equal(cq, counts1)
+        aq, fq = kernels.rollout_sort(lg, B, lmax, wq, q, P)
+        tq = kernels.rollout_finish(lg, B, lmax, cq, wq, aq, fq, q, P)
         assert int(tq) == T
         bd = kernels.part_bounds(wq, E, B, q, P).cpu()
         for b in range(B):

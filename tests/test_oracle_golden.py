@@ -128,9 +128,41 @@ def test_throughput_rollout_structure():
         k = counts[b]
         assert set(actions[:k, b].tolist()) == set(np.flatnonzero(removed[b]).tolist())
         assert actions[k, b] == E and np.all(actions[k + 1:, b] == -1)
-        keys = O.gumbel_keys(logits, b, 7, 3)
-        assert np.all(np.diff(keys[actions[:k, b]]) <= 0)
+        t = O.arrival_times(logits, b, 7, 3)
+        assert np.all(np.diff(t[actions[:k, b]]) >= 0) and np.all(t[actions[:k, b]] < t[E])
         assert np.all(fwd[b, k + 1:] == 1.0) and np.all(fwd[b, :k + 1] > 0)
+
+
+def test_det_expf_accuracy_and_range():
+    """det_expf: within 2 ulp of the correctly rounded e^x over its range, exact at 0, the
+    overflow/underflow clamps, and r_E = 1 exactly (the terminal's inverse rate)."""
+    rng = np.random.default_rng(5)
+    x = np.concatenate([rng.uniform(-87.3, 88.7, 200000), rng.uniform(-3, 3, 100000)]).astype(np.float32)
+    got = O.det_expf(x).astype(np.float64)
+    ref = np.exp(x.astype(np.float64))
+    ulp = np.spacing(ref.astype(np.float32)).astype(np.float64)
+    assert np.max(np.abs(got - ref) / ulp) < 2.0
+    assert O.det_expf(np.float32([0.0]))[0] == 1.0
+    assert O.det_expf(np.float32([89.0]))[0] == np.inf and O.det_expf(np.float32([-88.0]))[0] == 0.0
+    lg = rng.standard_normal(50).astype(np.float32)
+    assert O.inverse_rates(lg)[-1] == 1.0
+
+
+def test_arrival_race_matches_gumbel_keys():
+    """t_a < t_E decides the same removed set as the Gumbel keys l_a - ln q_a > l_E - ln q_E
+    (equal up to fp32 rounding at exact near-ties), and ascending t is descending key order."""
+    rng = np.random.default_rng(6)
+    logits = rng.standard_normal(20001).astype(np.float32)
+    logits[-1] = 1.2
+    for b in range(3):
+        t = O.arrival_times(logits, b, 5, 9).astype(np.float64)
+        q = -O.det_logf(O.philox_u(logits.size, b, 5, 9)).astype(np.float64)
+        key = logits.astype(np.float64) - np.log(q)
+        agree = (t[:-1] < t[-1]) == (key[:-1] > key[-1])
+        assert agree.mean() > 0.9995
+        win = np.flatnonzero(t[:-1] < t[-1])
+        o = win[np.argsort(t[win], kind="stable")]
+        assert np.mean(np.diff(key[o]) <= 1e-5) > 0.999
 
 
 def test_gumbel_topk_matches_sequential_distribution():

@@ -284,24 +284,45 @@ __global__ __launch_bounds__(kNT) void k_gram_fill_wide(int32_t n, int32_t line_
   for (int p = 0; p < W; ++p) s_act[p][t] = (valid && p < wrt) ? pat_act[(int64_t)jj * wrt + p] : -1;
   const double* gp = gram + (int64_t)(jj >> 6) * (T + W) * 64 + (jj & 63);
   const int nvl = min(kNT, line_end - (line_begin + lb * kNT));
+  // the slots' bitmap words of the next sample are loaded while the current one is solved
+  uint32_t wd[W];
+#pragma unroll
+  for (int p = 0; p < W; ++p) {
+    const int ap = s_act[p][t];
+    wd[p] = ap >= 0 ? removed[ap >> 5] : 0u;
+  }
 #pragma unroll 1
   for (int b = 0; b < B; ++b) {
-    const uint32_t* rb = removed + (int64_t)b * words;
     uint32_t keep = 0;
 #pragma unroll
     for (int p = 0; p < W; ++p) {
       const int ap = s_act[p][t];
-      if (ap >= 0 && !((rb[ap >> 5] >> (ap & 31)) & 1u)) keep |= 1u << p;
+      if (ap >= 0 && !((wd[p] >> (ap & 31)) & 1u)) keep |= 1u << p;
+    }
+    if (b + 1 < B) {
+      const uint32_t* rn = removed + (int64_t)(b + 1) * words;
+#pragma unroll
+      for (int p = 0; p < W; ++p) {
+        const int ap = s_act[p][t];
+        wd[p] = ap >= 0 ? rn[ap >> 5] : 0u;
+      }
     }
     double a[T], y[W];
 #pragma unroll
     for (int q = 0; q < T; ++q) a[q] = gp[q * 64];
     double r2 = 1.0;
     if constexpr (LSQ) {
+      // pivot floor relative to the line's largest diagonal (one register instead of W)
+      double dmax = 0.0;
+#pragma unroll
+      for (int k = 0; k < W; ++k) dmax = fmax(dmax, a[gidx<W>(k, k)]);
+      const double floor_ = 1e-13 * dmax;
+#pragma unroll
+      for (int k = 0; k < W; ++k) y[k] = gp[(T + k) * 64];  // c, solved in place below
 #pragma unroll
       for (int k = 0; k < W; ++k) {
         const double d = a[gidx<W>(k, k)];
-        const double ik = (((keep >> k) & 1u) && d > 1e-13 * gp[gidx<W>(k, k) * 64]) ? fast_rcp(d) : 0.0;
+        const double ik = (((keep >> k) & 1u) && d > floor_) ? fast_rcp(d) : 0.0;
         a[gidx<W>(k, k)] = ik;  // the diagonal slot now holds 1/D_k
         // rows i descending: row i's multiplier L_ik = EL_ik / D_k replaces EL_ik only after
         // every update that still reads it (rows j <= i use EL_jk)
@@ -314,8 +335,8 @@ __global__ __launch_bounds__(kNT) void k_gram_fill_wide(int32_t n, int32_t line_
         }
       }
 #pragma unroll
-      for (int k = 0; k < W; ++k) {
-        double v = gp[(T + k) * 64];
+      for (int k = 0; k < W; ++k) {  // forward substitution in place (y[q < k] are final)
+        double v = y[k];
 #pragma unroll
         for (int q = 0; q < k; ++q) v -= a[gidx<W>(q, k)] * y[q];
         y[k] = v;

@@ -182,6 +182,39 @@ def cpu_baseline(cfg, B, budget_s: float, logits, T_mean: float):
     return out
 
 
+def generic_residual_leg(env, log, reps: int = 10):
+    """The generic SpMM residual (spai_residual_lines: ||A M_b - I||_F^2 of B arbitrary sparse
+    M_b, preconditioner.py:79-93 for any M) on the step's B candidates: their stored LSQ values
+    with each candidate's own kept index set (removed slots -> -1).  Timed with HIP events on
+    the launch stream; algorithmic bytes per launch = B x (bytes(A) + bytes(M_b)) (SURVEY §8d:
+    A and M_b read once per sample).  Also checks the result against the fused fill kernel's
+    residual (they differ by d^T G d, d = the fp32 rounding of M)."""
+    from gflownet_spai_amd import kernels
+    pat, a = env.pattern, env.a_lines
+    bits = log.removed.view(torch.int32)
+    act = pat.act.long().clamp(min=0)
+    rem = ((bits[:, act >> 5] >> (act & 31)) & 1).bool()
+    idx = torch.where(rem | (pat.idx < 0), torch.full_like(pat.idx, -1), pat.idx).contiguous()
+    m = env.last_m.contiguous()
+    B, n, W = m.shape
+    res2 = kernels.residual_lines(idx, m, a)  # warm-up
+    kernels.TIMERS = {}
+    for _ in range(reps):
+        res2 = kernels.residual_lines(idx, m, a)
+    torch.cuda.synchronize()
+    ms = float(np.mean(kernels.timer_ms("residual_lines")))
+    kernels.TIMERS = None
+    ref = env.last_residual.double() ** 2
+    rel = float(((res2 - ref).abs() / ref).max())
+    bytes_a = a.idx.numel() * 4 + a.val.numel() * a.val.element_size()
+    bytes_m = n * W * (4 + m.element_size())
+    out = roofline_obj(f"k_resid<{W},{a.width},{str(a.val.dtype)[6:]},{str(m.dtype)[6:]}> (||A M_b - I||_F^2 of "
+                       f"B={B} arbitrary sparse M_b: the step's LSQ fills with their own kept index sets)",
+                       B * (bytes_a + bytes_m), ms)
+    out["max_rel_diff_vs_fused_fill"] = rel
+    return out
+
+
 def roofline_obj(kernel, nbytes, ms, traffic=None):
     achieved = nbytes / (ms * 1e-3) / 1e9
     return {"kernel": kernel, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -373,6 +406,9 @@ def main():
                                      f"reaches it through the env-constant Gram cache)", fb, fill_ms,
                                      measured_traffic(args.config, B)),
         }
+        if world == 1:
+            with torch.no_grad():
+                out["roofline_residual"] = generic_residual_leg(env, log)
         if not args.no_cpu_baseline and world == 1:
             with torch.no_grad():
                 lg_host = model.forward_policy.logits(model.state_to_data(s0[:1])[0])[0].reshape(-1).cpu().numpy()

@@ -63,6 +63,9 @@ SIGNATURES = {
                                           _c_i32, _c_p, _c_p, _c_i32, _c_i32, _c_p, _c_sz, _c_p]),
     "spai_policy_rows_constant": (ctypes.c_int, [_c_i32, _c_i32, _c_p, _c_p, _c_p]),
     "spai_rollout_ws_offset": (_c_i64, [_c_i32, _c_i32, _c_i32]),
+    "spai_residual_workspace_bytes": (_c_sz, [_c_i32, _c_i32]),
+    "spai_residual_lines": (ctypes.c_int, [_c_i32, _c_i32, _c_i32, _c_i32, _c_p, _c_i64, _c_p, _c_i32, _c_i64,
+                                           _c_i32, _c_p, _c_p, _c_i32, _c_i32, _c_p, _c_p, _c_sz, _c_p]),
     "spai_logp_grad_workspace_bytes": (_c_sz, [_c_i32, _c_i32, _c_i32, _c_i32]),
     "spai_logp_grad": (ctypes.c_int, [_c_p, _c_i64, _c_i32, _c_i32, _c_p, _c_p, _c_i64, _c_i32, _c_p, _c_i64, _c_p,
                                       _c_i64, _c_p, _c_i32, _c_p, _c_p, _c_sz, _c_p]),

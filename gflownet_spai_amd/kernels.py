@@ -189,6 +189,36 @@ def rollout_finish(lg, B, lmax, counts, ws, actions, fwd, part: int, nparts: int
     return t_dev
 
 
+def residual_lines(m_idx: torch.Tensor, m_val: torch.Tensor, a_lines: Lines, line_begin: int = 0,
+                   line_end: int | None = None) -> torch.Tensor:
+    """res2 [B] fp64 = sum over lines [begin, end) of ||sum_p M_b[l,p] A_line(idx_b[l,p]) - e_l||^2
+    for B ARBITRARY sparse M_b in ELL lines: m_idx [B, n, W] or [n, W] (one index set for every
+    sample) int32 with -1 = empty slot, m_val [B, n, W] fp32/fp64 (the generic SpMM residual of
+    preconditioner.py:79-93; spai_residual_lines)."""
+    _lib.require_device(m_val)
+    if m_val.dim() == 2:
+        m_val = m_val.unsqueeze(0)
+    B, n, W = m_val.shape
+    if line_end is None:
+        line_end = n
+    if m_val.dtype not in _DT or a_lines.val.dtype not in _DT:
+        raise ValueError("M and A must be fp32 or fp64")
+    m_idx = m_idx.to(torch.int32).contiguous()
+    m_val = m_val.contiguous()
+    if m_idx.shape[-2:] != (n, W) or (m_idx.dim() == 3 and m_idx.shape[0] != B):
+        raise ValueError(f"m_idx shape {tuple(m_idx.shape)} does not match m_val {tuple(m_val.shape)}")
+    res2 = torch.empty(B, dtype=torch.float64, device=m_val.device)
+    nb = _l().spai_residual_workspace_bytes(max(line_end - line_begin, 0), B)
+    ws = _lib.workspace(nb, m_val.device, "residual")
+    with _timed("residual_lines"):
+        st = _l().spai_residual_lines(n, line_begin, line_end, W, _lib.ptr(m_idx), n * W if m_idx.dim() == 3 else 0,
+                                      _lib.ptr(m_val), _DT[m_val.dtype], n * W, a_lines.width, _lib.ptr(a_lines.idx),
+                                      _lib.ptr(a_lines.val), _DT[a_lines.val.dtype], B, _lib.ptr(res2),
+                                      _lib.ptr(ws), ws.numel(), _lib.stream_ptr(m_val.device))
+    _lib.check(st, "spai_residual_lines")
+    return res2
+
+
 def actions_to_removed(actions_bt: torch.Tensor, E: int):
     """Removal bitmaps + unique counts from a [B, T] int64 action tensor (-1 padded)."""
     _lib.require_device(actions_bt)

@@ -173,6 +173,11 @@ class PreconditionerEnv(Env):
                                   torch.float64 if a.dtype == torch.float64 else torch.float32)
         m = updated_matrix.coalesce()
         mi = m.indices()
+        mval = torch.float64 if m.dtype == torch.float64 else torch.float32
+        pat = build_lines(mi[0], mi[1], m.values(), n, orient, self.device, mval)
+        if pat.width <= 13 and a_lines.width <= 7:  # the generic SpMM residual kernel
+            return torch.sqrt(kernels.residual_lines(pat.idx, pat.val, a_lines)[0])
+        # wider lines (e.g. spilu L@U patterns): the LDS-hash line kernel of the copy fill
         pat = build_lines(mi[0], mi[1], m.values(), n, orient, self.device, torch.float32)
         removed = torch.zeros(1, max((pat.n * pat.width + 31) // 32, 1), dtype=torch.int32, device=self.device)
         res2, _ = kernels.fill_residual(pat, a_lines, removed, lsq=False)

@@ -140,6 +140,21 @@ int spai_rollout_order(const float* logits, int64_t bstride, int32_t E, int32_t 
  * the exchange array in fp64 values.  -1 for an unknown field or bad shape. */
 int64_t spai_rollout_ws_offset(int32_t E, int32_t B, int32_t field);
 
+/* ---------------------------------------------------------------- generic residual
+ * res2_out[b] = sum over lines l in [line_begin, line_end) of
+ *   || sum_p M_b[l][p] A_line(idx_b[l][p]) - e_l ||^2
+ * for B ARBITRARY sparse M_b given as ELL lines (rows: ||M A - I||_F^2, columns: ||A M - I||_F^2;
+ * replaces the sparse torch.mm + identity subtraction + torch.norm of preconditioner.py:79-93,
+ * the calculate_residual of any M): m_idx [B][n][W] int32 (-1 = empty slot, sample stride
+ * idx_bstride elements, 0 = one index set for every sample), m_val [B][n][W] (stride
+ * val_bstride), A lines [n][WA].  Widths W <= 5/7/13 with WA <= 5/7; fp64 accumulation.
+ * Workspace: spai_residual_workspace_bytes(line_end - line_begin, B). */
+size_t spai_residual_workspace_bytes(int32_t n_lines, int32_t B);
+int spai_residual_lines(int32_t n, int32_t line_begin, int32_t line_end, int32_t W, const int32_t* m_idx,
+                        int64_t idx_bstride, const void* m_val, int32_t m_dtype, int64_t val_bstride, int32_t WA,
+                        const int32_t* a_idx, const void* a_val, int32_t a_dtype, int32_t B, double* res2_out,
+                        void* workspace, size_t workspace_bytes, void* stream);
+
 /* ---------------------------------------------------------------- actions -> removal sets
  * removed[b] = { a : 0 <= a < E, a in actions[b, :] } (preconditioner.py:37-43 +
  * utils.py:315-323: -1 padding and the terminal id E are ignored), and

@@ -643,3 +643,72 @@ def test_stream_counter_and_graph_replay():
         assert T == a_o.shape[0]
         assert np.array_equal(acts[:, :T].cpu().numpy(), a_o.T)
     assert not torch.equal(outs[0][2], outs[1][2])  # the fill ran again on the new removal sets
+
+
+@pytest.mark.parametrize("dims,W,adt,mdt,side", [(2, 5, np.float32, np.float32, "col"),
+                                                  (2, 7, np.float32, np.float64, "row"),
+                                                  (3, 7, np.float64, np.float64, "col"),
+                                                  (3, 13, np.float64, np.float32, "row")])
+def test_residual_lines_arbitrary_m_vs_scipy(dims, W, adt, mdt, side):
+    """The generic batched SpMM residual (spai_residual_lines) of B DISTINCT random sparse M
+    (random indices anywhere in [0, n), random values, empty slots) against scipy's exact fp64
+    ||M A - I||_F^2 (row lines) / ||A M - I||_F^2 (column lines), per sample; one shared index
+    set too (idx stride 0); line ranges sum to the whole."""
+    from gflownet_spai_amd import kernels
+    from gflownet_spai_amd.layout import build_lines
+    r, c, v, n = (O.poisson2d(12, adt) if dims == 2 else O.poisson3d(6, adt))
+    A = sp.csr_matrix((v.astype(np.float64), (r, c)), shape=(n, n))
+    a_lines = build_lines(torch.from_numpy(r), torch.from_numpy(c), torch.from_numpy(v), n, side, DEV)
+    rng = np.random.default_rng(W)
+    B = 3
+    idx = rng.integers(0, n, (B, n, W)).astype(np.int32)
+    idx[rng.random((B, n, W)) < 0.3] = -1
+    for b in range(B):  # distinct indices inside a line (the ELL lines of a sparse matrix)
+        for l in range(n):
+            row = idx[b, l]
+            seen = set()
+            for p in range(W):
+                if row[p] in seen:
+                    row[p] = -1
+                elif row[p] >= 0:
+                    seen.add(int(row[p]))
+    val = rng.standard_normal((B, n, W)).astype(mdt)
+    got = kernels.residual_lines(torch.from_numpy(idx).to(DEV), torch.from_numpy(val).to(DEV), a_lines).cpu().numpy()
+    I = sp.identity(n, format="csr")
+    for b in range(B):
+        ok = idx[b] >= 0
+        lines, slots = np.nonzero(ok)
+        other = idx[b][ok]
+        vals = val[b][ok].astype(np.float64)
+        M = sp.csr_matrix((vals, (lines, other) if side == "row" else (other, lines)), shape=(n, n))
+        P = (M @ A) if side == "row" else (A @ M)
+        ref = sp.linalg.norm(P - I) ** 2
+        assert got[b] == pytest.approx(ref, rel=1e-12)
+    # one index set for every sample (stride 0) and a split into line ranges
+    shared = kernels.residual_lines(torch.from_numpy(idx[0]).to(DEV), torch.from_numpy(val[:1]).to(DEV), a_lines)
+    assert float(shared[0]) == pytest.approx(float(got[0]), rel=1e-14)
+    h = n // 2
+    parts = (kernels.residual_lines(torch.from_numpy(idx).to(DEV), torch.from_numpy(val).to(DEV), a_lines, 0, h) +
+             kernels.residual_lines(torch.from_numpy(idx).to(DEV), torch.from_numpy(val).to(DEV), a_lines, h, n))
+    np.testing.assert_allclose(parts.cpu().numpy(), got, rtol=1e-13)
+
+
+def test_residual_lines_matches_fused_lsq_fill_residual():
+    """||A M - I||_F^2 of the candidates' stored LSQ fills M (distinct kept index sets per
+    sample) through the generic kernel equals the fused fill kernel's residual (which takes it
+    from the factorisation; they differ by d^T G d, d = fp32 rounding of M)."""
+    from gflownet_spai_amd import GFlowNet, PreconditionerEnv, kernels, poisson_2d
+    A = poisson_2d(32)
+    env = PreconditionerEnv(1024, A, A, side="AM", fill="lsq", keep_m=True)
+    E = env.num_actions - 1
+    lg = torch.randn(E + 1, generator=torch.Generator().manual_seed(2))
+    lg[E] = 1.0
+    log = GFlowNet(FixedLogits(lg), None, env, mode="throughput", seed=3).sample_states([A] * 4, return_log=True)
+    pat = env.pattern
+    bits = log.removed.view(torch.int32)
+    act = pat.act.long().clamp(min=0)
+    rem = ((bits[:, act >> 5] >> (act & 31)) & 1).bool()
+    idx = torch.where(rem | (pat.idx < 0), torch.full_like(pat.idx, -1), pat.idx)
+    got = kernels.residual_lines(idx, env.last_m, env.a_lines)
+    ref = env.last_residual.double() ** 2
+    np.testing.assert_allclose(got.cpu().numpy(), ref.cpu().numpy(), rtol=1e-6)

@@ -8,7 +8,11 @@ of M (column SPAI) and the ||A M - I||_F reward, all inputs resident in HBM.
 
 Multi-GPU (one process per GPU; `--gpus N` starts the N ranks itself, or run it under
 torch.distributed.run):
-  --shard columns (default; the north star's and BASELINE C4's split, strong scaling): the
+  --shard samples (default, strong scaling): the global batch of B candidates is split over
+      the ranks (rank r: candidates r*B/P .. (r+1)*B/P - 1, the same Philox draws as one GPU);
+      per step one all_gather of the rewards and one reduce of the best candidate's M to rank 0.
+      value = B*N / step.
+  --shard columns (the north star's column split, strong scaling): the
       same B candidates on every rank; rank r orders the r-th slice of every trajectory and
       fills lines shard_lines(N, r, P) of every candidate's M; ONE all_reduce per step (bucket
       weight sums + residual partials); the best candidate's M is assembled with ONE all_gather
@@ -247,7 +251,7 @@ def main():
     ap.add_argument("--batch", type=int, default=8)
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--shard", default="columns", choices=["columns", "candidates"])
+    ap.add_argument("--shard", default="samples", choices=["samples", "columns", "candidates"])
     ap.add_argument("--assemble", default="best", choices=["best", "all", "none"])
     ap.add_argument("--no-graph", action="store_true", help="time eager steps (host launches) instead of graph replays")
     args = ap.parse_args()
@@ -276,14 +280,24 @@ def main():
     E = env.num_actions - 1
     B = args.batch
     columns = args.shard == "columns"
+    samples = args.shard == "samples"
+    strong = columns or samples
     split = columns and world > 1
-    model = GFlowNet(make_policy(env, P, dev), None, env, mode="throughput", seed=1234,
-                     sample_base=0 if columns else rank * B, shard=(rank, world, None) if split else None)
-    s0 = [P] * B
+    if samples and B % world:
+        sys.exit(f"bench.py: --shard samples needs the batch ({B}) divisible by the GPU count ({world})")
+    bl = B // world if samples else B  # candidates this rank rolls out and fills
+    base = rank * bl if samples else (0 if columns else rank * B)
+    model = GFlowNet(make_policy(env, P, dev), None, env, mode="throughput", seed=1234, sample_base=base,
+                     shard=(rank, world, None) if split else None)
+    s0 = [P] * bl
     assembled = {}
 
     def assemble(log):
-        if not split or args.assemble == "none":
+        if world == 1 or args.assemble == "none" or not strong:
+            return
+        if samples:  # global rewards everywhere, the best candidate's M on rank 0
+            from gflownet_spai_amd.distributed import select_best_samples
+            assembled["r"], assembled["best"], assembled["m"] = select_best_samples(log.rewards, env.last_m)
             return
         m = env.last_m
         if args.assemble == "best":  # the candidate with the highest reward: the preconditioner kept
@@ -349,7 +363,7 @@ def main():
                 if split:
                     model.rollout_exchange(st)
                     g2.replay()
-                    assemble(glog)
+                assemble(glog)
                 return glog
 
             for _ in range(max(1, args.warmup)):
@@ -372,30 +386,33 @@ def main():
 
     if rank == 0:
         fill_ms = phases.get("fill_residual", float("nan"))
-        fb = fill_bytes(env, B)
+        fb = fill_bytes(env, bl)
         if split:  # the rank's fill covers its own lines only (rank 0: the first, largest shard)
             fb *= (model.lines[1] - model.lines[0]) / n
         gram_t = "f32" if env.gram is not None and env.gram.dtype == torch.float32 else "f64"
         out = {
             "metric": "SPAI columns/sec + final ||AM-I||_F, 2D Poisson 1024^2, at 1/2/4/8 GPU",
-            "value": B * n * (1 if columns else world) / dt,
+            "value": B * n * (1 if strong else world) / dt,
             "unit": "columns/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": dt * 1e3,
             "higher_is_better": True,
-            "scaling": "strong" if columns else "weak",
+            "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
             "dtype": "f32 storage, f64 solve/accumulate" if dtype == torch.float32 else "f64",
             "data": "synthetic (random-init seeded ForwardPolicy GATv2x2+fc, hid=4, evaluated on the state graph in "
                     "every step; terminal fc bias set for 20% expected removal; matrix from its stencil)",
-            "config": {"workload": text + (f", B={B} candidates, columns split over {world} GPUs (trajectory slices + "
-                                           f"lines of M per rank, one all_reduce, {args.assemble} M all_gather)"
-                                           if columns else f", B={B} candidates per GPU") +
+            "config": {"workload": text + {
+                "samples": f", B={B} candidates split over {world} GPUs ({bl} per GPU; one all_gather of the rewards "
+                           f"and one reduce of the best candidate's M per step)",
+                "columns": f", B={B} candidates, columns split over {world} GPUs (trajectory slices + lines of M per "
+                           f"rank, one all_reduce, {args.assemble} M all_gather)",
+                "candidates": f", B={B} candidates per GPU"}[args.shard] +
                                    ": ForwardPolicy logits + throughput rollout + LSQ fill + ||AM-I||_F",
-                       "N": n, "E": E, "global_batch": B * (1 if columns else world),
-                       "parallelism": f"{'columns' if columns else 'candidates'} sharded x{world}"},
+                       "N": n, "E": E, "global_batch": B * (1 if strong else world),
+                       "parallelism": f"{args.shard} sharded x{world}"},
             "graph": use_graph,
             "ms_per_step_eager": dt_eager * 1e3,
             "final_residual_fro": float(res[0]),
@@ -404,7 +421,7 @@ def main():
             "phases_ms": phases,
             "roofline": roofline_obj(f"k_gram_fill<{env.pattern.width},{gram_t},LSQ> (LSQ fill of M + ||AM-I||^2; A "
                                      f"reaches it through the env-constant Gram cache)", fb, fill_ms,
-                                     measured_traffic(args.config, B)),
+                                     measured_traffic(args.config, bl)),
         }
         if world == 1:
             with torch.no_grad():

@@ -9,6 +9,10 @@ Two ways to spread work:
     winner counts and the squared residual partials (``exchange_parts``); the chosen M is
     assembled with ONE
     all_gather of equal-size ELL blocks (``allgather_lines``).
+  * samples (strong scaling over a fixed global batch of B candidates, bench.py's default):
+    rank r rolls out and fills candidates r*B/P .. (r+1)*B/P - 1 (the same Philox sample ids,
+    hence the same draws, as a one-GPU batch); the step's exchange is one all_gather of the
+    rewards and one reduce of the best candidate's M (``select_best_samples``).
   * candidates (weak scaling): rank r samples candidates with Philox sample ids
     r*B .. r*B+B-1 (``GFlowNet(sample_base=r*B)``); every candidate's trajectory, fill and
     reward live on one rank, so the step needs no collective.
@@ -52,6 +56,27 @@ def allgather_lines(m_local: torch.Tensor, n: int, group=None) -> torch.Tensor:
         b, e = shard_lines(n, r, world)
         parts.append(out[r, :, : e - b])
     return torch.cat(parts, dim=1)
+
+
+def select_best_samples(rewards_local: torch.Tensor, m_local: torch.Tensor, group=None, dst: int = 0):
+    """The samples split's one exchange (no host round trip): every rank holds B/P candidates
+    (global sample ids rank*B/P ...); ``rewards_local`` [B/P], ``m_local`` [B/P, n, W].  One
+    all_gather makes the global rewards [B] known everywhere; the global argmax is found on the
+    device, the owning rank contributes that candidate's M and every other rank zeros, and one
+    reduce to ``dst`` delivers it there (x + 0 is exact).  Returns (rewards [B], best index
+    [1] int64, M of the best candidate [n, W] -- valid on ``dst``)."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    bl = rewards_local.numel()
+    allr = torch.empty(world * bl, dtype=rewards_local.dtype, device=rewards_local.device)
+    dist.all_gather_into_tensor(allr, rewards_local.contiguous(), group=group)
+    best = torch.argmax(allr).view(1)
+    mine = (best >= rank * bl) & (best < (rank + 1) * bl)
+    pick = m_local.index_select(0, (best - rank * bl).clamp(0, bl - 1)).squeeze(0)
+    out = torch.where(mine, pick, torch.zeros((), dtype=pick.dtype, device=pick.device)).contiguous()
+    dist.reduce(out, dst=dist.get_global_rank(group, dst) if group is not None else dst, op=dist.ReduceOp.SUM,
+                group=group)
+    return allr, best, out
 
 
 def gather_rewards(rewards: torch.Tensor, group=None) -> torch.Tensor:

@@ -13,8 +13,8 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from gflownet_spai_amd.distributed import (allgather_lines, allreduce_res2, exchange_parts, gather_rewards, gather_slices,
-                                          shard_lines)
+from gflownet_spai_amd.distributed import (allgather_lines, allreduce_res2, exchange_parts, gather_rewards,
+                                           gather_slices, select_best_samples, shard_lines)
 from oracle import spai_oracle as O
 
 
@@ -72,6 +72,11 @@ def _worker(rank, world, port, q):
         r2 = full_r2 * (0.25 if rank == 0 else 0.75)
         out["r2"] = exchange_parts(xch, r2).clone().numpy()
         out["bs"] = bs.numpy()
+        # the samples split: 2 local candidates per rank, global best's M reduced to rank 0
+        rw = torch.tensor([[0.5, 2.5], [1.5, -1.0]], dtype=torch.float64)[rank]
+        ml = torch.arange(2 * 3 * 4, dtype=torch.float64).view(2, 3, 4) + 100 * rank
+        allr, best, mbest = select_best_samples(rw, ml)
+        out["samples"] = (allr.numpy(), int(best), mbest.numpy())
         # the split log: rank q holds slice [bounds[b,0], bounds[b,1]) of each trajectory
         acts, fwd, cuts, T = _slices_fixture()
         bounds = torch.stack([cuts[:, rank], cuts[:, rank + 1]], 1)
@@ -145,4 +150,8 @@ def test_world2_column_sharded_reward_and_assembly():
         assert np.array_equal(res[rank]["bs"], full_bs.numpy())  # bit-exact: one non-zero term each
         np.testing.assert_allclose(res[rank]["r2"], full_r2.numpy(), rtol=1e-15)
         assert np.array_equal(res[rank]["slices"][0], acts.numpy())
+        allr, best, mbest = res[rank]["samples"]
+        np.testing.assert_array_equal(allr, [0.5, 2.5, 1.5, -1.0])
+        assert best == 1
         assert np.array_equal(res[rank]["slices"][1], fwd.numpy())
+    np.testing.assert_array_equal(res[0]["samples"][2], np.arange(24, dtype=np.float64).reshape(2, 3, 4)[1])

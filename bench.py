@@ -44,13 +44,19 @@ CONFIGS = {
     "c2": (2, 256, torch.float32, "C2: 256^2 5-pt Poisson (65,536 x 65,536 CSR, fp32), pattern = A"),
     "c3": (3, 64, torch.float64, "C3: 64^3 7-pt 3-D Laplacian (262,144 x 262,144, fp64), 13-wide axial pattern "
                                  "(nnz/col <= 13)"),
+    "c5s": ("thermal", 1108, torch.float64, "C5 stand-in: synthetic thermal2-like heat-conduction matrix "
+                                            "(1,227,664 x 1,227,664, 8,584,786 nnz, 7 per row, lognormal "
+                                            "conductivities, randomly permuted numbering, fp64), pattern = A"),
 }
 
 
 def config_matrices(cfg: str):
     """(A, candidate pattern) of a bench config."""
-    from gflownet_spai_amd import axial_pattern_3d, poisson_2d, poisson_3d
+    from gflownet_spai_amd import axial_pattern_3d, poisson_2d, poisson_3d, thermal_like
     dims, grid, dtype, _ = CONFIGS[cfg]
+    if dims == "thermal":
+        A = thermal_like(grid, 0, dtype)
+        return A, A
     if dims == 2:
         A = poisson_2d(grid, dtype)
         return A, A

@@ -12,8 +12,9 @@ from .policy import BackwardPolicy, ForwardPolicy
 from .preconditioner import Data, PreconditionerEnv
 from .gmres import solve_with_gmres, spai_power_pattern
 from .utils import (axial_pattern_3d, load_mtx_file, lu_candidate_matrix, market_matrix_to_sparse_tensor, poisson_2d, poisson_3d,
+                    thermal_like,
                     trajectory_balance_loss)
 
 __all__ = ["Env", "GFlowNet", "Log", "ForwardPolicy", "BackwardPolicy", "PreconditionerEnv", "Data",
            "trajectory_balance_loss", "market_matrix_to_sparse_tensor", "load_mtx_file", "lu_candidate_matrix",
-           "solve_with_gmres", "spai_power_pattern", "poisson_2d", "poisson_3d", "axial_pattern_3d"]
+           "solve_with_gmres", "spai_power_pattern", "poisson_2d", "poisson_3d", "axial_pattern_3d", "thermal_like"]

@@ -214,17 +214,18 @@ def gmres(A, b, x0=None, *, M=None, rtol=1e-5, atol=0.0, restart=None, maxiter=N
                   atol=atol, restart=restart, maxiter=maxiter, callback=callback)
 
 
-def solve_with_gmres(A, b, M=None, *, verbose: bool = True, device=None):
+def solve_with_gmres(A, b, M=None, *, verbose: bool = True, device=None, maxiter: int = 10260):
     """GFlowNet100.py:61-93: (x, residuals, num_iterations, elapsed_time) of GMRES from x0 = 0
-    with maxiter = 10260, recording the legacy callback's preconditioned relative residual of
-    every inner iteration; x is returned as a host numpy array like the reference's."""
+    with maxiter = 10260 (the driver's; a keyword lowers it for large evaluations), recording the
+    legacy callback's preconditioned relative residual of every inner iteration; x is returned
+    as a host numpy array like the reference's."""
     b = np.asarray(b, dtype=np.float64).reshape(-1) if not isinstance(b, torch.Tensor) else b.reshape(-1)
     n = A.n if isinstance(A, DeviceOperator) else A.shape[0]
     if b.shape[0] != n:
         raise ValueError(f"Shape mismatch: A is {tuple(A.shape)}, but b is {tuple(b.shape)}")
     residuals: list = []
     start = time.time()
-    x, exit_code = gmres(A, b, M=M, maxiter=10260, callback=residuals.append, device=device)
+    x, exit_code = gmres(A, b, M=M, maxiter=maxiter, callback=residuals.append, device=device)
     torch.cuda.synchronize(x.device)
     elapsed = time.time() - start
     if verbose:

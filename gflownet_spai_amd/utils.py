@@ -94,6 +94,38 @@ def poisson_2d(grid: int, dtype=torch.float32) -> Tensor:
     return torch.sparse_coo_tensor(torch.stack([rows[order], cols[order]]), vals[order].to(dtype), (n, n))
 
 
+def thermal_like(grid: int, seed: int = 0, dtype=torch.float64) -> Tensor:
+    """Synthetic stand-in for SuiteSparse thermal2 (C5: 1,227,087 unknowns, 8,579,355 nnz,
+    ~7 nnz/row, SPD, unstructured): a steady heat-conduction matrix on a triangulated grid^2
+    mesh — every node coupled to its 6 triangle neighbours (dx, dy) in {(+-1,0), (0,+-1),
+    (1,-1), (-1,1)} with lognormal edge conductivities k_e (sigma 1: coefficient jumps of
+    ~e^3 across the mesh), off-diagonals -k_e, diagonal = the node's conductance sum + 1e-3
+    (a Robin-type anchor, so the matrix is SPD) — with the node numbering randomly permuted
+    (no band or grid structure left in the ordering).  grid = 1108 gives 1,227,664 unknowns and
+    8,584,786 nnz.  Coalesced COO (rows, then columns ascending)."""
+    g = torch.Generator().manual_seed(seed)
+    n = grid * grid
+    i = torch.arange(n)
+    r, c = i // grid, i % grid
+    src, dst = [], []
+    for dr, dc in ((0, 1), (1, 0), (1, -1)):  # each undirected edge once
+        ok = (r + dr < grid) & (c + dc >= 0) & (c + dc < grid)
+        src.append(i[ok])
+        dst.append(((r + dr) * grid + (c + dc))[ok])
+    src, dst = torch.cat(src), torch.cat(dst)
+    k = torch.exp(torch.randn(src.numel(), generator=g, dtype=torch.float64))
+    perm = torch.randperm(n, generator=g)
+    src, dst = perm[src], perm[dst]
+    diag = torch.full((n,), 1e-3, dtype=torch.float64)
+    diag.index_add_(0, src, k)
+    diag.index_add_(0, dst, k)
+    rows = torch.cat([torch.arange(n), src, dst])
+    cols = torch.cat([torch.arange(n), dst, src])
+    vals = torch.cat([diag, -k, -k])
+    order = torch.argsort(rows * n + cols)
+    return torch.sparse_coo_tensor(torch.stack([rows[order], cols[order]]), vals[order].to(dtype), (n, n))
+
+
 def poisson_3d(grid: int, dtype=torch.float64) -> Tensor:
     """7-point Laplacian on a grid^3 lattice (diag 6, off-diag -1), row-major COO."""
     n = grid ** 3

@@ -3,7 +3,9 @@ MI355X: iterations and time of solve_with_gmres(A, b, M) for M = none, the drive
 baseline (host LinearOperator), the power-pattern SPAI baselines (pattern of A, A^2; LSQ fill
 on the GPU) and GFlowNet-sampled SPAI patterns (throughput rollout of the bench policy, LSQ
 fill), plus the spai_ell_spmv roofline (HIP events over repeated products).
-usage: python scripts/gmres_eval.py [--grid 256] [--out gpurun_out/gmres.json]"""
+usage: python scripts/gmres_eval.py [--matrix poisson|thermal] [--grid 256] [--maxiter 10260] [--no-spilu]
+                                    [--out gpurun_out/gmres.json]
+(--matrix thermal --grid 1108: the C5 stand-in, utils.thermal_like, 1.23 M unknowns, fp64)"""
 import argparse
 import json
 import os
@@ -19,7 +21,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 import bench  # noqa: E402
-from gflownet_spai_amd import BackwardPolicy, GFlowNet, PreconditionerEnv, poisson_2d  # noqa: E402
+from gflownet_spai_amd import BackwardPolicy, GFlowNet, PreconditionerEnv, poisson_2d, thermal_like  # noqa: E402
 from gflownet_spai_amd.gmres import DeviceOperator, solve_with_gmres, spai_power_pattern  # noqa: E402
 
 
@@ -46,22 +48,32 @@ def spmv_roofline(op: DeviceOperator, reps=200):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--grid", type=int, default=256)
+    ap.add_argument("--matrix", default="poisson", choices=["poisson", "thermal"])
+    ap.add_argument("--maxiter", type=int, default=10260)
+    ap.add_argument("--no-spilu", action="store_true")
+    ap.add_argument("--powers", default="1,2")
     ap.add_argument("--samples", type=int, default=2)
     ap.add_argument("--out", default=None)
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
-    A32 = poisson_2d(args.grid, torch.float32)
-    A64 = poisson_2d(args.grid, torch.float64).coalesce()
+    if args.matrix == "poisson":
+        A32 = poisson_2d(args.grid, torch.float32)
+        A64 = poisson_2d(args.grid, torch.float64).coalesce()
+    else:
+        A64 = thermal_like(args.grid).coalesce()
+        A32 = torch.sparse_coo_tensor(A64.indices(), A64.values().float(), A64.shape)
     n = A64.shape[0]
     Acsr = sp.csr_matrix((A64.values().numpy(), tuple(A64.indices().numpy())), shape=(n, n))
     b = np.random.default_rng(0).standard_normal(n)
     Aop = DeviceOperator(Acsr, device=dev)
-    out = {"matrix": f"{args.grid}^2 5-pt Poisson (n={n}), fp64", "b": "N(0,1), seed 0",
-           "gmres": "restart 20, rtol 1e-5, maxiter 10260 (GFlowNet100.py:81)", "runs": {}}
+    out = {"matrix": (f"{args.grid}^2 5-pt Poisson" if args.matrix == "poisson" else
+                      f"thermal2-like synthetic (utils.thermal_like({args.grid}))") + f" (n={n}, nnz={Acsr.nnz}), fp64",
+           "b": "N(0,1), seed 0",
+           "gmres": f"restart 20, rtol 1e-5, maxiter {args.maxiter} (GFlowNet100.py:81 uses 10260)", "runs": {}}
 
     def run(name, M, nnz=None):
-        solve_with_gmres(Aop, b, M, verbose=False) if name == "warmup" else None
-        x, res, it, el = solve_with_gmres(Aop, b, M, verbose=False)
+        solve_with_gmres(Aop, b, M, verbose=False, maxiter=2) if name == "warmup" else None
+        x, res, it, el = solve_with_gmres(Aop, b, M, verbose=False, maxiter=args.maxiter)
         rel = float(np.linalg.norm(b - Acsr @ x) / np.linalg.norm(b))
         out["runs"][name] = {"iterations": it, "seconds": el, "true_rel_residual": rel, "nnz_M": nnz}
         print(name, out["runs"][name], flush=True)
@@ -69,12 +81,13 @@ def main():
     run("warmup", None)
     out["runs"].pop("warmup")
     run("none", None)
-    t0 = time.perf_counter()
-    ilu = spla.spilu(Acsr.tocsc())
-    out["spilu_seconds"] = time.perf_counter() - t0
-    run("spilu (host LinearOperator, GFlowNet100.py:126-132)", spla.LinearOperator(Acsr.shape, ilu.solve),
-        int(ilu.L.nnz + ilu.U.nnz))
-    for p in (1, 2):
+    if not args.no_spilu:
+        t0 = time.perf_counter()
+        ilu = spla.spilu(Acsr.tocsc())
+        out["spilu_seconds"] = time.perf_counter() - t0
+        run("spilu (host LinearOperator, GFlowNet100.py:126-132)", spla.LinearOperator(Acsr.shape, ilu.solve),
+            int(ilu.L.nnz + ilu.U.nnz))
+    for p in (int(x) for x in args.powers.split(",")):
         M = spai_power_pattern(A64, p, device=dev).coalesce()
         run(f"SPAI pattern(A^{p}) LSQ", M, int(M._nnz()))
         if p == 1:

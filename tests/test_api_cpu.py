@@ -57,3 +57,24 @@ def test_assembled_m_fixture_matches_copy_fill():
         assert np.array_equal(g["indices"][:, off:off + nnz], np.stack([mr[order], mc[order]]))
         assert np.array_equal(g["values"][off:off + nnz], mv[order])
         off += nnz
+
+
+def test_thermal_like_standin_structure():
+    """The C5 stand-in generator (utils.thermal_like): symmetric, <= 7 entries per row,
+    diagonally dominant with positive diagonal (SPD), a permuted numbering (no band), and at
+    full size thermal2's scale (1.23 M unknowns, 8.58 M nnz)."""
+    import numpy as np
+    import scipy.sparse as sp
+    from gflownet_spai_amd import thermal_like
+    A = thermal_like(40, seed=3).coalesce()
+    n = A.shape[0]
+    i = A.indices().numpy()
+    M = sp.csr_matrix((A.values().numpy(), (i[0], i[1])), shape=(n, n))
+    assert abs(M - M.T).max() == 0
+    assert np.diff(M.indptr).max() <= 7
+    d = M.diagonal()
+    off = np.asarray(abs(M).sum(1)).ravel() - d
+    assert np.all(d > off)  # strictly diagonally dominant (the 1e-3 anchor)
+    bw = np.abs(i[0] - i[1]).max()
+    assert bw > n // 2  # numbering scattered: no band left
+    assert np.all(np.linalg.eigvalsh(M.toarray()) > 0)

@@ -127,6 +127,21 @@ def test_c3_lsq_fill_13_wide_fp64_vs_oracle():
     _lsq_vs_oracle(env, A_sp, P_sp, removed, tol=1e-11)
 
 
+def test_c5_standin_lsq_fill_full_size_vs_oracle():
+    """C5 stand-in (utils.thermal_like(1108): 1,227,664 unknowns, 8,584,786 nnz, 7 per row,
+    lognormal conductivities, permuted numbering, fp64; thermal2 itself is not in the
+    container): one candidate's LSQ M over all columns and ||AM - I||_F vs the oracle."""
+    from gflownet_spai_amd import PreconditionerEnv, thermal_like
+    A = thermal_like(1108)
+    n = A.shape[0]
+    env = PreconditionerEnv(n, A, A, side="AM", fill="lsq", keep_m=True)
+    assert env.pattern.width == 7 and env.gram is not None and env.gram.dtype == torch.float64
+    removed, _ = _candidate(env, 4321)
+    Ai = A.coalesce()
+    A_sp = sp.csr_matrix((Ai.values().numpy(), tuple(Ai.indices().numpy())), shape=(n, n))
+    _lsq_vs_oracle(env, A_sp, A_sp, removed, tol=1e-9)
+
+
 @pytest.mark.parametrize("fill", ["copy", "lsq"])
 def test_assemble_matches_reference_m(fill):
     """assemble() returns update_edges_and_convert_to_sparse's M (golden G7: the reference's

@@ -512,6 +512,18 @@ extern "C" int spai_debug_prof(unsigned long long* out, int reset) {
 #define PROF_END(base)
 #endif
 
+// w (fp32 in [0, 1]) as the fixed-point integer of k_tile's per-bucket sums: w * 2^47 for
+// w >= 2^-20, else w * 2^69, truncated — from the float's bits (mantissa shifted by its
+// exponent), identical to (uint64)(w * 2^s) in fp64 at a fraction of its instructions.
+__device__ __forceinline__ uint64_t weight_fixed(float w) {
+  const uint32_t bits = __float_as_uint(w);
+  const int ex = (int)(bits >> 23);  // w >= 0: no sign bit
+  if (ex == 0) return 0ull;          // zero or denormal (< 2^-126): below both units
+  const uint64_t man = (uint64_t)((bits & 0x7FFFFFu) | 0x800000u);  // w = man * 2^(ex - 150)
+  const int sh = ex - 150 + (ex >= 107 ? 47 : 69);                  // 2^-20 <=> ex >= 107
+  return sh >= 0 ? man << sh : man >> min(-sh, 63);
+}
+
 // ------------------------------------------------------------------ k_tile
 // Selection and grouping fused, one 16384-action tile of one sample per block: arrival times
 // of the tile (16 actions per thread; times and weights kept in registers), the removed
@@ -688,10 +700,8 @@ void k_tile(const float* __restrict__ rr, const float* __restrict__ ww, int64_t 
     if ((win >> q) & 1u) {
       const int bk = nbl - bc[q];
       br[q] = (uint32_t)bk | ((uint32_t)atomicAdd(&s_off[bk], 1) << 11);
-      const float wq = lvk[q];
-      const bool big = wq >= 9.5367431640625e-07f;  // 2^-20
-      const uint64_t fx = (uint64_t)((double)wq * (big ? 140737488355328.0 : 590295810358705651712.0));
-      atomicAdd((unsigned long long*)&s_fx[bk + (big ? 0 : kMaxB)], (unsigned long long)fx);
+      atomicAdd((unsigned long long*)&s_fx[bk + (lvk[q] >= 9.5367431640625e-07f ? 0 : kMaxB)],
+                (unsigned long long)weight_fixed(lvk[q]));
     }
   }
   __syncthreads();

@@ -1001,9 +1001,9 @@ __global__ __launch_bounds__(kSortNT) void k_sort2(int32_t E, int32_t B, int32_t
                                                    const double* __restrict__ bwsuf, int32_t* __restrict__ bigcnt,
                                                    int32_t* __restrict__ biglist, int32_t part, int32_t nparts) {
   __shared__ uint64_t A[kCap2];  // low half: gather map; high half: actions awaiting store
-  __shared__ float L[kCap2];     // weights in trajectory order
-  __shared__ float S[kCap2];     // step probabilities awaiting store
-  __shared__ int s_sub[kMaxSub + 1];
+  __shared__ __attribute__((aligned(16))) float L[kCap2];  // weights in trajectory order
+  __shared__ __attribute__((aligned(16))) float S[kCap2];  // step probabilities awaiting store
+  __shared__ __attribute__((aligned(16))) int s_sub[kMaxSub + 4];
   __shared__ int s_nbp[kMaxSamples + 1];
   __shared__ int s_wc[kSortNT / 64];
   __shared__ double s_wd[kSortNT / 64];
@@ -1135,7 +1135,7 @@ __global__ __launch_bounds__(kSortNT) void k_sort2(int32_t E, int32_t B, int32_t
       s_red[wave * 2 + 1] = mx;
     }
     const int nsub = max(1, min(kMaxSub, 2 * n));
-    for (int i = tid; i <= nsub; i += kSortNT) s_sub[i] = 0;
+    for (int i = tid; i < kMaxSub; i += kSortNT) s_sub[i] = 0;  // all of it: the scan reads whole int4s
     lds_barrier();
     PROF(2)
     mn = 0xFFFFFFFFu;
@@ -1157,23 +1157,18 @@ __global__ __launch_bounds__(kSortNT) void k_sort2(int32_t E, int32_t B, int32_t
     }
     lds_barrier();
     PROF(3)
-    {  // exclusive scan of the sub-bucket counts (kMaxSub / kSortNT per thread)
-      constexpr int kQ = kMaxSub / kSortNT;
-      int cv[kQ], loc = 0;
-#pragma unroll
-      for (int q = 0; q < kQ; ++q) {
-        const int i = tid * kQ + q;
-        cv[q] = i < nsub ? s_sub[i] : 0;
-        loc += cv[q];
-      }
+    {  // exclusive scan of the sub-bucket counts: 4 per thread, one 16-byte LDS access each way
+       // (conflict-free; entries at or past nsub are zero and their scanned values unused)
+      static_assert(kMaxSub == 4 * kSortNT, "one int4 of sub-buckets per thread");
+      int4 cv = reinterpret_cast<const int4*>(s_sub)[tid];
       int t2;
-      int run = block_excl_scan<kSortNT, true>(loc, s_wc, &t2);
-#pragma unroll
-      for (int q = 0; q < kQ; ++q) {
-        const int i = tid * kQ + q;
-        if (i < nsub) s_sub[i] = run;
-        run += cv[q];
-      }
+      int run = block_excl_scan<kSortNT, true>(cv.x + cv.y + cv.z + cv.w, s_wc, &t2);
+      int4 ex;
+      ex.x = run;
+      ex.y = ex.x + cv.x;
+      ex.z = ex.y + cv.y;
+      ex.w = ex.z + cv.z;
+      reinterpret_cast<int4*>(s_sub)[tid] = ex;
     }
     lds_barrier();
     PROF(4)
@@ -1203,16 +1198,20 @@ __global__ __launch_bounds__(kSortNT) void k_sort2(int32_t E, int32_t B, int32_t
       }
     lds_barrier();
     PROF(7)
-    // weights (computed at the gather) and fp64 in-bucket inclusive suffix sums: thread t owns
-    // the t-th chunk counted from the END (contiguous, fixed order -> deterministic)
-    const int per = (n + kSortNT - 1) / kSortNT;
-    const int hi_ = n - min(tid * per, n), lo_ = max(hi_ - per, 0);
+    // fp64 in-bucket inclusive suffix sums: thread t owns the kPer-record chunk
+    // c = kSortNT - 1 - t (chunks counted from the end of the bucket, so the exclusive scan over
+    // lower threads is the mass of every later record), read and written as aligned 16-byte
+    // vectors (conflict-free); fixed order -> deterministic
+    static_assert(kPer == 8 && kPer * kSortNT == kCap2, "two float4 per chunk");
+    const int cb = (kSortNT - 1 - tid) * kPer;  // first record of this thread's chunk
+    float lv[kPer];
+    {
+      const float4 l0 = reinterpret_cast<const float4*>(L)[cb / 4], l1 = reinterpret_cast<const float4*>(L)[cb / 4 + 1];
+      lv[0] = l0.x, lv[1] = l0.y, lv[2] = l0.z, lv[3] = l0.w, lv[4] = l1.x, lv[5] = l1.y, lv[6] = l1.z, lv[7] = l1.w;
+    }
     double loc = 0.0;
 #pragma unroll
-    for (int j = 0; j < kPer; ++j) {
-      const int i = hi_ - 1 - j;
-      loc += i >= lo_ ? (double)L[i] : 0.0;
-    }
+    for (int j = kPer - 1; j >= 0; --j) loc += cb + j < n ? (double)lv[j] : 0.0;
     uint32_t av[kPer];
 #pragma unroll
     for (int j = 0; j < kPer; ++j) {
@@ -1223,14 +1222,17 @@ __global__ __launch_bounds__(kSortNT) void k_sort2(int32_t E, int32_t B, int32_t
     double run = block_excl_scan_d<kSortNT, true>(loc, s_wd, &wsum);  // mass of all later records
     PROF(8)
     // (every read of A above is behind the scan's barriers)
+    float fv[kPer];
 #pragma unroll
-    for (int j = 0; j < kPer; ++j) {
-      const int i = hi_ - 1 - j;
-      if (i >= lo_) {
-        run += (double)L[i];
-        S[i] = (float)((double)L[i] / (later + run));
+    for (int j = kPer - 1; j >= 0; --j) {
+      fv[j] = 0.0f;
+      if (cb + j < n) {
+        run += (double)lv[j];
+        fv[j] = (float)((double)lv[j] / (later + run));
       }
     }
+    reinterpret_cast<float4*>(S)[cb / 4] = make_float4(fv[0], fv[1], fv[2], fv[3]);
+    reinterpret_cast<float4*>(S)[cb / 4 + 1] = make_float4(fv[4], fv[5], fv[6], fv[7]);
 #pragma unroll
     for (int j = 0; j < kPer; ++j) {
       const int i = j * kSortNT + tid;

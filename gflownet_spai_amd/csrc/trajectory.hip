@@ -63,6 +63,8 @@ constexpr int kSortNT = 1024;
 constexpr int kMaxTiles = 2048;            // E <= kMaxTiles * kTile actions
 constexpr int kFinNT = 256;
 constexpr int kMaxSamples = 1024;          // B per rollout call
+constexpr int kBufWord3 = 0x00020000;      // buffer resource dword 3 (raw byte addressing, gfx9 family)
+typedef unsigned int spai_u2 __attribute__((ext_vector_type(2)));
 constexpr int kBins = 4096;                // splitter histogram / bucket lookup table bins
 
 struct TrajWs {
@@ -131,14 +133,57 @@ static void traj_ws(void* base, int32_t E, int32_t B, TrajWs* w) {
   w->total_bytes = c.off;
 }
 
+// Wave scans on DPP row shifts + row broadcasts (no LDS-permute traffic, no per-lane address
+// registers): row_shr 1, 2, 4, 8 inside each 16-lane row, then row_bcast 15 (rows 1, 3) and
+// row_bcast 31 (rows 2, 3).  Lanes without a source add the identity (`old`).
+template <int kCtrl, int kRowMask>
+__device__ __forceinline__ int dpp_i(int ident, int v) {
+  return __builtin_amdgcn_update_dpp(ident, v, kCtrl, kRowMask, 0xf, false);
+}
 // Inclusive wave scan (int).
 __device__ __forceinline__ int wave_incl_scan(int v) {
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int y = __shfl_up(v, o, kWave);
-    if ((threadIdx.x & 63) >= o) v += y;
-  }
+  v += dpp_i<0x111, 0xf>(0, v);
+  v += dpp_i<0x112, 0xf>(0, v);
+  v += dpp_i<0x114, 0xf>(0, v);
+  v += dpp_i<0x118, 0xf>(0, v);
+  v += dpp_i<0x142, 0xa>(0, v);
+  v += dpp_i<0x143, 0xc>(0, v);
   return v;
+}
+template <int kCtrl, int kRowMask>
+__device__ __forceinline__ double dpp_d(double v) {
+  const uint64_t u = __double_as_longlong(v);
+  const int lo = dpp_i<kCtrl, kRowMask>(0, (int)(uint32_t)u), hi = dpp_i<kCtrl, kRowMask>(0, (int)(uint32_t)(u >> 32));
+  return __longlong_as_double((long long)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo));  // 0 bits = +0.0
+}
+// Inclusive wave scan (double, fixed association => deterministic).
+__device__ __forceinline__ double wave_incl_scan_d(double v) {
+  v += dpp_d<0x111, 0xf>(v);
+  v += dpp_d<0x112, 0xf>(v);
+  v += dpp_d<0x114, 0xf>(v);
+  v += dpp_d<0x118, 0xf>(v);
+  v += dpp_d<0x142, 0xa>(v);
+  v += dpp_d<0x143, 0xc>(v);
+  return v;
+}
+// Wave-wide min / max of uint32 (uniform result): an inclusive scan, lane 63 read out.
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+  v = min(v, (uint32_t)dpp_i<0x111, 0xf>(-1, (int)v));
+  v = min(v, (uint32_t)dpp_i<0x112, 0xf>(-1, (int)v));
+  v = min(v, (uint32_t)dpp_i<0x114, 0xf>(-1, (int)v));
+  v = min(v, (uint32_t)dpp_i<0x118, 0xf>(-1, (int)v));
+  v = min(v, (uint32_t)dpp_i<0x142, 0xa>(-1, (int)v));
+  v = min(v, (uint32_t)dpp_i<0x143, 0xc>(-1, (int)v));
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+  v = max(v, (uint32_t)dpp_i<0x111, 0xf>(0, (int)v));
+  v = max(v, (uint32_t)dpp_i<0x112, 0xf>(0, (int)v));
+  v = max(v, (uint32_t)dpp_i<0x114, 0xf>(0, (int)v));
+  v = max(v, (uint32_t)dpp_i<0x118, 0xf>(0, (int)v));
+  v = max(v, (uint32_t)dpp_i<0x142, 0xa>(0, (int)v));
+  v = max(v, (uint32_t)dpp_i<0x143, 0xc>(0, (int)v));
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
 }
 
 // Barrier for LDS hand-offs only: waits for this wave's LDS operations, not for its
@@ -173,12 +218,7 @@ __device__ __forceinline__ int block_excl_scan(int v, int* lds /* NT/64 */, int*
 // Same for doubles (fixed summation order => deterministic).
 template <int NT, bool kLdsOnly = false>
 __device__ __forceinline__ double block_excl_scan_d(double v, double* lds, double* total) {
-  double incl = v;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const double y = __shfl_up(incl, o, kWave);
-    if ((threadIdx.x & 63) >= o) incl += y;
-  }
+  const double incl = wave_incl_scan_d(v);
   scan_barrier<kLdsOnly>();
   if ((threadIdx.x & 63) == 63) lds[threadIdx.x >> 6] = incl;
   scan_barrier<kLdsOnly>();
@@ -1020,6 +1060,7 @@ __global__ __launch_bounds__(kSortNT) void k_sort2(int32_t E, int32_t B, int32_t
   __syncthreads();
   const int total = s_nbp[B];
   const int t0 = 2 * tid, t1 = 2 * tid + 1;
+  PROF_INIT
   // bucket f: sample, bucket index, start/size, and the count and tile-local offset of its
   // runs in tiles t0, t1
   auto fetch = [&](int f, int& bb, int& kk, int& s0, int& s1, uint32_t& r0, uint32_t& r1, double& lt) {
@@ -1037,31 +1078,37 @@ __global__ __launch_bounds__(kSortNT) void k_sort2(int32_t E, int32_t B, int32_t
       if (t0 < ntiles) r0 = rr[t0];
       if (t1 < ntiles) r1 = rr[t1];
     }
+    // block-uniform: scalar registers (scalar-base addressing of the gather and the stores)
+    bb = __builtin_amdgcn_readfirstlane(bb);
+    kk = __builtin_amdgcn_readfirstlane(kk);
+    s0 = __builtin_amdgcn_readfirstlane(s0);
+    s1 = __builtin_amdgcn_readfirstlane(s1);
   };
   int nxb, nxk, nxs0, nxs1;
   double nxl;
   uint32_t r0, r1;  // packed runs (offset << 16 | count) of the next bucket in tiles t0, t1
-  int* dlt = reinterpret_cast<int*>(A);
+  // gather map of the bucket being staged (in S: free from the flush until the suffix phase)
+  int* dlt = reinterpret_cast<int*>(S);
   uint32_t* a_out = reinterpret_cast<uint32_t*>(A) + kCap2;
-  // Outputs of a bucket are stored during the NEXT bucket, right after its gather has
-  // landed: stores issued at the end of a bucket would sit ahead of the next bucket's loads
-  // in the (in-order) vmcnt, and every wait on those loads would wait for them.
+  // Outputs of a bucket are stored during the NEXT bucket, after its records have landed.
   int pv_n = 0;
   int64_t* pv_act = nullptr;
   float* pv_fwd = nullptr;
-  auto flush = [&]() {
+  auto flush = [&]() {  // buffer stores: scalar bases, the range check drops the tail
+    const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(pv_act, 0, pv_n * 8, kBufWord3);
+    const __amdgpu_buffer_rsrc_t rf = __builtin_amdgcn_make_buffer_rsrc(pv_fwd, 0, pv_n * 4, kBufWord3);
 #pragma unroll
     for (int j = 0; j < kCap2 / kSortNT; ++j) {
       const int i = j * kSortNT + tid;
-      if (i < pv_n) {
-        pv_act[i] = (int64_t)a_out[i];
-        pv_fwd[i] = S[i];
+      if (j * kSortNT < pv_n) {
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(spai_u2, (uint64_t)a_out[i]), ra, i * 8, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(S[i]), rf, i * 4, 0, 0);
       }
     }
     pv_n = 0;
   };
-  // gather map of a bucket (in A, free until the scatter): record i sits at staging offset
-  // dlt[i] + i; each thread writes the entries of its two runs
+  // gather map of a bucket: record i sits at staging offset dlt[i] + i; each thread writes
+  // the entries of its two runs (after the scan's barriers: the flush has read S)
   auto build_map = [&]() {
     const int c0 = (int)(r0 & 0xFFFFu), l0 = (int)(r0 >> 16), c1 = (int)(r1 & 0xFFFFu), l1 = (int)(r1 >> 16);
     int tot;
@@ -1074,48 +1121,68 @@ __global__ __launch_bounds__(kSortNT) void k_sort2(int32_t E, int32_t B, int32_t
       for (int i = 0; i < c1; ++i) dlt[ex + c0 + i] = d1;
     }
   };
-  fetch(blockIdx.x, nxb, nxk, nxs0, nxs1, r0, r1, nxl);
-  // retire the first fetch here: the loop header then has no load pending on either path,
-  // so the map build below never waits behind the previous bucket's stores
-  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-  PROF_INIT
-#pragma unroll 1
-  for (int f = blockIdx.x; f < total; f += gridDim.x) {
-    const int b = nxb, k = nxk, s = nxs0, n = nxs1 - nxs0;
-    const double later = nxl;
+  // Software pipeline: the records of bucket f + G (G = gridDim.x) are gathered into gm/gw
+  // while bucket f goes through its LDS phases (LDS-only barriers keep them in flight), and
+  // the run table of bucket f + 2G is in flight with them.
+  constexpr int kPer = kCap2 / kSortNT;
+  int cb = 0, ck = 0, cs = 0, cn = 0;
+  double cl = 0.0;
+  uint64_t gm[kPer];
+  float gw[kPer];
+  auto stage = [&](int fnext) {  // the bucket whose runs are in r0/r1 becomes the staged one
+    cb = nxb;
+    ck = nxk;
+    cs = nxs0;
+    cn = nxs1 - nxs0;
+    cl = nxl;
     build_map();
-    // the next bucket's run table is in flight during the gather (whose wait retires it)
-    fetch(f + gridDim.x, nxb, nxk, nxs0, nxs1, r0, r1, nxl);
+    PROF(2)
+    fetch(fnext, nxb, nxk, nxs0, nxs1, r0, r1, nxl);
     lds_barrier();
-    PROF(0)
-    if (n == 0 || n > kCap2) {
-      if (n > kCap2 && tid == 0) biglist[atomicAdd(bigcnt, 1)] = (b << 16) | k;  // for k_sort2_big (rare)
-      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): retire the fetch (see above)
-      continue;
-    }
-    const uint64_t* stb = staging + (int64_t)b * ntiles * kTile;
-    const float* slb = stw + (int64_t)b * ntiles * kTile;
-    constexpr int kPer = kCap2 / kSortNT;
-    // flat gather: every record of the bucket in flight at once (one round trip)
-    int dv[kPer];
+    PROF(3)
+    const bool ok = cn > 0 && cn <= kCap2;  // empty / oversized buckets are not gathered
+    // buffer loads (scalar base, 32-bit offsets); positions past the bucket read out of
+    // range (0; never used)
+    const uint32_t nrec = (uint32_t)ntiles * kTile;
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(staging + (int64_t)cb * nrec), 0, nrec * 8, kBufWord3);
+    const __amdgpu_buffer_rsrc_t rw =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(stw + (int64_t)cb * nrec), 0, nrec * 4, kBufWord3);
 #pragma unroll
     for (int j = 0; j < kPer; ++j) {
       const int i = j * kSortNT + tid;
-      dv[j] = i < n ? dlt[i] + i : 0;
+      const bool in = ok && i < cn;
+      const uint32_t d = in ? (uint32_t)(dlt[i] + i) : 0x10000000u;  // >= nrec: out of range
+      gm[j] = __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(rs, d * 8, 0, 0));
+      gw[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rw, d * 4, 0, 0));
     }
+  };
+  fetch(blockIdx.x, nxb, nxk, nxs0, nxs1, r0, r1, nxl);
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+  stage(blockIdx.x + gridDim.x);
+#pragma unroll 1
+  for (int f = blockIdx.x; f < total; f += gridDim.x) {
+    // this bucket's records and the next bucket's run table have landed (and the previous
+    // bucket's stores drained)
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+    const int b = cb, k = ck, s = cs, n = cn;
+    const double later = cl;
     uint64_t mine[kPer];
     float lw[kPer];
 #pragma unroll
     for (int j = 0; j < kPer; ++j) {
-      const bool in = j * kSortNT + tid < n;
-      mine[j] = in ? stb[dv[j]] : ~0ull;
-      lw[j] = in ? slb[dv[j]] : 0.0f;
+      mine[j] = gm[j];
+      lw[j] = gw[j];
     }
-    PROF(1)
-    // every load of this bucket (and the next bucket's run table) retired on all paths, so
-    // the loop header does not wait behind this bucket's stores
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+    PROF(0)
     flush();  // the previous bucket's outputs (drain during this bucket's LDS phases)
+    PROF(1)
+    stage(f + 2 * gridDim.x);  // map + gather of the next bucket
+    PROF(4)
+    if (n == 0 || n > kCap2) {
+      if (n > kCap2 && tid == 0) biglist[atomicAdd(bigcnt, 1)] = (b << 16) | k;  // for k_sort2_big (rare)
+      continue;
+    }
     uint32_t mn = 0xFFFFFFFFu, mx = 0u;
 #pragma unroll
     for (int j = 0; j < kPer; ++j) {
@@ -1125,11 +1192,8 @@ __global__ __launch_bounds__(kSortNT) void k_sort2(int32_t E, int32_t B, int32_t
         mx = max(mx, (uint32_t)(mine[j] >> 32));
       }
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      mn = min(mn, (uint32_t)__shfl_xor((int)mn, o, kWave));
-      mx = max(mx, (uint32_t)__shfl_xor((int)mx, o, kWave));
-    }
+    mn = wave_min_u32(mn);
+    mx = wave_max_u32(mx);
     if (lane == 0) {
       s_red[wave * 2] = mn;
       s_red[wave * 2 + 1] = mx;
@@ -1137,7 +1201,7 @@ __global__ __launch_bounds__(kSortNT) void k_sort2(int32_t E, int32_t B, int32_t
     const int nsub = max(1, min(kMaxSub, 2 * n));
     for (int i = tid; i < kMaxSub; i += kSortNT) s_sub[i] = 0;  // all of it: the scan reads whole int4s
     lds_barrier();
-    PROF(2)
+    PROF(5)
     mn = 0xFFFFFFFFu;
     mx = 0u;
 #pragma unroll
@@ -1156,7 +1220,7 @@ __global__ __launch_bounds__(kSortNT) void k_sort2(int32_t E, int32_t B, int32_t
       }
     }
     lds_barrier();
-    PROF(3)
+    PROF(6)
     {  // exclusive scan of the sub-bucket counts: 4 per thread, one 16-byte LDS access each way
        // (conflict-free; entries at or past nsub are zero and their scanned values unused)
       static_assert(kMaxSub == 4 * kSortNT, "one int4 of sub-buckets per thread");
@@ -1171,13 +1235,13 @@ __global__ __launch_bounds__(kSortNT) void k_sort2(int32_t E, int32_t B, int32_t
       reinterpret_cast<int4*>(s_sub)[tid] = ex;
     }
     lds_barrier();
-    PROF(4)
+    PROF(7)
     // scatter by sub-bucket (the cursor is the start; afterwards s_sub[i] = END of i)
 #pragma unroll
     for (int j = 0; j < kPer; ++j)
       if (j * kSortNT + tid < n) A[atomicAdd(&s_sub[sb[j]], 1)] = mine[j];
     lds_barrier();
-    PROF(5)
+    PROF(8)
 #pragma unroll
     for (int j = 0; j < kPer; ++j) {
       if (j * kSortNT + tid < n) {
@@ -1189,7 +1253,7 @@ __global__ __launch_bounds__(kSortNT) void k_sort2(int32_t E, int32_t B, int32_t
       }
     }
     lds_barrier();
-    PROF(6)
+    PROF(9)
 #pragma unroll
     for (int j = 0; j < kPer; ++j)
       if (j * kSortNT + tid < n) {
@@ -1197,7 +1261,7 @@ __global__ __launch_bounds__(kSortNT) void k_sort2(int32_t E, int32_t B, int32_t
         L[sb[j]] = lw[j];
       }
     lds_barrier();
-    PROF(7)
+    PROF(10)
     // fp64 in-bucket inclusive suffix sums: thread t owns the kPer-record chunk
     // c = kSortNT - 1 - t (chunks counted from the end of the bucket, so the exclusive scan over
     // lower threads is the mass of every later record), read and written as aligned 16-byte
@@ -1220,7 +1284,7 @@ __global__ __launch_bounds__(kSortNT) void k_sort2(int32_t E, int32_t B, int32_t
     }
     double wsum;
     double run = block_excl_scan_d<kSortNT, true>(loc, s_wd, &wsum);  // mass of all later records
-    PROF(8)
+    PROF(11)
     // (every read of A above is behind the scan's barriers)
     float fv[kPer];
 #pragma unroll
@@ -1242,7 +1306,7 @@ __global__ __launch_bounds__(kSortNT) void k_sort2(int32_t E, int32_t B, int32_t
     pv_act = actions + (int64_t)b * t_cap + s;
     pv_fwd = fwd + (int64_t)b * t_cap + s;
     lds_barrier();  // LDS reuse by the next bucket
-    PROF(9)
+    PROF(12)
   }
   flush();
   PROF_END(0)

@@ -29,7 +29,8 @@ for it in range(iters + 1):
 lib.spai_debug_prof(buf, 0)
 ncu = torch.cuda.get_device_properties(0).multi_processor_count
 kern = {
-    "k_sort2": (0, ["table", "gather", "minmax", "subcount", "subscan", "scatter", "rank", "place", "wscan", "store"], ncu),
+    "k_sort2": (0, ["wait", "flush", "map", "mapbar", "issue", "minmax", "subcount", "subscan", "scatter", "rank", "place",
+                 "wscan", "store"], ncu),
     "k_tile": (32, ["prologue", "keys", "histogram", "offsets", "win_place", "win_write"], ncu),
 }
 for name, (base, phases, resident) in kern.items():

@@ -65,6 +65,8 @@ constexpr int kFinNT = 256;
 constexpr int kMaxSamples = 1024;          // B per rollout call
 constexpr int kBufWord3 = 0x00020000;      // buffer resource dword 3 (raw byte addressing, gfx9 family)
 typedef unsigned int spai_u2 __attribute__((ext_vector_type(2)));
+typedef unsigned int spai_u3 __attribute__((ext_vector_type(3)));
+typedef unsigned int spai_u4 __attribute__((ext_vector_type(4)));
 constexpr int kBins = 4096;                // splitter histogram / bucket lookup table bins
 
 struct TrajWs {
@@ -82,8 +84,7 @@ struct TrajWs {
   uint32_t* spl;          // [B][kMaxB] ascending orderable splitters
   uint16_t* lut;          // [B][kBins] bucket lookup table
   uint32_t* lut_base;     // [B][2] (min key, shift) of the table
-  uint64_t* staging;      // [B][ntiles][kTile] (~ord << 32 | action), grouped by bucket per tile
-  float* stw;             // [B][ntiles][kTile] weight w of each staged record
+  uint32_t* staging;      // [B][ntiles][kTile][3] records {action, ~ord, bits of w}, grouped by bucket per tile
   int64_t wstride;        // row stride of rr / ww: E + 1 rounded up to 4 (16-byte aligned rows)
   float* rr;              // [B][wstride] inverse rates r_a = e^(l_E - l_a) (row 0 only: shared logits)
   float* ww;              // [B][wstride] weights w_a = e^(l_a - lmax)
@@ -118,8 +119,7 @@ static void traj_ws(void* base, int32_t E, int32_t B, TrajWs* w) {
   w->spl = c.take<uint32_t>((size_t)B * kMaxB);
   w->lut = c.take<uint16_t>((size_t)B * kBins);
   w->lut_base = c.take<uint32_t>((size_t)B * 2);
-  w->staging = c.take<uint64_t>((size_t)B * w->ntiles * kTile);
-  w->stw = c.take<float>((size_t)B * w->ntiles * kTile);
+  w->staging = c.take<uint32_t>((size_t)B * w->ntiles * kTile * 3);
   w->wstride = ((int64_t)E + 1 + 3) & ~(int64_t)3;
   w->rr = c.take<float>((size_t)B * w->wstride);
   w->ww = c.take<float>((size_t)B * w->wstride);
@@ -586,7 +586,7 @@ void k_tile(const float* __restrict__ rr, const float* __restrict__ ww, int64_t 
             const uint64_t* __restrict__ sctr, int32_t sample_base, int32_t part, int32_t nparts,
             uint32_t* __restrict__ removed, int32_t words, const int32_t* __restrict__ nb_,
             const uint32_t* __restrict__ spl_, const uint16_t* __restrict__ lut_,
-            const uint32_t* __restrict__ lut_base, uint64_t* __restrict__ staging, float* __restrict__ stw,
+            const uint32_t* __restrict__ lut_base, uint32_t* __restrict__ staging,
             uint32_t* __restrict__ runs, double* __restrict__ tbw, double* __restrict__ tile_wrest) {
   __shared__ uint64_t w_rec[kWin];  // one window of the grouped output
   __shared__ float w_log[kWin];
@@ -784,8 +784,7 @@ void k_tile(const float* __restrict__ rr, const float* __restrict__ ww, int64_t 
     if (q & 1) pp[q >> 1] |= pos << 16;
     else pp[q >> 1] = pos;
   }
-  uint64_t* st = staging + ((int64_t)b * ntiles + tile) * kTile;
-  float* sl = stw + ((int64_t)b * ntiles + tile) * kTile;
+  uint3* st = reinterpret_cast<uint3*>(staging) + ((int64_t)b * ntiles + tile) * kTile;
   // positional windows of kWin records staged in LDS, written out as whole cache lines
 #pragma unroll 1
   for (int w0 = 0; w0 < tot; w0 += kWin) {
@@ -803,9 +802,9 @@ void k_tile(const float* __restrict__ rr, const float* __restrict__ ww, int64_t 
     __syncthreads();
     PROF(4)
     const int cnt = min(kWin, tot - w0);
-    for (int e = tid; e < cnt; e += kGrpNT) {
-      st[w0 + e] = w_rec[e];
-      sl[w0 + e] = w_log[e];
+    for (int e = tid; e < cnt; e += kGrpNT) {  // one 12-byte record per lane
+      const uint64_t r = w_rec[e];
+      st[w0 + e] = make_uint3((uint32_t)r, (uint32_t)(r >> 32), __float_as_uint(w_log[e]));
     }
     __syncthreads();
     PROF(5)
@@ -989,7 +988,7 @@ __device__ void big_bucket_sort(uint64_t* __restrict__ s0, uint64_t* __restrict_
 // Oversized bucket (the sampled splitters missed; rare): gather into scratch, exact
 // in-block radix in global memory, then the same outputs as the LDS path.
 __device__ __forceinline__ void big_bucket(const int n, const int ntiles, const int* s_pre, const int* s_loc,
-                                           const uint64_t* stb, const float* wrow, int64_t* act_out,
+                                           const uint32_t* stb, const float* wrow, int64_t* act_out,
                                            float* fwd_out, uint64_t* s0, uint64_t* s1, const double later,
                                            int* s_wc, double* s_wd, uint32_t* s_red) {
   const int tid = threadIdx.x;
@@ -1000,7 +999,8 @@ __device__ __forceinline__ void big_bucket(const int n, const int ntiles, const 
       if (s_pre[mid] <= i) lo = mid;
       else hi = mid - 1;
     }
-    s0[i] = stb[(int64_t)lo * kTile + s_loc[lo] + (i - s_pre[lo])];
+    const uint32_t* r = stb + 3 * ((int64_t)lo * kTile + s_loc[lo] + (i - s_pre[lo]));
+    s0[i] = ((uint64_t)r[1] << 32) | r[0];
   }
   __syncthreads();
   big_bucket_sort(s0, s1, n, s_wc, s_red);
@@ -1034,8 +1034,7 @@ __global__ __launch_bounds__(kSortNT) void k_sort2(int32_t E, int32_t B, int32_t
                                                    const int32_t* __restrict__ nb_,
                                                    const int32_t* __restrict__ bstart,
                                                    const uint32_t* __restrict__ runs,
-                                                   const uint64_t* __restrict__ staging,
-                                                   const float* __restrict__ stw,
+                                                   const uint32_t* __restrict__ staging,
                                                    int64_t t_cap, int64_t* __restrict__ actions,
                                                    float* __restrict__ fwd, const double* __restrict__ wrest,
                                                    const double* __restrict__ bwsuf, int32_t* __restrict__ bigcnt,
@@ -1094,15 +1093,32 @@ __global__ __launch_bounds__(kSortNT) void k_sort2(int32_t E, int32_t B, int32_t
   int pv_n = 0;
   int64_t* pv_act = nullptr;
   float* pv_fwd = nullptr;
-  auto flush = [&]() {  // buffer stores: scalar bases, the range check drops the tail
+  auto flush = [&]() {  // 16-byte buffer stores with scalar bases (2 actions / 4 step probabilities per lane)
     const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(pv_act, 0, pv_n * 8, kBufWord3);
     const __amdgpu_buffer_rsrc_t rf = __builtin_amdgcn_make_buffer_rsrc(pv_fwd, 0, pv_n * 4, kBufWord3);
+    int tv = tid;
+    asm volatile("" : "+v"(tv));  // opaque: the lane offsets are recomputed here, not held across the loop
 #pragma unroll
-    for (int j = 0; j < kCap2 / kSortNT; ++j) {
-      const int i = j * kSortNT + tid;
-      if (j * kSortNT < pv_n) {
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(spai_u2, (uint64_t)a_out[i]), ra, i * 8, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(S[i]), rf, i * 4, 0, 0);
+    for (int j = 0; j < kCap2 / (2 * kSortNT); ++j) {
+      const int e = 2 * (j * kSortNT + tv);
+      if (2 * j * kSortNT < pv_n) {
+        const uint2 a = reinterpret_cast<const uint2*>(a_out)[e >> 1];
+        if (e + 1 < pv_n) __builtin_amdgcn_raw_buffer_store_b128((spai_u4){a.x, 0u, a.y, 0u}, ra, e * 8, 0, 0);
+        else if (e < pv_n) __builtin_amdgcn_raw_buffer_store_b64((spai_u2){a.x, 0u}, ra, e * 8, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < kCap2 / (4 * kSortNT); ++j) {
+      const int e = 4 * (j * kSortNT + tv);
+      if (4 * j * kSortNT < pv_n) {
+        const uint4 v = reinterpret_cast<const uint4*>(S)[e >> 2];
+        if (e + 3 < pv_n) {
+          __builtin_amdgcn_raw_buffer_store_b128((spai_u4){v.x, v.y, v.z, v.w}, rf, e * 4, 0, 0);
+        } else if (e < pv_n) {  // the bucket's last 1-3 step probabilities
+          __builtin_amdgcn_raw_buffer_store_b32(v.x, rf, e * 4, 0, 0);
+          if (e + 1 < pv_n) __builtin_amdgcn_raw_buffer_store_b32(v.y, rf, e * 4 + 4, 0, 0);
+          if (e + 2 < pv_n) __builtin_amdgcn_raw_buffer_store_b32(v.z, rf, e * 4 + 8, 0, 0);
+        }
       }
     }
     pv_n = 0;
@@ -1141,20 +1157,19 @@ __global__ __launch_bounds__(kSortNT) void k_sort2(int32_t E, int32_t B, int32_t
     lds_barrier();
     PROF(3)
     const bool ok = cn > 0 && cn <= kCap2;  // empty / oversized buckets are not gathered
-    // buffer loads (scalar base, 32-bit offsets); positions past the bucket read out of
-    // range (0; never used)
+    // one 12-byte buffer load per record (scalar base, 32-bit offsets); positions past the
+    // bucket read out of range (0; never used)
     const uint32_t nrec = (uint32_t)ntiles * kTile;
     const __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc((void*)(staging + (int64_t)cb * nrec), 0, nrec * 8, kBufWord3);
-    const __amdgpu_buffer_rsrc_t rw =
-        __builtin_amdgcn_make_buffer_rsrc((void*)(stw + (int64_t)cb * nrec), 0, nrec * 4, kBufWord3);
+        __builtin_amdgcn_make_buffer_rsrc((void*)(staging + (int64_t)cb * nrec * 3), 0, nrec * 12, kBufWord3);
 #pragma unroll
     for (int j = 0; j < kPer; ++j) {
       const int i = j * kSortNT + tid;
       const bool in = ok && i < cn;
-      const uint32_t d = in ? (uint32_t)(dlt[i] + i) : 0x10000000u;  // >= nrec: out of range
-      gm[j] = __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(rs, d * 8, 0, 0));
-      gw[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rw, d * 4, 0, 0));
+      const uint32_t d = in ? (uint32_t)(dlt[i] + i) : 0x08000000u;  // >= nrec: out of range
+      const spai_u3 r = __builtin_amdgcn_raw_buffer_load_b96(rs, d * 12, 0, 0);
+      gm[j] = ((uint64_t)r.y << 32) | r.x;
+      gw[j] = __uint_as_float(r.z);
     }
   };
   fetch(blockIdx.x, nxb, nxk, nxs0, nxs1, r0, r1, nxl);
@@ -1317,7 +1332,7 @@ __global__ __launch_bounds__(kSortNT) void k_sort2_big(int32_t E, int32_t B, int
                                                        const int32_t* __restrict__ nb_,
                                                        const int32_t* __restrict__ bstart,
                                                        const uint32_t* __restrict__ runs,
-                                                       const uint64_t* __restrict__ staging,
+                                                       const uint32_t* __restrict__ staging,
                                                        const float* __restrict__ ww, int64_t wrow_stride,
                                                        int64_t t_cap,
                                                        int64_t* __restrict__ actions, float* __restrict__ fwd,
@@ -1357,7 +1372,7 @@ __global__ __launch_bounds__(kSortNT) void k_sort2_big(int32_t E, int32_t B, int
     if (tid == 0) s_pre[ntiles] = tot;
     __syncthreads();
     int64_t* act_out = actions + (int64_t)b * t_cap + s;
-    big_bucket(n, ntiles, s_pre, s_loc, staging + (int64_t)b * ntiles * kTile, ww + (int64_t)b * wrow_stride,
+    big_bucket(n, ntiles, s_pre, s_loc, staging + (int64_t)b * ntiles * kTile * 3, ww + (int64_t)b * wrow_stride,
                act_out, fwd + (int64_t)b * t_cap + s, scratch + (int64_t)b * E + s, reinterpret_cast<uint64_t*>(act_out),
                wrest[b] + bwsuf[(int64_t)b * kMaxB + k], s_wc, s_wd, s_red);
     __syncthreads();
@@ -1497,7 +1512,7 @@ extern "C" int spai_rollout_select(const float* logits, int64_t bstride, int32_t
   SPAI_CHECK_LAUNCH();
   k_tile<<<w.ntiles * B, kGrpNT, 0, s>>>(w.rr, w.ww, w.wstride, rowsel, E, B, w.ntiles, s0, s1, t0, t1, stream_ctr,
                                          sample_base, part, nparts, removed, words, w.nb, w.spl, w.lut, w.lut_base,
-                                         w.staging, w.stw, w.runs, w.tbw, w.tile_wrest);
+                                         w.staging, w.runs, w.tbw, w.tile_wrest);
   SPAI_CHECK_LAUNCH();
   k_bsum<<<dim3(max_buckets(E) + 1, B), kBsumNT, 0, s>>>(w.ntiles, w.nb, w.runs, w.tbw, w.xch, stream_ctr, part,
                                                          nparts);
@@ -1547,7 +1562,7 @@ extern "C" int spai_rollout_sort(const float* logits, int64_t bstride, int32_t E
   const int nbm = max_buckets(E);
   const int g2 = std::max(1, std::min((nbm + nparts - 1) / nparts * B, num_cus()));
   const int64_t wrs = bstride ? w.wstride : 0;
-  k_sort2<<<g2, kSortNT, 0, s>>>(E, B, w.ntiles, w.nb, w.bstart, w.runs, w.staging, w.stw, t_cap, actions, fwd_probs,
+  k_sort2<<<g2, kSortNT, 0, s>>>(E, B, w.ntiles, w.nb, w.bstart, w.runs, w.staging, t_cap, actions, fwd_probs,
                                  w.wrest, w.bwsuf, w.bigcnt, w.biglist, part, nparts);
   SPAI_CHECK_LAUNCH();
   k_sort2_big<<<g2, kSortNT, 0, s>>>(E, B, w.ntiles, w.nb, w.bstart, w.runs, w.staging, w.ww, wrs, t_cap, actions,

@@ -14,20 +14,23 @@
 //                w = e^(l - lmax) once per logits row (shared by every sample of the row).
 //   k_splitters  per sample: value-linear histogram quantiles of the sampled winner keys
 //                -> nb ~ est/4096 bucket splitters and a 4096-bin bucket lookup table.
-//   k_tile       one kTile (16384)-action tile of one sample per block (the samples of a
-//                tile share an XCD and its L2): Philox4x32-10 + deterministic fp32 arrival
-//                times (in registers), removal bitmap words, the fp64 mass of the untouched
-//                actions, bucket histogram with in-bucket ranks, and the tile's winners
-//                written grouped by bucket through LDS windows as one contiguous 8 B record
-//                stream + 4 B weight stream; per-(bucket, tile) runs in a bucket-major table
-//                (one contiguous row per bucket).
-//   k_bscan      per sample: bucket starts, winner count, untouched mass, T.
-//   k_sort2      persistent; per bucket: one-round-trip gather of its runs (one per tile)
-//                into registers, value-linear sub-buckets + rank counting in LDS, fp64
-//                in-bucket suffix sums of the weights.  Outputs stored during the next
-//                bucket.  Buckets above the LDS capacity: k_sort2_big.
-//   k_wscan      per sample suffix over the bucket weight sums (fixed order).
-//   k_final      fwd_probs = w / (W_rest + later buckets + in-bucket suffix).
+//   k_tile       one kTile (8192)-action tile of one sample per 512-thread block, two blocks
+//                per CU (the samples of a tile share an XCD and its L2): Philox4x32-10 +
+//                deterministic fp32 arrival times (in registers), removal bitmap words, the
+//                fp64 mass of the untouched actions, bucket histogram with in-bucket ranks
+//                and fixed-point per-bucket weight sums, and the tile's winners written
+//                grouped by bucket through an LDS window as 12-byte records {action, key,
+//                weight}; per-(bucket, tile) runs in a bucket-major table (one contiguous
+//                row per bucket).
+//   k_bsum       per (sample, bucket): winner count and weight sum over the tiles (the
+//                exchange array of a split rollout).
+//   k_bscan      per sample: bucket starts, winner count, untouched mass, later-bucket
+//                suffix sums, T.
+//   k_sort2      persistent, software-pipelined: the next bucket's runs (one per tile) are
+//                gathered into registers while the current bucket is ranked in value-linear
+//                LDS sub-buckets; fp64 in-bucket suffix sums and
+//                fwd_probs = w / (W_rest + later buckets + in-bucket suffix).  Outputs stored
+//                during the next bucket.  Buckets above the LDS capacity: k_sort2_big.
 //   k_pad        terminal step, -1 / 1.0 padding up to T = max_b k_b + 1.
 // The step probability is formed from the mass still available at step t (untouched
 // actions + trajectory suffix), so no "Z - prefix" cancellation occurs.  Every sum is taken
@@ -39,18 +42,18 @@ namespace spai {
 namespace {
 
 #ifndef KTILE
-#define KTILE 16384
+#define KTILE 8192
 #endif
 constexpr int kTile = KTILE;               // actions per tile (k_tile block; a run per bucket)
 static_assert(kTile <= 65535, "run offsets and counts are packed in 16 bits (k_tile, k_sort2)");
 #ifndef KGRPNT
-#define KGRPNT 1024
+#define KGRPNT 512
 #endif
 constexpr int kGrpNT = KGRPNT;             // threads of a k_tile block (16 actions each)
 #ifndef KWIN
-#define KWIN 8192
+#define KWIN 4096
 #endif
-constexpr int kWin = KWIN;                 // records per LDS output window of k_tile (1 block/CU)
+constexpr int kWin = KWIN;                 // records per LDS output window of k_tile (2 blocks/CU)
 constexpr int kSampM = 65536;              // subset size (power of two, capped by E)
 constexpr int kSampNT = 256;
 constexpr int kSampCap = 32768;            // sampled winners behind the splitters
@@ -565,7 +568,7 @@ __device__ __forceinline__ uint64_t weight_fixed(float w) {
 }
 
 // ------------------------------------------------------------------ k_tile
-// Selection and grouping fused, one 16384-action tile of one sample per block: arrival times
+// Selection and grouping fused, one 8192-action tile of one sample per block: arrival times
 // of the tile (16 actions per thread; times and weights kept in registers), the removed
 // bitmap, the rest mass of the tile's non-winners, then the grouping steps on the
 // register-resident winners: bucket histogram, per-(bucket, tile) runs, and the winners

@@ -666,16 +666,11 @@ void k_tile(const float* __restrict__ rr, const float* __restrict__ ww, int64_t 
     const float ts[4] = {t01.x, t01.y, t23.x, t23.y};
     uint32_t nib = 0;
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      ord[4 * g + s] = 0u;
-      if (a0 + s < E) {
-        if (ts[s] < tE) {
-          nib |= 1u << s;
-          ord[4 * g + s] = arrival_ord(ts[s]);
-        } else {
-          wr += (double)lvk[4 * g + s];
-        }
-      }
+    for (int s = 0; s < 4; ++s) {  // branch-free (selects, no exec-mask branches per slot)
+      const bool real = a0 + s < E, w = real && ts[s] < tE;
+      nib |= (uint32_t)w << s;
+      ord[4 * g + s] = w ? arrival_ord(ts[s]) : 0u;
+      wr += (real && !w) ? (double)lvk[4 * g + s] : 0.0;
     }
     win |= nib << (4 * g);
     // removed bitmap: 8 adjacent threads make one 32-bit word
@@ -1402,14 +1397,25 @@ __global__ __launch_bounds__(kFinNT) void k_pad(int32_t E, const int32_t* __rest
   if (!do_pad) return;  // the terminal step and the padding belong to the last part
   int64_t* ab = actions + (int64_t)b * t_cap;
   float* fb = fwd + (int64_t)b * t_cap;
-  for (int t = k + blockIdx.x * kFinNT + threadIdx.x; t < T; t += gridDim.x * kFinNT) {
-    if (t == k) {
-      const double wE = (double)ww[(int64_t)b * wrow_stride + E];
-      ab[t] = E;
-      fb[t] = (float)(wE / wrest[b]);
+  if (blockIdx.x == 0 && threadIdx.x == 0 && k < T) {  // the terminal step
+    const double wE = (double)ww[(int64_t)b * wrow_stride + E];
+    ab[k] = E;
+    fb[k] = (float)(wE / wrest[b]);
+  }
+  // padding k+1 .. T-1, four slots per thread: 2 x 16-byte action stores + one 16-byte
+  // probability store (4-byte alignment suffices for vector stores on gfx950)
+  const int p0 = k + 1;
+  for (int t = p0 + 4 * (blockIdx.x * kFinNT + threadIdx.x); t < T; t += 4 * gridDim.x * kFinNT) {
+    if (t + 3 < T) {
+      longlong2* a2 = reinterpret_cast<longlong2*>(ab + t);
+      a2[0] = make_longlong2(-1, -1);
+      a2[1] = make_longlong2(-1, -1);
+      *reinterpret_cast<float4*>(fb + t) = make_float4(1.0f, 1.0f, 1.0f, 1.0f);
     } else {
-      ab[t] = -1;
-      fb[t] = 1.0f;
+      for (int u = t; u < T; ++u) {
+        ab[u] = -1;
+        fb[u] = 1.0f;
+      }
     }
   }
 }

@@ -54,6 +54,7 @@ constexpr int kGrpNT = KGRPNT;             // threads of a k_tile block (16 acti
 #define KWIN 4096
 #endif
 constexpr int kWin = KWIN;                 // records per LDS output window of k_tile (2 blocks/CU)
+constexpr int kList = 2730;                // compacted winners per k_tile block (<= 1/3 of the tile; denser: slot path)
 constexpr int kSampM = 65536;              // subset size (power of two, capped by E)
 constexpr int kSampNT = 256;
 constexpr int kSampCap = 32768;            // sampled winners behind the splitters
@@ -583,7 +584,7 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
   const int x = orig % kXcd, q = nwg / kXcd, r = nwg % kXcd;
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + orig / kXcd;
 }
-__global__ __launch_bounds__(kGrpNT)
+__global__ __launch_bounds__(kGrpNT) __attribute__((amdgpu_waves_per_eu(2 * kGrpNT / 256)))  // two blocks per CU
 void k_tile(const float* __restrict__ rr, const float* __restrict__ ww, int64_t wstride, int64_t rowsel,
             int32_t E, int32_t B, int32_t ntiles, uint32_t seed0, uint32_t seed1, uint32_t st0, uint32_t st1,
             const uint64_t* __restrict__ sctr, int32_t sample_base, int32_t part, int32_t nparts,
@@ -591,8 +592,18 @@ void k_tile(const float* __restrict__ rr, const float* __restrict__ ww, int64_t 
             const uint32_t* __restrict__ spl_, const uint16_t* __restrict__ lut_,
             const uint32_t* __restrict__ lut_base, uint32_t* __restrict__ staging,
             uint32_t* __restrict__ runs, double* __restrict__ tbw, double* __restrict__ tile_wrest) {
-  __shared__ uint64_t w_rec[kWin];  // one window of the grouped output
-  __shared__ float w_log[kWin];
+  // LDS regions (two blocks per CU: <= 80 KB per block):
+  //   s_r0: the fixed-point bucket sums during the histogram, then the record window (slot
+  //         path: w_rec; compacted path: 12-byte records)
+  //   s_r1: the compacted winner list (keys, tile-local ids; slot path: the window's weights)
+  __shared__ __attribute__((aligned(16))) uint64_t s_r0[kWin];
+  __shared__ __attribute__((aligned(16))) uint32_t s_r1[kWin];
+  static_assert(kList * 3 <= kWin * 2 && kList * 6 <= kWin * 4 && kList % 2 == 0, "LDS region sizes");
+  uint64_t* w_rec = s_r0;  // one window of the grouped output
+  float* w_log = reinterpret_cast<float*>(s_r1);
+  uint32_t* l_ord = s_r1;
+  uint16_t* l_id = reinterpret_cast<uint16_t*>(s_r1 + kList);
+  uint32_t* w_r3 = reinterpret_cast<uint32_t*>(s_r0);  // compacted path: {action, ~key, w} per record
   __shared__ __attribute__((aligned(16))) uint32_t s_spl[kMaxB];
   __shared__ int s_off[kMaxB + 1];  // histogram, then tile-local bucket offsets
   __shared__ __attribute__((aligned(16))) uint16_t s_lut[kBins];
@@ -628,7 +639,7 @@ void k_tile(const float* __restrict__ rr, const float* __restrict__ ww, int64_t 
   // 2^-69 (a tile adds <= 2^14 terms, so neither overflows 64 bits; every w >= 2^-45 is exact).
   // The two [kMaxB] u64 arrays live in the record window, unused until the placement.
   static_assert(kWin * 8 >= 2 * kMaxB * 8, "fixed-point accumulators alias the record window");
-  uint64_t* s_fx = w_rec;
+  uint64_t* s_fx = s_r0;
   for (int k = tid; k < 2 * kMaxB; k += kGrpNT) s_fx[k] = 0ull;
   const uint32_t lmn = lut_base[2 * b];
   const int lsh = (int)lut_base[2 * b + 1];
@@ -708,12 +719,74 @@ void k_tile(const float* __restrict__ rr, const float* __restrict__ ww, int64_t 
   // bucket histogram of the part's winners; each winner keeps its bucket and its rank inside
   // the bucket (the histogram atomic's return; any order: the level-2 sort orders buckets fully)
   static_assert(kMaxB <= (1 << 11) && kTile <= (1 << 21), "bucket | rank << 11 packing");
-  // bucket of a winner's orderable key (buckets numbered in trajectory order, descending key):
-  // value-linear lookup table, then the splitters, for all the thread's slots at once: the table
-  // guesses of every slot are read together, then wave-uniform correction rounds over the
-  // splitters (usually one step and one check), so the LDS reads of the slots overlap instead of
-  // forming one dependent chain each
+  // Compacted path (the usual case: the part's winners fit the list, i.e. <= ~49 % of the tile):
+  // the winners are first packed into an LDS list, so the bucket lookup, the rank and weight
+  // atomics and the placement run once per WINNER over all lanes, instead of once per slot
+  // (16 per thread, mostly losers) as on the slot path below.
+  int totw;
+  const int wbase = block_excl_scan<kGrpNT>(__popc(win), s_wc, &totw);
+  const bool compact = totw <= kList;  // block-uniform
+  constexpr int kPerT = (kList + kGrpNT - 1) / kGrpNT;
+  uint32_t ebr[kPerT];  // bucket | rank << 11 of the thread's list entries (kept across the scan)
   int bc[4 * kTileG];
+  uint32_t br[4 * kTileG];
+  if (compact) {
+#pragma unroll
+    for (int q = 0; q < 4 * kTileG; ++q)
+      if ((win >> q) & 1u) {
+        const int k = wbase + __popc(win & ((1u << q) - 1u));
+        l_ord[k] = ord[q];
+        l_id[k] = (uint16_t)((q >> 2) * 4 * kGrpNT + 4 * tid + (q & 3));
+      }
+    __syncthreads();
+    PROF(6)
+    uint32_t eo[kPerT], eid[kPerT];
+    float ew[kPerT];
+#pragma unroll
+    for (int i = 0; i < kPerT; ++i) {
+      const int e = tid + i * kGrpNT;
+      const bool v = e < totw;
+      eo[i] = v ? l_ord[e] : 0u;
+      eid[i] = v ? (uint32_t)l_id[e] : 0u;
+    }
+#pragma unroll
+    for (int i = 0; i < kPerT; ++i)  // the weights again from the tile's row (L2: this block read it)
+      ew[i] = tid + i * kGrpNT < totw ? wrow[a_t + (int)eid[i]] : 0.0f;
+    int ebc[kPerT];
+#pragma unroll
+    for (int i = 0; i < kPerT; ++i) {
+      const uint32_t o = eo[i];
+      const uint32_t bin = o < lmn ? 0u : min((uint32_t)(kBins - 1), (o - lmn) >> lsh);
+      ebc[i] = s_lut[bin];
+    }
+    bool more;
+    do {
+      more = false;
+#pragma unroll
+      for (int i = 0; i < kPerT; ++i) {
+        const uint32_t sv = s_spl[max(0, min(ebc[i], nbl - 1))];
+        const bool step = tid + i * kGrpNT < totw && ebc[i] < nbl && sv <= eo[i];
+        ebc[i] += step;
+        more |= step;
+      }
+    } while (__any(more));
+    PROF(7)
+#pragma unroll
+    for (int i = 0; i < kPerT; ++i) {
+      ebr[i] = 0u;
+      if (tid + i * kGrpNT < totw) {
+        const int bk = nbl - ebc[i];
+        ebr[i] = (uint32_t)bk | ((uint32_t)atomicAdd(&s_off[bk], 1) << 11);
+        atomicAdd((unsigned long long*)&s_fx[bk + (ew[i] >= 9.5367431640625e-07f ? 0 : kMaxB)],
+                  (unsigned long long)weight_fixed(ew[i]));
+      }
+    }
+  } else {
+  // slot path (dense tiles): bucket of a winner's orderable key (buckets numbered in
+  // trajectory order, descending key): value-linear lookup table, then the splitters, for all
+  // the thread's slots at once: the table guesses of every slot are read together, then
+  // wave-uniform correction rounds over the splitters (usually one step and one check), so the
+  // LDS reads of the slots overlap instead of forming one dependent chain each
 #pragma unroll
   for (int q = 0; q < 4 * kTileG; ++q) {
     const uint32_t o = ord[q];
@@ -731,7 +804,6 @@ void k_tile(const float* __restrict__ rr, const float* __restrict__ ww, int64_t 
       more |= step;
     }
   } while (__any(more));
-  uint32_t br[4 * kTileG];
 #pragma unroll
   for (int q = 0; q < 4 * kTileG; ++q) {
     br[q] = 0u;
@@ -741,6 +813,7 @@ void k_tile(const float* __restrict__ rr, const float* __restrict__ ww, int64_t 
       atomicAdd((unsigned long long*)&s_fx[bk + (lvk[q] >= 9.5367431640625e-07f ? 0 : kMaxB)],
                 (unsigned long long)weight_fixed(lvk[q]));
     }
+  }
   }
   __syncthreads();
   PROF(2)
@@ -774,6 +847,27 @@ void k_tile(const float* __restrict__ rr, const float* __restrict__ ww, int64_t 
   }
   __syncthreads();
   PROF(3)
+  uint3* st = reinterpret_cast<uint3*>(staging) + ((int64_t)b * ntiles + tile) * kTile;
+  if (compact) {  // one window of 12-byte records holds the tile (tot <= kList); the list is intact
+#pragma unroll
+    for (int i = 0; i < kPerT; ++i) {
+      const int e = tid + i * kGrpNT;
+      if (e < totw) {
+        const int p = s_off[ebr[i] & 0x7FFu] + (int)(ebr[i] >> 11);
+        const uint32_t id = l_id[e];
+        w_r3[3 * p] = (uint32_t)a_t + id;
+        w_r3[3 * p + 1] = ~l_ord[e];
+        w_r3[3 * p + 2] = __float_as_uint(wrow[a_t + (int)id]);  // L2 (read twice by this block)
+      }
+    }
+    __syncthreads();
+    PROF(4)
+    for (int e = tid; e < tot; e += kGrpNT)  // one 12-byte record per lane (LDS stride 3: conflict-free)
+      st[e] = make_uint3(w_r3[3 * e], w_r3[3 * e + 1], w_r3[3 * e + 2]);
+    PROF(5)
+    PROF_END(32)
+    return;
+  }
   // final tile-local position of every winner, two per VGPR
   uint32_t pp[2 * kTileG];
 #pragma unroll
@@ -782,7 +876,6 @@ void k_tile(const float* __restrict__ rr, const float* __restrict__ ww, int64_t 
     if (q & 1) pp[q >> 1] |= pos << 16;
     else pp[q >> 1] = pos;
   }
-  uint3* st = reinterpret_cast<uint3*>(staging) + ((int64_t)b * ntiles + tile) * kTile;
   // positional windows of kWin records staged in LDS, written out as whole cache lines
 #pragma unroll 1
   for (int w0 = 0; w0 < tot; w0 += kWin) {

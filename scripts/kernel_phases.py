@@ -31,7 +31,7 @@ ncu = torch.cuda.get_device_properties(0).multi_processor_count
 kern = {
     "k_sort2": (0, ["wait", "flush", "map", "mapbar", "issue", "minmax", "subcount", "subscan", "scatter", "rank", "place",
                  "wscan", "store"], ncu),
-    "k_tile": (32, ["prologue", "keys", "atomics", "offsets", "win_place", "win_write", "lut", "rounds"], ncu),
+    "k_tile": (32, ["prologue", "keys", "atomics", "offsets", "win_place", "win_write", "list", "lut_rounds"], ncu),
 }
 for name, (base, phases, resident) in kern.items():
     tot = sum(buf[base + i] for i in range(len(phases)))

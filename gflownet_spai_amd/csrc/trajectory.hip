@@ -684,16 +684,17 @@ void k_tile(const float* __restrict__ rr, const float* __restrict__ ww, int64_t 
       wr += (real && !w) ? (double)lvk[4 * g + s] : 0.0;
     }
     win |= nib << (4 * g);
-    // removed bitmap: 8 adjacent threads make one 32-bit word
+    // removed bitmap: 8 adjacent threads make one 32-bit word (OR over the 8 lanes by DPP:
+    // quad_perm [1,0,3,2], [2,3,0,1], then row_half_mirror joins the two quads)
     uint32_t x = nib << ((tid & 7) * 4);
-    x |= __shfl_xor(x, 1, kWave);
-    x |= __shfl_xor(x, 2, kWave);
-    x |= __shfl_xor(x, 4, kWave);
+    x |= (uint32_t)dpp_i<0xB1, 0xf>(0, (int)x);
+    x |= (uint32_t)dpp_i<0x4E, 0xf>(0, (int)x);
+    x |= (uint32_t)dpp_i<0x141, 0xf>(0, (int)x);
     const int wi = a0 >> 5;
     if ((tid & 7) == 0 && a0 < E && wi < words) removed[(int64_t)b * words + wi] = x;
   }
-  wr = wave_sum(wr);
-  if (lane == 0) s_wr[wave] = wr;
+  wr = wave_incl_scan_d(wr);  // lane 63 holds the wave's total (DPP, fixed order)
+  if (lane == 63) s_wr[wave] = wr;
   __syncthreads();  // splitter tables, zeroed histogram
   PROF(1)
   if (tid == 0) {

@@ -54,7 +54,11 @@ constexpr int kGrpNT = KGRPNT;             // threads of a k_tile block (16 acti
 #define KWIN 4096
 #endif
 constexpr int kWin = KWIN;                 // records per LDS output window of k_tile (2 blocks/CU)
+#ifdef KTILE_LISTWIN
 constexpr int kList = 2730;                // compacted winners per k_tile block (<= 1/3 of the tile; denser: slot path)
+#else
+constexpr int kList = 4000;                // compacted winners per k_tile block (<= 49 % of the tile; denser: slot path)
+#endif
 constexpr int kSampM = 65536;              // subset size (power of two, capped by E)
 constexpr int kSampNT = 256;
 constexpr int kSampCap = 32768;            // sampled winners behind the splitters
@@ -597,8 +601,13 @@ void k_tile(const float* __restrict__ rr, const float* __restrict__ ww, int64_t 
   //         path: w_rec; compacted path: 12-byte records)
   //   s_r1: the compacted winner list (keys, tile-local ids; slot path: the window's weights)
   __shared__ __attribute__((aligned(16))) uint64_t s_r0[kWin];
+#ifdef KTILE_LISTWIN
   __shared__ __attribute__((aligned(16))) uint32_t s_r1[kWin];
   static_assert(kList * 3 <= kWin * 2 && kList * 6 <= kWin * 4 && kList % 2 == 0, "LDS region sizes");
+#else
+  __shared__ __attribute__((aligned(16))) uint32_t s_r1[kList + kList / 2];
+  static_assert(kWin <= kList + kList / 2 && kList % 2 == 0, "LDS region sizes");
+#endif
   uint64_t* w_rec = s_r0;  // one window of the grouped output
   float* w_log = reinterpret_cast<float*>(s_r1);
   uint32_t* l_ord = s_r1;
@@ -849,7 +858,24 @@ void k_tile(const float* __restrict__ rr, const float* __restrict__ ww, int64_t 
   __syncthreads();
   PROF(3)
   uint3* st = reinterpret_cast<uint3*>(staging) + ((int64_t)b * ntiles + tile) * kTile;
-  if (compact) {  // one window of 12-byte records holds the tile (tot <= kList); the list is intact
+  if (compact) {
+#ifndef KTILE_LISTWIN
+    // straight to the staging position (one 12-byte store per winner; the tile's region stays in L2)
+#pragma unroll
+    for (int i = 0; i < kPerT; ++i) {
+      const int e = tid + i * kGrpNT;
+      if (e < totw) {
+        const int p = s_off[ebr[i] & 0x7FFu] + (int)(ebr[i] >> 11);
+        const uint32_t id = l_id[e];
+        st[p] = make_uint3((uint32_t)a_t + id, ~l_ord[e], __float_as_uint(wrow[a_t + (int)id]));
+      }
+    }
+    PROF(4)
+    PROF(5)
+    PROF_END(32)
+    return;
+#endif
+    // one window of 12-byte records holds the tile (tot <= kList); the list is intact
 #pragma unroll
     for (int i = 0; i < kPerT; ++i) {
       const int e = tid + i * kGrpNT;

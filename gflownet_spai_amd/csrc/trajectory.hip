@@ -1274,14 +1274,19 @@ __global__ __launch_bounds__(kSortNT) void k_sort2(int32_t E, int32_t B, int32_t
     fetch(fnext, nxb, nxk, nxs0, nxs1, r0, r1, nxl);
     lds_barrier();
     PROF(3)
+  };
+  // the staged bucket's gather, records [j0, j0 + 2) of every thread: one 12-byte buffer load per
+  // record (scalar base, 32-bit offsets; positions past the bucket read out of range: 0, never
+  // used).  Issued two at a time between the current bucket's LDS phases, so the waves do not
+  // stall on one burst of memory instructions; the map stays in S until the suffix phase.
+  auto issue = [&](const int j0) {
     const bool ok = cn > 0 && cn <= kCap2;  // empty / oversized buckets are not gathered
-    // one 12-byte buffer load per record (scalar base, 32-bit offsets); positions past the
-    // bucket read out of range (0; never used)
     const uint32_t nrec = (uint32_t)ntiles * kTile;
     const __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc((void*)(staging + (int64_t)cb * nrec * 3), 0, nrec * 12, kBufWord3);
 #pragma unroll
-    for (int j = 0; j < kPer; ++j) {
+    for (int jj = 0; jj < 2; ++jj) {
+      const int j = j0 + jj;
       const int i = j * kSortNT + tid;
       const bool in = ok && i < cn;
       const uint32_t d = in ? (uint32_t)(dlt[i] + i) : 0x08000000u;  // >= nrec: out of range
@@ -1290,9 +1295,14 @@ __global__ __launch_bounds__(kSortNT) void k_sort2(int32_t E, int32_t B, int32_t
       gw[j] = __uint_as_float(r.z);
     }
   };
+  static_assert(kPer == 8, "four gather issues of two records");
   fetch(blockIdx.x, nxb, nxk, nxs0, nxs1, r0, r1, nxl);
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
   stage(blockIdx.x + gridDim.x);
+  issue(0);
+  issue(2);
+  issue(4);
+  issue(6);
 #pragma unroll 1
   for (int f = blockIdx.x; f < total; f += gridDim.x) {
     // this bucket's records and the next bucket's run table have landed (and the previous
@@ -1310,9 +1320,13 @@ __global__ __launch_bounds__(kSortNT) void k_sort2(int32_t E, int32_t B, int32_t
     PROF(0)
     flush();  // the previous bucket's outputs (drain during this bucket's LDS phases)
     PROF(1)
-    stage(f + 2 * gridDim.x);  // map + gather of the next bucket
+    stage(f + 2 * gridDim.x);  // map of the next bucket; its gather is issued in four parts below
+    issue(0);
     PROF(4)
     if (n == 0 || n > kCap2) {
+      issue(2);
+      issue(4);
+      issue(6);
       if (n > kCap2 && tid == 0) biglist[atomicAdd(bigcnt, 1)] = (b << 16) | k;  // for k_sort2_big (rare)
       continue;
     }
@@ -1335,6 +1349,7 @@ __global__ __launch_bounds__(kSortNT) void k_sort2(int32_t E, int32_t B, int32_t
     for (int i = tid; i < kMaxSub; i += kSortNT) s_sub[i] = 0;  // all of it: the scan reads whole int4s
     lds_barrier();
     PROF(5)
+    issue(2);
     mn = 0xFFFFFFFFu;
     mx = 0u;
 #pragma unroll
@@ -1369,6 +1384,7 @@ __global__ __launch_bounds__(kSortNT) void k_sort2(int32_t E, int32_t B, int32_t
     }
     lds_barrier();
     PROF(7)
+    issue(4);
     // scatter by sub-bucket (the cursor is the start; afterwards s_sub[i] = END of i)
 #pragma unroll
     for (int j = 0; j < kPer; ++j)
@@ -1387,6 +1403,7 @@ __global__ __launch_bounds__(kSortNT) void k_sort2(int32_t E, int32_t B, int32_t
     }
     lds_barrier();
     PROF(9)
+    issue(6);
 #pragma unroll
     for (int j = 0; j < kPer; ++j)
       if (j * kSortNT + tid < n) {

@@ -9,7 +9,7 @@ O=gpurun_out/round_$TAG
 mkdir -p $O
 step() { echo "== $1"; }
 step pytest
-timeout -k 10 600 python -m pytest tests -m gpu -q > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
 tail -1 $O/pytest.log
 step smoke
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }

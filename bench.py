@@ -196,8 +196,8 @@ def generic_residual_leg(env, log, reps: int = 10):
     """The generic SpMM residual (spai_residual_lines: ||A M_b - I||_F^2 of B arbitrary sparse
     M_b, preconditioner.py:79-93 for any M) on the step's B candidates: their stored LSQ values
     with each candidate's own kept index set (removed slots -> -1).  Timed with HIP events on
-    the launch stream; algorithmic bytes per launch = B x (bytes(A) + bytes(M_b)) (SURVEY §8d:
-    A and M_b read once per sample).  Also checks the result against the fused fill kernel's
+    the launch stream; algorithmic bytes per launch = bytes(A) + B x bytes(M_b) (SURVEY §8d
+    with A shared by the batch: the kernel reads each line of A once for all B samples).  Also checks the result against the fused fill kernel's
     residual (they differ by d^T G d, d = the fp32 rounding of M)."""
     from gflownet_spai_amd import kernels
     pat, a = env.pattern, env.a_lines
@@ -218,9 +218,10 @@ def generic_residual_leg(env, log, reps: int = 10):
     rel = float(((res2 - ref).abs() / ref).max())
     bytes_a = a.idx.numel() * 4 + a.val.numel() * a.val.element_size()
     bytes_m = n * W * (4 + m.element_size())
-    out = roofline_obj(f"k_resid<{W},{a.width},{str(a.val.dtype)[6:]},{str(m.dtype)[6:]}> (||A M_b - I||_F^2 of "
-                       f"B={B} arbitrary sparse M_b: the step's LSQ fills with their own kept index sets)",
-                       B * (bytes_a + bytes_m), ms)
+    name = "k_resid_shared" if W <= 7 else "k_resid"
+    out = roofline_obj(f"{name}<{W},{a.width},{str(a.val.dtype)[6:]},{str(m.dtype)[6:]}> (||A M_b - I||_F^2 of "
+                       f"B={B} arbitrary sparse M_b: the step's LSQ fills with their own kept index sets; "
+                       f"bytes = bytes(A) + B x bytes(M_b))", bytes_a + B * bytes_m, ms)
     out["max_rel_diff_vs_fused_fill"] = rel
     return out
 

@@ -8,14 +8,19 @@
 //     || sum_p m_p A_line(k_p) - e_l ||^2 = 1 - 2 sum_p m_p A_line(k_p)[l]
 //                                         + sum_{p,q} m_p m_q <A_line(k_p), A_line(k_q)>
 // (sparse dot products by index matching over the WA x WA entry pairs, one compare and one
-// select each; fp64 accumulation of the products, as k_line).  One thread per (line, sample): it reads the W slots of its line
-// of M_b and gathers the W lines of A they name.  A block covers 256 consecutive lines of one
-// sample; the B blocks of one line range are consecutive blocks of ONE XCD (bijective XCD
-// remap), so the A lines they gather (the same neighbourhood for every sample) are fetched
-// from HBM once and served to the other samples by that XCD's L2.  Per-block partial sums,
-// then a fixed-order reduction per sample: the result is bit-reproducible.
+// select each; fp64 accumulation of the products, as k_line).
 //
-// Algorithmic bytes per sample: bytes(A) + bytes(M_b).
+// W <= 7 (k_resid_shared): one thread per line for ALL B samples.  The Gram of the line's
+// slots (the index matching: all of the arithmetic) is formed once per chunk of 8 samples on
+// the union of their index sets when they agree slot by slot (sub-patterns of one pattern, the
+// GFlowNet candidates), then each sample is a W x W quadratic form; lanes whose samples
+// disagree evaluate each sample on its own index set.  A is read once per line for the batch:
+// algorithmic bytes per launch = bytes(A) + sum_b bytes(M_b) (SURVEY §8d with A shared by the
+// batch).  Consecutive line ranges run on one XCD (bijective XCD remap), so the A halo of
+// neighbouring blocks is served by that XCD's L2.
+// W = 13 (k_resid): one thread per (line, sample); the B blocks of one line range on one XCD.
+// Per-block partial sums, then a fixed-order reduction per sample: the result is
+// bit-reproducible, and both kernels evaluate a line with the same operations in the same order.
 #include "spai_device.h"
 #include "spai_status.h"
 
@@ -30,6 +35,93 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + orig / kXcd;
 }
 
+// The W lines of A named by k[0..W) (k < 0: empty, index -1 / value 0).  Every load is
+// unconditional from a clamped address (line 0 / the line's last slot) and masked afterwards:
+// no branch around a load, so all of them are in flight together.
+template <int W, int WA, typename TA>
+__device__ __forceinline__ void gather_a_lines(const int (&k)[W], int wart, const int32_t* __restrict__ a_idx,
+                                               const TA* __restrict__ a_val, int (&ai)[W][WA], TA (&av)[W][WA]) {
+#pragma unroll
+  for (int p = 0; p < W; ++p) {
+    const int64_t base = (int64_t)max(k[p], 0) * wart;
+#pragma unroll
+    for (int s = 0; s < WA; ++s) {
+      const int64_t o = base + min(s, wart - 1);
+      const int i = a_idx[o];
+      const TA x = a_val[o];
+      const bool on = k[p] >= 0 && s < wart;
+      ai[p][s] = on ? i : -1;
+      av[p][s] = on ? x : (TA)0;
+    }
+  }
+}
+
+// Line Gram of M's slots against line j of A-product space:
+//   c_p = A_line(k_p)[j],  G_pp = ||A_line(k_p)||^2,  G_pq = <A_line(k_p), A_line(k_q)> (q > p).
+// An index occurs at most once per line: entry s of line p meets at most one entry of line q,
+// so a select chain in A's own precision (one compare + one select per entry pair) finds its
+// partner's value; padding entries (index -1, value 0) add nothing.  fp64 accumulation.
+template <int W, int WA, typename TA>
+__device__ __forceinline__ void line_gram(const int (&ai)[W][WA], const TA (&av)[W][WA], int j, double (&c)[W],
+                                          double (&gd)[W], double (&go)[W * (W - 1) / 2]) {
+  int o = 0;
+#pragma unroll
+  for (int p = 0; p < W; ++p) {
+    double cp = 0.0, gpp = 0.0;
+#pragma unroll
+    for (int s = 0; s < WA; ++s) {
+      const double x = (double)av[p][s];
+      gpp += x * x;
+      cp += (ai[p][s] == j) ? x : 0.0;
+    }
+    c[p] = cp;
+    gd[p] = gpp;
+#pragma unroll
+    for (int q = p + 1; q < W; ++q) {
+      double g = 0.0;
+#pragma unroll
+      for (int s = 0; s < WA; ++s) {
+        TA m = (TA)0;
+#pragma unroll
+        for (int t = 0; t < WA; ++t) m = ai[p][s] == ai[q][t] ? av[q][t] : m;
+        g += (double)av[p][s] * (double)m;
+      }
+      go[o++] = g;
+    }
+  }
+}
+
+// ||sum_p v_p A_line(k_p) - e_j||^2 = 1 + sum_p v_p (v_p G_pp - 2 c_p + 2 sum_{q>p} v_q G_pq),
+// in this order (the same operations whichever kernel evaluates it).
+template <int W>
+__device__ __forceinline__ double line_res2(const double (&v)[W], const double (&c)[W], const double (&gd)[W],
+                                            const double (&go)[W * (W - 1) / 2]) {
+  double r2 = 1.0;
+  int o = 0;
+#pragma unroll
+  for (int p = 0; p < W; ++p) {
+    double acc = v[p] * gd[p] - 2.0 * c[p];
+#pragma unroll
+    for (int q = p + 1; q < W; ++q) acc += 2.0 * v[q] * go[o++];
+    r2 += v[p] * acc;
+  }
+  return r2;
+}
+
+// Any line of any M_b on its own: gather the A lines it names, Gram, residual.
+template <int W, int WA, typename TA>
+__device__ __forceinline__ double line_res2_any(const int (&k)[W], const double (&v)[W], int j, int wart,
+                                                const int32_t* __restrict__ a_idx, const TA* __restrict__ a_val) {
+  int ai[W][WA];
+  TA av[W][WA];
+  gather_a_lines<W, WA, TA>(k, wart, a_idx, a_val, ai, av);
+  double c[W], gd[W], go[W * (W - 1) / 2];
+  line_gram<W, WA, TA>(ai, av, j, c, gd, go);
+  return line_res2<W>(v, c, gd, go);
+}
+
+// Thread per (line, sample): W = 13 (the Gram of a line does not fit the registers of a
+// thread that keeps it across samples).
 template <int W, int WA, typename TA, typename TV>
 __global__ __launch_bounds__(kNT) void k_resid(int32_t line_begin, int32_t line_end, int32_t wrt, int32_t wart,
                                                int32_t B, int32_t nblk, const int32_t* __restrict__ m_idx,
@@ -51,54 +143,144 @@ __global__ __launch_bounds__(kNT) void k_resid(int32_t line_begin, int32_t line_
     k[p] = (valid && p < wrt) ? mi[p] : -1;
     v[p] = k[p] >= 0 ? (double)mv[p] : 0.0;  // empty slots contribute nothing (their value is not read)
   }
-  int ai[W][WA];
-  TA av[W][WA];
-#pragma unroll
-  for (int p = 0; p < W; ++p) {
-#pragma unroll
-    for (int s = 0; s < WA; ++s) {
-      ai[p][s] = -1;
-      av[p][s] = (TA)0;
-      if (k[p] >= 0 && s < wart) {
-        const int64_t o = (int64_t)k[p] * wart + s;
-        ai[p][s] = a_idx[o];
-        av[p][s] = a_val[o];
-      }
-    }
-  }
-  double r2 = 0.0;
-  if (valid) {
-    r2 = 1.0;
-#pragma unroll
-    for (int p = 0; p < W; ++p) {
-      double cp = 0.0, gpp = 0.0;
-#pragma unroll
-      for (int s = 0; s < WA; ++s) {
-        const double x = (double)av[p][s];
-        gpp += x * x;  // padding entries carry 0
-        cp += (ai[p][s] == j) ? x : 0.0;
-      }
-      double acc = v[p] * gpp - 2.0 * cp;
-#pragma unroll
-      for (int q = p + 1; q < W; ++q) {
-        // an index occurs at most once per line: entry s of line p meets at most one entry of
-        // line q, so a select chain in A's own precision (one compare + one select per entry
-        // pair) finds its partner's value; padding entries (index -1, value 0) add nothing
-        double g = 0.0;
-#pragma unroll
-        for (int s = 0; s < WA; ++s) {
-          TA m = (TA)0;
-#pragma unroll
-          for (int t = 0; t < WA; ++t) m = ai[p][s] == ai[q][t] ? av[q][t] : m;
-          g += (double)av[p][s] * (double)m;
-        }
-        acc += 2.0 * v[q] * g;
-      }
-      r2 += v[p] * acc;
-    }
-  }
+  double r2 = valid ? line_res2_any<W, WA, TA>(k, v, j, wart, a_idx, a_val) : 0.0;
   r2 = block_sum<kNT>(r2, sred);
   if (threadIdx.x == 0) partials[(int64_t)b * nblk + blk] = r2;
+}
+
+// Thread per line, all samples (W <= 7).  The B samples of a batch are mostly sub-patterns of
+// ONE line pattern (the GFlowNet candidates: the candidate pattern with removals), so the Gram
+// of a line — the index matching, all of the kernel's arithmetic — is formed once per chunk of
+// kChunk samples on the union pattern k*_p = max_b k_b[p], and each sample costs a W x W
+// quadratic form.  A lane whose samples disagree on a slot (two different valid indices)
+// evaluates those samples on their own index sets (line_res2_any), so any M is exact.
+// Pass 1 reads the chunk's index slots once (union, per-sample validity bits); pass 2 reads
+// the values.  A is read once per line for the whole batch: algorithmic bytes per launch =
+// bytes(A) + sum_b bytes(M_b).  Per-sample sums: wave sum, then the kNT/64 wave partials in
+// order — the same reduction tree as k_resid's block_sum, so the results are the same bits.
+#ifndef KCHUNK
+#define KCHUNK 8
+#endif
+constexpr int kChunk = KCHUNK;
+
+template <int W, int WA, typename TA, typename TV>
+__global__ __launch_bounds__(kNT) void k_resid_shared(int32_t line_begin, int32_t line_end, int32_t wrt,
+                                                      int32_t wart, int32_t B, int32_t nblk,
+                                                      const int32_t* __restrict__ m_idx, int64_t idx_bstride,
+                                                      const TV* __restrict__ m_val, int64_t val_bstride,
+                                                      const int32_t* __restrict__ a_idx, const TA* __restrict__ a_val,
+                                                      double* __restrict__ partials) {
+  static_assert(kChunk * W <= 64, "validity bits of a chunk in one u64");
+  __shared__ double sred[kChunk][kNT / 64];
+  const int blk = xcd_remap(blockIdx.x, gridDim.x);  // consecutive line ranges on one XCD (A halo in L2)
+  const int j = line_begin + blk * kNT + threadIdx.x;
+  const bool valid = j < line_end;
+  const int jj = valid ? j : line_begin;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int b0 = 0; b0 < B; b0 += kChunk) {
+    const int nb = min(kChunk, B - b0);
+    int kmax[W], kmin[W];
+#pragma unroll
+    for (int p = 0; p < W; ++p) {
+      kmax[p] = -1;
+      kmin[p] = INT_MAX;
+    }
+    // every index load of the chunk issued together (one round trip), then the union and the
+    // validity bits
+    // (unconditional loads from clamped addresses: sample min(b0 + i, B - 1), slot
+    // min(p, wrt - 1); masked afterwards)
+    int kk[kChunk][W];
+#pragma unroll
+    for (int i = 0; i < kChunk; ++i) {
+      const int32_t* mi = m_idx + (int64_t)min(b0 + i, B - 1) * idx_bstride + (int64_t)jj * wrt;
+#pragma unroll
+      for (int p = 0; p < W; ++p) {
+        const int k = mi[min(p, wrt - 1)];
+        kk[i][p] = (valid && i < nb && p < wrt) ? k : -1;
+      }
+    }
+    uint64_t bits = 0;
+#pragma unroll
+    for (int i = 0; i < kChunk; ++i) {
+#pragma unroll
+      for (int p = 0; p < W; ++p) {
+        const int k = kk[i][p];
+        if (k >= 0) {
+          bits |= (uint64_t)1 << (i * W + p);
+          kmax[p] = max(kmax[p], k);
+          kmin[p] = min(kmin[p], k);
+        }
+      }
+    }
+    bool shared = true;
+#pragma unroll
+    for (int p = 0; p < W; ++p) shared = shared && (kmax[p] < 0 || kmin[p] == kmax[p]);
+    // a lane is either on the shared pattern for the whole chunk (one Gram, quadratic forms)
+    // or evaluates every sample on its own index set; the two branches' registers are not
+    // live together
+    double r2s[kChunk];
+#pragma unroll
+    for (int i = 0; i < kChunk; ++i) r2s[i] = 0.0;
+    if (valid && shared) {
+      int ai[W][WA];
+      TA av[W][WA];
+      double c[W], gd[W], go[W * (W - 1) / 2];
+      gather_a_lines<W, WA, TA>(kmax, wart, a_idx, a_val, ai, av);
+      TV vv[kChunk][W];  // the chunk's values, in flight together with the A lines
+#pragma unroll
+      for (int i = 0; i < kChunk; ++i) {
+        const TV* mv = m_val + (int64_t)min(b0 + i, B - 1) * val_bstride + (int64_t)jj * wrt;
+#pragma unroll
+        for (int p = 0; p < W; ++p) vv[i][p] = mv[min(p, wrt - 1)];  // masked by the validity bits
+      }
+      line_gram<W, WA, TA>(ai, av, j, c, gd, go);
+#pragma unroll
+      for (int i = 0; i < kChunk; ++i) {
+        if (i < nb) {
+          double v[W];
+#pragma unroll
+          for (int p = 0; p < W; ++p) v[p] = ((bits >> (i * W + p)) & 1) ? (double)vv[i][p] : 0.0;  // empty: unused
+          r2s[i] = line_res2<W>(v, c, gd, go);
+        }
+      }
+    } else if (valid) {
+#pragma unroll 1
+      for (int i = 0; i < nb; ++i) {  // one sample at a time (registers)
+        {
+          const int32_t* mi = m_idx + (int64_t)(b0 + i) * idx_bstride + (int64_t)jj * wrt;
+          const TV* mv = m_val + (int64_t)(b0 + i) * val_bstride + (int64_t)jj * wrt;
+          int k[W];
+          double v[W];
+#pragma unroll
+          for (int p = 0; p < W; ++p) {
+            const bool on = (bits >> (i * W + p)) & 1;
+            const int kp = mi[min(p, wrt - 1)];
+            const TV x = mv[min(p, wrt - 1)];
+            k[p] = on ? kp : -1;
+            v[p] = on ? (double)x : 0.0;
+          }
+          const double r2 = line_res2_any<W, WA, TA>(k, v, j, wart, a_idx, a_val);
+#pragma unroll
+          for (int u = 0; u < kChunk; ++u) r2s[u] = u == i ? r2 : r2s[u];
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < kChunk; ++i) {
+      if (i < nb) {
+        const double r2 = wave_sum_dpp(r2s[i]);
+        if (lane == 0) sred[i][w] = r2;
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x < nb) {
+      double s = 0.0;
+#pragma unroll
+      for (int u = 0; u < kNT / 64; ++u) s += sred[threadIdx.x][u];
+      partials[(int64_t)(b0 + threadIdx.x) * nblk + blk] = s;
+    }
+    __syncthreads();
+  }
 }
 
 __global__ __launch_bounds__(kNT) void k_resid_reduce(const double* __restrict__ partials, int32_t nblk,
@@ -118,8 +300,12 @@ template <int W, int WA, typename TA, typename TV>
 void launch_resid(int32_t lb, int32_t le, int32_t wrt, int32_t wart, int32_t B, int32_t nblk, const int32_t* mi,
                   int64_t ib, const void* mv, int64_t vb, const int32_t* ai, const void* av, double* partials,
                   hipStream_t s) {
-  k_resid<W, WA, TA, TV><<<nblk * B, kNT, 0, s>>>(lb, le, wrt, wart, B, nblk, mi, ib, static_cast<const TV*>(mv), vb,
-                                                   ai, static_cast<const TA*>(av), partials);
+  if constexpr (W <= 7)
+    k_resid_shared<W, WA, TA, TV><<<nblk, kNT, 0, s>>>(lb, le, wrt, wart, B, nblk, mi, ib, static_cast<const TV*>(mv),
+                                                        vb, ai, static_cast<const TA*>(av), partials);
+  else
+    k_resid<W, WA, TA, TV><<<nblk * B, kNT, 0, s>>>(lb, le, wrt, wart, B, nblk, mi, ib, static_cast<const TV*>(mv), vb,
+                                                     ai, static_cast<const TA*>(av), partials);
 }
 
 struct ResidVariant {

@@ -141,39 +141,6 @@ static void traj_ws(void* base, int32_t E, int32_t B, TrajWs* w) {
   w->total_bytes = c.off;
 }
 
-// Wave scans on DPP row shifts + row broadcasts (no LDS-permute traffic, no per-lane address
-// registers): row_shr 1, 2, 4, 8 inside each 16-lane row, then row_bcast 15 (rows 1, 3) and
-// row_bcast 31 (rows 2, 3).  Lanes without a source add the identity (`old`).
-template <int kCtrl, int kRowMask>
-__device__ __forceinline__ int dpp_i(int ident, int v) {
-  return __builtin_amdgcn_update_dpp(ident, v, kCtrl, kRowMask, 0xf, false);
-}
-// Inclusive wave scan (int).
-__device__ __forceinline__ int wave_incl_scan(int v) {
-  v += dpp_i<0x111, 0xf>(0, v);
-  v += dpp_i<0x112, 0xf>(0, v);
-  v += dpp_i<0x114, 0xf>(0, v);
-  v += dpp_i<0x118, 0xf>(0, v);
-  v += dpp_i<0x142, 0xa>(0, v);
-  v += dpp_i<0x143, 0xc>(0, v);
-  return v;
-}
-template <int kCtrl, int kRowMask>
-__device__ __forceinline__ double dpp_d(double v) {
-  const uint64_t u = __double_as_longlong(v);
-  const int lo = dpp_i<kCtrl, kRowMask>(0, (int)(uint32_t)u), hi = dpp_i<kCtrl, kRowMask>(0, (int)(uint32_t)(u >> 32));
-  return __longlong_as_double((long long)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo));  // 0 bits = +0.0
-}
-// Inclusive wave scan (double, fixed association => deterministic).
-__device__ __forceinline__ double wave_incl_scan_d(double v) {
-  v += dpp_d<0x111, 0xf>(v);
-  v += dpp_d<0x112, 0xf>(v);
-  v += dpp_d<0x114, 0xf>(v);
-  v += dpp_d<0x118, 0xf>(v);
-  v += dpp_d<0x142, 0xa>(v);
-  v += dpp_d<0x143, 0xc>(v);
-  return v;
-}
 // Wave-wide min / max of uint32 (uniform result): an inclusive scan, lane 63 read out.
 __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
   v = min(v, (uint32_t)dpp_i<0x111, 0xf>(-1, (int)v));

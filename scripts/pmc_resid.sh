@@ -1,0 +1,27 @@
+#!/bin/bash
+# PMC passes (each its own rocprofv3 run, kernel-trace only) over scripts/resid_bench.py.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+OUT=${OUT:-gpurun_out/pmc_resid}
+mkdir -p $OUT
+i=0
+for CTRS in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_WAIT_INST_ANY SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_LDS GRBM_GUI_ACTIVE" \
+            "TA_TA_BUSY_sum TD_TD_BUSY_sum TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum GRBM_GUI_ACTIVE" \
+            "FETCH_SIZE"; do
+  i=$((i+1))
+  timeout -s KILL 90 rocprofv3 --kernel-trace --pmc $CTRS --output-format csv -d $OUT/p$i -o run -- python scripts/resid_bench.py --iters 5 "$@" > $OUT/p$i.log 2>&1
+  rc=$?; echo "pass $i rc=$rc"
+  if [ $rc -ne 0 ]; then tail -5 $OUT/p$i.log; exit $rc; fi
+done
+python - "$OUT" <<'PY'
+import csv, collections, glob, sys
+out = sys.argv[1]
+agg = collections.defaultdict(lambda: collections.defaultdict(list))
+for f in glob.glob(f"{out}/p*/run_counter_collection.csv"):
+    for r in csv.DictReader(open(f)):
+        k = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0][:60]
+        agg[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+for k, d in sorted(agg.items()):
+    if "resid" in k:
+        print(k, " ".join(f"{c}={sum(v)/len(v):.4g}" for c, v in sorted(d.items())))
+PY

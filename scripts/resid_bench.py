@@ -1,0 +1,63 @@
+"""Isolated timing of spai_residual_lines (the generic ||A M_b - I||_F^2) at C4 / C3.
+
+M_b = the candidate pattern (A's own lines) with an independent 25 % of the slots removed per
+sample and random values (the GFlowNet candidates' structure); --distinct gives every sample
+random indices instead (the per-sample path).  Prints ms per launch and the fraction of the HBM
+roofline at bytes(A) + B x bytes(M_b).
+usage: python scripts/resid_bench.py [--config c4] [--batch 8] [--iters 20] [--distinct]
+"""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402
+from gflownet_spai_amd import PreconditionerEnv, kernels, poisson_2d, poisson_3d  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="c4")
+    ap.add_argument("--batch", type=int, default=8)
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--distinct", action="store_true")
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    dims, grid, dtype, _ = bench.CONFIGS[args.config]
+    A = poisson_2d(grid, dtype) if dims == 2 else poisson_3d(grid, dtype)
+    n = A.shape[0]
+    env = PreconditionerEnv(n, A, A, side="AM", fill="copy", device=dev)
+    a = env.a_lines
+    B = args.batch
+    g = torch.Generator(device=dev).manual_seed(0)
+    pat = a.idx
+    W = pat.shape[1]
+    if args.distinct:
+        idx = torch.randint(0, n, (B, n, W), generator=g, device=dev, dtype=torch.int32)
+        idx = torch.sort(idx, dim=2).values
+        dup = torch.zeros_like(idx, dtype=torch.bool)
+        dup[:, :, 1:] = idx[:, :, 1:] == idx[:, :, :-1]
+        idx[dup] = -1
+    else:
+        idx = pat.unsqueeze(0).repeat(B, 1, 1)
+    idx[torch.rand(idx.shape, generator=g, device=dev) < 0.25] = -1
+    idx = idx.contiguous()
+    m = torch.randn((B, n, W), generator=g, device=dev, dtype=torch.float32)
+    kernels.residual_lines(idx, m, a)
+    kernels.TIMERS = {}
+    for _ in range(args.iters):
+        kernels.residual_lines(idx, m, a)
+    torch.cuda.synchronize()
+    ms = sum(kernels.timer_ms("residual_lines")) / args.iters
+    nbytes = a.idx.numel() * 4 + a.val.numel() * a.val.element_size() + B * n * W * (4 + m.element_size())
+    print(json.dumps({"config": args.config, "B": B, "distinct": args.distinct, "ms": ms, "bytes": nbytes,
+                      "frac": nbytes / (ms * 1e-3) / 8e12}))
+
+
+if __name__ == "__main__":
+    main()

@@ -712,3 +712,40 @@ def test_residual_lines_matches_fused_lsq_fill_residual():
     got = kernels.residual_lines(idx, env.last_m, env.a_lines)
     ref = env.last_residual.double() ** 2
     np.testing.assert_allclose(got.cpu().numpy(), ref.cpu().numpy(), rtol=1e-6)
+
+
+def test_residual_lines_shared_pattern_and_conflicting_lanes():
+    """k_resid_shared: B = 9 samples that are sub-patterns of ONE line pattern (A's own, with
+    random removals per sample: one Gram per line and chunk) except sample 3, which puts a
+    different valid index into one slot of ~10 % of the lines (those lanes evaluate every
+    sample of the chunk on its own index set).  Each sample vs scipy's exact fp64
+    ||A M_b - I||_F^2, and bit for bit vs the same sample evaluated alone (both paths apply the
+    same operations in the same order)."""
+    from gflownet_spai_amd import kernels
+    from gflownet_spai_amd.layout import build_lines
+    r, c, v, n = O.poisson2d(16, np.float32)
+    A = sp.csr_matrix((v.astype(np.float64), (r, c)), shape=(n, n))
+    a_lines = build_lines(torch.from_numpy(r), torch.from_numpy(c), torch.from_numpy(v), n, "col", DEV)
+    pat = a_lines.idx.cpu().numpy()  # [n, 5], -1 padded
+    rng = np.random.default_rng(5)
+    B, W = 9, pat.shape[1]
+    idx = np.repeat(pat[None], B, 0).copy()
+    idx[rng.random(idx.shape) < 0.25] = -1
+    conflict = rng.random(n) < 0.1
+    for l in np.nonzero(conflict)[0]:
+        p = int(np.argmax(pat[l] >= 0))
+        new = int(rng.integers(0, n))
+        while new in set(pat[l].tolist()):
+            new = int(rng.integers(0, n))
+        idx[3, l, p] = new
+    val = rng.standard_normal((B, n, W)).astype(np.float32)
+    got = kernels.residual_lines(torch.from_numpy(idx).to(DEV), torch.from_numpy(val).to(DEV), a_lines).cpu().numpy()
+    I = sp.identity(n, format="csr")
+    for b in range(B):
+        ok = idx[b] >= 0
+        lines, _ = np.nonzero(ok)
+        M = sp.csr_matrix((val[b][ok].astype(np.float64), (idx[b][ok], lines)), shape=(n, n))
+        assert got[b] == pytest.approx(sp.linalg.norm(A @ M - I) ** 2, rel=1e-12)
+        alone = kernels.residual_lines(torch.from_numpy(idx[b:b + 1]).to(DEV), torch.from_numpy(val[b:b + 1]).to(DEV),
+                                       a_lines).cpu().numpy()
+        assert alone[0] == got[b]

@@ -35,23 +35,48 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + orig / kXcd;
 }
 
+// The n slots of one ELL line, p[0 .. n), n = W at compile time when `full` (the stored width
+// equals the template width): 16-byte vector loads (4-byte alignment suffices for vector
+// memory instructions on gfx950) + a scalar tail — fewer, wider memory instructions for the
+// texture address/data units, which bound this kernel (TA/TD busy ~80 % with dword loads).
+// Otherwise clamped scalar loads (slot min(q, n - 1)), masked by the caller.
+template <int W, bool FULL, typename T>
+__device__ __forceinline__ void load_slots(const T* __restrict__ p, int n, T (&out)[W]) {
+  constexpr int kPer = 16 / sizeof(T);
+  typedef T vec_t __attribute__((ext_vector_type(kPer)));
+  if constexpr (FULL) {
+#pragma unroll
+    for (int q = 0; q + kPer <= W; q += kPer) {
+      const vec_t v = *reinterpret_cast<const vec_t*>(p + q);
+#pragma unroll
+      for (int e = 0; e < kPer; ++e) out[q + e] = v[e];
+    }
+#pragma unroll
+    for (int q = (W / kPer) * kPer; q < W; ++q) out[q] = p[q];
+  } else {
+#pragma unroll
+    for (int q = 0; q < W; ++q) out[q] = p[min(q, n - 1)];
+  }
+}
+
 // The W lines of A named by k[0..W) (k < 0: empty, index -1 / value 0).  Every load is
 // unconditional from a clamped address (line 0 / the line's last slot) and masked afterwards:
 // no branch around a load, so all of them are in flight together.
-template <int W, int WA, typename TA>
+template <int W, int WA, bool FULL, typename TA>
 __device__ __forceinline__ void gather_a_lines(const int (&k)[W], int wart, const int32_t* __restrict__ a_idx,
                                                const TA* __restrict__ a_val, int (&ai)[W][WA], TA (&av)[W][WA]) {
 #pragma unroll
   for (int p = 0; p < W; ++p) {
     const int64_t base = (int64_t)max(k[p], 0) * wart;
+    int ii[WA];
+    TA xx[WA];
+    load_slots<WA, FULL, int>(a_idx + base, wart, ii);
+    load_slots<WA, FULL, TA>(a_val + base, wart, xx);
 #pragma unroll
     for (int s = 0; s < WA; ++s) {
-      const int64_t o = base + min(s, wart - 1);
-      const int i = a_idx[o];
-      const TA x = a_val[o];
       const bool on = k[p] >= 0 && s < wart;
-      ai[p][s] = on ? i : -1;
-      av[p][s] = on ? x : (TA)0;
+      ai[p][s] = on ? ii[s] : -1;
+      av[p][s] = on ? xx[s] : (TA)0;
     }
   }
 }
@@ -109,12 +134,12 @@ __device__ __forceinline__ double line_res2(const double (&v)[W], const double (
 }
 
 // Any line of any M_b on its own: gather the A lines it names, Gram, residual.
-template <int W, int WA, typename TA>
+template <int W, int WA, bool FULL, typename TA>
 __device__ __forceinline__ double line_res2_any(const int (&k)[W], const double (&v)[W], int j, int wart,
                                                 const int32_t* __restrict__ a_idx, const TA* __restrict__ a_val) {
   int ai[W][WA];
   TA av[W][WA];
-  gather_a_lines<W, WA, TA>(k, wart, a_idx, a_val, ai, av);
+  gather_a_lines<W, WA, FULL, TA>(k, wart, a_idx, a_val, ai, av);
   double c[W], gd[W], go[W * (W - 1) / 2];
   line_gram<W, WA, TA>(ai, av, j, c, gd, go);
   return line_res2<W>(v, c, gd, go);
@@ -143,7 +168,7 @@ __global__ __launch_bounds__(kNT) void k_resid(int32_t line_begin, int32_t line_
     k[p] = (valid && p < wrt) ? mi[p] : -1;
     v[p] = k[p] >= 0 ? (double)mv[p] : 0.0;  // empty slots contribute nothing (their value is not read)
   }
-  double r2 = valid ? line_res2_any<W, WA, TA>(k, v, j, wart, a_idx, a_val) : 0.0;
+  double r2 = valid ? line_res2_any<W, WA, false, TA>(k, v, j, wart, a_idx, a_val) : 0.0;
   r2 = block_sum<kNT>(r2, sred);
   if (threadIdx.x == 0) partials[(int64_t)b * nblk + blk] = r2;
 }
@@ -163,15 +188,14 @@ __global__ __launch_bounds__(kNT) void k_resid(int32_t line_begin, int32_t line_
 #endif
 constexpr int kChunk = KCHUNK;
 
-template <int W, int WA, typename TA, typename TV>
-__global__ __launch_bounds__(kNT) void k_resid_shared(int32_t line_begin, int32_t line_end, int32_t wrt,
-                                                      int32_t wart, int32_t B, int32_t nblk,
-                                                      const int32_t* __restrict__ m_idx, int64_t idx_bstride,
-                                                      const TV* __restrict__ m_val, int64_t val_bstride,
-                                                      const int32_t* __restrict__ a_idx, const TA* __restrict__ a_val,
-                                                      double* __restrict__ partials) {
+template <int W, int WA, bool FULL, typename TA, typename TV>
+__device__ __forceinline__ void resid_shared_body(int32_t line_begin, int32_t line_end, int32_t wrt, int32_t wart,
+                                                  int32_t B, int32_t nblk, const int32_t* __restrict__ m_idx,
+                                                  int64_t idx_bstride, const TV* __restrict__ m_val,
+                                                  int64_t val_bstride, const int32_t* __restrict__ a_idx,
+                                                  const TA* __restrict__ a_val, double* __restrict__ partials,
+                                                  double (&sred)[kChunk][kNT / 64]) {
   static_assert(kChunk * W <= 64, "validity bits of a chunk in one u64");
-  __shared__ double sred[kChunk][kNT / 64];
   const int blk = xcd_remap(blockIdx.x, gridDim.x);  // consecutive line ranges on one XCD (A halo in L2)
   const int j = line_begin + blk * kNT + threadIdx.x;
   const bool valid = j < line_end;
@@ -193,11 +217,10 @@ __global__ __launch_bounds__(kNT) void k_resid_shared(int32_t line_begin, int32_
 #pragma unroll
     for (int i = 0; i < kChunk; ++i) {
       const int32_t* mi = m_idx + (int64_t)min(b0 + i, B - 1) * idx_bstride + (int64_t)jj * wrt;
+      int k[W];
+      load_slots<W, FULL, int>(mi, wrt, k);
 #pragma unroll
-      for (int p = 0; p < W; ++p) {
-        const int k = mi[min(p, wrt - 1)];
-        kk[i][p] = (valid && i < nb && p < wrt) ? k : -1;
-      }
+      for (int p = 0; p < W; ++p) kk[i][p] = (valid && i < nb && p < wrt) ? k[p] : -1;
     }
     uint64_t bits = 0;
 #pragma unroll
@@ -225,13 +248,12 @@ __global__ __launch_bounds__(kNT) void k_resid_shared(int32_t line_begin, int32_
       int ai[W][WA];
       TA av[W][WA];
       double c[W], gd[W], go[W * (W - 1) / 2];
-      gather_a_lines<W, WA, TA>(kmax, wart, a_idx, a_val, ai, av);
+      gather_a_lines<W, WA, FULL, TA>(kmax, wart, a_idx, a_val, ai, av);
       TV vv[kChunk][W];  // the chunk's values, in flight together with the A lines
 #pragma unroll
       for (int i = 0; i < kChunk; ++i) {
         const TV* mv = m_val + (int64_t)min(b0 + i, B - 1) * val_bstride + (int64_t)jj * wrt;
-#pragma unroll
-        for (int p = 0; p < W; ++p) vv[i][p] = mv[min(p, wrt - 1)];  // masked by the validity bits
+        load_slots<W, FULL, TV>(mv, wrt, vv[i]);  // masked by the validity bits
       }
       line_gram<W, WA, TA>(ai, av, j, c, gd, go);
 #pragma unroll
@@ -249,17 +271,18 @@ __global__ __launch_bounds__(kNT) void k_resid_shared(int32_t line_begin, int32_
         {
           const int32_t* mi = m_idx + (int64_t)(b0 + i) * idx_bstride + (int64_t)jj * wrt;
           const TV* mv = m_val + (int64_t)(b0 + i) * val_bstride + (int64_t)jj * wrt;
-          int k[W];
+          int k[W], kp[W];
+          TV x[W];
           double v[W];
+          load_slots<W, FULL, int>(mi, wrt, kp);
+          load_slots<W, FULL, TV>(mv, wrt, x);
 #pragma unroll
           for (int p = 0; p < W; ++p) {
             const bool on = (bits >> (i * W + p)) & 1;
-            const int kp = mi[min(p, wrt - 1)];
-            const TV x = mv[min(p, wrt - 1)];
-            k[p] = on ? kp : -1;
-            v[p] = on ? (double)x : 0.0;
+            k[p] = on ? kp[p] : -1;
+            v[p] = on ? (double)x[p] : 0.0;
           }
-          const double r2 = line_res2_any<W, WA, TA>(k, v, j, wart, a_idx, a_val);
+          const double r2 = line_res2_any<W, WA, FULL, TA>(k, v, j, wart, a_idx, a_val);
 #pragma unroll
           for (int u = 0; u < kChunk; ++u) r2s[u] = u == i ? r2 : r2s[u];
         }
@@ -283,6 +306,24 @@ __global__ __launch_bounds__(kNT) void k_resid_shared(int32_t line_begin, int32_
   }
 }
 
+// WAVES: the occupancy the register allocator must keep (4 waves/SIMD for the fp32 5-wide lines
+// of C4 without spills: 117 -> 81 us; the wider / fp64 variants spill there, so 1 = its choice)
+template <int W, int WA, typename TA, typename TV, int WAVES>
+__global__ __launch_bounds__(kNT, WAVES) void k_resid_shared(int32_t line_begin, int32_t line_end, int32_t wrt,
+                                                      int32_t wart, int32_t B, int32_t nblk,
+                                                      const int32_t* __restrict__ m_idx, int64_t idx_bstride,
+                                                      const TV* __restrict__ m_val, int64_t val_bstride,
+                                                      const int32_t* __restrict__ a_idx, const TA* __restrict__ a_val,
+                                                      double* __restrict__ partials) {
+  __shared__ double sred[kChunk][kNT / 64];
+  if (wrt == W && wart == WA)  // stored widths = template widths: 16-byte slot loads
+    resid_shared_body<W, WA, true, TA, TV>(line_begin, line_end, wrt, wart, B, nblk, m_idx, idx_bstride, m_val,
+                                           val_bstride, a_idx, a_val, partials, sred);
+  else
+    resid_shared_body<W, WA, false, TA, TV>(line_begin, line_end, wrt, wart, B, nblk, m_idx, idx_bstride, m_val,
+                                            val_bstride, a_idx, a_val, partials, sred);
+}
+
 __global__ __launch_bounds__(kNT) void k_resid_reduce(const double* __restrict__ partials, int32_t nblk,
                                                       double* __restrict__ out) {
   __shared__ double sred[kNT / 64];
@@ -300,8 +341,9 @@ template <int W, int WA, typename TA, typename TV>
 void launch_resid(int32_t lb, int32_t le, int32_t wrt, int32_t wart, int32_t B, int32_t nblk, const int32_t* mi,
                   int64_t ib, const void* mv, int64_t vb, const int32_t* ai, const void* av, double* partials,
                   hipStream_t s) {
+  constexpr int kWaves = (W == 5 && sizeof(TA) == 4 && sizeof(TV) == 4) ? 4 : 1;
   if constexpr (W <= 7)
-    k_resid_shared<W, WA, TA, TV><<<nblk, kNT, 0, s>>>(lb, le, wrt, wart, B, nblk, mi, ib, static_cast<const TV*>(mv),
+    k_resid_shared<W, WA, TA, TV, kWaves><<<nblk, kNT, 0, s>>>(lb, le, wrt, wart, B, nblk, mi, ib, static_cast<const TV*>(mv),
                                                         vb, ai, static_cast<const TA*>(av), partials);
   else
     k_resid<W, WA, TA, TV><<<nblk * B, kNT, 0, s>>>(lb, le, wrt, wart, B, nblk, mi, ib, static_cast<const TV*>(mv), vb,

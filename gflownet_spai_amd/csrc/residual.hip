@@ -168,7 +168,13 @@ __global__ __launch_bounds__(kNT) void k_resid(int32_t line_begin, int32_t line_
     k[p] = (valid && p < wrt) ? mi[p] : -1;
     v[p] = k[p] >= 0 ? (double)mv[p] : 0.0;  // empty slots contribute nothing (their value is not read)
   }
-  double r2 = valid ? line_res2_any<W, WA, false, TA>(k, v, j, wart, a_idx, a_val) : 0.0;
+  double r2 = 0.0;
+  if (valid) {
+    if (wart == WA)  // stored width of A = template width: 16-byte slot loads
+      r2 = line_res2_any<W, WA, true, TA>(k, v, j, wart, a_idx, a_val);
+    else
+      r2 = line_res2_any<W, WA, false, TA>(k, v, j, wart, a_idx, a_val);
+  }
   r2 = block_sum<kNT>(r2, sred);
   if (threadIdx.x == 0) partials[(int64_t)b * nblk + blk] = r2;
 }

@@ -192,7 +192,7 @@ def cpu_baseline(cfg, B, budget_s: float, logits, T_mean: float):
     return out
 
 
-def generic_residual_leg(env, log, reps: int = 10):
+def generic_residual_leg(env, log, cfg: str, reps: int = 10):
     """The generic SpMM residual (spai_residual_lines: ||A M_b - I||_F^2 of B arbitrary sparse
     M_b, preconditioner.py:79-93 for any M) on the step's B candidates: their stored LSQ values
     with each candidate's own kept index set (removed slots -> -1).  Timed with HIP events on
@@ -221,7 +221,8 @@ def generic_residual_leg(env, log, reps: int = 10):
     name = "k_resid_shared" if W <= 7 else "k_resid"
     out = roofline_obj(f"{name}<{W},{a.width},{str(a.val.dtype)[6:]},{str(m.dtype)[6:]}> (||A M_b - I||_F^2 of "
                        f"B={B} arbitrary sparse M_b: the step's LSQ fills with their own kept index sets; "
-                       f"bytes = bytes(A) + B x bytes(M_b))", bytes_a + B * bytes_m, ms)
+                       f"bytes = bytes(A) + B x bytes(M_b))", bytes_a + B * bytes_m, ms,
+                       traffic=measured_traffic(cfg + "_residual", B))
     out["max_rel_diff_vs_fused_fill"] = rel
     return out
 
@@ -432,7 +433,7 @@ def main():
         }
         if world == 1:
             with torch.no_grad():
-                out["roofline_residual"] = generic_residual_leg(env, log)
+                out["roofline_residual"] = generic_residual_leg(env, log, args.config)
         if not args.no_cpu_baseline and world == 1:
             with torch.no_grad():
                 lg_host = model.forward_policy.logits(model.state_to_data(s0[:1])[0])[0].reshape(-1).cpu().numpy()

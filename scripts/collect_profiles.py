@@ -71,6 +71,16 @@ def main():
         if "config" in allrec:  # older single-record form
             allrec = {allrec["config"]: allrec}
         allrec[args.config] = rec
+        # the generic residual leg's kernel (bench roofline_residual), when it ran in this command
+        res = [(k, v) for k, v in summary["kernels"].items()
+               if ("k_resid_shared<" in k or "k_resid<" in k) and "hbm_bytes_per_launch" in v]
+        if res:
+            k, v = res[0]
+            allrec[args.config + "_residual"] = {
+                "config": args.config, "batch": args.batch, "kernel": k, "avg_us": v.get("avg_us"),
+                "hbm_bytes_per_launch": v["hbm_bytes_per_launch"], "FETCH_SIZE_KB": v["pmc"].get("FETCH_SIZE"),
+                "WRITE_SIZE_KB": v["pmc"].get("WRITE_SIZE"), "source": f"profiles/pmc_{args.tag}.json",
+                "command": args.cmd}
         json.dump(allrec, open(path, "w"), indent=1)
         print(json.dumps(rec))
 

@@ -218,7 +218,7 @@ def generic_residual_leg(env, log, cfg: str, reps: int = 10):
     rel = float(((res2 - ref).abs() / ref).max())
     bytes_a = a.idx.numel() * 4 + a.val.numel() * a.val.element_size()
     bytes_m = n * W * (4 + m.element_size())
-    name = "k_resid_shared" if W <= 7 else "k_resid"
+    name = "k_resid_shared" if W <= 7 else "k_resid_wide"
     out = roofline_obj(f"{name}<{W},{a.width},{str(a.val.dtype)[6:]},{str(m.dtype)[6:]}> (||A M_b - I||_F^2 of "
                        f"B={B} arbitrary sparse M_b: the step's LSQ fills with their own kept index sets; "
                        f"bytes = bytes(A) + B x bytes(M_b))", bytes_a + B * bytes_m, ms,

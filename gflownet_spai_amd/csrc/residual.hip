@@ -18,7 +18,10 @@
 // algorithmic bytes per launch = bytes(A) + sum_b bytes(M_b) (SURVEY §8d with A shared by the
 // batch).  Consecutive line ranges run on one XCD (bijective XCD remap), so the A halo of
 // neighbouring blocks is served by that XCD's L2.
-// W = 13 (k_resid): one thread per (line, sample); the B blocks of one line range on one XCD.
+// W = 13 (k_resid_wide): one thread per line for chunks of 4 samples; the line's index matching
+// runs once per chunk and each pair's product <A_line(k_p), A_line(k_q)> goes straight into the
+// chunk's quadratic forms (the 91-value Gram is never held); round 2's thread per (line,
+// sample) kernel matched every pair once per SAMPLE (C3: 1.76 ms -> 0.54 ms).
 // Per-block partial sums, then a fixed-order reduction per sample: the result is
 // bit-reproducible, and both kernels evaluate a line with the same operations in the same order.
 #include "spai_device.h"
@@ -145,40 +148,6 @@ __device__ __forceinline__ double line_res2_any(const int (&k)[W], const double 
   return line_res2<W>(v, c, gd, go);
 }
 
-// Thread per (line, sample): W = 13 (the Gram of a line does not fit the registers of a
-// thread that keeps it across samples).
-template <int W, int WA, typename TA, typename TV>
-__global__ __launch_bounds__(kNT) void k_resid(int32_t line_begin, int32_t line_end, int32_t wrt, int32_t wart,
-                                               int32_t B, int32_t nblk, const int32_t* __restrict__ m_idx,
-                                               int64_t idx_bstride, const TV* __restrict__ m_val,
-                                               int64_t val_bstride, const int32_t* __restrict__ a_idx,
-                                               const TA* __restrict__ a_val, double* __restrict__ partials) {
-  __shared__ double sred[kNT / 64];
-  const int wg = xcd_remap(blockIdx.x, gridDim.x);
-  const int b = wg % B, blk = wg / B;
-  const int j = line_begin + blk * kNT + threadIdx.x;
-  const bool valid = j < line_end;
-  const int jj = valid ? j : line_begin;
-  const int32_t* mi = m_idx + (int64_t)b * idx_bstride + (int64_t)jj * wrt;
-  const TV* mv = m_val + (int64_t)b * val_bstride + (int64_t)jj * wrt;
-  int k[W];
-  double v[W];
-#pragma unroll
-  for (int p = 0; p < W; ++p) {
-    k[p] = (valid && p < wrt) ? mi[p] : -1;
-    v[p] = k[p] >= 0 ? (double)mv[p] : 0.0;  // empty slots contribute nothing (their value is not read)
-  }
-  double r2 = 0.0;
-  if (valid) {
-    if (wart == WA)  // stored width of A = template width: 16-byte slot loads
-      r2 = line_res2_any<W, WA, true, TA>(k, v, j, wart, a_idx, a_val);
-    else
-      r2 = line_res2_any<W, WA, false, TA>(k, v, j, wart, a_idx, a_val);
-  }
-  r2 = block_sum<kNT>(r2, sred);
-  if (threadIdx.x == 0) partials[(int64_t)b * nblk + blk] = r2;
-}
-
 // Thread per line, all samples (W <= 7).  The B samples of a batch are mostly sub-patterns of
 // ONE line pattern (the GFlowNet candidates: the candidate pattern with removals), so the Gram
 // of a line — the index matching, all of the kernel's arithmetic — is formed once per chunk of
@@ -188,7 +157,7 @@ __global__ __launch_bounds__(kNT) void k_resid(int32_t line_begin, int32_t line_
 // Pass 1 reads the chunk's index slots once (union, per-sample validity bits); pass 2 reads
 // the values.  A is read once per line for the whole batch: algorithmic bytes per launch =
 // bytes(A) + sum_b bytes(M_b).  Per-sample sums: wave sum, then the kNT/64 wave partials in
-// order — the same reduction tree as k_resid's block_sum, so the results are the same bits.
+// order (a fixed reduction tree), so a sample's result does not depend on the other samples.
 #ifndef KCHUNK
 #define KCHUNK 8
 #endif
@@ -330,6 +299,158 @@ __global__ __launch_bounds__(kNT, WAVES) void k_resid_shared(int32_t line_begin,
                                             val_bstride, a_idx, a_val, partials, sred);
 }
 
+// Thread per line, chunks of kChunkW samples, W > 7 (C3's 13-wide lines): the samples' index
+// sets are read together; when they agree slot by slot (sub-patterns of one pattern) the A
+// lines of the union pattern are gathered once per chunk and every entry pair is matched ONCE
+// for the chunk: c_p and G_pp open each sample's row accumulator, each G_pq (q > p) is added
+// to it as soon as it is formed, and the row is closed into the sample's sum — exactly
+// line_res2's operations in line_res2's order, so a sample gets the same bits as on its own.
+// The Gram itself is never stored (91 + 26 fp64 values would not fit beside the A lines).
+// Lanes whose samples disagree evaluate each sample on its own index set (line_res2_any).
+// Index matching per line: once per chunk instead of once per sample.
+constexpr int kChunkW = 4;
+template <int W, int WA, bool FULL, typename TA, typename TV>
+__device__ __forceinline__ void resid_wide_body(int32_t line_begin, int32_t line_end, int32_t wrt, int32_t wart,
+                                                int32_t B, int32_t nblk, const int32_t* __restrict__ m_idx,
+                                                int64_t idx_bstride, const TV* __restrict__ m_val,
+                                                int64_t val_bstride, const int32_t* __restrict__ a_idx,
+                                                const TA* __restrict__ a_val, double* __restrict__ partials,
+                                                double (&sred)[kChunkW][kNT / 64]) {
+  static_assert(kChunkW * W <= 64, "validity bits of a chunk in one u64");
+  const int blk = xcd_remap(blockIdx.x, gridDim.x);
+  const int j = line_begin + blk * kNT + threadIdx.x;
+  const bool valid = j < line_end;
+  const int jj = valid ? j : line_begin;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll 1
+  for (int b0 = 0; b0 < B; b0 += kChunkW) {
+    const int nb = min(kChunkW, B - b0);
+    int kmax[W], kmin[W];
+#pragma unroll
+    for (int p = 0; p < W; ++p) {
+      kmax[p] = -1;
+      kmin[p] = INT_MAX;
+    }
+    uint64_t bits = 0;
+#pragma unroll
+    for (int i = 0; i < kChunkW; ++i) {
+      const int32_t* mi = m_idx + (int64_t)min(b0 + i, B - 1) * idx_bstride + (int64_t)jj * wrt;
+      int k[W];
+      load_slots<W, FULL, int>(mi, wrt, k);
+#pragma unroll
+      for (int p = 0; p < W; ++p) {
+        const int kp = (valid && i < nb && p < wrt) ? k[p] : -1;
+        if (kp >= 0) {
+          bits |= (uint64_t)1 << (i * W + p);
+          kmax[p] = max(kmax[p], kp);
+          kmin[p] = min(kmin[p], kp);
+        }
+      }
+    }
+    bool shared = true;
+#pragma unroll
+    for (int p = 0; p < W; ++p) shared = shared && (kmax[p] < 0 || kmin[p] == kmax[p]);
+    double r2s[kChunkW];
+#pragma unroll
+    for (int i = 0; i < kChunkW; ++i) r2s[i] = 0.0;
+    if (valid && shared) {
+      int ai[W][WA];
+      TA av[W][WA];
+      gather_a_lines<W, WA, FULL, TA>(kmax, wart, a_idx, a_val, ai, av);
+      double v[kChunkW][W];
+#pragma unroll
+      for (int i = 0; i < kChunkW; ++i) {
+        TV x[W];
+        load_slots<W, FULL, TV>(m_val + (int64_t)min(b0 + i, B - 1) * val_bstride + (int64_t)jj * wrt, wrt, x);
+#pragma unroll
+        for (int p = 0; p < W; ++p) v[i][p] = ((bits >> (i * W + p)) & 1) ? (double)x[p] : 0.0;
+      }
+#pragma unroll
+      for (int i = 0; i < kChunkW; ++i) r2s[i] = 1.0;
+#pragma unroll
+      for (int p = 0; p < W; ++p) {
+        double cp = 0.0, gpp = 0.0;  // line_gram's c_p and G_pp
+#pragma unroll
+        for (int s = 0; s < WA; ++s) {
+          const double x = (double)av[p][s];
+          gpp += x * x;
+          cp += (ai[p][s] == j) ? x : 0.0;
+        }
+        double acc[kChunkW];
+#pragma unroll
+        for (int i = 0; i < kChunkW; ++i) acc[i] = v[i][p] * gpp - 2.0 * cp;
+#pragma unroll
+        for (int q = p + 1; q < W; ++q) {
+          double g = 0.0;  // line_gram's G_pq
+#pragma unroll
+          for (int s = 0; s < WA; ++s) {
+            TA m = (TA)0;
+#pragma unroll
+            for (int t = 0; t < WA; ++t) m = ai[p][s] == ai[q][t] ? av[q][t] : m;
+            g += (double)av[p][s] * (double)m;
+          }
+#pragma unroll
+          for (int i = 0; i < kChunkW; ++i) acc[i] += 2.0 * v[i][q] * g;
+        }
+#pragma unroll
+        for (int i = 0; i < kChunkW; ++i) r2s[i] += v[i][p] * acc[i];
+      }
+#pragma unroll
+      for (int i = 0; i < kChunkW; ++i) r2s[i] = i < nb ? r2s[i] : 0.0;
+    } else if (valid) {
+#pragma unroll 1
+      for (int i = 0; i < nb; ++i) {  // one sample at a time on its own index set
+        const int32_t* mi = m_idx + (int64_t)(b0 + i) * idx_bstride + (int64_t)jj * wrt;
+        const TV* mv = m_val + (int64_t)(b0 + i) * val_bstride + (int64_t)jj * wrt;
+        int k[W], kp[W];
+        TV x[W];
+        double v[W];
+        load_slots<W, FULL, int>(mi, wrt, kp);
+        load_slots<W, FULL, TV>(mv, wrt, x);
+#pragma unroll
+        for (int p = 0; p < W; ++p) {
+          const bool on = (bits >> (i * W + p)) & 1;
+          k[p] = on ? kp[p] : -1;
+          v[p] = on ? (double)x[p] : 0.0;
+        }
+        const double r2 = line_res2_any<W, WA, FULL, TA>(k, v, j, wart, a_idx, a_val);
+#pragma unroll
+        for (int u = 0; u < kChunkW; ++u) r2s[u] = u == i ? r2 : r2s[u];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < kChunkW; ++i) {
+      if (i < nb) {
+        const double r2 = wave_sum_dpp(r2s[i]);
+        if (lane == 0) sred[i][w] = r2;
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x < nb) {
+      double s = 0.0;
+#pragma unroll
+      for (int u = 0; u < kNT / 64; ++u) s += sred[threadIdx.x][u];
+      partials[(int64_t)(b0 + threadIdx.x) * nblk + blk] = s;
+    }
+    __syncthreads();
+  }
+}
+
+template <int W, int WA, typename TA, typename TV>
+__global__ __launch_bounds__(kNT) void k_resid_wide(int32_t line_begin, int32_t line_end, int32_t wrt, int32_t wart,
+                                                    int32_t B, int32_t nblk, const int32_t* __restrict__ m_idx,
+                                                    int64_t idx_bstride, const TV* __restrict__ m_val,
+                                                    int64_t val_bstride, const int32_t* __restrict__ a_idx,
+                                                    const TA* __restrict__ a_val, double* __restrict__ partials) {
+  __shared__ double sred[kChunkW][kNT / 64];
+  if (wrt == W && wart == WA)
+    resid_wide_body<W, WA, true, TA, TV>(line_begin, line_end, wrt, wart, B, nblk, m_idx, idx_bstride, m_val,
+                                         val_bstride, a_idx, a_val, partials, sred);
+  else
+    resid_wide_body<W, WA, false, TA, TV>(line_begin, line_end, wrt, wart, B, nblk, m_idx, idx_bstride, m_val,
+                                          val_bstride, a_idx, a_val, partials, sred);
+}
+
 __global__ __launch_bounds__(kNT) void k_resid_reduce(const double* __restrict__ partials, int32_t nblk,
                                                       double* __restrict__ out) {
   __shared__ double sred[kNT / 64];
@@ -352,8 +473,8 @@ void launch_resid(int32_t lb, int32_t le, int32_t wrt, int32_t wart, int32_t B, 
     k_resid_shared<W, WA, TA, TV, kWaves><<<nblk, kNT, 0, s>>>(lb, le, wrt, wart, B, nblk, mi, ib, static_cast<const TV*>(mv),
                                                         vb, ai, static_cast<const TA*>(av), partials);
   else
-    k_resid<W, WA, TA, TV><<<nblk * B, kNT, 0, s>>>(lb, le, wrt, wart, B, nblk, mi, ib, static_cast<const TV*>(mv), vb,
-                                                     ai, static_cast<const TA*>(av), partials);
+    k_resid_wide<W, WA, TA, TV><<<nblk, kNT, 0, s>>>(lb, le, wrt, wart, B, nblk, mi, ib, static_cast<const TV*>(mv), vb,
+                                                      ai, static_cast<const TA*>(av), partials);
 }
 
 struct ResidVariant {

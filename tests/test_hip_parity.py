@@ -714,19 +714,28 @@ def test_residual_lines_matches_fused_lsq_fill_residual():
     np.testing.assert_allclose(got.cpu().numpy(), ref.cpu().numpy(), rtol=1e-6)
 
 
-def test_residual_lines_shared_pattern_and_conflicting_lanes():
-    """k_resid_shared: B = 9 samples that are sub-patterns of ONE line pattern (A's own, with
-    random removals per sample: one Gram per line and chunk) except sample 3, which puts a
+@pytest.mark.parametrize("dims", [2, 3])
+def test_residual_lines_shared_pattern_and_conflicting_lanes(dims):
+    """k_resid_shared (2-D: A's own 5-wide pattern, fp32) and k_resid_wide (3-D: the 13-wide
+    axial C3 pattern, fp64): B = 9 samples that are sub-patterns of ONE line pattern (random
+    removals per sample: one index matching per line and chunk) except sample 3, which puts a
     different valid index into one slot of ~10 % of the lines (those lanes evaluate every
     sample of the chunk on its own index set).  Each sample vs scipy's exact fp64
     ||A M_b - I||_F^2, and bit for bit vs the same sample evaluated alone (both paths apply the
     same operations in the same order)."""
-    from gflownet_spai_amd import kernels
+    from gflownet_spai_amd import axial_pattern_3d, kernels
     from gflownet_spai_amd.layout import build_lines
-    r, c, v, n = O.poisson2d(16, np.float32)
+    dt = np.float32 if dims == 2 else np.float64
+    r, c, v, n = O.poisson2d(16, dt) if dims == 2 else O.poisson3d(7, dt)
     A = sp.csr_matrix((v.astype(np.float64), (r, c)), shape=(n, n))
     a_lines = build_lines(torch.from_numpy(r), torch.from_numpy(c), torch.from_numpy(v), n, "col", DEV)
-    pat = a_lines.idx.cpu().numpy()  # [n, 5], -1 padded
+    if dims == 2:
+        pat = a_lines.idx.cpu().numpy()  # [n, 5], -1 padded
+    else:
+        P = axial_pattern_3d(7, 2).coalesce()
+        pr, pc = P.indices()
+        pat = build_lines(pr, pc, P.values(), n, "col", DEV).idx.cpu().numpy()  # [n, 13]
+        assert pat.shape[1] == 13
     rng = np.random.default_rng(5)
     B, W = 9, pat.shape[1]
     idx = np.repeat(pat[None], B, 0).copy()
@@ -738,7 +747,7 @@ def test_residual_lines_shared_pattern_and_conflicting_lanes():
         while new in set(pat[l].tolist()):
             new = int(rng.integers(0, n))
         idx[3, l, p] = new
-    val = rng.standard_normal((B, n, W)).astype(np.float32)
+    val = rng.standard_normal((B, n, W)).astype(dt)
     got = kernels.residual_lines(torch.from_numpy(idx).to(DEV), torch.from_numpy(val).to(DEV), a_lines).cpu().numpy()
     I = sp.identity(n, format="csr")
     for b in range(B):

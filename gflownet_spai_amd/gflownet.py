@@ -36,6 +36,7 @@ class GFlowNet(nn.Module):
         self.backward_policy = backward_policy
         self.env = env
         self.mode = mode
+        self._alpha_mean = None  # (key, mean over the batch of a constant sigmoid(alpha), pin)
         self.seed = int(torch.initial_seed() if seed is None else seed) & (2**64 - 1)
         self.sample_base = sample_base
         self.rollouts = 0  # Philox stream id of the next throughput rollout (host mirror)
@@ -68,7 +69,14 @@ class GFlowNet(nn.Module):
         else:
             probs, a = self.forward_policy(data, torch.empty(0, dtype=torch.long))
             logits = torch.log(probs)
-        alpha = torch.stack([a] * batch_size, dim=0).mean()
+        if a.requires_grad or a._version != 0:
+            alpha = torch.stack([a] * batch_size, dim=0).mean()
+        else:  # a constant (the policy's cached sigmoid): its batch mean is cached with it
+            key = (id(a), a.data_ptr(), batch_size)
+            hit = self._alpha_mean
+            if hit is None or hit[0] != key:
+                hit = self._alpha_mean = (key, torch.stack([a] * batch_size, dim=0).mean(), a)  # a pins the id
+            alpha = hit[1]
         return logits.reshape(-1), alpha, lmax
 
     def forward_probs(self, s, data_list, actions=None):

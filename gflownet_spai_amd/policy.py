@@ -321,9 +321,18 @@ class ForwardPolicy(BasePolicy):
         params = tuple(self.parameters())
         if torch.is_grad_enabled() and any(p.requires_grad for p in params):
             logits, lmax = _HipLogits.apply(self, data, B, *params)
-        else:
-            logits, lmax = self._hip_logits(data, B)
-        return logits, torch.sigmoid(self.alpha), lmax
+            return logits, torch.sigmoid(self.alpha), lmax
+        logits, lmax = self._hip_logits(data, B)
+        return logits, self._sigmoid_alpha(), lmax
+
+    def _sigmoid_alpha(self) -> Tensor:
+        """sigmoid(alpha) without autograd, cached until alpha is modified in place (an
+        optimizer step bumps its version): a rollout does not relaunch the 1-element kernel."""
+        key = (self.alpha.data_ptr(), self.alpha._version)
+        hit = getattr(self, "_sig_alpha", None)
+        if hit is None or hit[0] != key:
+            hit = self._sig_alpha = (key, torch.sigmoid(self.alpha.detach()))
+        return hit[1]
 
     def logits(self, data) -> Tuple[Tensor, Tensor]:
         """Unmasked logits [1, E+1] and sigmoid(alpha)."""

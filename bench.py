@@ -227,6 +227,15 @@ def generic_residual_leg(env, log, cfg: str, reps: int = 10):
     return out
 
 
+def select_bytes(env, B: int, winners: float) -> float:
+    """Algorithmic HBM bytes of the select phase (k_presample + k_splitters + k_tile + k_bsum,
+    DESIGN.md §3): the shared logits row read once and its inverse rates / weights written
+    once (k_presample), read once more by k_tile (the B samples of a tile share them through
+    L2), the B removal bitmaps and 12 bytes per staged winner."""
+    E1 = env.num_actions
+    return 4 * E1 + 2 * 8 * E1 + B * 4 * math.ceil((E1 - 1) / 32) + 12 * winners
+
+
 def roofline_obj(kernel, nbytes, ms, traffic=None):
     achieved = nbytes / (ms * 1e-3) / 1e9
     return {"kernel": kernel, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -432,6 +441,11 @@ def main():
                                      measured_traffic(args.config, bl)),
         }
         if world == 1:
+            sel = roofline_obj("rollout_select phase: k_presample + k_splitters + k_tile + k_bsum (k_tile ~80 % of "
+                               "it; VALU-bound: Philox4x32-10 + one det_logf per action and the bucket placement, "
+                               "DESIGN.md §5)", select_bytes(env, bl, float(counts.sum())),
+                               phases.get("rollout_select", float("nan")))
+            out["roofline_select"] = sel
             with torch.no_grad():
                 out["roofline_residual"] = generic_residual_leg(env, log, args.config)
         if not args.no_cpu_baseline and world == 1:

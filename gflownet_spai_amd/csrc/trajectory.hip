@@ -284,51 +284,54 @@ __device__ __forceinline__ void stream_words(const uint64_t* sctr, uint32_t& st0
   }
 }
 
-constexpr int kWChunk = 1024;  // actions per rate/weight block of k_presample
+// Inverse rates r = e^(l_E - l) and weights w = e^(l - lmax) of one chunk (NT * 4 actions) of
+// one logits row, for k_tile; the row padding past E gets r = inf (never a winner), w = 0.
+// Run by the extra blocks of k_splitters, so this HBM stream overlaps the B splitter blocks.
+template <int NT>
+__device__ __forceinline__ void rates_weights_chunk(int q, const float* __restrict__ logits, int64_t bstride,
+                                                    int32_t E, const float* __restrict__ lmax,
+                                                    float* __restrict__ rr, float* __restrict__ ww, int64_t wstride) {
+  constexpr int kPer = 4, kChunkA = NT * kPer;
+  const int tid = threadIdx.x;
+  const int nwb = (int)((wstride + kChunkA - 1) / kChunkA);
+  const int row = q / nwb;
+  const float* lg = logits + (int64_t)row * bstride;
+  const int64_t beg = (int64_t)(q % nwb) * kChunkA + tid;
+  const float lE = lg[E], lm = lmax[row];
+  float* r = rr + (int64_t)row * wstride;
+  float* w = ww + (int64_t)row * wstride;
+  float l[kPer];
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {  // every load in flight before the math
+    const int64_t i = beg + j * NT;
+    l[j] = i <= E ? lg[i] : 0.0f;
+  }
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    const int64_t i = beg + j * NT;
+    if (i <= E) {
+      r[i] = det_expf(lE - l[j]);
+      w[i] = action_weight(l[j], lm);
+    } else if (i < wstride) {
+      r[i] = __uint_as_float(0x7f800000u);
+      w[i] = 0.0f;
+    }
+  }
+}
+
+constexpr int kRwChunk = 4 * kSortNT;  // actions per rate/weight block of k_splitters
 __global__ __launch_bounds__(kSampNT) void k_presample(const float* __restrict__ logits, int64_t bstride, int32_t E,
-                                                       int32_t M, int32_t nsb, int32_t nsmp, uint32_t seed0,
-                                                       uint32_t seed1,
+                                                       int32_t M, int32_t nsb, uint32_t seed0, uint32_t seed1,
                                                        uint32_t st0, uint32_t st1, const uint64_t* __restrict__ sctr,
                                                        int32_t sample_base,
                                                        uint32_t* __restrict__ samp, int32_t* __restrict__ samp_cnt,
-                                                       int32_t* __restrict__ ctl, int32_t nctl,
-                                                       const float* __restrict__ lmax, float* __restrict__ rr,
-                                                       float* __restrict__ ww, int64_t wstride) {
+                                                       int32_t* __restrict__ ctl, int32_t nctl) {
   const int tid = threadIdx.x;
   stream_words(sctr, st0, st1);
   {  // the rollout's control block (bucket totals, oversized-bucket list count, tdev) starts at 0;
      // its first users (k_tile, k_sort2, k_bscan) run after this launch on the same stream
     const int nthr = gridDim.x * kSampNT;
     for (int q = blockIdx.x * kSampNT + tid; q < nctl; q += nthr) ctl[q] = 0;
-  }
-  const int B = nsmp;  // blocks [0, nsb * B): presample; then nwb blocks per logits row: rates and weights
-  if (blockIdx.x >= nsb * B) {  // inverse rates and weights of one chunk of a row (k_tile reads them)
-    const int q = blockIdx.x - nsb * B, nwb = (int)((wstride + kWChunk - 1) / kWChunk);
-    const int row = q / nwb;
-    const float* lg = logits + (int64_t)row * bstride;
-    constexpr int kPer = kWChunk / kSampNT;
-    const int64_t beg = (int64_t)(q % nwb) * kWChunk + tid;
-    const float lE = lg[E], lm = lmax[row];
-    float* r = rr + (int64_t)row * wstride;
-    float* w = ww + (int64_t)row * wstride;
-    float l[kPer];
-#pragma unroll
-    for (int j = 0; j < kPer; ++j) {  // every load in flight before the math
-      const int64_t i = beg + j * kSampNT;
-      l[j] = i <= E ? lg[i] : 0.0f;
-    }
-#pragma unroll
-    for (int j = 0; j < kPer; ++j) {
-      const int64_t i = beg + j * kSampNT;
-      if (i <= E) {
-        r[i] = det_expf(lE - l[j]);
-        w[i] = action_weight(l[j], lm);
-      } else if (i < wstride) {  // row padding: never a winner, no mass
-        r[i] = __uint_as_float(0x7f800000u);
-        w[i] = 0.0f;
-      }
-    }
-    return;
   }
   const int b = blockIdx.x / nsb, blk = blockIdx.x % nsb;
   const float* lg = logits + (int64_t)b * bstride;
@@ -363,7 +366,14 @@ __global__ __launch_bounds__(kSortNT) void k_splitters(int32_t E, int32_t M, int
                                                        const uint32_t* __restrict__ samp,
                                                        const int32_t* __restrict__ samp_cnt,
                                                        int32_t* __restrict__ nb_out, uint32_t* __restrict__ spl,
-                                                       uint16_t* __restrict__ lut, uint32_t* __restrict__ lut_base) {
+                                                       uint16_t* __restrict__ lut, uint32_t* __restrict__ lut_base,
+                                                       int32_t B, const float* __restrict__ logits, int64_t bstride,
+                                                       const float* __restrict__ lmax, float* __restrict__ rr,
+                                                       float* __restrict__ ww, int64_t wstride) {
+  if ((int)blockIdx.x >= B) {  // blocks [B, ...): rates and weights of the logits rows
+    rates_weights_chunk<kSortNT>(blockIdx.x - B, logits, bstride, E, lmax, rr, ww, wstride);
+    return;
+  }
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   __shared__ uint32_t s_smp[kSampCap];  // the sampled winner keys, compacted
   __shared__ int hist[kBins + 1];
@@ -1615,13 +1625,14 @@ extern "C" int spai_rollout_select(const float* logits, int64_t bstride, int32_t
   const uint32_t s0 = (uint32_t)seed, s1 = (uint32_t)(seed >> 32);
   const uint32_t t0 = (uint32_t)stream_id, t1 = (uint32_t)(stream_id >> 32);
   const int nsb = (w.M + kSampNT - 1) / kSampNT;
-  const int nwb = (int)((w.wstride + kWChunk - 1) / kWChunk);  // rate/weight blocks per logits row
+  const int nwb = (int)((w.wstride + kRwChunk - 1) / kRwChunk);  // rate/weight blocks per logits row
   const int64_t rowsel = bstride ? 1 : 0;
-  k_presample<<<nsb * B + nwb * (bstride ? B : 1), kSampNT, 0, s>>>(
-      logits, bstride, E, w.M, nsb, B, s0, s1, t0, t1, stream_ctr, sample_base, w.samp, w.samp_cnt, w.ctl, 4, lmax,
-      w.rr, w.ww, w.wstride);
+  k_presample<<<nsb * B, kSampNT, 0, s>>>(logits, bstride, E, w.M, nsb, s0, s1, t0, t1, stream_ctr, sample_base,
+                                          w.samp, w.samp_cnt, w.ctl, 4);
   SPAI_CHECK_LAUNCH();
-  k_splitters<<<B, kSortNT, 0, s>>>(E, w.M, nsb, w.samp, w.samp_cnt, w.nb, w.spl, w.lut, w.lut_base);
+  k_splitters<<<B + nwb * (bstride ? B : 1), kSortNT, 0, s>>>(E, w.M, nsb, w.samp, w.samp_cnt, w.nb, w.spl, w.lut,
+                                                             w.lut_base, B, logits, bstride, lmax, w.rr, w.ww,
+                                                             w.wstride);
   SPAI_CHECK_LAUNCH();
   k_tile<<<w.ntiles * B, kGrpNT, 0, s>>>(w.rr, w.ww, w.wstride, rowsel, E, B, w.ntiles, s0, s1, t0, t1, stream_ctr,
                                          sample_base, part, nparts, removed, words, w.nb, w.spl, w.lut, w.lut_base,

@@ -222,10 +222,10 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(W <= 5 ? FI
         int e0 = 0;
         if ((reinterpret_cast<uintptr_t>(dst) & 15u) == 0) {
           for (int e = t; e < ne / V; e += kNT)
-            reinterpret_cast<uint4*>(dst)[e] = reinterpret_cast<const uint4*>(sm)[e];
+            nt_store(reinterpret_cast<nt_u4*>(dst) + e, reinterpret_cast<const nt_u4*>(sm)[e]);
           e0 = ne / V * V;
         }
-        for (int e = e0 + t; e < ne; e += kNT) dst[e] = sm[e];
+        for (int e = e0 + t; e < ne; e += kNT) nt_store(dst + e, sm[e]);
       }
       double r2 = 0.0;
       if (valid) {
@@ -375,10 +375,10 @@ __global__ __launch_bounds__(kNT) void k_gram_fill_wide(int32_t n, int32_t line_
       int e0 = 0;
       if ((reinterpret_cast<uintptr_t>(dst) & 15u) == 0) {
         for (int e = t; e < ne / V; e += kNT)
-          reinterpret_cast<uint4*>(dst)[e] = reinterpret_cast<const uint4*>(s_m)[e];
+          nt_store(reinterpret_cast<nt_u4*>(dst) + e, reinterpret_cast<const nt_u4*>(s_m)[e]);
         e0 = ne / V * V;
       }
-      for (int e = e0 + t; e < ne; e += kNT) dst[e] = s_m[e];
+      for (int e = e0 + t; e < ne; e += kNT) nt_store(dst + e, s_m[e]);
     }
     s_r2[t] = valid ? r2 : 0.0;
     __syncthreads();

@@ -8,6 +8,15 @@ namespace spai {
 
 constexpr int kWave = 64;  // CDNA wavefront
 
+// Streaming output stores (M of the fill, the trajectory log): `nt` stores, which do not keep
+// the written lines in the caches — nothing in the step reads these outputs back, and the
+// write stream runs faster without allocating them (fill: 73 -> 63 us at C4).
+typedef unsigned int nt_u4 __attribute__((ext_vector_type(4)));
+template <typename T>
+__device__ __forceinline__ void nt_store(T* p, T v) {
+  __builtin_nontemporal_store(v, p);
+}
+
 // Random123 Philox4x32-10 (KAT-checked in tests against oracle/spai_oracle.py).
 __device__ __forceinline__ uint4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
                                                uint32_t k0, uint32_t k1) {

@@ -75,6 +75,7 @@ constexpr int kBufWord3 = 0x00020000;      // buffer resource dword 3 (raw byte 
 typedef unsigned int spai_u2 __attribute__((ext_vector_type(2)));
 typedef unsigned int spai_u3 __attribute__((ext_vector_type(3)));
 typedef unsigned int spai_u4 __attribute__((ext_vector_type(4)));
+constexpr int kNtAux = 2;                 // buffer-store cache policy: nt (streaming output, gfx950)
 constexpr int kBins = 4096;                // splitter histogram / bucket lookup table bins
 
 struct TrajWs {
@@ -1198,8 +1199,8 @@ __global__ __launch_bounds__(kSortNT) void k_sort2(int32_t E, int32_t B, int32_t
       const int e = 2 * (j * kSortNT + tv);
       if (2 * j * kSortNT < pv_n) {
         const uint2 a = reinterpret_cast<const uint2*>(a_out)[e >> 1];
-        if (e + 1 < pv_n) __builtin_amdgcn_raw_buffer_store_b128((spai_u4){a.x, 0u, a.y, 0u}, ra, e * 8, 0, 0);
-        else if (e < pv_n) __builtin_amdgcn_raw_buffer_store_b64((spai_u2){a.x, 0u}, ra, e * 8, 0, 0);
+        if (e + 1 < pv_n) __builtin_amdgcn_raw_buffer_store_b128((spai_u4){a.x, 0u, a.y, 0u}, ra, e * 8, 0, kNtAux);
+        else if (e < pv_n) __builtin_amdgcn_raw_buffer_store_b64((spai_u2){a.x, 0u}, ra, e * 8, 0, kNtAux);
       }
     }
 #pragma unroll
@@ -1208,11 +1209,11 @@ __global__ __launch_bounds__(kSortNT) void k_sort2(int32_t E, int32_t B, int32_t
       if (4 * j * kSortNT < pv_n) {
         const uint4 v = reinterpret_cast<const uint4*>(S)[e >> 2];
         if (e + 3 < pv_n) {
-          __builtin_amdgcn_raw_buffer_store_b128((spai_u4){v.x, v.y, v.z, v.w}, rf, e * 4, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b128((spai_u4){v.x, v.y, v.z, v.w}, rf, e * 4, 0, kNtAux);
         } else if (e < pv_n) {  // the bucket's last 1-3 step probabilities
-          __builtin_amdgcn_raw_buffer_store_b32(v.x, rf, e * 4, 0, 0);
-          if (e + 1 < pv_n) __builtin_amdgcn_raw_buffer_store_b32(v.y, rf, e * 4 + 4, 0, 0);
-          if (e + 2 < pv_n) __builtin_amdgcn_raw_buffer_store_b32(v.z, rf, e * 4 + 8, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b32(v.x, rf, e * 4, 0, kNtAux);
+          if (e + 1 < pv_n) __builtin_amdgcn_raw_buffer_store_b32(v.y, rf, e * 4 + 4, 0, kNtAux);
+          if (e + 2 < pv_n) __builtin_amdgcn_raw_buffer_store_b32(v.z, rf, e * 4 + 8, 0, kNtAux);
         }
       }
     }
@@ -1522,9 +1523,11 @@ __global__ __launch_bounds__(kFinNT) void k_pad(int32_t E, const int32_t* __rest
   for (int t = p0 + 4 * (blockIdx.x * kFinNT + threadIdx.x); t < T; t += 4 * gridDim.x * kFinNT) {
     if (t + 3 < T) {
       longlong2* a2 = reinterpret_cast<longlong2*>(ab + t);
-      a2[0] = make_longlong2(-1, -1);
-      a2[1] = make_longlong2(-1, -1);
-      *reinterpret_cast<float4*>(fb + t) = make_float4(1.0f, 1.0f, 1.0f, 1.0f);
+      const nt_u4 m1 = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+      const nt_u4 one = {0x3F800000u, 0x3F800000u, 0x3F800000u, 0x3F800000u};
+      nt_store(reinterpret_cast<nt_u4*>(a2), m1);
+      nt_store(reinterpret_cast<nt_u4*>(a2 + 1), m1);
+      nt_store(reinterpret_cast<nt_u4*>(fb + t), one);
     } else {
       for (int u = t; u < T; ++u) {
         ab[u] = -1;

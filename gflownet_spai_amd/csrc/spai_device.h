@@ -8,9 +8,10 @@ namespace spai {
 
 constexpr int kWave = 64;  // CDNA wavefront
 
-// Streaming output stores (M of the fill, the trajectory log): `nt` stores, which do not keep
-// the written lines in the caches — nothing in the step reads these outputs back, and the
-// write stream runs faster without allocating them (fill: 73 -> 63 us at C4).
+// Streaming output stores (M of the fill, the trajectory log of k_sort2): `nt` stores, which do
+// not keep the written lines in the caches — nothing in the step reads these outputs back, and
+// these interleaved read/write streams run faster without allocating them (fill: 73 -> 64 us
+// at C4).  Not for a pure write stream: k_pad's padding took 2x longer with them.
 typedef unsigned int nt_u4 __attribute__((ext_vector_type(4)));
 template <typename T>
 __device__ __forceinline__ void nt_store(T* p, T v) {

@@ -7,20 +7,23 @@ mean pool + fc on the state graph, random-init weights), throughput rollout (Gum
 of M (column SPAI) and the ||A M - I||_F reward, all inputs resident in HBM.
 
 Multi-GPU (one process per GPU; `--gpus N` starts the N ranks itself, or run it under
-torch.distributed.run):
-  --shard samples (default, strong scaling): the global batch of B candidates is split over
-      the ranks (rank r: candidates r*B/P .. (r+1)*B/P - 1, the same Philox draws as one GPU);
-      per step one all_gather of the rewards and one reduce of the best candidate's M to rank 0.
-      value = B*N / step.
-  --shard columns (the north star's column split, strong scaling): the
-      same B candidates on every rank; rank r orders the r-th slice of every trajectory and
-      fills lines shard_lines(N, r, P) of every candidate's M; ONE all_reduce per step (bucket
-      weight sums + residual partials); the best candidate's M is assembled with ONE all_gather
-      (--assemble best; `all` gathers every candidate, `none` skips it).  value = B*N / step.
-  --shard candidates (weak scaling): B candidates per rank, no collective.  value = P*B*N / step.
-The timed steps replay HIP graphs of the collective-free phases (the rollout's Philox stream
-id lives on the device, so every replay draws a fresh rollout); the per-phase HIP-event
-timings come from an eager pass of the same step.  Prints ONE JSON line on rank 0.
+torch.distributed.run), DESIGN.md §6:
+  --shard columns (default; the north star's column split, weak scaling): every GPU rolls out
+      --batch candidates (global sample ids rank*batch ..: the same Philox draws as one GPU with
+      the whole batch); one all_to_all ships each GPU the bitmap words of its 256-line-aligned
+      column shard for every candidate; every GPU fills + scores its lines of ALL P*batch
+      candidates; one all_reduce of the exact residual sums (bit-identical to one GPU); one
+      all_gather assembles the best candidate's M.  value = P*batch*N / step (also reported
+      without the M all_gather).  --strong: --batch is the global batch instead.
+  --shard slices: the same B candidates on every rank, one slice of every trajectory per rank.
+  --shard samples (strong scaling): the global batch split over the ranks; one all_gather of the
+      rewards and one reduce of the best candidate's M to rank 0.
+  --shard candidates (weak scaling): --batch candidates per rank, no collective.
+The timed steps replay HIP graphs of every maximal run of collective-free phases
+(GFlowNet.rollout_phases; one GPU: one graph per step), the collectives run eagerly between
+them; the Philox stream id lives on the device, so every replay draws a fresh rollout.  The
+per-phase HIP-event timings come from an eager pass of the same step.  Prints ONE JSON line on
+rank 0.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config c4|c2|c3] [--batch B]
 """
@@ -268,7 +271,9 @@ def main():
     ap.add_argument("--batch", type=int, default=8)
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--shard", default="samples", choices=["samples", "columns", "candidates"])
+    ap.add_argument("--shard", default="columns", choices=["columns", "slices", "samples", "candidates"])
+    ap.add_argument("--strong", action="store_true",
+                    help="columns split: --batch is the GLOBAL batch (batch/P rollouts per GPU) instead of per GPU")
     ap.add_argument("--assemble", default="best", choices=["best", "all", "none"])
     ap.add_argument("--no-graph", action="store_true", help="time eager steps (host launches) instead of graph replays")
     args = ap.parse_args()
@@ -288,49 +293,50 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     from gflownet_spai_amd import GFlowNet, PreconditionerEnv, kernels
-    from gflownet_spai_amd.distributed import allgather_lines
+    from gflownet_spai_amd.distributed import LINE_ALIGN, allgather_lines
 
     dims, grid, dtype, text = CONFIGS[args.config]
     A, P = config_matrices(args.config)
     n = A.shape[0]
     env = PreconditionerEnv(n, P, A, side="AM", fill="lsq", keep_m=True, device=dev)
     E = env.num_actions - 1
-    B = args.batch
-    columns = args.shard == "columns"
-    samples = args.shard == "samples"
-    strong = columns or samples
-    split = columns and world > 1
-    if samples and B % world:
-        sys.exit(f"bench.py: --shard samples needs the batch ({B}) divisible by the GPU count ({world})")
-    bl = B // world if samples else B  # candidates this rank rolls out and fills
-    base = rank * bl if samples else (0 if columns else rank * B)
+    shard = args.shard if world > 1 else "columns"  # one GPU: every split is the same one-GPU step
+    if shard in ("samples", "slices") or (shard == "columns" and args.strong):
+        if args.batch % world:
+            sys.exit(f"bench.py: --shard {shard} needs the batch ({args.batch}) divisible by the GPU count ({world})")
+        B, bl, strong = args.batch, args.batch // world if shard != "slices" else args.batch, True
+    else:  # columns (weak: --batch rollouts per GPU, fill of every candidate by column shard) / candidates
+        B, bl, strong = args.batch * world, args.batch, False
+    base = {"samples": rank * bl, "candidates": rank * bl}.get(shard, 0)
+    split = {"columns": "columns", "slices": "slices"}.get(shard)
     model = GFlowNet(make_policy(env, P, dev), None, env, mode="throughput", seed=1234, sample_base=base,
-                     shard=(rank, world, None) if split else None)
+                     shard=(rank, world, None) if split else None, split=split or "columns")
     s0 = [P] * bl
     assembled = {}
+    do_assemble = [args.assemble != "none" and world > 1 and shard != "candidates"]
 
     def assemble(log):
-        if world == 1 or args.assemble == "none" or not strong:
+        if not do_assemble[0]:
             return
-        if samples:  # global rewards everywhere, the best candidate's M on rank 0
+        if shard == "samples":  # global rewards everywhere, the best candidate's M on rank 0
             from gflownet_spai_amd.distributed import select_best_samples
             assembled["r"], assembled["best"], assembled["m"] = select_best_samples(log.rewards, env.last_m)
             return
-        m = env.last_m
+        m = env.last_m  # columns: [B, this shard's lines, W] of EVERY candidate; slices: the same B on every rank
         if args.assemble == "best":  # the candidate with the highest reward: the preconditioner kept
-            m = m.index_select(0, torch.argmax(log.rewards).view(1))
-        assembled["m"] = allgather_lines(m, n)
+            m = m.index_select(0, torch.argmax(log.rewards_all).view(1))
+        assembled["m"] = allgather_lines(m, n, align=LINE_ALIGN if shard == "columns" else 1)
+
+    phases = model.rollout_phases()
 
     def eager_step():
-        with kernels._timed("begin"):
-            st = model.rollout_begin(s0)
-        with kernels._timed("exchange"):
-            model.rollout_exchange(st)
-        with kernels._timed("end"):
-            log = model.rollout_end(st)
+        st = {"s0": s0}
+        for i, (fn, coll) in enumerate(phases):
+            with kernels._timed(f"phase{i}_{fn.__name__.strip('_')}"):
+                fn(st)
         with kernels._timed("assemble"):
-            assemble(log)
-        return log
+            assemble(st["log"])
+        return st["log"]
 
     def barrier():
         if world > 1:
@@ -349,37 +355,41 @@ def main():
             log = eager_step()
         barrier()
         dt_eager = (time.perf_counter() - t0) / k_eager
-        phases = {k: float(np.mean(kernels.timer_ms(k))) for k in kernels.TIMERS}
+        phase_ms = {k: float(np.mean(kernels.timer_ms(k))) for k in kernels.TIMERS}
         kernels.TIMERS = None
 
         use_graph = not args.no_graph
         if use_graph:
-            # capture: world 1 -> one graph of the whole step; split -> the collective-free
-            # phases (begin, end) as two graphs around the eager all_reduce and all_gather
+            # capture every maximal run of collective-free phases as one HIP graph (one GPU: the
+            # whole step is one graph); the collectives run eagerly between the replays
             side = torch.cuda.Stream(dev)
             side.wait_stream(torch.cuda.current_stream(dev))
             with torch.cuda.stream(side):
                 eager_step()
             torch.cuda.current_stream(dev).wait_stream(side)
             barrier()
-            g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-            if not split:
-                with torch.cuda.graph(g1):
-                    st = model.rollout_begin(s0)
-                    model.rollout_exchange(st)
-                    glog = model.rollout_end(st)
-            else:
-                with torch.cuda.graph(g1):
-                    st = model.rollout_begin(s0)
-                model.rollout_exchange(st)  # allocates the persistent exchange buffer the end phase reads
-                with torch.cuda.graph(g2, pool=g1.pool()):
-                    glog = model.rollout_end(st)
+            st = {"s0": s0}
+            program, pool, run = [], None, []
+            for fn, coll in phases + [(None, True)]:
+                if fn is not None and not coll:
+                    run.append(fn)
+                    continue
+                if run:
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g, pool=pool):
+                        for f in run:
+                            f(st)
+                    pool = g.pool()
+                    program.append(g.replay)
+                    run = []
+                if fn is not None:
+                    fn(st)  # a collective, eagerly (allocates its persistent buffers before the next capture)
+                    program.append(lambda f=fn: f(st))
+            glog = st["log"]
 
             def step():
-                g1.replay()
-                if split:
-                    model.rollout_exchange(st)
-                    g2.replay()
+                for p in program:
+                    p()
                 assemble(glog)
                 return glog
 
@@ -394,22 +404,46 @@ def main():
             log = step()
         barrier()
         dt = (time.perf_counter() - t0) / args.steps
+        dt_noasm = dt
+        if do_assemble[0]:  # the same steps without the M all_gather (reported apart)
+            do_assemble[0] = False
+            barrier()
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                log = step()
+            barrier()
+            dt_noasm = (time.perf_counter() - t0) / args.steps
+            do_assemble[0] = True
     if world > 1:
-        t = torch.tensor([dt, dt_eager], device=dev, dtype=torch.float64)
+        t = torch.tensor([dt, dt_eager, dt_noasm], device=dev, dtype=torch.float64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        dt, dt_eager = float(t[0]), float(t[1])
+        dt, dt_eager, dt_noasm = float(t[0]), float(t[1]), float(t[2])
     res = env.last_residual.double().cpu().numpy()
     counts = log.counts.cpu().numpy()
 
     if rank == 0:
-        fill_ms = phases.get("fill_residual", float("nan"))
-        fb = fill_bytes(env, bl)
-        if split:  # the rank's fill covers its own lines only (rank 0: the first, largest shard)
+        fill_ms = phase_ms.get("fill_residual", float("nan"))
+        fb = fill_bytes(env, B if shard == "columns" else bl)
+        if split:  # the rank's fill covers its own lines only (rank 0: the first shard)
             fb *= (model.lines[1] - model.lines[0]) / n
         gram_t = "f32" if env.gram is not None and env.gram.dtype == torch.float32 else "f64"
+        workload = text + {
+            "columns": (f", {bl} rollouts per GPU x {world} GPUs = B={B} candidates; columns of M sharded over the "
+                        f"GPUs (256-line-aligned shards, fill + ||AM-I|| of every candidate per shard)" +
+                        (": one all_to_all of the bitmap windows, one all_reduce of the exact residual sums, one "
+                         "all_gather of the best candidate's M" if world > 1 else "")),
+            "slices": f", B={B} candidates, trajectory slices + lines of M per GPU over {world} GPUs (one all_reduce, "
+                      f"{args.assemble} M all_gather)",
+            "samples": f", B={B} candidates split over {world} GPUs ({bl} per GPU; one all_gather of the rewards "
+                       f"and one reduce of the best candidate's M per step)",
+            "candidates": f", B={bl} candidates per GPU, no collective"}[shard]
+        metric = {"c4": "SPAI columns/sec + final ||AM-I||_F, 2D Poisson 1024^2, at 1/2/4/8 GPU",
+                  "c2": "SPAI columns/sec + final ||AM-I||_F, 2D Poisson 256^2 (C2)",
+                  "c3": "SPAI columns/sec + final ||AM-I||_F, 3D Laplacian 64^3 fp64 (C3)",
+                  "c5s": "SPAI columns/sec + final ||AM-I||_F, thermal2-like stand-in fp64 (C5 stand-in)"}[args.config]
         out = {
-            "metric": "SPAI columns/sec + final ||AM-I||_F, 2D Poisson 1024^2, at 1/2/4/8 GPU",
-            "value": B * n * (1 if strong else world) / dt,
+            "metric": metric,
+            "value": B * n / dt,
             "unit": "columns/s",
             "n_gpus": world,
             "steps": args.steps,
@@ -421,21 +455,17 @@ def main():
             "dtype": "f32 storage, f64 solve/accumulate" if dtype == torch.float32 else "f64",
             "data": "synthetic (random-init seeded ForwardPolicy GATv2x2+fc, hid=4, evaluated on the state graph in "
                     "every step; terminal fc bias set for 20% expected removal; matrix from its stencil)",
-            "config": {"workload": text + {
-                "samples": f", B={B} candidates split over {world} GPUs ({bl} per GPU; one all_gather of the rewards "
-                           f"and one reduce of the best candidate's M per step)",
-                "columns": f", B={B} candidates, columns split over {world} GPUs (trajectory slices + lines of M per "
-                           f"rank, one all_reduce, {args.assemble} M all_gather)",
-                "candidates": f", B={B} candidates per GPU"}[args.shard] +
-                                   ": ForwardPolicy logits + throughput rollout + LSQ fill + ||AM-I||_F",
-                       "N": n, "E": E, "global_batch": B * (1 if strong else world),
-                       "parallelism": f"{args.shard} sharded x{world}"},
+            "config": {"workload": workload + ": ForwardPolicy logits + throughput rollout + LSQ fill + ||AM-I||_F",
+                       "N": n, "E": E, "global_batch": B, "rollouts_per_gpu": bl,
+                       "parallelism": f"{shard} sharded x{world}"},
+            "value_without_assembly": B * n / dt_noasm,
+            "ms_per_step_without_assembly": dt_noasm * 1e3,
             "graph": use_graph,
             "ms_per_step_eager": dt_eager * 1e3,
             "final_residual_fro": float(res[0]),
             "final_residual_fro_mean": float(res.mean()),
             "removed_per_candidate_mean": float(counts.mean()),
-            "phases_ms": phases,
+            "phases_ms": phase_ms,
             "roofline": roofline_obj(f"k_gram_fill<{env.pattern.width},{gram_t},LSQ> (LSQ fill of M + ||AM-I||^2; A "
                                      f"reaches it through the env-constant Gram cache)", fb, fill_ms,
                                      measured_traffic(args.config, bl)),
@@ -444,7 +474,7 @@ def main():
             sel = roofline_obj("rollout_select phase: k_presample + k_splitters + k_tile + k_bsum (k_tile ~80 % of "
                                "it; VALU-bound: Philox4x32-10 + one det_logf per action and the bucket placement, "
                                "DESIGN.md §5)", select_bytes(env, bl, float(counts.sum())),
-                               phases.get("rollout_select", float("nan")))
+                               phase_ms.get("rollout_select", float("nan")))
             out["roofline_select"] = sel
             with torch.no_grad():
                 out["roofline_residual"] = generic_residual_leg(env, log, args.config)

@@ -21,7 +21,8 @@ if os.environ.get("SPAI_LIB_VARIANT"):  # A/B timing of kernel variants built un
 SPAI_OK, SPAI_ERR_INVALID, SPAI_ERR_HIP, SPAI_ERR_UNSUPPORTED = 0, 1, 2, 3
 FILL_COPY, FILL_LSQ = 0, 1
 DTYPE_F32, DTYPE_F64 = 0, 1
-ABI_VERSION = 12
+ABI_VERSION = 13
+RES2_LIMBS = 8  # SPAI_RES2_LIMBS
 
 _c_i32, _c_i64, _c_u64, _c_sz, _c_p = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_size_t, ctypes.c_void_p
 
@@ -53,10 +54,10 @@ SIGNATURES = {
     "spai_gram_bytes": (_c_sz, [_c_i32, _c_i32]),
     "spai_gram_build": (ctypes.c_int, [_c_i32, _c_i32, _c_p, _c_i32, _c_p, _c_p, _c_i32, _c_p, _c_p]),
     "spai_fill_residual_gram": (ctypes.c_int, [_c_i32, _c_i32, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_i32, _c_i32,
-                                               _c_p, _c_i32, _c_p, _c_i32, _c_p, _c_p, _c_sz, _c_p]),
+                                               _c_p, _c_i32, _c_i32, _c_p, _c_i32, _c_p, _c_p, _c_sz, _c_p]),
     "spai_gram_compact": (ctypes.c_int, [_c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p]),
     "spai_fill_lines_gram": (ctypes.c_int, [_c_i32, _c_i32, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_i32, _c_i32,
-                                            _c_p, _c_i32, _c_p, _c_i32, _c_p, _c_sz, _c_p]),
+                                            _c_p, _c_i32, _c_i32, _c_p, _c_i32, _c_p, _c_sz, _c_p]),
     "spai_policy_params": (_c_sz, [_c_i32, _c_i32, _c_i32]),
     "spai_policy_workspace_bytes": (_c_sz, [_c_i32, _c_i32, _c_i32]),
     "spai_policy_logits": (ctypes.c_int, [_c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p,
@@ -81,9 +82,11 @@ SIGNATURES = {
     "spai_lstm_backward_workspace_bytes": (_c_sz, [_c_i32, _c_i32, _c_i32]),
     "spai_lstm_backward": (ctypes.c_int, [_c_i32, _c_i32, _c_p, _c_i64, _c_p, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_p,
                                           _c_p, _c_p, _c_p, _c_sz, _c_p]),
-    "spai_fill_reduce": (ctypes.c_int, [_c_i32, _c_i32, _c_p, _c_p, _c_p]),
+    "spai_fill_reduce": (ctypes.c_int, [_c_i32, _c_i32, _c_p, _c_p, _c_p, _c_p]),
     "spai_fill_residual": (ctypes.c_int, [_c_i32, _c_i32, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_i32, _c_p, _c_p,
-                                          _c_i32, _c_i32, _c_p, _c_i32, _c_p, _c_i32, _c_p, _c_p, _c_sz, _c_p]),
+                                          _c_i32, _c_i32, _c_p, _c_i32, _c_i32, _c_p, _c_i32, _c_p, _c_p, _c_p, _c_sz,
+                                          _c_p]),
+    "spai_res2_from_limbs": (ctypes.c_int, [_c_i32, _c_p, _c_p, _c_p]),
 }
 
 _lib = None

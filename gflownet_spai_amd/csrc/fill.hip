@@ -27,7 +27,8 @@ __global__ __launch_bounds__(kNT) void k_line(int32_t line_begin, int32_t line_e
                                               const float* __restrict__ pat_val, const int32_t* __restrict__ a_idx,
                                               const TA* __restrict__ a_val, int32_t B,
                                               const uint32_t* __restrict__ removed, int32_t words,
-                                              TM* __restrict__ m_out, double* __restrict__ partials) {
+                                              int32_t word_base, TM* __restrict__ m_out,
+                                              double* __restrict__ partials) {
   __shared__ double sred[kNT / 64];
   const int j = line_begin + blockIdx.x * kNT + threadIdx.x;
   const bool valid = j < line_end;
@@ -96,7 +97,10 @@ __global__ __launch_bounds__(kNT) void k_line(int32_t line_begin, int32_t line_e
     const uint32_t* rb = removed + (int64_t)b * words;
     bool keep[W];
 #pragma unroll
-    for (int p = 0; p < W; ++p) keep[p] = idx[p] >= 0 && !((rb[act[p] >> 5] >> (act[p] & 31)) & 1u);
+    for (int p = 0; p < W; ++p) {
+      const int wo = idx[p] >= 0 ? (act[p] >> 5) - word_base : 0;  // row-relative word (window rows)
+      keep[p] = idx[p] >= 0 && !((rb[wo] >> (act[p] & 31)) & 1u);
+    }
 
     double mr[W];
     if constexpr (!LSQ) {
@@ -185,8 +189,8 @@ __global__ __launch_bounds__(kNT) void k_line_hash(int32_t line_begin, int32_t l
                                                    const float* __restrict__ pat_val,
                                                    const int32_t* __restrict__ a_idx, const TA* __restrict__ a_val,
                                                    int32_t B, const uint32_t* __restrict__ removed, int32_t words,
-                                                   float* __restrict__ m_out, double* __restrict__ partials,
-                                                   int32_t tb) {
+                                                   int32_t word_base, float* __restrict__ m_out,
+                                                   double* __restrict__ partials, int32_t tb) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   double* vals = reinterpret_cast<double*>(smem);
   int* keys = reinterpret_cast<int*>(smem + (size_t)tb * sizeof(double));
@@ -206,7 +210,7 @@ __global__ __launch_bounds__(kNT) void k_line_hash(int32_t line_begin, int32_t l
     if (m_out != nullptr) {
       for (int p = threadIdx.x; p < wrt; p += kNT) {
         const int k = pat_idx[base + p], a = pat_act[base + p];
-        const bool keep = k >= 0 && !((rb[a >> 5] >> (a & 31)) & 1u);
+        const bool keep = k >= 0 && !((rb[(a >> 5) - word_base] >> (a & 31)) & 1u);
         m_out[((int64_t)b * nloc + (j - line_begin)) * wrt + p] = keep ? pat_val[base + p] : 0.0f;
       }
     }
@@ -215,7 +219,7 @@ __global__ __launch_bounds__(kNT) void k_line_hash(int32_t line_begin, int32_t l
       const int k = pat_idx[base + p];
       if (k < 0) continue;
       const int a = pat_act[base + p];
-      if ((rb[a >> 5] >> (a & 31)) & 1u) continue;
+      if ((rb[(a >> 5) - word_base] >> (a & 31)) & 1u) continue;
       const int64_t o = (int64_t)k * wart + s;
       const int l = a_idx[o];
       if (l < 0) continue;
@@ -236,24 +240,14 @@ constexpr int kHashMaxEntries = 13000;  // 13000 x 12 B = 152 KiB of the 160 KiB
 template <typename TA>
 hipError_t launch_hash(int32_t lb, int32_t le, int32_t wrt, int32_t wart, const int32_t* pi, const int32_t* pa,
                        const float* pv, const int32_t* ai, const void* av, int32_t B, const uint32_t* rm,
-                       int32_t words, void* mo, double* partials, int32_t tb, hipStream_t s) {
+                       int32_t words, int32_t wb, void* mo, double* partials, int32_t tb, hipStream_t s) {
   const size_t lds = (size_t)tb * (sizeof(double) + sizeof(int));
   hipError_t e = hipFuncSetAttribute((const void*)k_line_hash<TA>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      (int)lds);
   if (e != hipSuccess) return e;
   k_line_hash<TA><<<le - lb, kNT, lds, s>>>(lb, le, wrt, wart, pi, pa, pv, ai, static_cast<const TA*>(av), B, rm,
-                                             words, static_cast<float*>(mo), partials, tb);
+                                             words, wb, static_cast<float*>(mo), partials, tb);
   return hipGetLastError();
-}
-
-__global__ __launch_bounds__(kNT) void k_reduce(const double* __restrict__ partials, int32_t nparts,
-                                                double* __restrict__ out) {
-  __shared__ double sred[kNT / 64];
-  const int b = blockIdx.x;
-  double s = 0.0;
-  for (int i = threadIdx.x; i < nparts; i += kNT) s += partials[(int64_t)b * nparts + i];
-  s = block_sum<kNT>(s, sred);
-  if (threadIdx.x == 0) out[b] = s;
 }
 
 // Reward of preconditioner.py:55-66 + 137-165 for every sample, with the reference's
@@ -280,15 +274,15 @@ __global__ void k_rewards(const double* __restrict__ res2, const int32_t* __rest
 template <int W, int WA, typename TA, typename TM, bool LSQ>
 hipError_t launch_line(int32_t lb, int32_t le, int32_t wrt, int32_t wart, const int32_t* pi, const int32_t* pa,
                        const float* pv, const int32_t* ai, const void* av, int32_t B, const uint32_t* rm,
-                       int32_t words, void* mo, double* partials, int32_t nparts, hipStream_t s) {
+                       int32_t words, int32_t wb, void* mo, double* partials, int32_t nparts, hipStream_t s) {
   k_line<W, WA, TA, TM, LSQ><<<nparts, kNT, 0, s>>>(lb, le, wrt, wart, pi, pa, pv, ai, static_cast<const TA*>(av), B,
-                                                     rm, words, static_cast<TM*>(mo), partials);
+                                                     rm, words, wb, static_cast<TM*>(mo), partials);
   return hipGetLastError();
 }
 
 using LaunchFn = hipError_t (*)(int32_t, int32_t, int32_t, int32_t, const int32_t*, const int32_t*, const float*,
-                                const int32_t*, const void*, int32_t, const uint32_t*, int32_t, void*, double*,
-                                int32_t, hipStream_t);
+                                const int32_t*, const void*, int32_t, const uint32_t*, int32_t, int32_t, void*,
+                                double*, int32_t, hipStream_t);
 
 struct Variant {
   int W, WA, a_dtype, m_dtype, mode;
@@ -322,20 +316,22 @@ extern "C" size_t spai_fill_workspace_bytes(int32_t n_lines, int32_t B) {
 extern "C" int spai_fill_residual(int32_t fill_mode, int32_t n, int32_t line_begin, int32_t line_end, int32_t W,
                                   const int32_t* pat_idx, const int32_t* pat_act, const float* pat_val, int32_t WA,
                                   const int32_t* a_idx, const void* a_val, int32_t a_dtype, int32_t B,
-                                  const uint32_t* removed, int32_t words, void* m_out, int32_t m_dtype,
-                                  double* res2_out, void* workspace, size_t workspace_bytes, void* stream) {
+                                  const uint32_t* removed, int32_t words, int32_t word_base, void* m_out,
+                                  int32_t m_dtype, double* res2_out, int64_t* limbs_out, void* workspace,
+                                  size_t workspace_bytes, void* stream) {
   SPAI_CHECK_ARG(fill_mode == SPAI_FILL_COPY || fill_mode == SPAI_FILL_LSQ, "spai_fill_residual: bad fill_mode %d",
                  fill_mode);
   SPAI_CHECK_ARG(a_dtype == SPAI_DTYPE_F32 || a_dtype == SPAI_DTYPE_F64, "spai_fill_residual: bad a_dtype");
   SPAI_CHECK_ARG(m_dtype == SPAI_DTYPE_F32 || m_dtype == SPAI_DTYPE_F64, "spai_fill_residual: bad m_dtype");
   SPAI_CHECK_ARG(n >= 1 && line_begin >= 0 && line_end >= line_begin && line_end <= n && W >= 1 && WA >= 1 &&
-                     B >= 1 && words >= 0,
+                     B >= 1 && words >= 1 && word_base >= 0,
                  "spai_fill_residual: bad shape");
-  SPAI_CHECK_ARG(res2_out && workspace, "spai_fill_residual: null output/workspace");
+  SPAI_CHECK_ARG((res2_out || limbs_out) && workspace, "spai_fill_residual: null output/workspace");
   hipStream_t s = (hipStream_t)stream;
   const int32_t nl = line_end - line_begin;
   if (nl == 0) {
-    SPAI_CHECK_HIP(hipMemsetAsync(res2_out, 0, sizeof(double) * B, s));
+    if (res2_out) SPAI_CHECK_HIP(hipMemsetAsync(res2_out, 0, sizeof(double) * B, s));
+    if (limbs_out) SPAI_CHECK_HIP(hipMemsetAsync(limbs_out, 0, sizeof(int64_t) * kLimbSlots * B, s));
     return SPAI_OK;
   }
   SPAI_CHECK_ARG(pat_idx && pat_act && pat_val && a_idx && a_val && removed, "spai_fill_residual: null input");
@@ -357,11 +353,11 @@ extern "C" int spai_fill_residual(int32_t fill_mode, int32_t n, int32_t line_beg
       double* partials = static_cast<double*>(workspace);
       hipError_t e = a_dtype == SPAI_DTYPE_F32
                          ? launch_hash<float>(line_begin, line_end, W, WA, pat_idx, pat_act, pat_val, a_idx, a_val, B,
-                                              removed, words, m_out, partials, tb, s)
+                                              removed, words, word_base, m_out, partials, tb, s)
                          : launch_hash<double>(line_begin, line_end, W, WA, pat_idx, pat_act, pat_val, a_idx, a_val,
-                                               B, removed, words, m_out, partials, tb, s);
+                                               B, removed, words, word_base, m_out, partials, tb, s);
       SPAI_CHECK_HIP(e);
-      k_reduce<<<B, kNT, 0, s>>>(partials, nl, res2_out);
+      k_fixed_reduce<kNT><<<B, kNT, 0, s>>>(partials, nl, res2_out, limbs_out);
       SPAI_CHECK_LAUNCH();
       return SPAI_OK;
     }
@@ -371,9 +367,9 @@ extern "C" int spai_fill_residual(int32_t fill_mode, int32_t n, int32_t line_beg
   }
   const int32_t nparts = (nl + kNT - 1) / kNT;
   double* partials = static_cast<double*>(workspace);
-  SPAI_CHECK_HIP(v->fn(line_begin, line_end, W, WA, pat_idx, pat_act, pat_val, a_idx, a_val, B, removed, words, m_out,
-                       partials, nparts, s));
-  k_reduce<<<B, kNT, 0, s>>>(partials, nparts, res2_out);
+  SPAI_CHECK_HIP(v->fn(line_begin, line_end, W, WA, pat_idx, pat_act, pat_val, a_idx, a_val, B, removed, words,
+                       word_base, m_out, partials, nparts, s));
+  k_fixed_reduce<kNT><<<B, kNT, 0, s>>>(partials, nparts, res2_out, limbs_out);
   SPAI_CHECK_LAUNCH();
   return SPAI_OK;
 }

@@ -105,7 +105,8 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(W <= 5 ? FI
                                                    const float* __restrict__ pat_val,
                                                    const GT* __restrict__ gram, int32_t B,
                                                    const uint32_t* __restrict__ removed, int32_t words,
-                                                   TM* __restrict__ m_out, double* __restrict__ partials) {
+                                                   int32_t word_base, TM* __restrict__ m_out,
+                                                   double* __restrict__ partials) {
   constexpr int T = tri(W);
   __shared__ double s_r2[kChunk][kNT];
   __shared__ __attribute__((aligned(16))) TM s_m[2][kNT * W];
@@ -132,7 +133,7 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(W <= 5 ? FI
   for (int p = 0; p < W; ++p) c[p] = (double)gp[(T + p) * 64];
   int wofs[W];  // bitmap word offsets / bit positions of the slots
 #pragma unroll
-  for (int p = 0; p < W; ++p) wofs[p] = act[p] >= 0 ? act[p] >> 5 : 0;
+  for (int p = 0; p < W; ++p) wofs[p] = act[p] >= 0 ? (act[p] >> 5) - word_base : 0;  // row-relative
   const int nvl = min(kNT, line_end - (line_begin + lb * kNT));  // valid lines of the block
 
   // the bitmap words of the next sample are loaded while the current one is solved
@@ -268,7 +269,8 @@ __global__ __launch_bounds__(kNT) void k_gram_fill_wide(int32_t n, int32_t line_
                                                         const float* __restrict__ pat_val,
                                                         const double* __restrict__ gram, int32_t B,
                                                         const uint32_t* __restrict__ removed, int32_t words,
-                                                        TM* __restrict__ m_out, double* __restrict__ partials) {
+                                                        int32_t word_base, TM* __restrict__ m_out,
+                                                        double* __restrict__ partials) {
   constexpr int T = tri(W);
   static_assert(W <= 32, "keep mask is one 32-bit word");
   __shared__ double s_r2[kNT];
@@ -289,7 +291,7 @@ __global__ __launch_bounds__(kNT) void k_gram_fill_wide(int32_t n, int32_t line_
 #pragma unroll
   for (int p = 0; p < W; ++p) {
     const int ap = s_act[p][t];
-    wd[p] = ap >= 0 ? removed[ap >> 5] : 0u;
+    wd[p] = ap >= 0 ? removed[(ap >> 5) - word_base] : 0u;
   }
 #pragma unroll 1
   for (int b = 0; b < B; ++b) {
@@ -304,7 +306,7 @@ __global__ __launch_bounds__(kNT) void k_gram_fill_wide(int32_t n, int32_t line_
 #pragma unroll
       for (int p = 0; p < W; ++p) {
         const int ap = s_act[p][t];
-        wd[p] = ap >= 0 ? rn[ap >> 5] : 0u;
+        wd[p] = ap >= 0 ? rn[(ap >> 5) - word_base] : 0u;
       }
     }
     double a[T], y[W];
@@ -312,17 +314,14 @@ __global__ __launch_bounds__(kNT) void k_gram_fill_wide(int32_t n, int32_t line_
     for (int q = 0; q < T; ++q) a[q] = gp[q * 64];
     double r2 = 1.0;
     if constexpr (LSQ) {
-      // pivot floor relative to the line's largest diagonal (one register instead of W)
-      double dmax = 0.0;
-#pragma unroll
-      for (int k = 0; k < W; ++k) dmax = fmax(dmax, a[gidx<W>(k, k)]);
-      const double floor_ = 1e-13 * dmax;
 #pragma unroll
       for (int k = 0; k < W; ++k) y[k] = gp[(T + k) * 64];  // c, solved in place below
 #pragma unroll
       for (int k = 0; k < W; ++k) {
         const double d = a[gidx<W>(k, k)];
-        const double ik = (((keep >> k) & 1u) && d > floor_) ? fast_rcp(d) : 0.0;
+        // per-pivot floor 1e-13 G_kk, as k_gram_fill and fill.hip's k_line (G_kk re-read from the
+        // cache line this sample just read: no W extra registers)
+        const double ik = (((keep >> k) & 1u) && d > 1e-13 * gp[gidx<W>(k, k) * 64]) ? fast_rcp(d) : 0.0;
         a[gidx<W>(k, k)] = ik;  // the diagonal slot now holds 1/D_k
         // rows i descending: row i's multiplier L_ik = EL_ik / D_k replaces EL_ik only after
         // every update that still reads it (rows j <= i use EL_jk)
@@ -393,31 +392,21 @@ __global__ __launch_bounds__(kNT) void k_gram_fill_wide(int32_t n, int32_t line_
   }
 }
 
-__global__ __launch_bounds__(kNT) void k_gram_reduce(const double* __restrict__ partials, int32_t nparts,
-                                                     double* __restrict__ out) {
-  __shared__ double sred[kNT / 64];
-  const int b = blockIdx.x;
-  double s = 0.0;
-  for (int i = threadIdx.x; i < nparts; i += kNT) s += partials[(int64_t)b * nparts + i];
-  s = block_sum<kNT>(s, sred);
-  if (threadIdx.x == 0) out[b] = s;
-}
-
 static int gram_width(int32_t W) { return W <= 5 ? 5 : (W <= 7 ? 7 : (W <= 13 ? 13 : 0)); }
 
 template <int W, typename TM, bool LSQ>
 hipError_t launch_fill(int32_t n, int32_t lb, int32_t le, int32_t wrt, const int32_t* pa, const float* pv,
-                       const void* g, bool g32, int32_t B, const uint32_t* rm, int32_t words, void* mo,
-                       double* partials, int32_t nparts, hipStream_t s) {
+                       const void* g, bool g32, int32_t B, const uint32_t* rm, int32_t words, int32_t wb,
+                       void* mo, double* partials, int32_t nparts, hipStream_t s) {
   if constexpr (W > 7)
     k_gram_fill_wide<W, TM, LSQ><<<nparts, kNT, 0, s>>>(n, lb, le, wrt, pa, pv, static_cast<const double*>(g), B, rm,
-                                                       words, static_cast<TM*>(mo), partials);
+                                                       words, wb, static_cast<TM*>(mo), partials);
   else if (g32)
     k_gram_fill<W, TM, LSQ, float><<<nparts, kNT, 0, s>>>(n, lb, le, wrt, pa, pv, static_cast<const float*>(g), B, rm,
-                                                           words, static_cast<TM*>(mo), partials);
+                                                           words, wb, static_cast<TM*>(mo), partials);
   else
     k_gram_fill<W, TM, LSQ, double><<<nparts, kNT, 0, s>>>(n, lb, le, wrt, pa, pv, static_cast<const double*>(g), B,
-                                                            rm, words, static_cast<TM*>(mo), partials);
+                                                            rm, words, wb, static_cast<TM*>(mo), partials);
   return hipGetLastError();
 }
 
@@ -492,14 +481,14 @@ extern "C" int spai_gram_compact(int32_t n, int32_t W, const double* gram, float
 // Fill + per-block partial sums only (res2 partials stay in the workspace for spai_fill_reduce).
 extern "C" int spai_fill_lines_gram(int32_t fill_mode, int32_t n, int32_t line_begin, int32_t line_end, int32_t W,
                                     const int32_t* pat_act, const float* pat_val, const void* gram,
-                                    int32_t gram_dtype, int32_t B,
-                                    const uint32_t* removed, int32_t words, void* m_out, int32_t m_dtype,
-                                    void* workspace, size_t workspace_bytes, void* stream) {
+                                    int32_t gram_dtype, int32_t B, const uint32_t* removed, int32_t words,
+                                    int32_t word_base, void* m_out, int32_t m_dtype, void* workspace,
+                                    size_t workspace_bytes, void* stream) {
   SPAI_CHECK_ARG(fill_mode == SPAI_FILL_COPY || fill_mode == SPAI_FILL_LSQ,
                  "spai_fill_lines_gram: bad fill_mode %d", fill_mode);
   SPAI_CHECK_ARG(m_dtype == SPAI_DTYPE_F32 || m_dtype == SPAI_DTYPE_F64, "spai_fill_lines_gram: bad m_dtype");
   SPAI_CHECK_ARG(n >= 1 && line_begin >= 0 && line_end >= line_begin && line_end <= n && W >= 1 && B >= 1 &&
-                     words >= 0,
+                     words >= 1 && word_base >= 0,
                  "spai_fill_lines_gram: bad shape");
   SPAI_CHECK_ARG(workspace != nullptr, "spai_fill_lines_gram: null workspace");
   SPAI_CHECK_ARG(fill_mode != SPAI_FILL_COPY || m_dtype == SPAI_DTYPE_F32,
@@ -520,55 +509,67 @@ extern "C" int spai_fill_lines_gram(int32_t fill_mode, int32_t n, int32_t line_b
   const int32_t nparts = (nl + kNT - 1) / kNT;
   SPAI_CHECK_ARG(workspace_bytes >= sizeof(double) * (size_t)nparts * B, "spai_fill_lines_gram: workspace too small");
   double* partials = static_cast<double*>(workspace);
+  const uint32_t* rm = removed;
+  const int32_t wb = word_base;
   hipError_t e;
   const bool lsq = fill_mode == SPAI_FILL_LSQ, f64 = m_dtype == SPAI_DTYPE_F64;
+#define SPAI_FILL_ARGS n, line_begin, line_end, W, pat_act, pat_val, gram, g32, B, rm, words, wb, m_out, partials, nparts, s
   if (wc == 5) {
-    e = !lsq ? launch_fill<5, float, false>(n, line_begin, line_end, W, pat_act, pat_val, gram, g32, B, removed, words,
-                                            m_out, partials, nparts, s)
-        : f64 ? launch_fill<5, double, true>(n, line_begin, line_end, W, pat_act, pat_val, gram, g32, B, removed, words,
-                                             m_out, partials, nparts, s)
-              : launch_fill<5, float, true>(n, line_begin, line_end, W, pat_act, pat_val, gram, g32, B, removed, words,
-                                            m_out, partials, nparts, s);
+    e = !lsq ? launch_fill<5, float, false>(SPAI_FILL_ARGS)
+        : f64 ? launch_fill<5, double, true>(SPAI_FILL_ARGS)
+              : launch_fill<5, float, true>(SPAI_FILL_ARGS);
   } else if (wc == 7) {
-    e = !lsq ? launch_fill<7, float, false>(n, line_begin, line_end, W, pat_act, pat_val, gram, g32, B, removed, words,
-                                            m_out, partials, nparts, s)
-        : f64 ? launch_fill<7, double, true>(n, line_begin, line_end, W, pat_act, pat_val, gram, g32, B, removed, words,
-                                             m_out, partials, nparts, s)
-              : launch_fill<7, float, true>(n, line_begin, line_end, W, pat_act, pat_val, gram, g32, B, removed, words,
-                                            m_out, partials, nparts, s);
+    e = !lsq ? launch_fill<7, float, false>(SPAI_FILL_ARGS)
+        : f64 ? launch_fill<7, double, true>(SPAI_FILL_ARGS)
+              : launch_fill<7, float, true>(SPAI_FILL_ARGS);
   } else {
-    e = !lsq ? launch_fill<13, float, false>(n, line_begin, line_end, W, pat_act, pat_val, gram, g32, B, removed, words,
-                                             m_out, partials, nparts, s)
-        : f64 ? launch_fill<13, double, true>(n, line_begin, line_end, W, pat_act, pat_val, gram, g32, B, removed, words,
-                                              m_out, partials, nparts, s)
-              : launch_fill<13, float, true>(n, line_begin, line_end, W, pat_act, pat_val, gram, g32, B, removed, words,
-                                             m_out, partials, nparts, s);
+    e = !lsq ? launch_fill<13, float, false>(SPAI_FILL_ARGS)
+        : f64 ? launch_fill<13, double, true>(SPAI_FILL_ARGS)
+              : launch_fill<13, float, true>(SPAI_FILL_ARGS);
   }
+#undef SPAI_FILL_ARGS
   SPAI_CHECK_HIP(e);
   return SPAI_OK;
 }
 
-extern "C" int spai_fill_reduce(int32_t n_lines, int32_t B, const void* workspace, double* res2_out, void* stream) {
-  SPAI_CHECK_ARG(n_lines >= 0 && B >= 1 && workspace && res2_out, "spai_fill_reduce: bad arguments");
+extern "C" int spai_fill_reduce(int32_t n_lines, int32_t B, const void* workspace, double* res2_out,
+                                int64_t* limbs_out, void* stream) {
+  SPAI_CHECK_ARG(n_lines >= 0 && B >= 1 && workspace && (res2_out || limbs_out), "spai_fill_reduce: bad arguments");
   hipStream_t s = (hipStream_t)stream;
   if (n_lines == 0) {
-    SPAI_CHECK_HIP(hipMemsetAsync(res2_out, 0, sizeof(double) * B, s));
+    if (res2_out) SPAI_CHECK_HIP(hipMemsetAsync(res2_out, 0, sizeof(double) * B, s));
+    if (limbs_out) SPAI_CHECK_HIP(hipMemsetAsync(limbs_out, 0, sizeof(int64_t) * kLimbSlots * B, s));
     return SPAI_OK;
   }
-  k_gram_reduce<<<B, kNT, 0, s>>>(static_cast<const double*>(workspace), (n_lines + kNT - 1) / kNT, res2_out);
+  k_fixed_reduce<kNT><<<B, kNT, 0, s>>>(static_cast<const double*>(workspace), (n_lines + kNT - 1) / kNT, res2_out,
+                                        limbs_out);
   SPAI_CHECK_LAUNCH();
   return SPAI_OK;
 }
 
 extern "C" int spai_fill_residual_gram(int32_t fill_mode, int32_t n, int32_t line_begin, int32_t line_end, int32_t W,
                                        const int32_t* pat_act, const float* pat_val, const void* gram,
-                                       int32_t gram_dtype, int32_t B,
-                                       const uint32_t* removed, int32_t words, void* m_out, int32_t m_dtype,
-                                       double* res2_out, void* workspace, size_t workspace_bytes, void* stream) {
+                                       int32_t gram_dtype, int32_t B, const uint32_t* removed, int32_t words,
+                                       int32_t word_base, void* m_out, int32_t m_dtype, double* res2_out,
+                                       void* workspace, size_t workspace_bytes, void* stream) {
   SPAI_CHECK_ARG(res2_out != nullptr, "spai_fill_residual_gram: null res2_out");
   const int st = spai_fill_lines_gram(fill_mode, n, line_begin, line_end, W, pat_act, pat_val, gram, gram_dtype, B,
-                                      removed,
-                                      words, m_out, m_dtype, workspace, workspace_bytes, stream);
+                                      removed, words, word_base, m_out, m_dtype, workspace, workspace_bytes, stream);
   if (st != SPAI_OK) return st;
-  return spai_fill_reduce(line_end - line_begin, B, workspace, res2_out, stream);
+  return spai_fill_reduce(line_end - line_begin, B, workspace, res2_out, nullptr, stream);
+}
+
+namespace spai {
+namespace {
+__global__ void k_limbs_to_res2(int32_t B, const int64_t* __restrict__ limbs, double* __restrict__ res2) {
+  for (int b = threadIdx.x; b < B; b += blockDim.x) res2[b] = fixed_value(limbs + (int64_t)b * kLimbSlots);
+}
+}  // namespace
+}  // namespace spai
+
+extern "C" int spai_res2_from_limbs(int32_t B, const int64_t* limbs, double* res2_out, void* stream) {
+  SPAI_CHECK_ARG(B >= 1 && limbs && res2_out, "spai_res2_from_limbs: bad arguments");
+  k_limbs_to_res2<<<1, 256, 0, (hipStream_t)stream>>>(B, limbs, res2_out);
+  SPAI_CHECK_LAUNCH();
+  return SPAI_OK;
 }

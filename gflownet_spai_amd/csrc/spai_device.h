@@ -202,4 +202,72 @@ __device__ __forceinline__ T block_sum(T v, T* lds /* NT/64 */) {
   return s;
 }
 
+// ---- exact, partition-invariant sums of fp64 partials (SPAI_RES2_LIMBS in spai_hip.h)
+// A partial x is truncated (toward zero) to a multiple of 2^-96 and held as six signed 32-bit
+// limbs in int64 slots, value = sum_i L_i 2^(32 i - 96), |x| < 2^94; slot 6 counts the partials
+// that are not representable (NaN: bit 32 up, inf / |x| >= 2^94: bit 0 up).  Integer sums are
+// associative, so summing the slots in any order, over any partition of the partials (the line
+// shards of a multi-GPU job: one all_reduce of the slots), gives the same bits.
+constexpr int kLimbSlots = 8;  // 6 limbs + flags + 1 pad (64 bytes per sample)
+__device__ __forceinline__ void fixed_add(double x, int64_t (&L)[kLimbSlots]) {
+  const uint64_t u = (uint64_t)__double_as_longlong(x);
+  const int ex = (int)((u >> 52) & 0x7ff);
+  if (ex == 0x7ff) {
+    L[6] += (u & ((1ull << 52) - 1)) ? (1ll << 32) : 1ll;
+    return;
+  }
+  if (ex >= 1023 + 94) {
+    L[6] += 1;
+    return;
+  }
+  const uint64_t m = (u & ((1ull << 52) - 1)) | (ex ? (1ull << 52) : 0ull);
+  const int shift = (ex ? ex : 1) - 1075 + 96;  // x = m * 2^(shift - 96)
+  const bool neg = (u >> 63) != 0;
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    const int k = 32 * i - shift;  // limb i holds bits [k, k + 32) of m
+    uint64_t c;
+    if (k >= 0) c = k < 64 ? (m >> k) & 0xffffffffull : 0ull;
+    else c = -k < 32 ? (m << -k) & 0xffffffffull : 0ull;
+    L[i] += neg ? -(int64_t)c : (int64_t)c;
+  }
+}
+__device__ __forceinline__ double fixed_value(const int64_t* L) {
+  const int64_t fl = L[6];
+  if (fl >> 32) return __longlong_as_double(0x7ff8000000000000ll);  // NaN
+  if (fl) return __longlong_as_double(0x7ff0000000000000ll);        // +inf
+  int64_t c[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) c[i] = L[i];
+#pragma unroll
+  for (int i = 0; i < 5; ++i) {  // carry-normalise: c[0..4] in [0, 2^32), c[5] signed
+    const int64_t carry = c[i] >> 32;
+    c[i] -= carry * 4294967296ll;
+    c[i + 1] += carry;
+  }
+  double v = (double)c[5];
+#pragma unroll
+  for (int i = 4; i >= 0; --i) v = fma(v, 4294967296.0, (double)c[i]);
+  return v * 0x1p-96;
+}
+// res2_out[b] and/or limbs_out[b][kLimbSlots] from per-block fp64 partials [B][nparts], one block
+// per sample (the fill kernels' second half).
+template <int NT>
+__global__ __launch_bounds__(NT) void k_fixed_reduce(const double* __restrict__ partials, int32_t nparts,
+                                                     double* __restrict__ res2_out, int64_t* __restrict__ limbs_out) {
+  __shared__ int64_t sred[NT / 64];
+  const int b = blockIdx.x;
+  int64_t L[kLimbSlots] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int i = threadIdx.x; i < nparts; i += NT) fixed_add(partials[(int64_t)b * nparts + i], L);
+#pragma unroll
+  for (int q = 0; q < 7; ++q) L[q] = block_sum<NT>(L[q], sred);
+  if (threadIdx.x == 0) {
+    if (limbs_out) {
+#pragma unroll
+      for (int q = 0; q < kLimbSlots; ++q) limbs_out[(int64_t)b * kLimbSlots + q] = L[q];
+    }
+    if (res2_out) res2_out[b] = fixed_value(L);
+  }
+}
+
 }  // namespace spai

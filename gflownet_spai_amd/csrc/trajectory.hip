@@ -85,8 +85,8 @@ struct TrajWs {
   int32_t* tdev;
   int32_t* lastbig;       // bigcnt of the last sort (kept for tests / diagnostics)
   int32_t* biglist;       // [B][kMaxB] their flattened (sample, bucket) indices
-  double* xch;            // exchange array: [B][2][kMaxB] bucket weight sums | winner counts, then [B]
-                          // residual partials (the caller's slot); a part fills its own buckets
+  double* xch;            // exchange array: [B][2][kMaxB] bucket weight sums | winner counts, then
+                          // [B][8] caller slots (the residual limbs); a part fills its own buckets
   int32_t* samp_cnt;      // [B][M / kSampNT] winners per presample block
   uint32_t* samp;         // [B][M] winner keys (orderable), block-compacted
   int32_t* nb;            // [B] buckets
@@ -107,7 +107,7 @@ struct TrajWs {
   size_t total_bytes;
 };
 
-static size_t xch_doubles(int32_t B) { return (size_t)B * 2 * kMaxB + B; }
+static size_t xch_doubles(int32_t B) { return (size_t)B * 2 * kMaxB + (size_t)B * 8; }
 
 static void traj_ws(void* base, int32_t E, int32_t B, TrajWs* w) {
   Carve c(base);
@@ -1570,7 +1570,8 @@ extern "C" size_t spai_rollout_workspace_bytes(int32_t E, int32_t B) {
 //   0 = int32 oversized buckets of the last sort (k_sort2 -> k_sort2_big)
 //   1 = int32 T of the last rollout
 //   2 = fp64 exchange array: [B][2][kMaxB] bucket weight sums | bucket winner counts (a part
-//       fills its own buckets, the rest are 0), then [B] slots for the caller's residual partials
+//       fills its own buckets, the rest are 0 — so the int64 bit patterns of the parts' arrays
+//       sum exactly too), then [B][8] slots for the caller's exact residual limbs
 //   3 = kMaxB (the row length of field 2), as a value, not an offset
 //   4 = int32 [B][kMaxB + 1] trajectory position of each bucket's first winner (bucket nb: count)
 //   5 = int32 [B] buckets of each sample

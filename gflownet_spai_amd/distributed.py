@@ -1,63 +1,165 @@
 """Multi-GPU layout of the hot path: one process per GPU, torch.distributed (RCCL over xGMI on
-MI355X, gloo in the CPU tests).
+MI355X, gloo in the CPU tests).  The reference has no parallelism at all.
 
-Two ways to spread work:
-  * columns (default of bench.py, the north star's split, strong scaling): every rank draws
-    the same B candidates; rank r orders the r-th slice of every trajectory (rollout parts:
-    a contiguous range of the presampled key buckets) and fills lines shard_lines(n, r, P) of
-    every candidate's M.  ONE all_reduce per step carries the parts' bucket weight sums and
-    winner counts and the squared residual partials (``exchange_parts``); the chosen M is
-    assembled with ONE
-    all_gather of equal-size ELL blocks (``allgather_lines``).
-  * samples (strong scaling over a fixed global batch of B candidates, bench.py's default):
-    rank r rolls out and fills candidates r*B/P .. (r+1)*B/P - 1 (the same Philox sample ids,
-    hence the same draws, as a one-GPU batch); the step's exchange is one all_gather of the
-    rewards and one reduce of the best candidate's M (``select_best_samples``).
-  * candidates (weak scaling): rank r samples candidates with Philox sample ids
-    r*B .. r*B+B-1 (``GFlowNet(sample_base=r*B)``); every candidate's trajectory, fill and
-    reward live on one rank, so the step needs no collective.
-The reference has no parallelism at all.
+Three ways to spread the work; ``GFlowNet(shard=(rank, world, group), split=...)``:
+  * columns (bench.py's default for --gpus > 1; the north star's "columns of M shard across the
+    GPUs, one all-gather assembles M"): rank r rolls out ITS candidates (global sample ids
+    r*Bl .. r*Bl + Bl - 1: the same Philox draws as a one-GPU batch of P*Bl), then
+      1. one all_to_all of the removal bitmaps: rank q receives, for every candidate, only the
+         bitmap words its lines' action ids span, plus the candidate's removal count
+         (``bitmap_pack_index`` / ``exchange_bitmaps``);
+      2. every rank fills lines ``shard_lines(n, r, P, align=256)`` of ALL P*Bl candidates;
+      3. one all_reduce of the exact (integer-limb) squared-residual sums [P*Bl] — bit-identical
+         to one GPU whatever P, because the shards are 256-line aligned and integer sums are
+         associative (spai_hip.h SPAI_RES2_LIMBS);
+      4. one all_gather of the best candidate's M lines (``allgather_lines``).
+  * slices (strong scaling over the trajectory): every rank draws all E actions of the same B
+    candidates and orders one contiguous slice of every trajectory; one all_reduce of the bucket
+    sums + residual partials (``exchange_parts``).  The full log needs the explicit collective
+    ``Log.gather_parts()`` on every rank.
+  * samples (bench.py --shard samples): rank r rolls out and fills candidates r*B/P ..; one
+    all_gather of the rewards and one reduce of the best candidate's M (``select_best_samples``).
+  * candidates (weak scaling, ``GFlowNet(sample_base=r*B)``): no collective.
 """
 from __future__ import annotations
 
 import torch
 import torch.distributed as dist
 
+LINE_ALIGN = 256  # lines per fill block (gram.hip / fill.hip kNT): the exact-sum invariance unit
 
-def shard_lines(n: int, rank: int, world: int) -> tuple[int, int]:
-    """Contiguous, balanced [begin, end) line range of ``rank`` (sizes differ by <= 1)."""
+
+def shard_lines(n: int, rank: int, world: int, align: int = 1) -> tuple[int, int]:
+    """Contiguous, balanced [begin, end) line range of ``rank``.  With ``align`` > 1 the ranges
+    are made of whole ``align``-line blocks (sizes differ by <= one block; the last is cut at n)."""
     if not 0 <= rank < world:
         raise ValueError("rank out of range")
-    q, r = divmod(n, world)
-    begin = rank * q + min(rank, r)
-    return begin, begin + q + (1 if rank < r else 0)
+    if align < 1:
+        raise ValueError("align must be >= 1")
+    nb = -(-n // align)
+    q, r = divmod(nb, world)
+    b0 = rank * q + min(rank, r)
+    b1 = b0 + q + (1 if rank < r else 0)
+    return min(n, b0 * align), min(n, b1 * align)
+
+
+def _host_staged(t: torch.Tensor, group) -> bool:
+    """gloo has no device kernels for the ops used here: stage device tensors through the host."""
+    return t.is_cuda and dist.get_backend(group) == "gloo"
+
+
+def all_reduce_(t: torch.Tensor, group=None) -> torch.Tensor:
+    """In-place SUM all_reduce (host-staged on gloo)."""
+    if _host_staged(t, group):
+        h = t.cpu()
+        dist.all_reduce(h, op=dist.ReduceOp.SUM, group=group)
+        t.copy_(h)
+    else:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+    return t
+
+
+def all_gather_into_(out: torch.Tensor, inp: torch.Tensor, group=None) -> torch.Tensor:
+    if _host_staged(inp, group):
+        h = torch.empty(out.shape, dtype=out.dtype)
+        dist.all_gather_into_tensor(h, inp.cpu(), group=group)
+        out.copy_(h)
+    else:
+        dist.all_gather_into_tensor(out, inp, group=group)
+    return out
+
+
+class _Done:
+    def wait(self):
+        return None
+
+
+def all_to_all_(out: torch.Tensor, inp: torch.Tensor, out_splits: list, in_splits: list, group=None,
+                async_op: bool = False):
+    """all_to_all_single with uneven splits; returns a work handle (``wait()`` orders the current
+    stream after it on RCCL; host-staged and synchronous on gloo)."""
+    if _host_staged(inp, group):
+        h = torch.empty(out.shape, dtype=out.dtype)
+        dist.all_to_all_single(h, inp.cpu(), out_splits, in_splits, group=group)
+        out.copy_(h)
+        return _Done()
+    w = dist.all_to_all_single(out, inp, out_splits, in_splits, group=group, async_op=async_op)
+    return w if async_op else _Done()
 
 
 def allreduce_res2(res2: torch.Tensor, group=None) -> torch.Tensor:
     """Sum per-sample squared residual partials over the column shards (in place)."""
-    dist.all_reduce(res2, op=dist.ReduceOp.SUM, group=group)
-    return res2
+    return all_reduce_(res2, group)
 
 
-def allgather_lines(m_local: torch.Tensor, n: int, group=None) -> torch.Tensor:
-    """Assemble [B, n, W] line values from every rank's [B, n_r, W] block (one all_gather).
+def allgather_lines(m_local: torch.Tensor, n: int, group=None, align: int = 1) -> torch.Tensor:
+    """Assemble [B, n, W] line values from every rank's [B, n_r, W] block (one all_gather);
+    rank r's block is lines ``shard_lines(n, r, P, align)``.
 
-    Blocks are padded to ceil(n / P) lines so every rank contributes an equal-size chunk
+    Blocks are padded to the largest shard so every rank contributes an equal-size chunk
     (the ring all-gather over xGMI is per-link bound: equal chunks keep every link busy)."""
     world = dist.get_world_size(group)
     B, n_loc, W = m_local.shape
-    chunk = -(-n // world)
-    buf = torch.zeros(B, chunk, W, dtype=m_local.dtype, device=m_local.device)
-    buf[:, :n_loc] = m_local
+    rng = [shard_lines(n, r, world, align) for r in range(world)]
+    chunk = max(e - b for b, e in rng)
+    if n_loc == chunk:
+        buf = m_local.contiguous()
+    else:
+        buf = torch.zeros(B, chunk, W, dtype=m_local.dtype, device=m_local.device)
+        buf[:, :n_loc] = m_local
     out = torch.empty(world, B, chunk, W, dtype=m_local.dtype, device=m_local.device)
-    dist.all_gather_into_tensor(out.view(-1), buf.view(-1).contiguous(), group=group)
+    all_gather_into_(out.view(-1), buf.view(-1), group)
+    if all(e - b == chunk for b, e in rng):
+        return out.permute(1, 0, 2, 3).reshape(B, world * chunk, W)
+    return torch.cat([out[r, :, : e - b] for r, (b, e) in enumerate(rng)], dim=1)
+
+
+# ---------------------------------------------------------------- columns split: bitmap exchange
+def word_spans(env, world: int) -> list:
+    """[(w0, w1)] per rank: the bitmap words the action ids of rank q's lines span (one host
+    sync, once per model).  For stencil matrices in row-major raw order a column shard's action
+    ids are one contiguous range (its rows +- the stencil's reach), so a rank needs ~1/P of every
+    bitmap; a randomly numbered matrix degrades to whole bitmaps (an all_gather's volume)."""
+    act = env.pattern.act
+    spans = []
+    for q in range(world):
+        b, e = shard_lines(env.matrix_size, q, world, LINE_ALIGN)
+        a = act[b:e].reshape(-1)
+        a = a[a >= 0]
+        if a.numel() == 0:
+            spans.append((0, 1))
+            continue
+        lo, hi = int(a.min()) >> 5, (int(a.max()) >> 5) + 1
+        spans.append((lo, hi))
+    return spans
+
+
+def bitmap_pack_index(spans: list, bl: int, words: int, device) -> torch.Tensor:
+    """int64 gather index over a rank's [bl * words + bl] buffer (bitmaps, then the bl removal
+    counts) producing its all_to_all send buffer: for destination q, rows b = 0..bl-1 of
+    (words w0_q .. w1_q - 1 of bitmap b, then count b)."""
     parts = []
-    for r in range(world):
-        b, e = shard_lines(n, r, world)
-        parts.append(out[r, :, : e - b])
-    return torch.cat(parts, dim=1)
+    for w0, w1 in spans:
+        rows = torch.arange(bl, device=device, dtype=torch.int64).view(-1, 1)
+        cols = torch.arange(w0, w1, device=device, dtype=torch.int64).view(1, -1)
+        blk = torch.cat([rows * words + cols, bl * words + rows], dim=1)  # [bl, span + 1]
+        parts.append(blk.reshape(-1))
+    return torch.cat(parts)
 
 
+def exchange_bitmaps(send: torch.Tensor, recv: torch.Tensor, spans: list, bl: int, rank: int, group=None,
+                     async_op: bool = False):
+    """The columns split's all_to_all: ``send`` (from ``bitmap_pack_index``) -> ``recv`` int32
+    [P * bl, span_r + 1] = every candidate's window of this rank's words + its removal count, in
+    global sample order (rank q's candidates are rows q*bl ..)."""
+    world = len(spans)
+    span_r = spans[rank][1] - spans[rank][0]
+    in_splits = [bl * (w1 - w0 + 1) for w0, w1 in spans]
+    out_splits = [bl * (span_r + 1)] * world
+    return all_to_all_(recv.view(-1), send, out_splits, in_splits, group, async_op)
+
+
+# ---------------------------------------------------------------- samples split
 def select_best_samples(rewards_local: torch.Tensor, m_local: torch.Tensor, group=None, dst: int = 0):
     """The samples split's one exchange (no host round trip): every rank holds B/P candidates
     (global sample ids rank*B/P ...); ``rewards_local`` [B/P], ``m_local`` [B/P, n, W].  One
@@ -69,13 +171,18 @@ def select_best_samples(rewards_local: torch.Tensor, m_local: torch.Tensor, grou
     rank = dist.get_rank(group)
     bl = rewards_local.numel()
     allr = torch.empty(world * bl, dtype=rewards_local.dtype, device=rewards_local.device)
-    dist.all_gather_into_tensor(allr, rewards_local.contiguous(), group=group)
+    all_gather_into_(allr, rewards_local.contiguous(), group)
     best = torch.argmax(allr).view(1)
     mine = (best >= rank * bl) & (best < (rank + 1) * bl)
     pick = m_local.index_select(0, (best - rank * bl).clamp(0, bl - 1)).squeeze(0)
     out = torch.where(mine, pick, torch.zeros((), dtype=pick.dtype, device=pick.device)).contiguous()
-    dist.reduce(out, dst=dist.get_global_rank(group, dst) if group is not None else dst, op=dist.ReduceOp.SUM,
-                group=group)
+    dst_g = dist.get_global_rank(group, dst) if group is not None else dst
+    if _host_staged(out, group):
+        h = out.cpu()
+        dist.reduce(h, dst=dst_g, op=dist.ReduceOp.SUM, group=group)
+        out.copy_(h)
+    else:
+        dist.reduce(out, dst=dst_g, op=dist.ReduceOp.SUM, group=group)
     return allr, best, out
 
 
@@ -83,20 +190,22 @@ def gather_rewards(rewards: torch.Tensor, group=None) -> torch.Tensor:
     """[P*B] rewards of every rank's candidates, in rank order (for logging a global batch)."""
     world = dist.get_world_size(group)
     out = torch.empty(world * rewards.numel(), dtype=rewards.dtype, device=rewards.device)
-    dist.all_gather_into_tensor(out, rewards.contiguous(), group=group)
-    return out
+    return all_gather_into_(out, rewards.contiguous(), group)
 
 
-def exchange_parts(xch: torch.Tensor, res2: torch.Tensor, group=None) -> torch.Tensor:
-    """The split rollout's one collective, in place on the rollout workspace's exchange array
+# ---------------------------------------------------------------- slices split
+def exchange_parts(xch: torch.Tensor, limbs: torch.Tensor, group=None) -> torch.Tensor:
+    """The slices split's one collective, in place on the rollout workspace's exchange array
     (kernels.exchange_array: per-bucket weight sums and winner counts, each part non-zero on
-    its own buckets only, so the sum is exact and equals the one-GPU array; then B slots):
-    the lines' squared residual partials [B] go into the slots, one all_reduce sums
-    everything, and the summed residuals (a view of the slots) are returned."""
-    B = res2.numel()
-    slots = xch[xch.numel() - B:]
-    slots.copy_(res2.reshape(-1))
-    dist.all_reduce(xch, op=dist.ReduceOp.SUM, group=group)
+    its own buckets only, then B * RES2_LIMBS caller slots): the lines' exact residual limbs
+    [B, RES2_LIMBS] go into the slots and ONE all_reduce of the array's int64 bit patterns sums
+    everything (a bucket entry has one non-zero term: its bits come through unchanged; the limbs
+    add as integers).  Returns the summed limbs (a view of the slots)."""
+    nl = limbs.numel()
+    x64 = xch.view(torch.int64)
+    slots = x64[x64.numel() - nl:].view_as(limbs)
+    slots.copy_(limbs)
+    all_reduce_(x64, group)
     return slots
 
 
@@ -107,6 +216,6 @@ def gather_slices(actions: torch.Tensor, fwd: torch.Tensor, bounds: torch.Tensor
     mine = (pos >= bounds[:, :1]) & (pos < bounds[:, 1:])
     a = torch.where(mine, actions[:, :T], torch.zeros((), dtype=actions.dtype, device=actions.device)).contiguous()
     f = torch.where(mine, fwd[:, :T], torch.zeros((), dtype=fwd.dtype, device=fwd.device)).contiguous()
-    dist.all_reduce(a, group=group)
-    dist.all_reduce(f, group=group)
+    all_reduce_(a, group)
+    all_reduce_(f, group)
     return a, f

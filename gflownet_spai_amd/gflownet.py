@@ -27,10 +27,12 @@ from .preconditioner import Data
 
 class GFlowNet(nn.Module):
     def __init__(self, forward_policy, backward_policy, env, *, mode: str = "parity", seed: int | None = None,
-                 sample_base: int = 0, shard: tuple | None = None):
+                 sample_base: int = 0, shard: tuple | None = None, split: str = "columns"):
         super().__init__()
         if mode not in ("parity", "throughput"):
             raise ValueError("mode must be 'parity' or 'throughput'")
+        if split not in ("columns", "slices"):
+            raise ValueError("split must be 'columns' or 'slices'")
         self.register_buffer("total_flow", torch.ones(1))
         self.forward_policy = forward_policy
         self.backward_policy = backward_policy
@@ -39,18 +41,38 @@ class GFlowNet(nn.Module):
         self._alpha_mean = None  # (key, mean over the batch of a constant sigmoid(alpha), pin)
         self.seed = int(torch.initial_seed() if seed is None else seed) & (2**64 - 1)
         self.sample_base = sample_base
-        self.rollouts = 0  # Philox stream id of the next throughput rollout (host mirror)
-        self._ctr = None   # the same counter on the device (advanced by the select phase itself)
+        self._rollouts0 = 0  # Philox stream id of the first throughput rollout
+        self._ctr = None     # the stream id on the device (advanced by the select phase itself)
         self._data_cache = {}
-        # (rank, world, group): the columns split of DESIGN.md §6 (throughput mode).  Every rank
-        # draws the same B candidates; rank r orders the r-th slice of every trajectory
-        # (rollout parts) and fills lines shard_lines(n, r, world) of every candidate's M; one
-        # all_reduce carries the parts' bucket weight sums and the squared residual partials.
-        self.shard = shard
-        if shard is not None:
-            from .distributed import shard_lines
-            rank, world, _ = shard
-            self.lines = shard_lines(env.matrix_size, rank, world) if env is not None else None
+        self._bufs = {}      # persistent exchange buffers of the columns split (graph-replay safe)
+        # (rank, world, group): the multi-GPU split of DESIGN.md §6 (throughput mode)
+        #   split="columns": rank r rolls out its own len(s0) candidates (global sample ids
+        #     sample_base + r*len(s0) ..), one all_to_all ships each rank the bitmap words of its
+        #     256-line-aligned column shard for EVERY candidate, every rank fills its lines of all
+        #     P*len(s0) candidates, one all_reduce sums the exact residual limbs (distributed.py).
+        #   split="slices": every rank draws the same B candidates and orders one slice of every
+        #     trajectory; one all_reduce of the bucket sums + residual partials.
+        self.shard = shard if shard is not None and shard[1] > 1 else None
+        self.split = split if self.shard is not None else None
+        if self.shard is not None:
+            if mode != "throughput":
+                raise ValueError("a sharded GFlowNet needs mode='throughput'")
+            from .distributed import LINE_ALIGN, shard_lines
+            rank, world, _ = self.shard
+            align = LINE_ALIGN if split == "columns" else 1
+            self.lines = shard_lines(env.matrix_size, rank, world, align) if env is not None else None
+
+    @property
+    def rollouts(self) -> int:
+        """Philox stream id of the next throughput rollout.  The device counter is the only source
+        of truth once a rollout ran (graph replays advance it without the host): reading it syncs."""
+        return self._rollouts0 if self._ctr is None else int(self._ctr.item())
+
+    @rollouts.setter
+    def rollouts(self, value: int) -> None:
+        self._rollouts0 = int(value)
+        if self._ctr is not None:
+            self._ctr.fill_(int(value))  # replays from here draw stream ids value, value + 1, ...
 
     # ------------------------------------------------------------------ policy
     def policy_logits(self, data, batch_size: int):
@@ -152,10 +174,10 @@ class GFlowNet(nn.Module):
     def sample_states(self, s0, return_log: bool = False):
         """gflownet.py:125-197: sample B trajectories from the initial states, score them, log."""
         if self.mode == "throughput":
-            st = self.rollout_begin(s0)
-            self.rollout_exchange(st)
-            log = self.rollout_end(st)
-            return log if return_log else None
+            st = {"s0": s0}
+            for phase, _ in self.rollout_phases():
+                phase(st)
+            return st["log"] if return_log else None
         env = self.env
         B = len(s0)
         E = env.num_actions - 1
@@ -195,41 +217,69 @@ class GFlowNet(nn.Module):
         lg, lmax, z = kernels.logits_stats(logits.detach().to(env.device), B)
         return logits, alpha, lg, lmax, z
 
-    # The throughput step in three phases, so a caller can capture the collective-free ones in
-    # HIP graphs (bench.py): begin = policy, select, fill of this rank's lines; exchange = the
-    # split's one all_reduce (nothing on one GPU); end = merge (split only), sort of this rank's
-    # trajectory slice with its fwd_probs, terminal step / padding, rewards, the Log.  No
-    # phase synchronises with the host; the Philox stream id lives on the device and the select
-    # phase advances it, so a replayed graph draws a fresh rollout.
+    # ------------------------------------------------------------------ throughput step
+    # The throughput step as a list of phases (``rollout_phases``), so a caller can capture the
+    # collective-free ones in HIP graphs (bench.py).  No phase synchronises with the host; the
+    # Philox stream id lives on the device and the select phase advances it, so a replayed graph
+    # draws a fresh rollout.  Every phase takes the step's state dict (``{"s0": s0}`` to start;
+    # the last phase leaves the Log in ``st["log"]``).
+    def rollout_phases(self) -> list:
+        """[(phase, is_collective)] in execution order."""
+        if self.split == "columns":
+            return [(self._c_begin, False), (self._c_send, True), (self._c_order, False), (self._c_recv, True),
+                    (self._c_fill, False), (self._c_reduce, True), (self._c_end, False)]
+        if self.split == "slices":
+            return [(self._begin, False), (self.rollout_exchange, True), (self._end, False)]
+        return [(self._begin, False), (self.rollout_exchange, False), (self._end, False)]
+
+    def _counter(self, dev):
+        if self._ctr is None or self._ctr.device != dev:
+            self._ctr = torch.tensor([self._rollouts0], dtype=torch.int64, device=dev)
+        return self._ctr
+
+    def _buf(self, key, shape, dtype, dev):
+        t = self._bufs.get(key)
+        if t is None or t.shape != torch.Size(shape) or t.dtype != dtype or t.device != dev:
+            t = self._bufs[key] = torch.empty(shape, dtype=dtype, device=dev)
+        return t
+
+    # one GPU, or the slices split
     def rollout_begin(self, s0) -> dict:
-        env = self.env
+        st = {"s0": s0}
+        self._begin(st)
+        return st
+
+    def _begin(self, st: dict) -> None:
+        env, s0 = self.env, st["s0"]
         B = len(s0)
         E = env.num_actions - 1
         logits, alpha, lg, lmax, _ = self._logits(s0)
-        if self._ctr is None or self._ctr.device != lg.device:
-            self._ctr = torch.tensor([self.rollouts], dtype=torch.int64, device=lg.device)
-        self.rollouts += 1
         rank, world, group = self.shard if self.shard is not None else (0, 1, None)
-        removed, counts, ws = kernels.rollout_select(lg, B, lmax, self.seed, 0, self.sample_base, self._ctr, rank,
-                                                     world)
+        removed, counts, ws = kernels.rollout_select(lg, B, lmax, self.seed, 0, self.sample_base, self._counter(lg.device),
+                                                     rank, world)
         lines = self.lines if self.shard is not None else (0, None)
-        res2 = env.fill_partial(removed, *lines)
-        return dict(s0=s0, B=B, E=E, logits=logits, alpha=alpha, lg=lg, lmax=lmax, removed=removed, counts=counts,
-                    ws=ws, res2_part=res2, part=(rank, world, group))
+        res2 = env.fill_partial(removed, *lines, limbs=world > 1)  # a split sums exact limbs
+        st.update(B=B, E=E, logits=logits, alpha=alpha, lg=lg, lmax=lmax, removed=removed, counts=counts, ws=ws,
+                  res2_part=res2, part=(rank, world, group))
 
     def rollout_exchange(self, st: dict) -> None:
-        """ONE all_reduce over the split, in place on the rollout workspace's exchange array:
+        """The slices split's ONE all_reduce, in place on the rollout workspace's exchange array:
         the parts' bucket weight sums and winner counts (disjoint supports: the sum is exact and
-        equals the one-GPU array) and the lines' squared residual partials.  The summed
-        residuals are a view of that array (a captured ``rollout_end`` graph keeps reading it)."""
+        equals the one-GPU array) and the lines' exact residual limbs (the same bits as one GPU).
+        Nothing on one GPU."""
         rank, world, group = st["part"]
         if world == 1:
             st["res2"] = st["res2_part"]
             return
         from .distributed import exchange_parts
-        st["res2"] = exchange_parts(kernels.exchange_array(st["ws"], st["E"], st["B"]), st["res2_part"], group)
+        limbs = exchange_parts(kernels.exchange_array(st["ws"], st["E"], st["B"]), st["res2_part"], group)
+        st["res2"] = kernels.res2_from_limbs(limbs)
 
     def rollout_end(self, st: dict) -> Log:
+        self._end(st)
+        return st["log"]
+
+    def _end(self, st: dict) -> None:
         env = self.env
         rank, world, group = st["part"]
         B, E, lg, lmax, counts, ws = st["B"], st["E"], st["lg"], st["lmax"], st["counts"], st["ws"]
@@ -244,7 +294,72 @@ class GFlowNet(nn.Module):
             log._set_part(rank, world, group, kernels.part_bounds(ws, E, B, rank, world))
         log.removed, log.counts = st["removed"], counts
         log.rewards = rewards.detach().to(torch.float32)
-        return log
+        log.rewards_all = rewards
+        st["log"] = log
+
+    # the columns split: rollouts by candidates, fill + residual by column shards
+    def _c_begin(self, st: dict) -> None:
+        env, s0 = self.env, st["s0"]
+        rank, world, group = self.shard
+        bl = len(s0)
+        E = env.num_actions - 1
+        words = (E + 31) // 32
+        logits, alpha, lg, lmax, _ = self._logits(s0)
+        dev = lg.device
+        sel = self._buf("select", (bl * words + bl,), torch.int32, dev)
+        removed, counts, ws = kernels.rollout_select(lg, bl, lmax, self.seed, 0, self.sample_base + rank * bl,
+                                                     self._counter(dev), out=sel)
+        spans = env.word_spans(world)
+        key = ("pack", bl, words)
+        idx = self._bufs.get(key)
+        if idx is None:
+            from .distributed import bitmap_pack_index
+            idx = self._bufs[key] = bitmap_pack_index(spans, bl, words, dev)
+        send = self._buf("send", (idx.numel(),), torch.int32, dev)
+        torch.index_select(sel, 0, idx, out=send)
+        w0, w1 = spans[rank]
+        recv = self._buf("recv", (world * bl, w1 - w0 + 1), torch.int32, dev)
+        st.update(B=bl, E=E, logits=logits, alpha=alpha, lg=lg, lmax=lmax, removed=removed, counts=counts, ws=ws,
+                  send=send, recv=recv, spans=spans, part=(rank, world, group))
+
+    def _c_send(self, st: dict) -> None:
+        from .distributed import exchange_bitmaps
+        rank, _, group = st["part"]
+        st["a2a"] = exchange_bitmaps(st["send"], st["recv"], st["spans"], st["B"], rank, group, async_op=True)
+
+    def _c_order(self, st: dict) -> None:
+        # this rank's own trajectories, while the bitmaps are in flight
+        B, lg, lmax, ws = st["B"], st["lg"], st["lmax"], st["ws"]
+        actions, fwd = kernels.rollout_sort(lg, B, lmax, ws, 0, 1)
+        st["traj"] = (actions, fwd, kernels.rollout_finish(lg, B, lmax, st["counts"], ws, actions, fwd, 0, 1))
+
+    def _c_recv(self, st: dict) -> None:
+        st.pop("a2a").wait()
+
+    def _c_fill(self, st: dict) -> None:
+        rank = st["part"][0]
+        w0, w1 = st["spans"][rank]
+        recv = st["recv"]
+        st["limbs"] = self.env.fill_partial(recv, *self.lines, word_base=w0, limbs=True)
+        st["counts_all"] = recv[:, w1 - w0].contiguous()
+
+    def _c_reduce(self, st: dict) -> None:
+        from .distributed import all_reduce_
+        all_reduce_(st["limbs"], st["part"][2])
+
+    def _c_end(self, st: dict) -> None:
+        env = self.env
+        rank, world, group = st["part"]
+        bl = st["B"]
+        res2 = kernels.res2_from_limbs(st["limbs"])
+        rewards = env.rewards_from_res2(res2, st["counts_all"], st["alpha"])  # all P*bl candidates
+        actions, fwd, t_dev = st["traj"]
+        log = Log(st["s0"], self.backward_policy, self.total_flow, env)
+        log._set_rollout(st["logits"], actions, fwd, t_dev, lmax=st["lmax"])
+        log.removed, log.counts = st["removed"], st["counts"]
+        log.rewards = rewards[rank * bl:(rank + 1) * bl].detach().to(torch.float32)
+        log.rewards_all = rewards  # [P*bl] fp64, global sample order (the M lines of every one are here)
+        st["log"] = log
 
     def _parity_rollout(self, lg: Tensor, B: int, lmax: Tensor, z: Tensor):
         E1 = lg.shape[-1]

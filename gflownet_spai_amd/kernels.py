@@ -74,18 +74,26 @@ def parity_step(lg: torch.Tensor, B: int, noise: torch.Tensor, lmax, chosen, act
 
 
 def rollout_select(lg: torch.Tensor, B: int, lmax: torch.Tensor, seed: int, stream_id: int, sample_base: int = 0,
-                   stream_ctr: torch.Tensor | None = None, part: int = 0, nparts: int = 1, ws_tag: str = "rollout"):
+                   stream_ctr: torch.Tensor | None = None, part: int = 0, nparts: int = 1, ws_tag: str = "rollout",
+                   out: torch.Tensor | None = None):
     """Phase 1 of the throughput rollout: removal bitmaps [B, ceil(E/32)] and counts [B] (for
     nparts > 1 the counts are written by rollout_merge, after the exchange).
 
     stream_ctr: optional device uint64 (int64 tensor) holding the Philox stream id, advanced
     by one on the device (graph replays draw fresh rollouts); part/nparts: this process orders
-    buckets [nb*part/nparts, nb*(part+1)/nparts) of every sample (the multi-GPU split)."""
+    buckets [nb*part/nparts, nb*(part+1)/nparts) of every sample (the slices split); out:
+    optional int32 buffer [B * words + B] that receives the bitmaps, then the counts (the
+    columns split gathers its all_to_all send buffer from it)."""
     _lib.require_device(lg)
     E = lg.shape[-1] - 1
     words = (E + 31) // 32
-    removed = torch.empty(B, words, dtype=torch.int32, device=lg.device)
-    counts = torch.empty(B, dtype=torch.int32, device=lg.device)
+    if out is not None:
+        if out.dtype != torch.int32 or out.numel() != B * words + B or not out.is_contiguous():
+            raise ValueError(f"out must be a contiguous int32 buffer of {B * words + B} elements")
+        removed, counts = out[:B * words].view(B, words), out[B * words:]
+    else:
+        removed = torch.empty(B, words, dtype=torch.int32, device=lg.device)
+        counts = torch.empty(B, dtype=torch.int32, device=lg.device)
     nb = _l().spai_rollout_workspace_bytes(E, B)
     if nb == 0:
         raise RuntimeError("spai_rollout_workspace_bytes failed: " + _l().spai_last_error().decode())
@@ -121,9 +129,9 @@ def rollout_order(lg, B, lmax, counts, ws):
 
 def exchange_array(ws: torch.Tensor, E: int, B: int) -> torch.Tensor:
     """fp64 view of the exchange array inside a rollout workspace: [B][2][kMaxB] bucket weight
-    sums | winner counts (a part fills its own buckets, the rest are 0), then B slots the caller
-    uses for the residual partials.  The parts of a split rollout sum it (one all_reduce)
-    before rollout_merge."""
+    sums | winner counts (a part fills its own buckets, the rest are 0), then B * RES2_LIMBS
+    slots the caller uses for the exact residual limbs.  The parts of a split rollout sum its
+    int64 bit patterns (one all_reduce) before rollout_merge."""
     lib = _l()
     off, n = lib.spai_rollout_ws_offset(E, B, 2), lib.spai_rollout_ws_offset(E, B, 6)
     if off < 0 or n <= 0:
@@ -233,12 +241,22 @@ def actions_to_removed(actions_bt: torch.Tensor, E: int):
     return removed, counts
 
 
+def _fill_out(B: int, device, limbs: bool):
+    if limbs:
+        return None, torch.empty(B, _lib.RES2_LIMBS, dtype=torch.int64, device=device)
+    return torch.empty(B, dtype=torch.float64, device=device), None
+
+
 def fill_residual(pattern: Lines, a_lines: Lines, removed: torch.Tensor, lsq: bool, line_begin: int = 0,
-                  line_end: int | None = None, store_m: bool = False, m_dtype=torch.float32):
-    """res2 [B] fp64 (= sum over lines [begin, end) of ||line residual||^2) and optional M values."""
+                  line_end: int | None = None, store_m: bool = False, m_dtype=torch.float32, word_base: int = 0,
+                  limbs: bool = False):
+    """(res2 [B] fp64 = sum over lines [begin, end) of ||line residual||^2, or with ``limbs`` the
+    exact sums [B, RES2_LIMBS] int64 to be summed across line shards; M values or None).
+    ``removed`` [B, words]: row b holds bitmap words word_base .. word_base + words - 1 of sample b."""
     _lib.require_device(removed)
     if line_end is None:
         line_end = pattern.n
+    removed = removed.contiguous()
     B, words = removed.shape
     if a_lines.val.dtype not in _DT:
         raise ValueError(f"A dtype {a_lines.val.dtype} not supported (fp32/fp64)")
@@ -246,7 +264,7 @@ def fill_residual(pattern: Lines, a_lines: Lines, removed: torch.Tensor, lsq: bo
     if not lsq:
         m_dtype = torch.float32
     n_loc = line_end - line_begin
-    res2 = torch.empty(B, dtype=torch.float64, device=removed.device)
+    res2, lb = _fill_out(B, removed.device, limbs)
     m = torch.empty(B, n_loc, pattern.width, dtype=m_dtype, device=removed.device) if store_m else None
     nb = _l().spai_fill_workspace_bytes(max(n_loc, 1), B)
     ws = _lib.workspace(nb, removed.device, "fill")
@@ -254,10 +272,10 @@ def fill_residual(pattern: Lines, a_lines: Lines, removed: torch.Tensor, lsq: bo
         st = _l().spai_fill_residual(mode, pattern.n, line_begin, line_end, pattern.width, _lib.ptr(pattern.idx),
                                        _lib.ptr(pattern.act), _lib.ptr(pattern.val), a_lines.width,
                                        _lib.ptr(a_lines.idx), _lib.ptr(a_lines.val), _DT[a_lines.val.dtype], B,
-                                       _lib.ptr(removed), words, _lib.ptr(m), _DT[m_dtype], _lib.ptr(res2),
-                                       _lib.ptr(ws), ws.numel(), _lib.stream_ptr(removed.device))
+                                       _lib.ptr(removed), words, word_base, _lib.ptr(m), _DT[m_dtype], _lib.ptr(res2),
+                                       _lib.ptr(lb), _lib.ptr(ws), ws.numel(), _lib.stream_ptr(removed.device))
     _lib.check(st, "spai_fill_residual")
-    return res2, m
+    return (lb if limbs else res2), m
 
 
 def gram_build(pattern: Lines, a_lines: Lines) -> torch.Tensor:
@@ -288,30 +306,43 @@ def gram_compact(gram: torch.Tensor, pattern: Lines):
 
 
 def fill_residual_gram(pattern: Lines, gram: torch.Tensor, removed: torch.Tensor, lsq: bool, line_begin: int = 0,
-                       line_end: int | None = None, store_m: bool = False, m_dtype=torch.float32):
+                       line_end: int | None = None, store_m: bool = False, m_dtype=torch.float32, word_base: int = 0,
+                       limbs: bool = False):
     """fill_residual from the env's Gram cache (same outputs)."""
     _lib.require_device(removed)
     if line_end is None:
         line_end = pattern.n
+    removed = removed.contiguous()
     B, words = removed.shape
     mode = _lib.FILL_LSQ if lsq else _lib.FILL_COPY
     if not lsq:
         m_dtype = torch.float32
     n_loc = line_end - line_begin
-    res2 = torch.empty(B, dtype=torch.float64, device=removed.device)
+    res2, lb = _fill_out(B, removed.device, limbs)
     m = torch.empty(B, n_loc, pattern.width, dtype=m_dtype, device=removed.device) if store_m else None
     nb = _l().spai_fill_workspace_bytes(max(n_loc, 1), B)
     ws = _lib.workspace(nb, removed.device, "fill")
     with _timed("fill_residual"):  # the fill kernel alone (the bench's roofline kernel)
         st = _l().spai_fill_lines_gram(mode, pattern.n, line_begin, line_end, pattern.width, _lib.ptr(pattern.act),
                                        _lib.ptr(pattern.val), _lib.ptr(gram), _DT[gram.dtype], B, _lib.ptr(removed),
-                                       words,
-                                       _lib.ptr(m), _DT[m_dtype], _lib.ptr(ws), ws.numel(),
+                                       words, word_base, _lib.ptr(m), _DT[m_dtype], _lib.ptr(ws), ws.numel(),
                                        _lib.stream_ptr(removed.device))
     _lib.check(st, "spai_fill_lines_gram")
-    _lib.check(_l().spai_fill_reduce(n_loc, B, _lib.ptr(ws), _lib.ptr(res2), _lib.stream_ptr(removed.device)),
-               "spai_fill_reduce")
-    return res2, m
+    _lib.check(_l().spai_fill_reduce(n_loc, B, _lib.ptr(ws), _lib.ptr(res2), _lib.ptr(lb),
+                                     _lib.stream_ptr(removed.device)), "spai_fill_reduce")
+    return (lb if limbs else res2), m
+
+
+def res2_from_limbs(limbs: torch.Tensor) -> torch.Tensor:
+    """[B] fp64 squared residuals from exact sums [B, RES2_LIMBS] int64 (spai_res2_from_limbs)."""
+    _lib.require_device(limbs)
+    if limbs.dtype != torch.int64 or limbs.dim() != 2 or limbs.shape[1] != _lib.RES2_LIMBS:
+        raise ValueError(f"limbs must be int64 [B, {_lib.RES2_LIMBS}]")
+    limbs = limbs.contiguous()
+    out = torch.empty(limbs.shape[0], dtype=torch.float64, device=limbs.device)
+    _lib.check(_l().spai_res2_from_limbs(limbs.shape[0], _lib.ptr(limbs), _lib.ptr(out),
+                                         _lib.stream_ptr(limbs.device)), "spai_res2_from_limbs")
+    return out
 
 
 def rewards(res2: torch.Tensor, counts: torch.Tensor, nnz0: int, n: int, r0: float, f0: int, alpha: torch.Tensor):

@@ -77,6 +77,7 @@ class Log:
         self._lmax = None
         self.removed = None
         self.counts = None
+        self.rewards_all = None  # fp64 rewards of every candidate of a columns-split step (all ranks')
 
     def log(self, s, probs: Tensor, actions: Tensor, done: Tensor):
         """Per-step logging, log.py:24-89 semantics (used by custom loops)."""
@@ -102,10 +103,10 @@ class Log:
             self._full = (actions_bt, fwd_bt, t_dev)
 
     def _set_part(self, rank: int, world: int, group, bounds: Tensor):
-        """The rollout was split over ``world`` processes: this rank's buffers hold
-        only the trajectory slice [bounds[b, 0], bounds[b, 1]) of each sample.  The full log is
-        assembled on first use (one all_reduce of the zero-masked slices: the slices are
-        disjoint, so the sum is exact); ``local_slice`` reads the rank's part without it."""
+        """The rollout was split over ``world`` processes by trajectory slices:
+        this rank's buffers hold only the slice [bounds[b, 0], bounds[b, 1]) of each sample.
+        ``local_slice`` reads the rank's part; the full log needs ``gather_parts()`` — a
+        collective every rank of the group must call — before ``actions`` / ``fwd_probs``."""
         self._part = (rank, world, group, bounds)
 
     def local_slice(self):
@@ -113,14 +114,29 @@ class Log:
         a, f, _ = self._full
         return a, f, self._part[3]
 
-    def _materialize(self):
-        if self._full is not None:
+    def gather_parts(self) -> "Log":
+        """Assemble the full trajectories of a slices-split rollout: one all_reduce of the
+        zero-masked slices (disjoint, so the sum is exact).  A COLLECTIVE: call it on every rank
+        of the group, or on none.  A no-op for an unsplit rollout."""
+        part = getattr(self, "_part", None)
+        if self._full is not None and part is not None and part[1] > 1:
+            from .distributed import gather_slices
             a, f, t = self._full
             T = int(t)
+            a, f = gather_slices(a, f, part[3], T, part[2])
+            self._actions_bt, self._fwd_probs = a, f
+            self._act_tb = a.t()
+            self._full = None
+        return self
+
+    def _materialize(self):
+        if self._full is not None:
             part = getattr(self, "_part", None)
             if part is not None and part[1] > 1:
-                from .distributed import gather_slices
-                a, f = gather_slices(a, f, part[3], T, part[2])
+                raise RuntimeError("this Log holds one rank's slice of a split rollout: call log.gather_parts() on "
+                                   "every rank first (a collective), or read log.local_slice()")
+            a, f, t = self._full
+            T = int(t)
             self._actions_bt, self._fwd_probs = a[:, :T], f[:, :T]
             self._act_tb = self._actions_bt.t()
             self._full = None

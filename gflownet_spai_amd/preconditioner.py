@@ -79,6 +79,7 @@ class PreconditionerEnv(Env):
         self.a_lines: Lines = build_lines(ai[0], ai[1], a.values(), matrix_size, orient, self.device, a_dtype)
         self.last_m = None
         self.last_removed = None  # removal bitmaps [B, ceil(E/32)] of the last batch (assemble)
+        self._word_spans = {}     # world -> per-rank bitmap word spans of the column shards
         # Gram cache of the fixed pattern (G = A_J^T A_J, c = A[l, J] per line): the per-rollout
         # fill then streams it instead of re-gathering A (pattern widths <= 13, A widths <= 7;
         # wider patterns use the generic kernels)
@@ -107,26 +108,40 @@ class PreconditionerEnv(Env):
     def rewards_from_removed(self, removed: Tensor, counts: Tensor, alpha, line_begin: int = 0,
                              line_end: int | None = None, group=None) -> Tensor:
         """[B] fp64 rewards from removal bitmaps; with ``group`` the lines are a shard and the
-        per-sample squared norms are summed across the process group (one all_reduce)."""
-        res2 = self.fill_partial(removed, line_begin, line_end)
-        if group is not None:
-            import torch.distributed as dist
-            dist.all_reduce(res2, group=group)
-        return self.rewards_from_res2(res2, counts, alpha)
+        per-sample squared norms are summed exactly across the process group (one all_reduce of
+        the integer limbs: the same bits as one process when the shards are 256-line aligned)."""
+        if group is None:
+            return self.rewards_from_res2(self.fill_partial(removed, line_begin, line_end), counts, alpha)
+        from .distributed import all_reduce_
+        limbs = all_reduce_(self.fill_partial(removed, line_begin, line_end, limbs=True), group)
+        return self.rewards_from_res2(kernels.res2_from_limbs(limbs), counts, alpha)
 
-    def fill_partial(self, removed: Tensor, line_begin: int = 0, line_end: int | None = None) -> Tensor:
+    def fill_partial(self, removed: Tensor, line_begin: int = 0, line_end: int | None = None, word_base: int = 0,
+                     limbs: bool = False) -> Tensor:
         """Fill lines [line_begin, line_end) of M for every sample and return the per-sample
-        squared residual norms of those lines, [B] fp64 (kept in ``last_m`` / ``last_removed``)."""
+        squared residual norms of those lines, [B] fp64 (kept in ``last_m`` / ``last_removed``);
+        with ``limbs`` their exact sums [B, RES2_LIMBS] int64 instead (summable across line
+        shards, spai_hip.h).  ``removed`` rows may be windows of the bitmaps starting at word
+        ``word_base`` (the columns split's all_to_all delivers only a shard's words)."""
+        kw = dict(store_m=self.keep_m, m_dtype=self.a_lines.val.dtype, word_base=word_base, limbs=limbs)
         if self.gram is not None:
             res2, m = kernels.fill_residual_gram(self.pattern, self.gram, removed, self.fill == "lsq", line_begin,
-                                                 line_end, store_m=self.keep_m, m_dtype=self.a_lines.val.dtype)
+                                                 line_end, **kw)
         else:
             res2, m = kernels.fill_residual(self.pattern, self.a_lines, removed, self.fill == "lsq", line_begin,
-                                            line_end, store_m=self.keep_m, m_dtype=self.a_lines.val.dtype)
+                                            line_end, **kw)
         if self.keep_m:
             self.last_m = m
-        self.last_removed = removed
+        self.last_removed = removed if word_base == 0 else None  # a window cannot be assembled
         return res2
+
+    def word_spans(self, world: int) -> list:
+        """Bitmap word span [(w0, w1)] of each of ``world`` 256-line-aligned column shards
+        (distributed.word_spans; one host sync per world size, cached)."""
+        if world not in self._word_spans:
+            from .distributed import word_spans
+            self._word_spans[world] = word_spans(self, world)
+        return self._word_spans[world]
 
     def rewards_from_res2(self, res2: Tensor, counts: Tensor, alpha) -> Tensor:
         """Residuals (``last_residual``) and rewards [B] fp64 from the summed squared norms."""
@@ -179,7 +194,7 @@ class PreconditionerEnv(Env):
             return torch.sqrt(kernels.residual_lines(pat.idx, pat.val, a_lines)[0])
         # wider lines (e.g. spilu L@U patterns): the LDS-hash line kernel of the copy fill
         pat = build_lines(mi[0], mi[1], m.values(), n, orient, self.device, torch.float32)
-        removed = torch.zeros(1, max((pat.n * pat.width + 31) // 32, 1), dtype=torch.int32, device=self.device)
+        removed = torch.zeros(1, max((m._nnz() + 31) // 32, 1), dtype=torch.int32, device=self.device)
         res2, _ = kernels.fill_residual(pat, a_lines, removed, lsq=False)
         return torch.sqrt(res2[0])
 

@@ -109,8 +109,10 @@ int spai_parity_step(const float* logits, int64_t bstride, int32_t E1, int32_t B
  * draws all E actions (removed and the untouched mass are complete on every part), but only
  * its own winners are bucketed, staged and sorted.  Its select fills the exchange array
  * (spai_rollout_ws_offset fields 2/6: per-bucket weight sums and winner counts of its own
- * buckets, 0 elsewhere, and B caller slots); the caller sums that array over the parts (an
- * all-reduce: x + 0 is exact, so the sum equals the one-part array bit for bit), then calls
+ * buckets, 0 elsewhere, then B * SPAI_RES2_LIMBS caller slots); the caller sums that array over
+ * the parts (an all-reduce of its int64 bit patterns: every entry is non-zero on one part only,
+ * so the sum equals the one-part array bit for bit, and the slots carry the exact residual
+ * limbs), then calls
  * spai_rollout_merge (counts, T, bucket positions and masses), spai_rollout_sort (actions and
  * fwd_probs of its slice) and spai_rollout_finish (the last part writes the terminal step and
  * the padding; t_out is written by every part). */
@@ -134,7 +136,7 @@ int spai_rollout_order(const float* logits, int64_t bstride, int32_t E, int32_t 
 /* Byte offset inside the rollout workspace (tests, the multi-part exchange): field 0 = int32
  * oversized buckets the last sort handed to the global-memory sort, 1 = int32 T of the last
  * rollout, 2 = fp64 exchange array ([B][2][kMaxB] bucket weight sums | bucket winner counts,
- * then [B] caller slots), 4 = int32 [B][kMaxB + 1] trajectory position of each bucket's first
+ * then [B][SPAI_RES2_LIMBS] int64 caller slots), 4 = int32 [B][kMaxB + 1] trajectory position of each bucket's first
  * winner, 5 = int32 [B] buckets per sample (a part's slice of sample b is
  * [pos[b][nb*p/np], pos[b][nb*(p+1)/np])); field 3 returns kMaxB itself, field 6 the length of
  * the exchange array in fp64 values.  -1 for an unknown field or bad shape. */
@@ -163,6 +165,18 @@ int spai_actions_to_removed(const int64_t* actions, int64_t stride_b, int64_t st
                             int32_t T, int32_t E, uint32_t* removed, int32_t words, int32_t* counts,
                             void* stream);
 
+/* ---------------------------------------------------------------- exact residual sums
+ * The squared residual of a batch is a sum of per-block fp64 partials.  Each partial is
+ * truncated toward zero to a multiple of 2^-96 and summed as integers: SPAI_RES2_LIMBS int64
+ * slots per sample (six signed 32-bit limbs, value = sum_i L_i 2^(32 i - 96), then a count of
+ * non-representable partials: NaN in bits 32.., inf or |x| >= 2^94 in bits 0..31, then a pad).
+ * Integer addition is associative, so the slots of a sample summed over ANY partition of its
+ * lines into 256-line-aligned ranges (the column shards of a multi-GPU job: one all-reduce SUM
+ * of the int64 slots) give the same bits as one launch over all lines; res2 = the slots'
+ * value rounded once to fp64 (NaN / +inf when flagged). */
+#define SPAI_RES2_LIMBS 8
+int spai_res2_from_limbs(int32_t B, const int64_t* limbs, double* res2_out, void* stream);
+
 /* ---------------------------------------------------------------- fill + residual
  * For lines [line_begin, line_end) of the pattern and every sample b:
  *   keep_p = (pat_idx[l,p] >= 0) && !removed[b][pat_act[l,p]]
@@ -174,6 +188,12 @@ int spai_actions_to_removed(const int64_t* actions, int64_t stride_b, int64_t st
  * the lines (e.g. the ranks of a column-sharded job) gives the full square norm.
  * M is evaluated from its STORED precision (m_dtype).  m_out (may be NULL) receives
  * [B][line_end - line_begin][W] values in m_dtype (0 where not kept).
+ * Bitmap windows: row b of `removed` (row stride `words` uint32) holds bitmap words
+ * word_base, word_base + 1, ... of sample b (word_base 0, words = ceil(E/32): whole bitmaps);
+ * every word an action id of the lines names must lie inside the row (a column shard needs
+ * only the words its lines' action ids span: the multi-GPU all-to-all ships just those).
+ * res2_out (fp64 [B]) and/or limbs_out ([B][SPAI_RES2_LIMBS], the exact sums above) receive
+ * the per-sample sums; either may be NULL, not both.
  * a_idx/a_val: [n][WA] lines of the original matrix A (n x n) in the same orientation.
  * Widths W, WA <= 7 run the register kernel (one thread per line, all samples); wider
  * COPY lines run the LDS hash kernel (one workgroup per line and sample, bounded by
@@ -183,8 +203,8 @@ size_t spai_fill_workspace_bytes(int32_t n_lines, int32_t B);
 int spai_fill_residual(int32_t fill_mode, int32_t n, int32_t line_begin, int32_t line_end, int32_t W,
                        const int32_t* pat_idx, const int32_t* pat_act, const float* pat_val, int32_t WA,
                        const int32_t* a_idx, const void* a_val, int32_t a_dtype, int32_t B,
-                       const uint32_t* removed, int32_t words, void* m_out, int32_t m_dtype,
-                       double* res2_out, void* workspace, size_t workspace_bytes, void* stream);
+                       const uint32_t* removed, int32_t words, int32_t word_base, void* m_out, int32_t m_dtype,
+                       double* res2_out, int64_t* limbs_out, void* workspace, size_t workspace_bytes, void* stream);
 
 /* ---------------------------------------------------------------- Gram-cached fill + residual
  * The LSQ fill and the residual of line l need only G_pq = <A_line(k_p), A_line(k_q)> and
@@ -210,17 +230,18 @@ int spai_gram_build(int32_t n, int32_t W, const int32_t* pat_idx, int32_t WA, co
 int spai_gram_compact(int32_t n, int32_t W, const double* gram, float* gram32, int32_t* exact, void* stream);
 int spai_fill_residual_gram(int32_t fill_mode, int32_t n, int32_t line_begin, int32_t line_end, int32_t W,
                             const int32_t* pat_act, const float* pat_val, const void* gram, int32_t gram_dtype,
-                            int32_t B,
-                            const uint32_t* removed, int32_t words, void* m_out, int32_t m_dtype,
-                            double* res2_out, void* workspace, size_t workspace_bytes, void* stream);
-/* The two halves of spai_fill_residual_gram: the fill kernel leaves per-block fp64 partial
- * sums in the workspace; spai_fill_reduce (n_lines = line_end - line_begin of that call)
- * sums them per sample in a fixed order into res2_out. */
+                            int32_t B, const uint32_t* removed, int32_t words, int32_t word_base, void* m_out,
+                            int32_t m_dtype, double* res2_out, void* workspace, size_t workspace_bytes,
+                            void* stream);
+/* The two halves of spai_fill_residual_gram: the fill kernel leaves per-block (256-line) fp64
+ * partial sums in the workspace; spai_fill_reduce (n_lines = line_end - line_begin of that
+ * call) sums them per sample exactly (SPAI_RES2_LIMBS) into res2_out and/or limbs_out. */
 int spai_fill_lines_gram(int32_t fill_mode, int32_t n, int32_t line_begin, int32_t line_end, int32_t W,
                          const int32_t* pat_act, const float* pat_val, const void* gram, int32_t gram_dtype, int32_t B,
-                         const uint32_t* removed, int32_t words, void* m_out, int32_t m_dtype,
+                         const uint32_t* removed, int32_t words, int32_t word_base, void* m_out, int32_t m_dtype,
                          void* workspace, size_t workspace_bytes, void* stream);
-int spai_fill_reduce(int32_t n_lines, int32_t B, const void* workspace, double* res2_out, void* stream);
+int spai_fill_reduce(int32_t n_lines, int32_t B, const void* workspace, double* res2_out, int64_t* limbs_out,
+                     void* stream);
 
 /* ---------------------------------------------------------------- forward policy
  * logits[a] = fc(mean_pool(relu(GATv2_2(relu(GATv2_1(x))))))[a] for a < num_actions and

@@ -396,6 +396,60 @@ def reward(residual, nnz_m, alpha, r0, f0, n):
 
 
 # --------------------------------------------------------------------------------------
+# Exact residual sums (the build's multi-GPU reduction; no reference counterpart: the reference
+# sums ||M A - I||_F^2 inside one torch.norm, preconditioner.py:90).  Restates spai_device.h
+# fixed_add / fixed_value (spai_hip.h SPAI_RES2_LIMBS): every partial truncated toward zero to a
+# multiple of 2^-96, summed as integers, rounded once.
+# --------------------------------------------------------------------------------------
+
+RES2_LIMBS = 8
+
+
+def fixed_limbs(x: float) -> np.ndarray:
+    """int64 [8] slots of one fp64 partial: six signed 32-bit limbs (value = sum L_i 2^(32i-96)),
+    then the NaN (<< 32) / inf-or-|x|>=2^94 count, then a pad."""
+    L = np.zeros(RES2_LIMBS, dtype=np.int64)
+    x = float(x)
+    if np.isnan(x):
+        L[6] = 1 << 32
+        return L
+    if np.isinf(x) or abs(x) >= 2.0 ** 94:
+        L[6] = 1
+        return L
+    F = int(abs(x) * 2.0 ** 96)  # |x| 2^96 is exact (a power-of-two scaling); int() truncates toward 0
+    for i in range(6):
+        c = (F >> (32 * i)) & 0xFFFFFFFF
+        L[i] = -c if x < 0 else c
+    return L
+
+
+def fixed_value(L) -> float:
+    """fp64 value of summed slots (carry-normalise, then Horner from the top limb, as the kernel)."""
+    L = [int(v) for v in L]
+    if L[6] >> 32:
+        return float("nan")
+    if L[6]:
+        return float("inf")
+    c = L[:6]
+    for i in range(5):
+        carry = c[i] >> 32
+        c[i] -= carry << 32
+        c[i + 1] += carry
+    v = float(c[5])
+    for i in range(4, -1, -1):
+        v = v * 4294967296.0 + float(c[i])  # the kernel's fma: v * 2^32 is exact, one rounding
+    return v * 2.0 ** -96
+
+
+def fixed_sum(partials) -> float:
+    """The exact sum of fp64 partials as the GPU reduction returns it (partition-invariant)."""
+    acc = np.zeros(RES2_LIMBS, dtype=object)
+    for x in partials:
+        acc = acc + fixed_limbs(x).astype(object)
+    return fixed_value(acc)
+
+
+# --------------------------------------------------------------------------------------
 # Least-squares fill (north-star extension) — PARITY UNPINNED BY THE REFERENCE.
 # m_j = argmin || A[:, J_j] m - e_j ||_2, J_j = kept pattern rows of column j.
 # Oracle: stacked Householder QR in fp64 (numpy), cross-checked by lstsq.

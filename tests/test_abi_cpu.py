@@ -35,8 +35,8 @@ def test_library_exports_every_symbol():
 def test_argument_validation_without_gpu():
     """Argument checks run before any HIP call, so they are exercisable on a CPU host."""
     lib = _lib.load()
-    rc = lib.spai_fill_residual(7, 10, 0, 10, 5, None, None, None, 5, None, None, 0, 1, None, 1, None, 0,
-                                None, None, 0, None)
+    rc = lib.spai_fill_residual(7, 10, 0, 10, 5, None, None, None, 5, None, None, 0, 1, None, 1, 0, None, 0,
+                                None, None, None, 0, None)
     assert rc == _lib.SPAI_ERR_INVALID
     assert b"fill_mode" in lib.spai_last_error()
     rc = lib.spai_rollout_select(None, 0, 10, 1, None, 0, 0, None, 0, 0, 1, None, 1, None, None, 0, None)
@@ -45,7 +45,7 @@ def test_argument_validation_without_gpu():
     assert rc == _lib.SPAI_ERR_INVALID and b"null pointer" in lib.spai_last_error()
     rc = lib.spai_rollout_merge(None, 0, 10, 1, None, 0, 2, None, None, 0, None)
     assert rc == _lib.SPAI_ERR_INVALID and b"null pointer" in lib.spai_last_error()
-    assert lib.spai_rollout_ws_offset(1000, 2, 6) == 2 * 2 * 2048 + 2
+    assert lib.spai_rollout_ws_offset(1000, 2, 6) == 2 * 2 * 2048 + 2 * 8
     assert lib.spai_rollout_ws_offset(1000, 2, 3) == 2048 and lib.spai_rollout_ws_offset(1000, 2, 9) == -1
     assert 0 < lib.spai_rollout_ws_offset(1000, 2, 2) < lib.spai_rollout_workspace_bytes(1000, 2)
     with pytest.raises(ValueError):

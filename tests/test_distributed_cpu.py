@@ -13,8 +13,9 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from gflownet_spai_amd.distributed import (allgather_lines, allreduce_res2, exchange_parts, gather_rewards,
-                                           gather_slices, select_best_samples, shard_lines)
+from gflownet_spai_amd.distributed import (LINE_ALIGN, allgather_lines, allreduce_res2, bitmap_pack_index,
+                                           exchange_bitmaps, exchange_parts, gather_rewards, gather_slices,
+                                           select_best_samples, shard_lines, word_spans)
 from oracle import spai_oracle as O
 
 
@@ -60,18 +61,22 @@ def _worker(rank, world, port, q):
         out["res2"] = res2.numpy()
         out["m"] = full_m.numpy()
         out["rewards"] = gather_rewards(torch.arange(B, dtype=torch.float64) + 10 * rank).numpy()
-        # the split rollout's exchange: each part fills the bucket weight sums and winner counts
+        # the slices split's exchange: each part fills the bucket weight sums and winner counts
         # of its own bucket range (zero elsewhere, the exchange array's [B][2][kMaxB] layout)
-        # and its lines' residual partials go into the B trailing slots; one all_reduce in place
-        full_bs, full_r2 = _split_fixture()
+        # and its lines' exact residual limbs go into the B x 8 trailing slots; one all_reduce
+        # of the int64 bit patterns in place
+        full_bs, partials = _split_fixture()
         B3, nb = full_bs.shape[0], full_bs.shape[2]
         k0, k1 = nb * rank // world, nb * (rank + 1) // world
-        xch = torch.zeros(full_bs.numel() + B3, dtype=torch.float64)
+        xch = torch.zeros(full_bs.numel() + B3 * O.RES2_LIMBS, dtype=torch.float64)
         bs = xch[:full_bs.numel()].view_as(full_bs)
         bs[:, :, k0:k1] = full_bs[:, :, k0:k1]
-        r2 = full_r2 * (0.25 if rank == 0 else 0.75)
-        out["r2"] = exchange_parts(xch, r2).clone().numpy()
+        mine = partials[:, rank::world]  # this rank's per-block partials of every sample
+        limbs = torch.from_numpy(np.stack([sum(O.fixed_limbs(x) for x in row) for row in mine]))
+        summed = exchange_parts(xch, limbs)
+        out["r2"] = [O.fixed_value(row) for row in summed.numpy()]
         out["bs"] = bs.numpy()
+        out["cols"] = _columns_exchange(rank, world)
         # the samples split: 2 local candidates per rank, global best's M reduced to rank 0
         rw = torch.tensor([[0.5, 2.5], [1.5, -1.0]], dtype=torch.float64)[rank]
         ml = torch.arange(2 * 3 * 4, dtype=torch.float64).view(2, 3, 4) + 100 * rank
@@ -97,7 +102,42 @@ def _split_fixture():
     g = torch.Generator().manual_seed(3)
     sums = torch.rand(3, 1, 37, generator=g, dtype=torch.float64) * 1e3
     counts = torch.randint(0, 5000, (3, 1, 37), generator=g).double()
-    return torch.cat([sums, counts], 1), torch.rand(3, generator=g, dtype=torch.float64)
+    partials = np.random.default_rng(3).random((3, 11)) * np.logspace(-12, 6, 11)  # per-block partials
+    return torch.cat([sums, counts], 1), partials
+
+
+class _Pattern:
+    """The attributes distributed.word_spans reads from a PreconditionerEnv (CPU stand-in)."""
+
+    def __init__(self, grid):
+        r, c, v, n = O.poisson2d(grid)
+        idx, act, _ = O.lines_from_coo(r, c, v, n, "col")
+        self.matrix_size, self.E = n, len(r)
+        self.pattern = type("P", (), {"act": torch.from_numpy(act), "idx": torch.from_numpy(idx)})()
+
+
+def _columns_fixture(world, bl):
+    env = _Pattern(24)  # 576 lines: 256-line blocks split 2 + 1 over two ranks
+    words = (env.E + 31) // 32
+    rng = np.random.default_rng(7)
+    bits = rng.integers(0, 2 ** 32, size=(world * bl, words), dtype=np.uint64).astype(np.uint32).view(np.int32)
+    counts = rng.integers(0, env.E, size=world * bl).astype(np.int32)
+    return env, words, torch.from_numpy(bits), torch.from_numpy(counts)
+
+
+def _columns_exchange(rank, world, bl=3):
+    """The columns split's all_to_all: rank r holds candidates r*bl .. (its bitmaps + counts in
+    one buffer, as rollout_select(out=) writes them) and receives every candidate's window of
+    the words its 256-line shard spans, plus the counts."""
+    env, words, bits, counts = _columns_fixture(world, bl)
+    spans = word_spans(env, world)
+    mine = slice(rank * bl, (rank + 1) * bl)
+    buf = torch.cat([bits[mine].reshape(-1), counts[mine]])
+    send = buf[bitmap_pack_index(spans, bl, words, "cpu")]
+    w0, w1 = spans[rank]
+    recv = torch.full((world * bl, w1 - w0 + 1), -7, dtype=torch.int32)
+    exchange_bitmaps(send, recv, spans, bl, rank).wait()
+    return spans, recv.numpy()
 
 
 def _slices_fixture():
@@ -144,14 +184,51 @@ def test_world2_column_sharded_reward_and_assembly():
             assert res[rank]["res2"][b] == pytest.approx(full, rel=1e-12)
             np.testing.assert_allclose(res[rank]["m"][b], m, rtol=1e-12, atol=1e-15)
     np.testing.assert_array_equal(res[0]["rewards"], [0, 1, 2, 10, 11, 12])
-    full_bs, full_r2 = _split_fixture()
+    full_bs, partials = _split_fixture()
     acts, fwd, _, _ = _slices_fixture()
+    env, words, bits, counts = _columns_fixture(2, 3)
+    lines = [shard_lines(env.matrix_size, q, 2, LINE_ALIGN) for q in (0, 1)]
+    assert lines == [(0, 512), (512, 576)]
     for rank in (0, 1):
         assert np.array_equal(res[rank]["bs"], full_bs.numpy())  # bit-exact: one non-zero term each
-        np.testing.assert_allclose(res[rank]["r2"], full_r2.numpy(), rtol=1e-15)
+        for b in range(3):  # exact sums: the same bits as one process summing every partial
+            assert res[rank]["r2"][b] == O.fixed_sum(partials[b])
+        spans, recv = res[rank]["cols"]
+        w0, w1 = spans[rank]
+        b0, b1 = lines[rank]
+        a = env.pattern.act[b0:b1].numpy()
+        assert w0 == a[a >= 0].min() >> 5 and w1 == (a[a >= 0].max() >> 5) + 1
+        assert np.array_equal(recv[:, :w1 - w0], bits[:, w0:w1].numpy())  # every candidate, global order
+        assert np.array_equal(recv[:, w1 - w0], counts.numpy())
         assert np.array_equal(res[rank]["slices"][0], acts.numpy())
         allr, best, mbest = res[rank]["samples"]
         np.testing.assert_array_equal(allr, [0.5, 2.5, 1.5, -1.0])
         assert best == 1
         assert np.array_equal(res[rank]["slices"][1], fwd.numpy())
     np.testing.assert_array_equal(res[0]["samples"][2], np.arange(24, dtype=np.float64).reshape(2, 3, 4)[1])
+
+
+def test_shard_lines_aligned():
+    for n in (1, 255, 256, 576, 1048576, 262144 + 17):
+        for world in (1, 2, 3, 8):
+            rngs = [shard_lines(n, r, world, LINE_ALIGN) for r in range(world)]
+            assert rngs[0][0] == 0 and rngs[-1][1] == n
+            assert all(rngs[i][1] == rngs[i + 1][0] for i in range(world - 1))
+            assert all(b % LINE_ALIGN == 0 or b == n for b, _ in rngs)
+
+
+def test_fixed_point_sums_are_partition_invariant():
+    """The oracle restatement of the exact residual sums (spai_device.h fixed_add/fixed_value):
+    any split of the partials sums to the same bits, close to the fp64 sum, NaN / inf flagged."""
+    rng = np.random.default_rng(11)
+    x = rng.random(500) * np.logspace(-20, 8, 500)
+    x[::7] *= -1
+    whole = O.fixed_sum(x)
+    assert abs(whole - x.sum()) <= 1e-12 * np.abs(x).sum()
+    for cut in (1, 17, 250, 499):
+        a = sum(O.fixed_limbs(v).astype(object) for v in x[:cut])
+        b = sum(O.fixed_limbs(v).astype(object) for v in x[cut:])
+        assert O.fixed_value(a + b) == whole
+    assert O.fixed_value(O.fixed_limbs(2.0 ** -100)) == 0.0  # below 2^-96: truncated
+    assert O.fixed_value(O.fixed_limbs(1.5) + O.fixed_limbs(float("inf"))) == float("inf")
+    assert np.isnan(O.fixed_value(O.fixed_limbs(float("nan")) + O.fixed_limbs(float("inf"))))

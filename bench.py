@@ -276,6 +276,10 @@ def main():
                     help="columns split: --batch is the GLOBAL batch (batch/P rollouts per GPU) instead of per GPU")
     ap.add_argument("--assemble", default="best", choices=["best", "all", "none"])
     ap.add_argument("--no-graph", action="store_true", help="time eager steps (host launches) instead of graph replays")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="process-group backend (nccl = RCCL over xGMI; gloo only to rehearse the flow)")
+    ap.add_argument("--share-gpu", action="store_true",
+                    help="every rank on GPU 0 (rehearsal of the multi-rank flow on a one-GPU box, with --backend gloo)")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -286,11 +290,16 @@ def main():
                  f"torch.distributed.run --nproc-per-node {args.gpus} or without WORLD_SIZE")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.share_gpu:  # rehearsal of the multi-rank flow on a one-GPU box (with --backend gloo)
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.backend)
 
     from gflownet_spai_amd import GFlowNet, PreconditionerEnv, kernels
     from gflownet_spai_amd.distributed import LINE_ALIGN, allgather_lines
@@ -308,7 +317,7 @@ def main():
     else:  # columns (weak: --batch rollouts per GPU, fill of every candidate by column shard) / candidates
         B, bl, strong = args.batch * world, args.batch, False
     base = {"samples": rank * bl, "candidates": rank * bl}.get(shard, 0)
-    split = {"columns": "columns", "slices": "slices"}.get(shard)
+    split = {"columns": "columns", "slices": "slices"}.get(shard) if world > 1 else None
     model = GFlowNet(make_policy(env, P, dev), None, env, mode="throughput", seed=1234, sample_base=base,
                      shard=(rank, world, None) if split else None, split=split or "columns")
     s0 = [P] * bl

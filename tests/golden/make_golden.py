@@ -29,6 +29,7 @@ Harness-side workarounds for the reference's latent bugs:
 Usage:  python tests/golden/make_golden.py            (writes *.npz + meta.json)
         python tests/golden/make_golden.py g6         (C2/C4 parity rollouts, appended)
         python tests/golden/make_golden.py g7         (C1 assembled M of three removal sets, appended)
+        python tests/golden/make_golden.py g8         (C2 long parity rollout, T > 1000, appended)
 """
 import gc
 import json
@@ -286,6 +287,43 @@ def parity_rollouts_large():
         json.dump(meta, f, indent=1)
 
 
+def parity_rollout_long():
+    """G8: a LONG reference rollout at C2 (256^2, E = 326,656) through GFlowNet.sample_states:
+    the terminal logit is set so that a sample stops with probability ~2.8e-4 per step (T > 1,000 steps
+    of the reference's fp32 masked softmax -> renormalisation -> Categorical chain
+    (policy.py:65-73, gflownet.py:116-119,148), B = 2.  Stored like G6.  Appends to meta.json."""
+    preconditioner, policy, gfn_mod, ref_utils = _import_reference()
+    meta_path = os.path.join(HERE, "meta.json")
+    meta = json.load(open(meta_path))
+    tag, grid, logit_seed, term_logit, seed, B = "c2long", 256, 21, 5.0, 31, 2
+    A = poisson2d(grid)
+    order = np.lexsort((A.col, A.row))
+    rows, cols, vals = A.row[order].astype(np.int64), A.col[order].astype(np.int64), A.data[order].astype(np.float32)
+    n = grid * grid
+    A_t = to_torch_coo(rows, cols, vals, n)
+    env = make_env(preconditioner, A_t, n)
+    E = env.num_actions - 1
+    logits = torch.randn(E + 1, generator=torch.Generator().manual_seed(logit_seed))
+    logits[E] = term_logit
+    model = gfn_mod.GFlowNet(FixedLogitPolicy(logits), None, env)
+    s0 = [A_t.clone() for _ in range(B)]
+    torch.manual_seed(seed)
+    t0 = time.time()
+    lg = model.sample_states(s0, return_log=True)
+    dt = time.time() - t0
+    np.savez_compressed(os.path.join(HERE, f"{tag}_rollout.npz"), grid=grid, logit_seed=logit_seed,
+                        terminal_logit=term_logit, seed=seed, B=B, actions=lg.actions.numpy(),
+                        fwd_probs=lg.fwd_probs.detach().numpy(), rewards=lg.rewards.numpy())
+    meta["cases"][f"{tag}_rollout"] = {
+        "B": B, "T": int(lg.actions.shape[0]), "E": E, "grid": grid,
+        "logits": f"torch.randn(E + 1, generator=torch.Generator().manual_seed({logit_seed})); [E] = {term_logit}",
+        "rollout_seed": f"torch.manual_seed({seed}) before sample_states", "seconds": round(dt, 3),
+        "cpu": torch.backends.cpu.get_cpu_capability()}
+    print(tag, "T", lg.actions.shape[0], "rewards", lg.rewards.tolist(), "s", round(dt, 1))
+    with open(meta_path, "w") as f:
+        json.dump(meta, f, indent=1)
+
+
 def assembled_m():
     """G7: the reference's M (update_edges_and_convert_to_sparse + resize_sparse_tensor,
     utils.py:295-356, 89-126) for three removal sets of the permuted-raw-order C1 pattern
@@ -318,5 +356,7 @@ if __name__ == "__main__":
         parity_rollouts_large()
     elif len(sys.argv) > 1 and sys.argv[1] == "g7":
         assembled_m()
+    elif len(sys.argv) > 1 and sys.argv[1] == "g8":
+        parity_rollout_long()
     else:
         main()

@@ -531,11 +531,10 @@ extern "C" size_t spai_policy_workspace_bytes(int32_t n_nodes, int32_t hid, int3
 extern "C" int spai_policy_rows_constant(int32_t n_nodes, int32_t fin, const float* x, int32_t* flag, void* stream) {
   SPAI_CHECK_ARG(x && flag && n_nodes > 0 && fin > 0, "spai_policy_rows_constant: bad argument");
   hipStream_t s = (hipStream_t)stream;
-  const int32_t one = 1;
-  if (hipMemcpyAsync(flag, &one, sizeof(one), hipMemcpyHostToDevice, s) != hipSuccess) {
-    set_error("spai_policy_rows_constant: hipMemcpyAsync failed");
-    return SPAI_ERR_HIP;
-  }
+  // *flag = 1 (0x00000001) by a byte memset of its low byte after zeroing: no pageable host
+  // source, so the call is capturable in a HIP graph and never stages through the host
+  SPAI_CHECK_HIP(hipMemsetAsync(flag, 0, sizeof(int32_t), s));
+  SPAI_CHECK_HIP(hipMemsetAsync(flag, 1, 1, s));
   const int64_t total = (int64_t)n_nodes * fin;
   const int grid = (int)std::min<int64_t>(2048, (total + kNT - 1) / kNT);
   k_rows_const<<<grid, kNT, 0, s>>>(n_nodes, fin, x, flag);

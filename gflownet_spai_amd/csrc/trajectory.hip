@@ -276,7 +276,7 @@ __device__ __forceinline__ uint64_t block_excl_scan_u64(uint64_t c, uint64_t* ld
 
 // ------------------------------------------------------------------ k_presample
 // Philox stream id of this rollout: the kernel argument, or the device counter when the caller
-// keeps one (graph replays draw fresh rollouts; k_bscan advances it after the select phase).
+// keeps one (graph replays draw fresh rollouts; k_bsum advances it at the end of the select phase).
 __device__ __forceinline__ void stream_words(const uint64_t* sctr, uint32_t& st0, uint32_t& st1) {
   if (sctr) {
     const uint64_t v = *sctr;

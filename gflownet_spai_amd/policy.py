@@ -228,6 +228,10 @@ class ForwardPolicy(BasePolicy):
         key = (x.data_ptr(), x._version, tuple(x.shape), x.dtype, str(x.device))
         if self._const is not None and self._const[0] == key:
             return self._const[1]
+        if torch.cuda.is_current_stream_capturing():
+            # no host sync inside a HIP-graph capture: an x first seen here takes the general
+            # GATv2 kernels (same logits up to fp32 rounding, capturable); warm the cache eagerly
+            return False
         xf = x.detach().float().contiguous()
         flag = torch.empty(1, dtype=torch.int32, device=x.device)
         lib = _lib.load()

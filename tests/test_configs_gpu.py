@@ -167,3 +167,52 @@ def test_assemble_matches_reference_m(fill):
         if fill == "copy":
             assert np.array_equal(M.values().cpu().numpy(), g["values"][off:off + nnz])
         off += nnz
+
+
+def test_wide_fill_badly_scaled_columns_per_pivot_floor():
+    """13-wide LSQ fill (k_gram_fill_wide) on a 3-D Laplacian whose every 5th column is scaled by
+    1e-7 (G_kk ~ 1e-14 of its neighbours): the pivot floor is per pivot (1e-13 G_kk, as the
+    narrow Gram kernel and fill.hip's k_line), so the small columns are solved, not dropped —
+    M and ||AM - I||_F match the QR oracle.  (A floor relative to the line's largest diagonal
+    would zero those slots.)"""
+    from gflownet_spai_amd import PreconditionerEnv, axial_pattern_3d, kernels, poisson_3d
+    grid = 10
+    A0 = poisson_3d(grid).coalesce()
+    n = A0.shape[0]
+    scale = np.where(np.arange(n) % 5 == 0, 1e-7, 1.0)
+    r, c = A0.indices().numpy()
+    v = A0.values().numpy() * scale[c]
+    A = torch.sparse_coo_tensor(torch.from_numpy(np.stack([r, c])), torch.from_numpy(v), (n, n))
+    P = axial_pattern_3d(grid)
+    env = PreconditionerEnv(n, P, A, side="AM", fill="lsq", keep_m=True)
+    assert env.pattern.width == 13 and env.gram is not None and env.gram.dtype == torch.float64
+    E = env.init_nnz
+    rng = np.random.default_rng(8)
+    removed = rng.random(E) < 0.2
+    acts = torch.from_numpy(np.where(removed, np.arange(E), -1))
+    rb, counts = kernels.actions_to_removed(acts.view(1, -1).to(DEV), E)
+    env.rewards_from_removed(rb, counts, 0.5)
+    A_sp = sp.csr_matrix((v, (r, c)), shape=(n, n))
+    Pi = P.coalesce()
+    P_sp = sp.coo_matrix((Pi.values().numpy(), tuple(Pi.indices().numpy())), shape=(n, n))
+    _lsq_vs_oracle(env, A_sp, P_sp, removed, tol=1e-8)
+
+
+def test_rollouts_counter_is_the_device_stream_id():
+    """GFlowNet.rollouts reads the device stream counter (graph replays advance it without the
+    host) and setting it re-seeds the device counter: a replayed stream id draws the same
+    removal sets again."""
+    from gflownet_spai_amd import GFlowNet, PreconditionerEnv, poisson_2d
+    A = poisson_2d(32)
+    env = PreconditionerEnv(A.shape[0], A, A, side="AM", fill="lsq")
+    E = env.num_actions - 1
+    logits = torch.randn(E + 1, generator=torch.Generator().manual_seed(4))
+    logits[E] = 2.5
+    g = GFlowNet(FixedLogits(logits), None, env, mode="throughput", seed=3)
+    assert g.rollouts == 0
+    logs = [g.sample_states([A] * 2, return_log=True) for _ in range(3)]
+    assert g.rollouts == 3
+    g.rollouts = 1
+    again = g.sample_states([A] * 2, return_log=True)
+    assert g.rollouts == 2
+    assert torch.equal(again.removed, logs[1].removed) and not torch.equal(again.removed, logs[0].removed)

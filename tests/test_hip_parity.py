@@ -83,11 +83,14 @@ def test_parity_rollout_bit_exact_vs_reference(seed):
     np.testing.assert_allclose(pol.l.grad.view(-1).numpy(), gref, rtol=2e-4, atol=2e-6 * np.abs(gref).max())
 
 
-@pytest.mark.parametrize("name", ["c2_rollout.npz", "c4_rollout.npz"])
+@pytest.mark.parametrize("name", ["c2_rollout.npz", "c4_rollout.npz", "c2long_rollout.npz"])
 def test_parity_rollout_bit_exact_vs_reference_large(name):
-    """C2 (E = 326,656) and C4 (E = 5,238,784) reference rollouts (G6, make_golden.py g6):
-    the HIP parity step reproduces the reference's actions from the same torch seed, its
-    fwd_probs within 1e-6 and its rewards (copy fill, ||MA - I||)."""
+    """C2 (E = 326,656) and C4 (E = 5,238,784) reference rollouts (G6, make_golden.py g6) and a
+    LONG C2 rollout (G8: T = 4,605 steps, make_golden.py g8): the HIP parity step reproduces the
+    reference's actions from the same torch seed, its fwd_probs within 1e-6 and its rewards
+    (copy fill, ||MA - I||).  The kernel ranks w_a / q_a with w_a = e^(l_a - lmax) instead of the
+    reference's renormalised fp32 softmax p_a (a flip needs the two best ratios
+    within ~3 ulp, ~1e-7 per step)."""
     from gflownet_spai_amd import GFlowNet, PreconditionerEnv, poisson_2d
     from .test_oracle_golden import large_rollout_logits
     d = load(name)

@@ -50,7 +50,9 @@ SIGNATURES = {
                                                _c_p]),
     "spai_fill_workspace_bytes": (_c_sz, [_c_i32, _c_i32]),
     "spai_rewards": (ctypes.c_int, [_c_p, _c_p, _c_i32, _c_i64, _c_i32, ctypes.c_double, ctypes.c_double, _c_p, _c_p,
-                                    _c_p, _c_p]),
+                                    _c_p, _c_p, _c_p]),
+    "spai_fill_reduce_rewards": (ctypes.c_int, [_c_i32, _c_i32, _c_p, _c_p, _c_i64, _c_i32, ctypes.c_double,
+                                                ctypes.c_double, _c_p, _c_p, _c_p, _c_p, _c_p]),
     "spai_gram_bytes": (_c_sz, [_c_i32, _c_i32]),
     "spai_gram_build": (ctypes.c_int, [_c_i32, _c_i32, _c_p, _c_i32, _c_p, _c_p, _c_i32, _c_p, _c_p]),
     "spai_fill_residual_gram": (ctypes.c_int, [_c_i32, _c_i32, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_i32, _c_i32,

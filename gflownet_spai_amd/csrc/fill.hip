@@ -250,25 +250,8 @@ hipError_t launch_hash(int32_t lb, int32_t le, int32_t wrt, int32_t wart, const 
   return hipGetLastError();
 }
 
-// Reward of preconditioner.py:55-66 + 137-165 for every sample, with the reference's
-// torch type promotion reproduced op for op: alpha is fp32, the residual ratio fp64, the
-// flop ratio a python float, (1 - alpha) * (1 - flop_ratio) is an fp32 product and the sum
-// is fp64.  Contraction is disabled so every op rounds as torch's separate kernels do.
-__global__ void k_rewards(const double* __restrict__ res2, const int32_t* __restrict__ removed_counts, int32_t B,
-                          int64_t nnz0, int32_t n, double r0, double f0, const float* __restrict__ alpha,
-                          double* __restrict__ residual, double* __restrict__ reward) {
-#pragma clang fp contract(off)
-  for (int b = threadIdx.x; b < B; b += blockDim.x) {
-    const double r = sqrt(res2[b]);
-    residual[b] = r;
-    const double rr = r0 != 0.0 ? r / r0 : INFINITY;
-    const double flops = (double)(nnz0 - removed_counts[b]) * 2.0 * (double)n;
-    const double cr = f0 != 0.0 ? flops / f0 : INFINITY;
-    const float a = *alpha;
-    const double t1 = (double)a * (1.0 - rr);
-    const float t2 = (1.0f - a) * (float)(1.0 - cr);
-    reward[b] = (t1 + (double)t2) * 1000.0;
-  }
+__global__ void k_rewards(const double* __restrict__ res2, int32_t B, RewardArgs ra) {
+  for (int b = threadIdx.x; b < B; b += blockDim.x) write_reward(b, res2[b], ra);
 }
 
 template <int W, int WA, typename TA, typename TM, bool LSQ>
@@ -357,7 +340,7 @@ extern "C" int spai_fill_residual(int32_t fill_mode, int32_t n, int32_t line_beg
                          : launch_hash<double>(line_begin, line_end, W, WA, pat_idx, pat_act, pat_val, a_idx, a_val,
                                                B, removed, words, word_base, m_out, partials, tb, s);
       SPAI_CHECK_HIP(e);
-      k_fixed_reduce<kNT><<<B, kNT, 0, s>>>(partials, nl, res2_out, limbs_out);
+      k_fixed_reduce<1024><<<B, 1024, 0, s>>>(partials, nl, res2_out, limbs_out, RewardArgs{});
       SPAI_CHECK_LAUNCH();
       return SPAI_OK;
     }
@@ -369,16 +352,18 @@ extern "C" int spai_fill_residual(int32_t fill_mode, int32_t n, int32_t line_beg
   double* partials = static_cast<double*>(workspace);
   SPAI_CHECK_HIP(v->fn(line_begin, line_end, W, WA, pat_idx, pat_act, pat_val, a_idx, a_val, B, removed, words,
                        word_base, m_out, partials, nparts, s));
-  k_fixed_reduce<kNT><<<B, kNT, 0, s>>>(partials, nparts, res2_out, limbs_out);
+  k_fixed_reduce<1024><<<B, 1024, 0, s>>>(partials, nparts, res2_out, limbs_out, RewardArgs{});
   SPAI_CHECK_LAUNCH();
   return SPAI_OK;
 }
 
 extern "C" int spai_rewards(const double* res2, const int32_t* removed_counts, int32_t B, int64_t nnz0, int32_t n,
-                            double r0, double f0, const float* alpha, double* residual, double* reward, void* stream) {
+                            double r0, double f0, const float* alpha, double* residual, double* reward, float* reward32,
+                            void* stream) {
   SPAI_CHECK_ARG(res2 && removed_counts && alpha && residual && reward && B >= 1 && n >= 1 && nnz0 >= 0,
                  "spai_rewards: bad arguments");
-  k_rewards<<<1, 256, 0, (hipStream_t)stream>>>(res2, removed_counts, B, nnz0, n, r0, f0, alpha, residual, reward);
+  const RewardArgs ra{removed_counts, nnz0, n, r0, f0, alpha, residual, reward, reward32};
+  k_rewards<<<1, 256, 0, (hipStream_t)stream>>>(res2, B, ra);
   SPAI_CHECK_LAUNCH();
   return SPAI_OK;
 }

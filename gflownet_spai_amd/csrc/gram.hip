@@ -541,8 +541,24 @@ extern "C" int spai_fill_reduce(int32_t n_lines, int32_t B, const void* workspac
     if (limbs_out) SPAI_CHECK_HIP(hipMemsetAsync(limbs_out, 0, sizeof(int64_t) * kLimbSlots * B, s));
     return SPAI_OK;
   }
-  k_fixed_reduce<kNT><<<B, kNT, 0, s>>>(static_cast<const double*>(workspace), (n_lines + kNT - 1) / kNT, res2_out,
-                                        limbs_out);
+  k_fixed_reduce<1024><<<B, 1024, 0, s>>>(static_cast<const double*>(workspace), (n_lines + kNT - 1) / kNT, res2_out,
+                                          limbs_out, RewardArgs{});
+  SPAI_CHECK_LAUNCH();
+  return SPAI_OK;
+}
+
+// One GPU: the fill's partial sums ARE the whole residuals, so the reward formula is applied in
+// the same launch (replaces spai_fill_reduce + spai_rewards + the fp32 copy of the rewards).
+extern "C" int spai_fill_reduce_rewards(int32_t n_lines, int32_t B, const void* workspace,
+                                        const int32_t* removed_counts, int64_t nnz0, int32_t n, double r0, double f0,
+                                        const float* alpha, double* residual, double* reward, float* reward32,
+                                        void* stream) {
+  SPAI_CHECK_ARG(n_lines >= 1 && B >= 1 && workspace && removed_counts && alpha && residual && reward && n >= 1 &&
+                     nnz0 >= 0,
+                 "spai_fill_reduce_rewards: bad arguments");
+  const RewardArgs ra{removed_counts, nnz0, n, r0, f0, alpha, residual, reward, reward32};
+  k_fixed_reduce<1024><<<B, 1024, 0, (hipStream_t)stream>>>(static_cast<const double*>(workspace),
+                                                            (n_lines + kNT - 1) / kNT, nullptr, nullptr, ra);
   SPAI_CHECK_LAUNCH();
   return SPAI_OK;
 }

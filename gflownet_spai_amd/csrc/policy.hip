@@ -352,14 +352,47 @@ __global__ __launch_bounds__(kRedNT) void k_pool(int32_t n, int32_t nblk, const 
 
 constexpr int kFcPer = 4;  // actions per thread of k_fc (strided by kNT inside a block)
 
-template <int C>
+// The pooled embedding of the constant-row closed form (k_const_pool's arithmetic, same fmaf
+// order): h1 = relu(W_l1 x0 + b_l1 + bias1), h = relu(W_l2 h1 + b_l2 + bias2).  Uniform loads
+// (scalar unit); k_fc evaluates it in every thread instead of a separate one-block launch.
+template <int F, int C>
+__device__ __forceinline__ void const_pool(const float* __restrict__ x0, const float* __restrict__ p1,
+                                           const float* __restrict__ p2, float (&hv)[C]) {
+  constexpr int HC = kH1 * C;
+  const float* bl = p1 + HC * F;
+  const float* bias1 = p1 + 2 * HC * F + 5 * HC - HC;
+  float h1[HC];
+#pragma unroll
+  for (int k = 0; k < HC; ++k) {
+    float v = bl[k];
+#pragma unroll
+    for (int f = 0; f < F; ++f) v = fmaf(p1[k * F + f], x0[f], v);
+    h1[k] = fmaxf(v + bias1[k], 0.0f);
+  }
+  const float* bl2 = p2 + C * HC;
+  const float* bias2 = p2 + 2 * C * HC + 5 * C - C;
+#pragma unroll
+  for (int o = 0; o < C; ++o) {
+    float v = 0.0f;
+#pragma unroll
+    for (int k = 0; k < HC; ++k) v = fmaf(p2[o * HC + k], h1[k], v);
+    hv[o] = fmaxf((v + bl2[o]) + bias2[o], 0.0f);
+  }
+}
+
+template <int F, int C, bool kConst>
 __global__ __launch_bounds__(kNT) void k_fc(int32_t na, const float* __restrict__ W, const float* __restrict__ b,
-                                            const float* __restrict__ hpool, float* __restrict__ logits,
-                                            float* __restrict__ pmax) {
+                                            const float* __restrict__ hpool, const float* __restrict__ x0,
+                                            const float* __restrict__ p1, const float* __restrict__ p2,
+                                            float* __restrict__ logits, float* __restrict__ pmax) {
   typedef float f4v __attribute__((ext_vector_type(4)));
   float hv[C];
+  if constexpr (kConst) {
+    const_pool<F, C>(x0, p1, p2, hv);
+  } else {
 #pragma unroll
-  for (int c = 0; c < C; ++c) hv[c] = hpool[c];
+    for (int c = 0; c < C; ++c) hv[c] = hpool[c];
+  }
   float l = -INFINITY;
   f4v q[kFcPer][C / 4];
   float bv[kFcPer];
@@ -435,31 +468,6 @@ __global__ __launch_bounds__(kNT) void k_rows_const(int32_t n, int32_t F, const 
   if (__any(!same) && (threadIdx.x & 63) == 0) *flag = 0;
 }
 
-template <int F, int C>
-__global__ __launch_bounds__(64) void k_const_pool(const float* __restrict__ x0, const float* __restrict__ p1,
-                                                   const float* __restrict__ p2, float* __restrict__ hpool) {
-  constexpr int HC = kH1 * C;
-  __shared__ float h1[HC];
-  const float* Wl = p1;
-  const float* bl = Wl + HC * F;
-  const float* bias1 = p1 + 2 * HC * F + 5 * HC - HC;
-  for (int k = threadIdx.x; k < HC; k += 64) {
-    float v = bl[k];
-#pragma unroll
-    for (int f = 0; f < F; ++f) v = fmaf(Wl[k * F + f], x0[f], v);
-    h1[k] = fmaxf(v + bias1[k], 0.0f);
-  }
-  __syncthreads();
-  const float* Wl2 = p2;
-  const float* bl2 = Wl2 + C * HC;
-  const float* bias2 = p2 + 2 * C * HC + 5 * C - C;
-  for (int o = threadIdx.x; o < C; o += 64) {
-    float v = 0.0f;
-    for (int k = 0; k < HC; ++k) v = fmaf(Wl2[o * HC + k], h1[k], v);
-    hpool[o] = fmaxf((v + bl2[o]) + bias2[o], 0.0f);
-  }
-}
-
 struct PolicyWs {
   float* xlr2;
   double* part;
@@ -486,14 +494,14 @@ void launch_policy(int32_t n, const float* x, const int32_t* rp, const int32_t* 
   constexpr int HPT = C <= 8 ? kH1 : 1;
   const int64_t t1 = (int64_t)n * (kH1 / HPT);
   const int g2 = (n + kNT - 1) / kNT, gf = fc_blocks(na);
-  if (const_rows) {
-    k_const_pool<F, C><<<1, 64, 0, s>>>(x, p1, p2, w.hpool);
+  if (const_rows) {  // the pooled embedding is computed inside k_fc (const_pool)
+    k_fc<F, C, true><<<gf, kNT, 0, s>>>(na, fw, fb, w.hpool, x, p1, p2, logits, w.pmax);
   } else {
     k_gat1<F, C, HPT><<<(int)((t1 + kNT - 1) / kNT), kNT, 0, s>>>(n, x, rp, src, ea, p1, p2, w.xlr2);
     k_gat2<C><<<g2, kNT, 0, s>>>(n, rp, src, ea, p2, w.xlr2, w.part);
     k_pool<C><<<1, kRedNT, 0, s>>>(n, g2, w.part, w.hpool);
+    k_fc<F, C, false><<<gf, kNT, 0, s>>>(na, fw, fb, w.hpool, x, p1, p2, logits, w.pmax);
   }
-  k_fc<C><<<gf, kNT, 0, s>>>(na, fw, fb, w.hpool, logits, w.pmax);
   k_max<<<1, kRedNT, 0, s>>>(gf, w.pmax, lmax, B);
 }
 

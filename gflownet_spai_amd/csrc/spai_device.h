@@ -210,29 +210,27 @@ __device__ __forceinline__ T block_sum(T v, T* lds /* NT/64 */) {
 // shards of a multi-GPU job: one all_reduce of the slots), gives the same bits.
 constexpr int kLimbSlots = 8;  // 6 limbs + flags + 1 pad (64 bytes per sample)
 __device__ __forceinline__ void fixed_add(double x, int64_t (&L)[kLimbSlots]) {
+  // branch-free (selects only): keeps L in registers
   const uint64_t u = (uint64_t)__double_as_longlong(x);
   const int ex = (int)((u >> 52) & 0x7ff);
-  if (ex == 0x7ff) {
-    L[6] += (u & ((1ull << 52) - 1)) ? (1ll << 32) : 1ll;
-    return;
-  }
-  if (ex >= 1023 + 94) {
-    L[6] += 1;
-    return;
-  }
-  const uint64_t m = (u & ((1ull << 52) - 1)) | (ex ? (1ull << 52) : 0ull);
+  const uint64_t frac = u & ((1ull << 52) - 1);
+  const bool nan = ex == 0x7ff && frac != 0;
+  const bool over = !nan && ex >= 1023 + 94;  // inf or |x| >= 2^94
+  const uint64_t m = (nan || over) ? 0ull : (frac | (ex ? (1ull << 52) : 0ull));
   const int shift = (ex ? ex : 1) - 1075 + 96;  // x = m * 2^(shift - 96)
   const bool neg = (u >> 63) != 0;
 #pragma unroll
   for (int i = 0; i < 6; ++i) {
     const int k = 32 * i - shift;  // limb i holds bits [k, k + 32) of m
-    uint64_t c;
-    if (k >= 0) c = k < 64 ? (m >> k) & 0xffffffffull : 0ull;
-    else c = -k < 32 ? (m << -k) & 0xffffffffull : 0ull;
+    const uint64_t hi = (m >> min(max(k, 0), 63)) & 0xffffffffull;
+    const uint64_t lo = (m << min(max(-k, 0), 63)) & 0xffffffffull;
+    const uint64_t c = k >= 0 ? (k < 64 ? hi : 0ull) : (-k < 32 ? lo : 0ull);
     L[i] += neg ? -(int64_t)c : (int64_t)c;
   }
+  L[6] += nan ? (1ll << 32) : (over ? 1ll : 0ll);
 }
-__device__ __forceinline__ double fixed_value(const int64_t* L) {
+template <typename LA>
+__device__ __forceinline__ double fixed_value(const LA& L) {
   const int64_t fl = L[6];
   if (fl >> 32) return __longlong_as_double(0x7ff8000000000000ll);  // NaN
   if (fl) return __longlong_as_double(0x7ff0000000000000ll);        // +inf
@@ -250,23 +248,78 @@ __device__ __forceinline__ double fixed_value(const int64_t* L) {
   for (int i = 4; i >= 0; --i) v = fma(v, 4294967296.0, (double)c[i]);
   return v * 0x1p-96;
 }
+// Reward of preconditioner.py:55-66 + 137-165 with the reference's torch type promotion
+// reproduced op for op: alpha is fp32, the residual ratio fp64, the flop ratio a python float,
+// (1 - alpha) * (1 - flop_ratio) an fp32 product and the sum fp64.  Contraction is disabled so
+// every op rounds as torch's separate kernels do.
+struct RewardArgs {
+  const int32_t* counts;  // removed per sample (nnz(M) = nnz0 - counts[b])
+  int64_t nnz0;
+  int32_t n;
+  double r0, f0;
+  const float* alpha;     // device fp32 scalar
+  double* residual;       // [B] sqrt(res2)
+  double* reward;         // [B] fp64
+  float* reward32;        // [B] fp32 copy (Log.rewards' dtype, gflownet.py:193) or null
+};
+__device__ __forceinline__ void write_reward(int b, double res2, const RewardArgs& ra) {
+#pragma clang fp contract(off)
+  const double r = sqrt(res2);
+  ra.residual[b] = r;
+  const double rr = ra.r0 != 0.0 ? r / ra.r0 : INFINITY;
+  const double flops = (double)(ra.nnz0 - ra.counts[b]) * 2.0 * (double)ra.n;
+  const double cr = ra.f0 != 0.0 ? flops / ra.f0 : INFINITY;
+  const float a = *ra.alpha;
+  const double t1 = (double)a * (1.0 - rr);
+  const float t2 = (1.0f - a) * (float)(1.0 - cr);
+  const double rw = (t1 + (double)t2) * 1000.0;
+  ra.reward[b] = rw;
+  if (ra.reward32) ra.reward32[b] = (float)rw;
+}
+
 // res2_out[b] and/or limbs_out[b][kLimbSlots] from per-block fp64 partials [B][nparts], one block
-// per sample (the fill kernels' second half).
+// per sample (the fill kernels' second half).  Every load of a round is issued before the
+// conversions (a dependent load per partial made this a 16 us latency chain at C4).
 template <int NT>
 __global__ __launch_bounds__(NT) void k_fixed_reduce(const double* __restrict__ partials, int32_t nparts,
-                                                     double* __restrict__ res2_out, int64_t* __restrict__ limbs_out) {
-  __shared__ int64_t sred[NT / 64];
-  const int b = blockIdx.x;
+                                                     double* __restrict__ res2_out, int64_t* __restrict__ limbs_out,
+                                                     RewardArgs ra) {
+  constexpr int kPer = 4;
+  __shared__ int64_t sred[NT / 64][kLimbSlots];
+  const int b = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const double* p = partials + (int64_t)b * nparts;
   int64_t L[kLimbSlots] = {0, 0, 0, 0, 0, 0, 0, 0};
-  for (int i = threadIdx.x; i < nparts; i += NT) fixed_add(partials[(int64_t)b * nparts + i], L);
+#pragma unroll 1
+  for (int i0 = 0; i0 < nparts; i0 += kPer * NT) {
+    double v[kPer];
 #pragma unroll
-  for (int q = 0; q < 7; ++q) L[q] = block_sum<NT>(L[q], sred);
+    for (int j = 0; j < kPer; ++j) {
+      const int i = i0 + j * NT + (int)threadIdx.x;
+      v[j] = i < nparts ? p[i] : 0.0;
+    }
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) fixed_add(v[j], L);
+  }
+#pragma unroll
+  for (int q = 0; q < 7; ++q) L[q] = wave_sum(L[q]);
+  if (lane == 0) {
+#pragma unroll
+    for (int q = 0; q < 7; ++q) sred[wave][q] = L[q];
+  }
+  __syncthreads();
   if (threadIdx.x == 0) {
+    int64_t T[kLimbSlots] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int w = 0; w < NT / 64; ++w)
+#pragma unroll
+      for (int q = 0; q < 7; ++q) T[q] += sred[w][q];
     if (limbs_out) {
 #pragma unroll
-      for (int q = 0; q < kLimbSlots; ++q) limbs_out[(int64_t)b * kLimbSlots + q] = L[q];
+      for (int q = 0; q < kLimbSlots; ++q) limbs_out[(int64_t)b * kLimbSlots + q] = T[q];
     }
-    if (res2_out) res2_out[b] = fixed_value(L);
+    const double r2 = fixed_value(T);
+    if (res2_out) res2_out[b] = r2;
+    if (ra.reward) write_reward(b, r2, ra);  // fused reward (one GPU: the sums are complete here)
   }
 }
 

@@ -30,7 +30,8 @@
 //                gathered into registers while the current bucket is ranked in value-linear
 //                LDS sub-buckets; fp64 in-bucket suffix sums and
 //                fwd_probs = w / (W_rest + later buckets + in-bucket suffix).  Outputs stored
-//                during the next bucket.  Buckets above the LDS capacity: k_sort2_big.
+//                during the next bucket.  Buckets above the LDS capacity: an exact radix in
+//                global memory by the block that meets them (big_bucket; rare).
 //   k_pad        terminal step, -1 / 1.0 padding up to T = max_b k_b + 1.
 // The step probability is formed from the mass still available at step t (untouched
 // actions + trajectory suffix), so no "Z - prefix" cancellation occurs.  Every sum is taken
@@ -67,6 +68,7 @@ constexpr int kTarget = 4096;              // winners per bucket (target)
 constexpr int kMaxB = 2048;                // buckets per sample (11 bits in the LDS record)
 constexpr int kCap2 = 8192;               // LDS capacity of k_sort2 (records per bucket)
 constexpr int kMaxSub = 4096;              // value sub-buckets per bucket in k_sort2
+constexpr int kBigWords = 256;             // k_sort2: buckets per block tracked for the oversized pass (x32)
 constexpr int kSortNT = 1024;
 constexpr int kMaxTiles = 2048;            // E <= kMaxTiles * kTile actions
 constexpr int kFinNT = 256;
@@ -81,10 +83,9 @@ constexpr int kBins = 4096;                // splitter histogram / bucket lookup
 struct TrajWs {
   int32_t ntiles, M;
   int32_t* ctl;           // zeroed per rollout: bigcnt | tdev | lastbig | pad
-  int32_t* bigcnt;        // number of oversized buckets (k_sort2 -> k_sort2_big); back to 0 after each sort
+  int32_t* bigcnt;        // number of oversized buckets k_sort2 met (k_pad moves it to lastbig, then 0)
   int32_t* tdev;
   int32_t* lastbig;       // bigcnt of the last sort (kept for tests / diagnostics)
-  int32_t* biglist;       // [B][kMaxB] their flattened (sample, bucket) indices
   double* xch;            // exchange array: [B][2][kMaxB] bucket weight sums | winner counts, then
                           // [B][8] caller slots (the residual limbs); a part fills its own buckets
   int32_t* samp_cnt;      // [B][M / kSampNT] winners per presample block
@@ -120,7 +121,6 @@ static void traj_ws(void* base, int32_t E, int32_t B, TrajWs* w) {
   w->bigcnt = w->ctl;
   w->tdev = w->ctl + 1;
   w->lastbig = w->ctl + 2;
-  w->biglist = c.take<int32_t>((size_t)B * kMaxB);
   w->xch = c.take<double>(xch_doubles(B));
   w->samp_cnt = c.take<int32_t>((size_t)B * nsb);
   w->samp = c.take<uint32_t>((size_t)B * M);
@@ -1125,7 +1125,7 @@ __device__ __forceinline__ void big_bucket(const int n, const int ntiles, const 
 // probabilities fwd = w / (W_rest + later buckets + in-bucket suffix) and coalesced stores.
 // The next bucket's run
 // table is prefetched while the current one is processed (LDS-only barriers keep it in
-// flight).  Oversized buckets are left to k_sort2_big.
+// flight).  Oversized buckets are sorted in global memory by the block that meets them.
 __global__ __launch_bounds__(kSortNT) void k_sort2(int32_t E, int32_t B, int32_t ntiles,
                                                    const int32_t* __restrict__ nb_,
                                                    const int32_t* __restrict__ bstart,
@@ -1134,16 +1134,21 @@ __global__ __launch_bounds__(kSortNT) void k_sort2(int32_t E, int32_t B, int32_t
                                                    int64_t t_cap, int64_t* __restrict__ actions,
                                                    float* __restrict__ fwd, const double* __restrict__ wrest,
                                                    const double* __restrict__ bwsuf, int32_t* __restrict__ bigcnt,
-                                                   int32_t* __restrict__ biglist, int32_t part, int32_t nparts) {
-  __shared__ uint64_t A[kCap2];  // low half: gather map; high half: actions awaiting store
+                                                   const float* __restrict__ ww, int64_t wrow_stride,
+                                                   uint64_t* __restrict__ scratch, int32_t part, int32_t nparts) {
+  __shared__ uint64_t A[kCap2];  // the bucket's records (ranked in place); high half: actions awaiting store
   __shared__ __attribute__((aligned(16))) float L[kCap2];  // weights in trajectory order
   __shared__ __attribute__((aligned(16))) float S[kCap2];  // step probabilities awaiting store
   __shared__ __attribute__((aligned(16))) int s_sub[kMaxSub + 4];
   __shared__ int s_nbp[kMaxSamples + 1];
   __shared__ int s_wc[kSortNT / 64];
   __shared__ double s_wd[kSortNT / 64];
-  __shared__ uint32_t s_red[2 * (kSortNT / 64)];
+  __shared__ uint32_t s_red[4 * (kSortNT / 64)];
+  __shared__ uint32_t s_bigm[kBigWords];  // bit j: this block's j-th bucket is oversized (sorted after the loop)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  __shared__ int s_anybig;
+  for (int i = tid; i < kBigWords; i += kSortNT) s_bigm[i] = 0u;
+  if (tid == 0) s_anybig = 0;
   {  // prefix of the part's bucket counts over the samples (parallel loads)
     const int nbb = tid < B ? nb_[tid] : 0;
     const int v = part_lo(nbb, part + 1, nparts) - part_lo(nbb, part, nparts);
@@ -1281,8 +1286,10 @@ __global__ __launch_bounds__(kSortNT) void k_sort2(int32_t E, int32_t B, int32_t
   issue(2);
   issue(4);
   issue(6);
+  int it = -1;  // this block's iteration (bit of s_bigm)
 #pragma unroll 1
   for (int f = blockIdx.x; f < total; f += gridDim.x) {
+    ++it;
     // this bucket's records and the next bucket's run table have landed (and the previous
     // bucket's stores drained)
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
@@ -1305,7 +1312,11 @@ __global__ __launch_bounds__(kSortNT) void k_sort2(int32_t E, int32_t B, int32_t
       issue(2);
       issue(4);
       issue(6);
-      if (n > kCap2 && tid == 0) biglist[atomicAdd(bigcnt, 1)] = (b << 16) | k;  // for k_sort2_big (rare)
+      if (n > kCap2 && tid == 0) {  // oversized (the sampled splitters missed; rare): sorted after the loop
+        s_bigm[it >> 5] |= 1u << (it & 31);
+        s_anybig = 1;
+        atomicAdd(bigcnt, 1);  // diagnostic count (spai_rollout_ws_offset field 0)
+      }
       continue;
     }
     uint32_t mn = 0xFFFFFFFFu, mx = 0u;
@@ -1438,57 +1449,47 @@ __global__ __launch_bounds__(kSortNT) void k_sort2(int32_t E, int32_t B, int32_t
   }
   flush();
   PROF_END(0)
-}
-
-// Buckets above the LDS capacity (rare): one block each, exact radix in global memory.
-__global__ __launch_bounds__(kSortNT) void k_sort2_big(int32_t E, int32_t B, int32_t ntiles,
-                                                       const int32_t* __restrict__ nb_,
-                                                       const int32_t* __restrict__ bstart,
-                                                       const uint32_t* __restrict__ runs,
-                                                       const uint32_t* __restrict__ staging,
-                                                       const float* __restrict__ ww, int64_t wrow_stride,
-                                                       int64_t t_cap,
-                                                       int64_t* __restrict__ actions, float* __restrict__ fwd,
-                                                       const double* __restrict__ wrest,
-                                                       const double* __restrict__ bwsuf, uint64_t* __restrict__ scratch,
-                                                       const int32_t* __restrict__ bigcnt,
-                                                       const int32_t* __restrict__ biglist) {
-  __shared__ int s_pre[kMaxTiles + 1];
-  __shared__ int s_loc[kMaxTiles];
-  __shared__ int s_wc[kSortNT / 64];
-  __shared__ double s_wd[kSortNT / 64];
-  __shared__ uint32_t s_red[4 * (kSortNT / 64)];
-  const int tid = threadIdx.x;
-  const int nbig = *bigcnt;  // oversized buckets k_sort2 skipped (usually none: the whole grid exits here)
-  if (nbig == 0) return;
+  // the oversized buckets this block met: exact radix in global memory (rare; the loop's
+  // registers are dead here, so this path costs the main loop nothing)
+  __syncthreads();
+  if (!s_anybig) return;  // the usual case: no oversized bucket met
 #pragma unroll 1
-  for (int q = blockIdx.x; q < nbig; q += gridDim.x) {
-    const int f = biglist[q];
-    const int b = f >> 16, k = f & 0xFFFF;
-    const int32_t* bs = bstart + (int64_t)b * (kMaxB + 1);
-    const int s = bs[k], n = bs[k + 1] - s;
-    if (n <= kCap2) continue;
-    const uint32_t* rr = runs + ((int64_t)b * kMaxB + k) * ntiles;  // [b][bucket][tile]
-    const int t0 = 2 * tid, t1 = 2 * tid + 1;
-    const uint32_t r0 = t0 < ntiles ? rr[t0] : 0u, r1 = t1 < ntiles ? rr[t1] : 0u;
-    const int c0 = (int)(r0 & 0xFFFFu);
-    int tot;
-    const int ex = block_excl_scan<kSortNT>(c0 + (int)(r1 & 0xFFFFu), s_wc, &tot);
-    if (t0 < ntiles) {
-      s_pre[t0] = ex;
-      s_loc[t0] = (int)(r0 >> 16);
+  for (int wd = 0; wd <= (it >> 5); ++wd) {
+    uint32_t m = s_bigm[wd];
+#pragma unroll 1
+    while (m) {
+      const int j = wd * 32 + __ffs((int)m) - 1;
+      m &= m - 1u;
+      const int f = blockIdx.x + j * gridDim.x;
+      int bb = 0;
+      while (s_nbp[bb + 1] <= f) ++bb;
+      const int kk = f - s_nbp[bb] + part_lo(nb_[bb], part, nparts);
+      const int32_t* bs = bstart + (int64_t)bb * (kMaxB + 1);
+      const int s0 = bs[kk], n = bs[kk + 1] - s0;
+      const double later = wrest[bb] + bwsuf[(int64_t)bb * kMaxB + kk];
+      int* s_pre = reinterpret_cast<int*>(L);
+      int* s_loc = s_pre + (kMaxTiles + 1);
+      const uint32_t* rr = runs + ((int64_t)bb * kMaxB + kk) * ntiles;  // [b][bucket][tile]
+      const uint32_t q0 = t0 < ntiles ? rr[t0] : 0u, q1 = t1 < ntiles ? rr[t1] : 0u;
+      const int c0 = (int)(q0 & 0xFFFFu);
+      int tot;
+      const int ex = block_excl_scan<kSortNT>(c0 + (int)(q1 & 0xFFFFu), s_wc, &tot);
+      if (t0 < ntiles) {
+        s_pre[t0] = ex;
+        s_loc[t0] = (int)(q0 >> 16);
+      }
+      if (t1 < ntiles) {
+        s_pre[t1] = ex + c0;
+        s_loc[t1] = (int)(q1 >> 16);
+      }
+      if (tid == 0) s_pre[ntiles] = tot;
+      __syncthreads();
+      int64_t* act_out = actions + (int64_t)bb * t_cap + s0;
+      big_bucket(n, ntiles, s_pre, s_loc, staging + (int64_t)bb * ntiles * kTile * 3, ww + (int64_t)bb * wrow_stride,
+                 act_out, fwd + (int64_t)bb * t_cap + s0, scratch + (int64_t)bb * E + s0,
+                 reinterpret_cast<uint64_t*>(act_out), later, s_wc, s_wd, s_red);
+      __syncthreads();
     }
-    if (t1 < ntiles) {
-      s_pre[t1] = ex + c0;
-      s_loc[t1] = (int)(r1 >> 16);
-    }
-    if (tid == 0) s_pre[ntiles] = tot;
-    __syncthreads();
-    int64_t* act_out = actions + (int64_t)b * t_cap + s;
-    big_bucket(n, ntiles, s_pre, s_loc, staging + (int64_t)b * ntiles * kTile * 3, ww + (int64_t)b * wrow_stride,
-               act_out, fwd + (int64_t)b * t_cap + s, scratch + (int64_t)b * E + s, reinterpret_cast<uint64_t*>(act_out),
-               wrest[b] + bwsuf[(int64_t)b * kMaxB + k], s_wc, s_wd, s_red);
-    __syncthreads();
   }
 }
 
@@ -1504,8 +1505,8 @@ __global__ __launch_bounds__(kFinNT) void k_pad(int32_t E, const int32_t* __rest
   const int k = counts[b], T = *tdev;
   if (b == 0 && blockIdx.x == 0 && threadIdx.x == 0) {
     if (t_out) *t_out = T;
-    // retire the oversized-bucket list of this sort (k_sort2_big, its only reader, ran before
-    // this launch on the same stream): a second sort on the same select starts from 0
+    // retire the oversized-bucket count of this sort (k_sort2, its only writer, ran before this
+    // launch on the same stream): a second sort on the same select starts from 0
     *lastbig = *bigcnt;
     *bigcnt = 0;
   }
@@ -1567,7 +1568,7 @@ extern "C" size_t spai_rollout_workspace_bytes(int32_t E, int32_t B) {
 
 // Byte offset of a diagnostic / exchange array inside the rollout workspace (tests and the
 // multi-part exchange address it in the caller-owned buffer instead of hard-coding the carve):
-//   0 = int32 oversized buckets of the last sort (k_sort2 -> k_sort2_big)
+//   0 = int32 oversized buckets of the last sort (sorted in global memory by k_sort2)
 //   1 = int32 T of the last rollout
 //   2 = fp64 exchange array: [B][2][kMaxB] bucket weight sums | bucket winner counts (a part
 //       fills its own buckets, the rest are 0 — so the int64 bit patterns of the parts' arrays
@@ -1686,13 +1687,12 @@ extern "C" int spai_rollout_sort(const float* logits, int64_t bstride, int32_t E
   if (st != SPAI_OK) return st;
   hipStream_t s = (hipStream_t)stream;
   const int nbm = max_buckets(E);
-  const int g2 = std::max(1, std::min((nbm + nparts - 1) / nparts * B, num_cus()));
+  const int nbt = (nbm + nparts - 1) / nparts * B;  // buckets of the part over the samples (upper bound)
+  // persistent blocks, enough that none walks more than the 32 * kBigWords its oversized mask tracks
+  const int g2 = std::max(std::max(1, std::min(nbt, num_cus())), (nbt + 32 * kBigWords - 1) / (32 * kBigWords));
   const int64_t wrs = bstride ? w.wstride : 0;
   k_sort2<<<g2, kSortNT, 0, s>>>(E, B, w.ntiles, w.nb, w.bstart, w.runs, w.staging, t_cap, actions, fwd_probs,
-                                 w.wrest, w.bwsuf, w.bigcnt, w.biglist, part, nparts);
-  SPAI_CHECK_LAUNCH();
-  k_sort2_big<<<g2, kSortNT, 0, s>>>(E, B, w.ntiles, w.nb, w.bstart, w.runs, w.staging, w.ww, wrs, t_cap, actions,
-                                     fwd_probs, w.wrest, w.bwsuf, w.scratch, w.bigcnt, w.biglist);
+                                 w.wrest, w.bwsuf, w.bigcnt, w.ww, wrs, w.scratch, part, nparts);
   SPAI_CHECK_LAUNCH();
   return SPAI_OK;
 }

@@ -185,10 +185,10 @@ class GFlowNet(nn.Module):
         logits, alpha, lg, lmax, z = self._logits(s0, need_z=True)
         actions_bt, fwd_bt = self._parity_rollout(lg, B, lmax, z)
         removed, counts = kernels.actions_to_removed(actions_bt, E)
-        rewards = self._rewards(removed, counts, alpha)
+        self._rewards(removed, counts, alpha)
         log._set_rollout(logits, actions_bt, fwd_bt, lmax=lmax)
         log.removed, log.counts = removed, counts
-        log.rewards = rewards.detach().to(torch.float32)
+        log.rewards = env.last_reward32
         return log if return_log else None
 
     def _logits(self, s0, need_z: bool = False):
@@ -257,10 +257,12 @@ class GFlowNet(nn.Module):
         rank, world, group = self.shard if self.shard is not None else (0, 1, None)
         removed, counts, ws = kernels.rollout_select(lg, B, lmax, self.seed, 0, self.sample_base, self._counter(lg.device),
                                                      rank, world)
-        lines = self.lines if self.shard is not None else (0, None)
-        res2 = env.fill_partial(removed, *lines, limbs=world > 1)  # a split sums exact limbs
         st.update(B=B, E=E, logits=logits, alpha=alpha, lg=lg, lmax=lmax, removed=removed, counts=counts, ws=ws,
-                  res2_part=res2, part=(rank, world, group))
+                  part=(rank, world, group))
+        if world == 1:  # all lines here: fill, exact sums and rewards (one launch after the fill)
+            st["rewards"] = env.fill_rewards(removed, counts, alpha)
+        else:  # a split sums exact limbs of its lines
+            st["res2_part"] = env.fill_partial(removed, *self.lines, limbs=True)
 
     def rollout_exchange(self, st: dict) -> None:
         """The slices split's ONE all_reduce, in place on the rollout workspace's exchange array:
@@ -269,7 +271,6 @@ class GFlowNet(nn.Module):
         Nothing on one GPU."""
         rank, world, group = st["part"]
         if world == 1:
-            st["res2"] = st["res2_part"]
             return
         from .distributed import exchange_parts
         limbs = exchange_parts(kernels.exchange_array(st["ws"], st["E"], st["B"]), st["res2_part"], group)
@@ -287,13 +288,13 @@ class GFlowNet(nn.Module):
             kernels.rollout_merge(lg, B, lmax, ws, rank, world, counts)
         actions, fwd = kernels.rollout_sort(lg, B, lmax, ws, rank, world)
         t_dev = kernels.rollout_finish(lg, B, lmax, counts, ws, actions, fwd, rank, world)
-        rewards = env.rewards_from_res2(st["res2"], counts, st["alpha"])
+        rewards = st["rewards"] if world == 1 else env.rewards_from_res2(st["res2"], counts, st["alpha"])
         log = Log(st["s0"], self.backward_policy, self.total_flow, env)
         log._set_rollout(st["logits"], actions, fwd, t_dev, lmax=lmax)
         if world > 1:
             log._set_part(rank, world, group, kernels.part_bounds(ws, E, B, rank, world))
         log.removed, log.counts = st["removed"], counts
-        log.rewards = rewards.detach().to(torch.float32)
+        log.rewards = env.last_reward32
         log.rewards_all = rewards
         st["log"] = log
 
@@ -357,7 +358,7 @@ class GFlowNet(nn.Module):
         log = Log(st["s0"], self.backward_policy, self.total_flow, env)
         log._set_rollout(st["logits"], actions, fwd, t_dev, lmax=st["lmax"])
         log.removed, log.counts = st["removed"], st["counts"]
-        log.rewards = rewards[rank * bl:(rank + 1) * bl].detach().to(torch.float32)
+        log.rewards = env.last_reward32[rank * bl:(rank + 1) * bl]
         log.rewards_all = rewards  # [P*bl] fp64, global sample order (the M lines of every one are here)
         st["log"] = log
 

@@ -345,15 +345,53 @@ def res2_from_limbs(limbs: torch.Tensor) -> torch.Tensor:
     return out
 
 
+def _reward_args(counts, alpha):
+    return counts.to(torch.int32).contiguous(), alpha.detach().to(device=counts.device, dtype=torch.float32).reshape(1)
+
+
 def rewards(res2: torch.Tensor, counts: torch.Tensor, nnz0: int, n: int, r0: float, f0: int, alpha: torch.Tensor):
-    """(residual [B] fp64, reward [B] fp64) with the reference's reward formula and type promotion."""
+    """(residual [B] fp64, reward [B] fp64, reward [B] fp32) with the reference's reward formula
+    and type promotion (spai_rewards)."""
     B = res2.numel()
-    a = alpha.detach().to(device=res2.device, dtype=torch.float32).reshape(1)
+    c, a = _reward_args(counts, alpha)
     residual = torch.empty(B, dtype=torch.float64, device=res2.device)
     reward = torch.empty(B, dtype=torch.float64, device=res2.device)
-    _lib.check(_l().spai_rewards(_lib.ptr(res2), _lib.ptr(counts), B, nnz0, n, float(r0), float(f0), _lib.ptr(a),
-                                 _lib.ptr(residual), _lib.ptr(reward), _lib.stream_ptr(res2.device)), "spai_rewards")
-    return residual, reward
+    reward32 = torch.empty(B, dtype=torch.float32, device=res2.device)
+    with _timed("rewards"):
+        st = _l().spai_rewards(_lib.ptr(res2), _lib.ptr(c), B, nnz0, n, float(r0), float(f0), _lib.ptr(a),
+                               _lib.ptr(residual), _lib.ptr(reward), _lib.ptr(reward32), _lib.stream_ptr(res2.device))
+    _lib.check(st, "spai_rewards")
+    return residual, reward, reward32
+
+
+def fill_rewards_gram(pattern: Lines, gram: torch.Tensor, removed: torch.Tensor, lsq: bool, counts: torch.Tensor,
+                      nnz0: int, r0: float, f0: int, alpha: torch.Tensor, store_m: bool = False,
+                      m_dtype=torch.float32):
+    """One GPU, all lines: the Gram-cached fill, then the exact residual sums and the rewards in
+    one launch (spai_fill_lines_gram + spai_fill_reduce_rewards).  Returns (residual, reward,
+    reward fp32, M or None)."""
+    _lib.require_device(removed)
+    removed = removed.contiguous()
+    B, words = removed.shape
+    n = pattern.n
+    mode = _lib.FILL_LSQ if lsq else _lib.FILL_COPY
+    if not lsq:
+        m_dtype = torch.float32
+    m = torch.empty(B, n, pattern.width, dtype=m_dtype, device=removed.device) if store_m else None
+    ws = _lib.workspace(_l().spai_fill_workspace_bytes(n, B), removed.device, "fill")
+    with _timed("fill_residual"):  # the fill kernel alone (the bench's roofline kernel)
+        st = _l().spai_fill_lines_gram(mode, n, 0, n, pattern.width, _lib.ptr(pattern.act), _lib.ptr(pattern.val),
+                                       _lib.ptr(gram), _DT[gram.dtype], B, _lib.ptr(removed), words, 0, _lib.ptr(m),
+                                       _DT[m_dtype], _lib.ptr(ws), ws.numel(), _lib.stream_ptr(removed.device))
+    _lib.check(st, "spai_fill_lines_gram")
+    c, a = _reward_args(counts, alpha)
+    residual = torch.empty(B, dtype=torch.float64, device=removed.device)
+    reward = torch.empty(B, dtype=torch.float64, device=removed.device)
+    reward32 = torch.empty(B, dtype=torch.float32, device=removed.device)
+    _lib.check(_l().spai_fill_reduce_rewards(n, B, _lib.ptr(ws), _lib.ptr(c), nnz0, n, float(r0), float(f0),
+                                             _lib.ptr(a), _lib.ptr(residual), _lib.ptr(reward), _lib.ptr(reward32),
+                                             _lib.stream_ptr(removed.device)), "spai_fill_reduce_rewards")
+    return residual, reward, reward32, m
 
 
 def logp_grad(logits: torch.Tensor, lmax: torch.Tensor, actions_bt: torch.Tensor, probs_bt: torch.Tensor,

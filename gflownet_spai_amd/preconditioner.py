@@ -78,6 +78,7 @@ class PreconditionerEnv(Env):
         ai = a.indices()
         self.a_lines: Lines = build_lines(ai[0], ai[1], a.values(), matrix_size, orient, self.device, a_dtype)
         self.last_m = None
+        self.last_reward32 = None  # fp32 rewards of the last batch (Log.rewards)
         self.last_removed = None  # removal bitmaps [B, ceil(E/32)] of the last batch (assemble)
         self._word_spans = {}     # world -> per-rank bitmap word spans of the column shards
         # Gram cache of the fixed pattern (G = A_J^T A_J, c = A[l, J] per line): the per-rollout
@@ -111,6 +112,8 @@ class PreconditionerEnv(Env):
         per-sample squared norms are summed exactly across the process group (one all_reduce of
         the integer limbs: the same bits as one process when the shards are 256-line aligned)."""
         if group is None:
+            if line_begin == 0 and (line_end is None or line_end == self.matrix_size):
+                return self.fill_rewards(removed, counts, alpha)
             return self.rewards_from_res2(self.fill_partial(removed, line_begin, line_end), counts, alpha)
         from .distributed import all_reduce_
         limbs = all_reduce_(self.fill_partial(removed, line_begin, line_end, limbs=True), group)
@@ -144,11 +147,28 @@ class PreconditionerEnv(Env):
         return self._word_spans[world]
 
     def rewards_from_res2(self, res2: Tensor, counts: Tensor, alpha) -> Tensor:
-        """Residuals (``last_residual``) and rewards [B] fp64 from the summed squared norms."""
+        """Residuals (``last_residual``) and rewards [B] fp64 from the summed squared norms (their
+        fp32 copy, Log.rewards' dtype, in ``last_reward32``)."""
         if not torch.is_tensor(alpha):
             alpha = torch.tensor(float(alpha), dtype=torch.float32)
-        self.last_residual, reward = kernels.rewards(res2, counts, self.init_nnz, self.matrix_size, self._r0,
-                                                     self.orig_flops, alpha)
+        self.last_residual, reward, self.last_reward32 = kernels.rewards(res2, counts, self.init_nnz,
+                                                                         self.matrix_size, self._r0, self.orig_flops,
+                                                                         alpha)
+        return reward
+
+    def fill_rewards(self, removed: Tensor, counts: Tensor, alpha) -> Tensor:
+        """fill_partial over ALL lines + rewards_from_res2 (one GPU): with the Gram cache the exact
+        residual sums and the reward formula run in one launch (spai_fill_reduce_rewards)."""
+        if self.gram is None:
+            return self.rewards_from_res2(self.fill_partial(removed), counts, alpha)
+        if not torch.is_tensor(alpha):
+            alpha = torch.tensor(float(alpha), dtype=torch.float32)
+        self.last_residual, reward, self.last_reward32, m = kernels.fill_rewards_gram(
+            self.pattern, self.gram, removed, self.fill == "lsq", counts, self.init_nnz, self._r0, self.orig_flops,
+            alpha, store_m=self.keep_m, m_dtype=self.a_lines.val.dtype)
+        if self.keep_m:
+            self.last_m = m
+        self.last_removed = removed
         return reward
 
     def _performance(self, residual: Tensor, nnz: Tensor, alpha) -> Tensor:

@@ -242,6 +242,11 @@ int spai_fill_lines_gram(int32_t fill_mode, int32_t n, int32_t line_begin, int32
                          void* workspace, size_t workspace_bytes, void* stream);
 int spai_fill_reduce(int32_t n_lines, int32_t B, const void* workspace, double* res2_out, int64_t* limbs_out,
                      void* stream);
+/* One GPU (the lines are all of M): spai_fill_reduce + spai_rewards in one launch, from the
+ * workspace spai_fill_lines_gram left (n_lines = all n lines); same outputs as spai_rewards. */
+int spai_fill_reduce_rewards(int32_t n_lines, int32_t B, const void* workspace, const int32_t* removed_counts,
+                             int64_t nnz0, int32_t n, double r0, double f0, const float* alpha, double* residual,
+                             double* reward, float* reward32, void* stream);
 
 /* ---------------------------------------------------------------- forward policy
  * logits[a] = fc(mean_pool(relu(GATv2_2(relu(GATv2_1(x))))))[a] for a < num_actions and
@@ -329,9 +334,11 @@ int spai_lstm_backward(int32_t B, int32_t H, const int64_t* traj, int64_t ldt, c
  * residual[b] = sqrt(res2[b]) and reward[b] = 1000 * (alpha (1 - r/r0) + (1 - alpha)(1 - f/f0))
  * with f = 2 n (nnz0 - removed_counts[b]) (preconditioner.py:55-66, 68-77, 137-165; alpha is
  * the device fp32 scalar the rollout passes, not the never-set self.alpha of :163).  The
- * fp32/fp64 mix of the reference's torch type promotion is reproduced op for op. */
+ * fp32/fp64 mix of the reference's torch type promotion is reproduced op for op.  reward32
+ * (may be NULL) receives the fp32 copy Log.rewards holds (gflownet.py:193). */
 int spai_rewards(const double* res2, const int32_t* removed_counts, int32_t B, int64_t nnz0, int32_t n,
-                 double r0, double f0, const float* alpha, double* residual, double* reward, void* stream);
+                 double r0, double f0, const float* alpha, double* residual, double* reward, float* reward32,
+                 void* stream);
 
 /* ---------------------------------------------------------------- Krylov evaluation
  * y = A x (fp64 x, y; fp32 or fp64 values) over row-ELL lines idx/val [n][W] (-1 = padding),

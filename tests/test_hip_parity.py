@@ -209,7 +209,7 @@ def test_throughput_rollout_clustered_keys_overflow_path():
 def test_throughput_rollout_tied_keys_oversized_bucket():
     """All 20,000 actions win with one and the same fp32 key (logit 1e30 swamps its Gumbel
     noise; the terminal's 9.9e29 loses to it) and fall into one bucket beyond k_sort2's
-    8192-record LDS capacity: k_sort2 lists it and k_sort2_big orders it (ties by action id,
+    8192-record LDS capacity: the k_sort2 block that meets it sorts it in global memory (ties by action id,
     as the oracle).  The terminal's own probability is 0/0 in both and is not compared."""
     from gflownet_spai_amd import kernels
     E, B = 20000, 2

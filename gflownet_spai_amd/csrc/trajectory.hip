@@ -614,11 +614,16 @@ void k_tile(const float* __restrict__ rr, const float* __restrict__ ww, int64_t 
   // splitter tables (consumed only after the times; their latency hides behind the Philox work)
   static_assert((kBins * 2 == 512 * 16 && kMaxB * 4 == 512 * 16 && kGrpNT % 512 == 0) || kGrpNT == 512,
                 "prologue vector widths");
-  for (int i = tid; i < 1024; i += kGrpNT) {
-    if (i < 512)
-      reinterpret_cast<uint4*>(s_lut)[i] = reinterpret_cast<const uint4*>(lut_ + (int64_t)b * kBins)[i];
+  // direct global -> LDS loads (no VGPR destination, nothing waits on them until the barrier
+  // after the times): 16 bytes per lane into a wave-contiguous 1 KB of the table
+  for (int i0 = 0; i0 < 1024; i0 += kGrpNT) {
+    const int i = i0 + tid, wb = i0 + (tid & ~63);  // wave base (uniform within the wave)
+    if (wb < 512)
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const uint4*>(lut_ + (int64_t)b * kBins) + i,
+                                       reinterpret_cast<uint4*>(s_lut) + wb, 16, 0, 0);
     else if ((i - 512) * 4 < nb - 1)
-      reinterpret_cast<uint4*>(s_spl)[i - 512] = reinterpret_cast<const uint4*>(spl_ + (int64_t)b * kMaxB)[i - 512];
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const uint4*>(spl_ + (int64_t)b * kMaxB) + (i - 512),
+                                       reinterpret_cast<uint4*>(s_spl) + (wb - 512), 16, 0, 0);
   }
   for (int k = tid; k < nb; k += kGrpNT) s_off[k] = 0;
   // per-bucket weight sums of the tile's winners as exact fixed point (integer LDS atomics: the

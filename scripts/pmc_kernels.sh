@@ -8,11 +8,12 @@ mkdir -p $OUT
 i=0
 for CTRS in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT" \
             "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SMEM GRBM_GUI_ACTIVE" \
-            "FETCH_SIZE" "WRITE_SIZE"; do
+            "FETCH_SIZE" "WRITE_SIZE" \
+            "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_VMEM SQ_INST_CYCLES_SALU SQ_THREAD_CYCLES_VALU"; do
   i=$((i+1))
   timeout -k 10 ${PMC_TIMEOUT:-200} rocprofv3 --kernel-trace --pmc $CTRS --output-format csv -d $OUT/p$i -o run -- "$@" > $OUT/p$i.log 2>&1
   rc=$?; echo "pass $i rc=$rc"
-  if [ $rc -ne 0 ]; then tail -5 $OUT/p$i.log; exit $rc; fi
+  if [ $rc -ne 0 ]; then tail -5 $OUT/p$i.log; [ $i -le 4 ] && exit $rc; fi
 done
 python - "$OUT" <<'PY'
 import csv, collections, glob, json, sys

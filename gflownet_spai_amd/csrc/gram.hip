@@ -258,10 +258,9 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(W <= 5 ? FI
 }
 
 // Wide lines (8 <= W <= 13, e.g. the 13-point 3-D star of config C3): the same stream and
-// outputs as k_gram_fill, but the factorisation runs in place on one packed copy of G per
-// sample (right-looking LDL^T, T = W(W+1)/2 doubles in registers, re-read from the Gram
-// cache for every sample: the block's Gram data stays in L2), one wave per SIMD.
-// Elimination order and masking are those of k_gram_fill: a removed slot k only gets
+// outputs as k_gram_fill, but the factorisation runs in place on one packed working copy of G
+// per sample (left-looking LDL^T, T = W(W+1)/2 doubles in registers), one wave per SIMD.
+// Masking and the per-pivot floor are those of k_gram_fill: a removed slot k only gets
 // 1/D_k := 0, so L[.][k] = 0 and m_k = 0.
 template <int W, typename TM, bool LSQ>
 __global__ __launch_bounds__(kNT) void k_gram_fill_wide(int32_t n, int32_t line_begin, int32_t line_end, int32_t wrt,
@@ -310,28 +309,40 @@ __global__ __launch_bounds__(kNT) void k_gram_fill_wide(int32_t n, int32_t line_
       }
     }
     double a[T], y[W];
+    // loop-invariant: the compiler keeps one copy of the line's Gram values in registers across
+    // the samples and factors a second, working copy per sample (463 VGPRs, one wave per SIMD,
+    // no spills).  Re-reading them per sample instead (an opaque address, 254 VGPRs, two waves
+    // per SIMD) measured 286 vs 183 us at C3: the L2 re-reads cost more than the occupancy buys.
+    const double* gps = gp;
 #pragma unroll
-    for (int q = 0; q < T; ++q) a[q] = gp[q * 64];
+    for (int q = 0; q < T; ++q) a[q] = gps[q * 64];
     double r2 = 1.0;
     if constexpr (LSQ) {
 #pragma unroll
-      for (int k = 0; k < W; ++k) y[k] = gp[(T + k) * 64];  // c, solved in place below
+      for (int k = 0; k < W; ++k) y[k] = gps[(T + k) * 64];  // c, solved in place below
+      // left-looking LDL^T in place (column k of the packed upper triangle at step k), so the
+      // pivot test reads the ORIGINAL G_kk: the per-pivot floor 1e-13 G_kk of k_gram_fill and
+      // fill.hip's k_line, with no extra registers.  Column k first becomes u_jk = G_jk -
+      // sum_{q<j} l_qj u_qk (j < k), then l_qk = u_qk / D_q; the diagonal slot ends as 1/D_k
+      // (0 for a removed or singular pivot: l_k. = 0 and m_k = 0, as in k_gram_fill).
 #pragma unroll
       for (int k = 0; k < W; ++k) {
-        const double d = a[gidx<W>(k, k)];
-        // per-pivot floor 1e-13 G_kk, as k_gram_fill and fill.hip's k_line (G_kk re-read from the
-        // cache line this sample just read: no W extra registers)
-        const double ik = (((keep >> k) & 1u) && d > 1e-13 * gp[gidx<W>(k, k) * 64]) ? fast_rcp(d) : 0.0;
-        a[gidx<W>(k, k)] = ik;  // the diagonal slot now holds 1/D_k
-        // rows i descending: row i's multiplier L_ik = EL_ik / D_k replaces EL_ik only after
-        // every update that still reads it (rows j <= i use EL_jk)
 #pragma unroll
-        for (int i = W - 1; i > k; --i) {
-          const double li = a[gidx<W>(k, i)] * ik;
+        for (int j = 1; j < k; ++j) {
+          double u = a[gidx<W>(j, k)];
 #pragma unroll
-          for (int jx = k + 1; jx <= i; ++jx) a[gidx<W>(jx, i)] -= li * a[gidx<W>(k, jx)];
-          a[gidx<W>(k, i)] = li;
+          for (int q = 0; q < j; ++q) u -= a[gidx<W>(q, j)] * a[gidx<W>(q, k)];
+          a[gidx<W>(j, k)] = u;
         }
+        const double gkk = a[gidx<W>(k, k)];
+        double d = gkk;
+#pragma unroll
+        for (int q = 0; q < k; ++q) {
+          const double l = a[gidx<W>(q, k)] * a[gidx<W>(q, q)];  // u_qk / D_q
+          d -= l * a[gidx<W>(q, k)];
+          a[gidx<W>(q, k)] = l;
+        }
+        a[gidx<W>(k, k)] = (((keep >> k) & 1u) && d > 1e-13 * gkk) ? fast_rcp(d) : 0.0;
       }
 #pragma unroll
       for (int k = 0; k < W; ++k) {  // forward substitution in place (y[q < k] are final)
@@ -355,7 +366,7 @@ __global__ __launch_bounds__(kNT) void k_gram_fill_wide(int32_t n, int32_t line_
         y[p] = ((keep >> p) & 1u) ? (double)pat_val[(int64_t)jj * wrt + (p < wrt ? p : 0)] : 0.0;
 #pragma unroll
       for (int p = 0; p < W; ++p) {
-        double acc = y[p] * a[gidx<W>(p, p)] - 2.0 * gp[(T + p) * 64];
+        double acc = y[p] * a[gidx<W>(p, p)] - 2.0 * gps[(T + p) * 64];
 #pragma unroll
         for (int q = p + 1; q < W; ++q) acc += 2.0 * y[q] * a[gidx<W>(p, q)];
         r2 += y[p] * acc;

@@ -51,21 +51,14 @@ static_assert(kTile <= 65535, "run offsets and counts are packed in 16 bits (k_t
 #define KGRPNT 512
 #endif
 constexpr int kGrpNT = KGRPNT;             // threads of a k_tile block (16 actions each)
-#ifndef KWIN
-#define KWIN 4096
-#endif
-constexpr int kWin = KWIN;                 // records per LDS output window of k_tile (2 blocks/CU)
-#ifdef KTILE_LISTWIN
-constexpr int kList = 2730;                // compacted winners per k_tile block (<= 1/3 of the tile; denser: slot path)
-#else
+constexpr int kWin = 2048;                 // records per LDS output window of k_tile's slot path
 constexpr int kList = 4000;                // compacted winners per k_tile block (<= 49 % of the tile; denser: slot path)
-#endif
 constexpr int kSampM = 65536;              // subset size (power of two, capped by E)
 constexpr int kSampNT = 256;
 constexpr int kSampCap = 32768;            // sampled winners behind the splitters
 constexpr int kMaxNsb = kSampM / kSampNT;  // presample blocks per sample (256)
 constexpr int kTarget = 4096;              // winners per bucket (target)
-constexpr int kMaxB = 2048;                // buckets per sample (11 bits in the LDS record)
+constexpr int kMaxB = 1024;                // buckets per sample (11 bits in the LDS record)
 constexpr int kCap2 = 8192;               // LDS capacity of k_sort2 (records per bucket)
 constexpr int kMaxSub = 4096;              // value sub-buckets per bucket in k_sort2
 constexpr int kBigWords = 256;             // k_sort2: buckets per block tracked for the oversized pass (x32)
@@ -575,22 +568,17 @@ void k_tile(const float* __restrict__ rr, const float* __restrict__ ww, int64_t 
             const uint32_t* __restrict__ lut_base, uint32_t* __restrict__ staging,
             uint32_t* __restrict__ runs, double* __restrict__ tbw, double* __restrict__ tile_wrest) {
   // LDS regions (two blocks per CU: <= 80 KB per block):
-  //   s_r0: the fixed-point bucket sums during the histogram, then the record window (slot
-  //         path: w_rec; compacted path: 12-byte records)
-  //   s_r1: the compacted winner list (keys, tile-local ids; slot path: the window's weights)
+  //   s_r0: the fixed-point bucket sums during the histogram, then the slot path's record window
+  //   s_r1: the compacted winner list: keys, weights, tile-local ids (slot path: the window's
+  //         weights)
   __shared__ __attribute__((aligned(16))) uint64_t s_r0[kWin];
-#ifdef KTILE_LISTWIN
-  __shared__ __attribute__((aligned(16))) uint32_t s_r1[kWin];
-  static_assert(kList * 3 <= kWin * 2 && kList * 6 <= kWin * 4 && kList % 2 == 0, "LDS region sizes");
-#else
-  __shared__ __attribute__((aligned(16))) uint32_t s_r1[kList + kList / 2];
-  static_assert(kWin <= kList + kList / 2 && kList % 2 == 0, "LDS region sizes");
-#endif
-  uint64_t* w_rec = s_r0;  // one window of the grouped output
+  __shared__ __attribute__((aligned(16))) uint32_t s_r1[2 * kList + kList / 2];
+  static_assert(kWin <= 2 * kList + kList / 2 && kList % 2 == 0, "LDS region sizes");
+  uint64_t* w_rec = s_r0;  // one window of the slot path's grouped output
   float* w_log = reinterpret_cast<float*>(s_r1);
   uint32_t* l_ord = s_r1;
-  uint16_t* l_id = reinterpret_cast<uint16_t*>(s_r1 + kList);
-  uint32_t* w_r3 = reinterpret_cast<uint32_t*>(s_r0);  // compacted path: {action, ~key, w} per record
+  float* l_w = reinterpret_cast<float*>(s_r1 + kList);  // the weight travels with the winner: no reload
+  uint16_t* l_id = reinterpret_cast<uint16_t*>(s_r1 + 2 * kList);
   __shared__ __attribute__((aligned(16))) uint32_t s_spl[kMaxB];
   __shared__ int s_off[kMaxB + 1];  // histogram, then tile-local bucket offsets
   __shared__ __attribute__((aligned(16))) uint16_t s_lut[kBins];
@@ -612,8 +600,7 @@ void k_tile(const float* __restrict__ rr, const float* __restrict__ ww, int64_t 
   // the bucket totals and the untouched mass cover every action in every part)
   const int k0 = part_lo(nb, part, nparts), k1 = part_lo(nb, part + 1, nparts);
   // splitter tables (consumed only after the times; their latency hides behind the Philox work)
-  static_assert((kBins * 2 == 512 * 16 && kMaxB * 4 == 512 * 16 && kGrpNT % 512 == 0) || kGrpNT == 512,
-                "prologue vector widths");
+  static_assert(kBins * 2 == 512 * 16 && kMaxB * 4 <= 512 * 16 && kGrpNT == 512, "prologue vector widths");
   // direct global -> LDS loads (no VGPR destination, nothing waits on them until the barrier
   // after the times): 16 bytes per lane into a wave-contiguous 1 KB of the table
   for (int i0 = 0; i0 < 1024; i0 += kGrpNT) {
@@ -721,6 +708,8 @@ void k_tile(const float* __restrict__ rr, const float* __restrict__ ww, int64_t 
   const bool compact = totw <= kList;  // block-uniform
   constexpr int kPerT = (kList + kGrpNT - 1) / kGrpNT;
   uint32_t ebr[kPerT];  // bucket | rank << 11 of the thread's list entries (kept across the scan)
+  uint32_t eo[kPerT], eid[kPerT];  // key, tile-local id, weight of the thread's list entries
+  float ew[kPerT];
   int bc[4 * kTileG];
   uint32_t br[4 * kTileG];
   if (compact) {
@@ -729,22 +718,19 @@ void k_tile(const float* __restrict__ rr, const float* __restrict__ ww, int64_t 
       if ((win >> q) & 1u) {
         const int k = wbase + __popc(win & ((1u << q) - 1u));
         l_ord[k] = ord[q];
+        l_w[k] = lvk[q];
         l_id[k] = (uint16_t)((q >> 2) * 4 * kGrpNT + 4 * tid + (q & 3));
       }
     __syncthreads();
     PROF(6)
-    uint32_t eo[kPerT], eid[kPerT];
-    float ew[kPerT];
 #pragma unroll
     for (int i = 0; i < kPerT; ++i) {
       const int e = tid + i * kGrpNT;
       const bool v = e < totw;
       eo[i] = v ? l_ord[e] : 0u;
       eid[i] = v ? (uint32_t)l_id[e] : 0u;
+      ew[i] = v ? l_w[e] : 0.0f;
     }
-#pragma unroll
-    for (int i = 0; i < kPerT; ++i)  // the weights again from the tile's row (L2: this block read it)
-      ew[i] = tid + i * kGrpNT < totw ? wrow[a_t + (int)eid[i]] : 0.0f;
     int ebc[kPerT];
 #pragma unroll
     for (int i = 0; i < kPerT; ++i) {
@@ -842,38 +828,16 @@ void k_tile(const float* __restrict__ rr, const float* __restrict__ ww, int64_t 
   PROF(3)
   uint3* st = reinterpret_cast<uint3*>(staging) + ((int64_t)b * ntiles + tile) * kTile;
   if (compact) {
-#ifndef KTILE_LISTWIN
-    // straight to the staging position (one 12-byte store per winner; the tile's region stays in L2)
+    // straight to the staging position from the registers (one 12-byte store per winner; the
+    // tile's region stays in L2)
 #pragma unroll
     for (int i = 0; i < kPerT; ++i) {
-      const int e = tid + i * kGrpNT;
-      if (e < totw) {
+      if (tid + i * kGrpNT < totw) {
         const int p = s_off[ebr[i] & 0x7FFu] + (int)(ebr[i] >> 11);
-        const uint32_t id = l_id[e];
-        st[p] = make_uint3((uint32_t)a_t + id, ~l_ord[e], __float_as_uint(wrow[a_t + (int)id]));
+        st[p] = make_uint3((uint32_t)a_t + eid[i], ~eo[i], __float_as_uint(ew[i]));
       }
     }
     PROF(4)
-    PROF(5)
-    PROF_END(32)
-    return;
-#endif
-    // one window of 12-byte records holds the tile (tot <= kList); the list is intact
-#pragma unroll
-    for (int i = 0; i < kPerT; ++i) {
-      const int e = tid + i * kGrpNT;
-      if (e < totw) {
-        const int p = s_off[ebr[i] & 0x7FFu] + (int)(ebr[i] >> 11);
-        const uint32_t id = l_id[e];
-        w_r3[3 * p] = (uint32_t)a_t + id;
-        w_r3[3 * p + 1] = ~l_ord[e];
-        w_r3[3 * p + 2] = __float_as_uint(wrow[a_t + (int)id]);  // L2 (read twice by this block)
-      }
-    }
-    __syncthreads();
-    PROF(4)
-    for (int e = tid; e < tot; e += kGrpNT)  // one 12-byte record per lane (LDS stride 3: conflict-free)
-      st[e] = make_uint3(w_r3[3 * e], w_r3[3 * e + 1], w_r3[3 * e + 2]);
     PROF(5)
     PROF_END(32)
     return;
@@ -1284,16 +1248,24 @@ __global__ __launch_bounds__(kSortNT) void k_sort2(int32_t E, int32_t B, int32_t
     }
   };
   static_assert(kPer == 8, "four gather issues of two records");
-  fetch(blockIdx.x, nxb, nxk, nxs0, nxs1, r0, r1, nxl);
+  // XCD-aware bucket order: in each round the blocks of one XCD take consecutive buckets, so
+  // the cache lines two neighbouring runs share in a tile's staging region (bucket k's run ends
+  // where bucket k + 1's begins) are fetched once into that XCD's L2
+#ifdef KSORT_NOXCD
+  const int slot = blockIdx.x;
+#else
+  const int slot = xcd_remap(blockIdx.x, gridDim.x);
+#endif
+  fetch(slot, nxb, nxk, nxs0, nxs1, r0, r1, nxl);
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-  stage(blockIdx.x + gridDim.x);
+  stage(slot + gridDim.x);
   issue(0);
   issue(2);
   issue(4);
   issue(6);
   int it = -1;  // this block's iteration (bit of s_bigm)
 #pragma unroll 1
-  for (int f = blockIdx.x; f < total; f += gridDim.x) {
+  for (int f = slot; f < total; f += gridDim.x) {
     ++it;
     // this bucket's records and the next bucket's run table have landed (and the previous
     // bucket's stores drained)
@@ -1465,7 +1437,7 @@ __global__ __launch_bounds__(kSortNT) void k_sort2(int32_t E, int32_t B, int32_t
     while (m) {
       const int j = wd * 32 + __ffs((int)m) - 1;
       m &= m - 1u;
-      const int f = blockIdx.x + j * gridDim.x;
+      const int f = slot + j * gridDim.x;
       int bb = 0;
       while (s_nbp[bb + 1] <= f) ++bb;
       const int kk = f - s_nbp[bb] + part_lo(nb_[bb], part, nparts);
@@ -1500,42 +1472,56 @@ __global__ __launch_bounds__(kSortNT) void k_sort2(int32_t E, int32_t B, int32_t
 
 // Terminal step and the -1 / 1.0 padding up to T (grid-stride: the padding of a sample
 // with few removals can be millions of steps).
-__global__ __launch_bounds__(kFinNT) void k_pad(int32_t E, const int32_t* __restrict__ counts,
+__global__ __launch_bounds__(kFinNT) void k_pad(int32_t E, int32_t B, const int32_t* __restrict__ counts,
                                                 const int32_t* __restrict__ tdev, const double* __restrict__ wrest,
                                                 const float* __restrict__ ww, int64_t wrow_stride, int64_t t_cap,
                                                 int64_t* __restrict__ actions, float* __restrict__ fwd,
                                                 int32_t* __restrict__ t_out, int32_t* __restrict__ bigcnt,
                                                 int32_t* __restrict__ lastbig, int32_t do_pad) {
-  const int b = blockIdx.y;
-  const int k = counts[b], T = *tdev;
-  if (b == 0 && blockIdx.x == 0 && threadIdx.x == 0) {
-    if (t_out) *t_out = T;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (t_out) *t_out = *tdev;
     // retire the oversized-bucket count of this sort (k_sort2, its only writer, ran before this
     // launch on the same stream): a second sort on the same select starts from 0
     *lastbig = *bigcnt;
     *bigcnt = 0;
   }
   if (!do_pad) return;  // the terminal step and the padding belong to the last part
-  int64_t* ab = actions + (int64_t)b * t_cap;
-  float* fb = fwd + (int64_t)b * t_cap;
-  if (blockIdx.x == 0 && threadIdx.x == 0 && k < T) {  // the terminal step
-    const double wE = (double)ww[(int64_t)b * wrow_stride + E];
-    ab[k] = E;
-    fb[k] = (float)(wE / wrest[b]);
-  }
-  // padding k+1 .. T-1, four slots per thread: 2 x 16-byte action stores + one 16-byte
-  // probability store (4-byte alignment suffices for vector stores on gfx950)
-  const int p0 = k + 1;
-  for (int t = p0 + 4 * (blockIdx.x * kFinNT + threadIdx.x); t < T; t += 4 * gridDim.x * kFinNT) {
-    if (t + 3 < T) {
-      longlong2* a2 = reinterpret_cast<longlong2*>(ab + t);
-      a2[0] = make_longlong2(-1, -1);  // (plain stores: nt stores make this pure write stream 2x slower)
-      a2[1] = make_longlong2(-1, -1);
-      *reinterpret_cast<float4*>(fb + t) = make_float4(1.0f, 1.0f, 1.0f, 1.0f);
-    } else {
-      for (int u = t; u < T; ++u) {
-        ab[u] = -1;
-        fb[u] = 1.0f;
+  // every block takes the same share of every sample's padding (samples differ by up to ~1e6
+  // slots: a per-sample grid left most blocks idle behind the longest pad), in 16-byte vectors
+  // on 16-byte aligned addresses; block 0 also stores the terminal steps and the unaligned ends
+  const int T = *tdev, G = gridDim.x, g = blockIdx.x;
+#pragma unroll 1
+  for (int b = 0; b < B; ++b) {
+    const int k = counts[b];
+    int64_t* ab = actions + (int64_t)b * t_cap;
+    float* fb = fwd + (int64_t)b * t_cap;
+    if (g == 0 && threadIdx.x == 0 && k < T) {  // the terminal step
+      const double wE = (double)ww[(int64_t)b * wrow_stride + E];
+      ab[k] = E;
+      fb[k] = (float)(wE / wrest[b]);
+    }
+    const int lo = k + 1, hi = T;
+    if (lo >= hi) continue;
+    {  // actions: pairs of int64 (-1)
+      const int a0 = min(hi, lo + (int)((((uintptr_t)(ab + lo)) >> 3) & 1));
+      const int nv = (hi - a0) >> 1, a1 = a0 + 2 * nv;
+      const int v0 = (int)((int64_t)nv * g / G), v1 = (int)((int64_t)nv * (g + 1) / G);
+      longlong2* av = reinterpret_cast<longlong2*>(ab + a0);
+      for (int v = v0 + threadIdx.x; v < v1; v += kFinNT) av[v] = make_longlong2(-1, -1);
+      if (g == 0 && threadIdx.x == 0) {
+        for (int t = lo; t < a0; ++t) ab[t] = -1;
+        for (int t = a1; t < hi; ++t) ab[t] = -1;
+      }
+    }
+    {  // step probabilities: float4 of 1.0
+      const int a0 = min(hi, lo + (int)((4 - ((((uintptr_t)(fb + lo)) >> 2) & 3)) & 3));
+      const int nv = (hi - a0) >> 2, a1 = a0 + 4 * nv;
+      const int v0 = (int)((int64_t)nv * g / G), v1 = (int)((int64_t)nv * (g + 1) / G);
+      float4* fv = reinterpret_cast<float4*>(fb + a0);
+      for (int v = v0 + threadIdx.x; v < v1; v += kFinNT) fv[v] = make_float4(1.0f, 1.0f, 1.0f, 1.0f);
+      if (g == 0 && threadIdx.x == 0) {
+        for (int t = lo; t < a0; ++t) fb[t] = 1.0f;
+        for (int t = a1; t < hi; ++t) fb[t] = 1.0f;
       }
     }
   }
@@ -1713,7 +1699,7 @@ extern "C" int spai_rollout_finish(const float* logits, int64_t bstride, int32_t
   SPAI_CHECK_ARG(counts, "spai_rollout_finish: null pointer");
   hipStream_t s = (hipStream_t)stream;
   const int last = part == nparts - 1;
-  k_pad<<<dim3(last ? std::max(1, 1024 / B) : 1, B), kFinNT, 0, s>>>(E, counts, w.tdev, w.wrest, w.ww,
+  k_pad<<<last ? 4 * num_cus() : 1, kFinNT, 0, s>>>(E, B, counts, w.tdev, w.wrest, w.ww,
                                                                      bstride ? w.wstride : 0, t_cap, actions,
                                                                      fwd_probs, t_out, w.bigcnt, w.lastbig, last);
   SPAI_CHECK_LAUNCH();

@@ -6,8 +6,10 @@
            back_probs: BackwardPolicy, LSTM recurrence = spai_lstm_forward / _backward
     skip the update when the loss is NaN/Inf (GFlowNet100.py:298-300; one host sync, as there)
     scheduler.step(loss); loss.backward(); opt.step(); opt.zero_grad()
-The ForwardPolicy's own backward (GATv2 x2 + fc) differentiates its torch restatement
-(policy._HipLogits).  Adam is torch's (fused kernels on the device).
+The ForwardPolicy's own backward (GATv2 x2 + mean pool + fc) runs the gfx950 kernels of
+spai_policy_backward (policy._HipLogits; hidden sizes 4 and 8, the reference driver's hid = 4,
+GFlowNet100.py:178-180); other hidden sizes differentiate the torch restatement on the device.
+Adam is torch's (fused kernels on the device).
 """
 from __future__ import annotations
 

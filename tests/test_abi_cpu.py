@@ -45,8 +45,8 @@ def test_argument_validation_without_gpu():
     assert rc == _lib.SPAI_ERR_INVALID and b"null pointer" in lib.spai_last_error()
     rc = lib.spai_rollout_merge(None, 0, 10, 1, None, 0, 2, None, None, 0, None)
     assert rc == _lib.SPAI_ERR_INVALID and b"null pointer" in lib.spai_last_error()
-    assert lib.spai_rollout_ws_offset(1000, 2, 6) == 2 * 2 * 2048 + 2 * 8
-    assert lib.spai_rollout_ws_offset(1000, 2, 3) == 2048 and lib.spai_rollout_ws_offset(1000, 2, 9) == -1
+    assert lib.spai_rollout_ws_offset(1000, 2, 6) == 2 * 2 * 1024 + 2 * 8
+    assert lib.spai_rollout_ws_offset(1000, 2, 3) == 1024 and lib.spai_rollout_ws_offset(1000, 2, 9) == -1
     assert 0 < lib.spai_rollout_ws_offset(1000, 2, 2) < lib.spai_rollout_workspace_bytes(1000, 2)
     with pytest.raises(ValueError):
         _lib.check(rc, "spai_rollout_select")

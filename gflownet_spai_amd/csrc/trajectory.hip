@@ -1100,6 +1100,7 @@ __global__ __launch_bounds__(kSortNT) void k_sort2(int32_t E, int32_t B, int32_t
                                                    const int32_t* __restrict__ bstart,
                                                    const uint32_t* __restrict__ runs,
                                                    const uint32_t* __restrict__ staging,
+                                                   const uint32_t* __restrict__ spl,
                                                    int64_t t_cap, int64_t* __restrict__ actions,
                                                    float* __restrict__ fwd, const double* __restrict__ wrest,
                                                    const double* __restrict__ bwsuf, int32_t* __restrict__ bigcnt,
@@ -1126,16 +1127,23 @@ __global__ __launch_bounds__(kSortNT) void k_sort2(int32_t E, int32_t B, int32_t
     if (tid < B) s_nbp[tid] = ex;
     if (tid == 0) s_nbp[B] = tot;
   }
+  for (int i = tid; i < kMaxSub + 4; i += kSortNT) s_sub[i] = 0;  // zero again after each bucket's ranking
   __syncthreads();
   const int total = s_nbp[B];
   const int t0 = 2 * tid, t1 = 2 * tid + 1;
   PROF_INIT
   // bucket f: sample, bucket index, start/size, and the count and tile-local offset of its
   // runs in tiles t0, t1
-  auto fetch = [&](int f, int& bb, int& kk, int& s0, int& s1, uint32_t& r0, uint32_t& r1, double& lt) {
+  // and, for an interior bucket, its key range from the splitters: bucket kk holds the keys o with
+  // spl[j - 1] <= o < spl[j], j = nb - 1 - kk (records carry ~o), so no min / max reduction is
+  // needed to lay out its sub-buckets (the two end buckets have an open side: reduced)
+  auto fetch = [&](int f, int& bb, int& kk, int& s0, int& s1, uint32_t& r0, uint32_t& r1, double& lt, uint32_t& bmn,
+                   uint32_t& bmx, bool& bnd) {
     r0 = r1 = 0u;
     bb = kk = s0 = s1 = 0;
     lt = 0.0;
+    uint32_t lo = 0u, hi = 0u;
+    int nbl = 0;
     if (f < total) {
       while (s_nbp[bb + 1] <= f) ++bb;
       kk = f - s_nbp[bb] + part_lo(nb_[bb], part, nparts);
@@ -1146,6 +1154,18 @@ __global__ __launch_bounds__(kSortNT) void k_sort2(int32_t E, int32_t B, int32_t
       const uint32_t* rr = runs + ((int64_t)bb * kMaxB + kk) * ntiles;  // [b][bucket][tile]
       if (t0 < ntiles) r0 = rr[t0];
       if (t1 < ntiles) r1 = rr[t1];
+      nbl = nb_[bb] - 1;
+      const int j = nbl - kk;
+      if (j >= 1 && j <= nbl - 1) {
+        lo = spl[(int64_t)bb * kMaxB + j - 1];
+        hi = spl[(int64_t)bb * kMaxB + j];
+      }
+    }
+    {
+      const int j = __builtin_amdgcn_readfirstlane(nbl - kk);
+      bnd = f < total && j >= 1 && j <= __builtin_amdgcn_readfirstlane(nbl) - 1;
+      bmn = ~(uint32_t)__builtin_amdgcn_readfirstlane((int)hi) + 1u;  // ~o of the largest o < hi
+      bmx = ~(uint32_t)__builtin_amdgcn_readfirstlane((int)lo);
     }
     // block-uniform: scalar registers (scalar-base addressing of the gather and the stores)
     bb = __builtin_amdgcn_readfirstlane(bb);
@@ -1154,6 +1174,8 @@ __global__ __launch_bounds__(kSortNT) void k_sort2(int32_t E, int32_t B, int32_t
     s1 = __builtin_amdgcn_readfirstlane(s1);
   };
   int nxb, nxk, nxs0, nxs1;
+  bool nxbnd;
+  uint32_t nxmn, nxmx;
   double nxl;
   uint32_t r0, r1;  // packed runs (offset << 16 | count) of the next bucket in tiles t0, t1
   // gather map of the bucket being staged (in S: free from the flush until the suffix phase)
@@ -1212,6 +1234,8 @@ __global__ __launch_bounds__(kSortNT) void k_sort2(int32_t E, int32_t B, int32_t
   // the run table of bucket f + 2G is in flight with them.
   constexpr int kPer = kCap2 / kSortNT;
   int cb = 0, ck = 0, cs = 0, cn = 0;
+  bool cbnd = false;
+  uint32_t cmn = 0u, cmx = 0u;
   double cl = 0.0;
   uint64_t gm[kPer];
   float gw[kPer];
@@ -1221,9 +1245,12 @@ __global__ __launch_bounds__(kSortNT) void k_sort2(int32_t E, int32_t B, int32_t
     cs = nxs0;
     cn = nxs1 - nxs0;
     cl = nxl;
+    cbnd = nxbnd;
+    cmn = nxmn;
+    cmx = nxmx;
     build_map();
     PROF(2)
-    fetch(fnext, nxb, nxk, nxs0, nxs1, r0, r1, nxl);
+    fetch(fnext, nxb, nxk, nxs0, nxs1, r0, r1, nxl, nxmn, nxmx, nxbnd);
     lds_barrier();
     PROF(3)
   };
@@ -1251,12 +1278,8 @@ __global__ __launch_bounds__(kSortNT) void k_sort2(int32_t E, int32_t B, int32_t
   // XCD-aware bucket order: in each round the blocks of one XCD take consecutive buckets, so
   // the cache lines two neighbouring runs share in a tile's staging region (bucket k's run ends
   // where bucket k + 1's begins) are fetched once into that XCD's L2
-#ifdef KSORT_NOXCD
-  const int slot = blockIdx.x;
-#else
   const int slot = xcd_remap(blockIdx.x, gridDim.x);
-#endif
-  fetch(slot, nxb, nxk, nxs0, nxs1, r0, r1, nxl);
+  fetch(slot, nxb, nxk, nxs0, nxs1, r0, r1, nxl, nxmn, nxmx, nxbnd);
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
   stage(slot + gridDim.x);
   issue(0);
@@ -1270,7 +1293,9 @@ __global__ __launch_bounds__(kSortNT) void k_sort2(int32_t E, int32_t B, int32_t
     // this bucket's records and the next bucket's run table have landed (and the previous
     // bucket's stores drained)
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-    const int b = cb, k = ck, s = cs, n = cn;
+    const int b = cb, s = cs, n = cn;
+    const bool bbnd = cbnd;
+    uint32_t mn = cmn, mx = cmx;
     const double later = cl;
     uint64_t mine[kPer];
     float lw[kPer];
@@ -1296,40 +1321,44 @@ __global__ __launch_bounds__(kSortNT) void k_sort2(int32_t E, int32_t B, int32_t
       }
       continue;
     }
-    uint32_t mn = 0xFFFFFFFFu, mx = 0u;
+    if (!bbnd) {  // an end bucket: the key range by a block reduction (s_sub is already zero)
+      mn = 0xFFFFFFFFu;
+      mx = 0u;
 #pragma unroll
-    for (int j = 0; j < kPer; ++j) {
-      const int i = j * kSortNT + tid;
-      if (i < n) {
-        mn = min(mn, (uint32_t)(mine[j] >> 32));
-        mx = max(mx, (uint32_t)(mine[j] >> 32));
+      for (int j = 0; j < kPer; ++j) {
+        const int i = j * kSortNT + tid;
+        if (i < n) {
+          mn = min(mn, (uint32_t)(mine[j] >> 32));
+          mx = max(mx, (uint32_t)(mine[j] >> 32));
+        }
+      }
+      mn = wave_min_u32(mn);
+      mx = wave_max_u32(mx);
+      if (lane == 0) {
+        s_red[wave * 2] = mn;
+        s_red[wave * 2 + 1] = mx;
+      }
+      lds_barrier();
+      mn = 0xFFFFFFFFu;
+      mx = 0u;
+#pragma unroll
+      for (int w = 0; w < kSortNT / 64; ++w) {
+        mn = min(mn, s_red[2 * w]);
+        mx = max(mx, s_red[2 * w + 1]);
       }
     }
-    mn = wave_min_u32(mn);
-    mx = wave_max_u32(mx);
-    if (lane == 0) {
-      s_red[wave * 2] = mn;
-      s_red[wave * 2 + 1] = mx;
-    }
     const int nsub = max(1, min(kMaxSub, 2 * n));
-    for (int i = tid; i < kMaxSub; i += kSortNT) s_sub[i] = 0;  // all of it: the scan reads whole int4s
-    lds_barrier();
     PROF(5)
     issue(2);
-    mn = 0xFFFFFFFFu;
-    mx = 0u;
-#pragma unroll
-    for (int w = 0; w < kSortNT / 64; ++w) {
-      mn = min(mn, s_red[2 * w]);
-      mx = max(mx, s_red[2 * w + 1]);
-    }
-    const uint64_t span = (uint64_t)(mx - mn) + 1ull;
+    // sub-bucket = floor((key - mn) * nsub / span) in fp32, clamped: monotone in the key (all
+    // that the ranking needs), no 64-bit division per record
+    const float scale = (float)nsub / ((float)(mx - mn) + 1.0f);
     int sb[kPer];
 #pragma unroll
     for (int j = 0; j < kPer; ++j) {
       sb[j] = 0;
       if (j * kSortNT + tid < n) {
-        sb[j] = (int)((((uint64_t)((uint32_t)(mine[j] >> 32) - mn)) * (uint64_t)nsub) / span);
+        sb[j] = min(nsub - 1, (int)((float)((uint32_t)(mine[j] >> 32) - mn) * scale));
         atomicAdd(&s_sub[sb[j]], 1);
       }
     }
@@ -1369,6 +1398,8 @@ __global__ __launch_bounds__(kSortNT) void k_sort2(int32_t E, int32_t B, int32_t
     }
     lds_barrier();
     PROF(9)
+    // the sub-bucket counts are dead until the next bucket's histogram (several barriers away)
+    for (int i = tid; i < kMaxSub; i += kSortNT) s_sub[i] = 0;  // all of it: the scan reads whole int4s
     issue(6);
 #pragma unroll
     for (int j = 0; j < kPer; ++j)
@@ -1682,7 +1713,7 @@ extern "C" int spai_rollout_sort(const float* logits, int64_t bstride, int32_t E
   // persistent blocks, enough that none walks more than the 32 * kBigWords its oversized mask tracks
   const int g2 = std::max(std::max(1, std::min(nbt, num_cus())), (nbt + 32 * kBigWords - 1) / (32 * kBigWords));
   const int64_t wrs = bstride ? w.wstride : 0;
-  k_sort2<<<g2, kSortNT, 0, s>>>(E, B, w.ntiles, w.nb, w.bstart, w.runs, w.staging, t_cap, actions, fwd_probs,
+  k_sort2<<<g2, kSortNT, 0, s>>>(E, B, w.ntiles, w.nb, w.bstart, w.runs, w.staging, w.spl, t_cap, actions, fwd_probs,
                                  w.wrest, w.bwsuf, w.bigcnt, w.ww, wrs, w.scratch, part, nparts);
   SPAI_CHECK_LAUNCH();
   return SPAI_OK;

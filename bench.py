@@ -481,8 +481,8 @@ def main():
         }
         if world == 1:
             sel = roofline_obj("rollout_select phase: k_presample + k_splitters + k_tile + k_bsum (k_tile ~80 % of "
-                               "it; VALU-bound: Philox4x32-10 + one det_logf per action and the bucket placement, "
-                               "DESIGN.md §5)", select_bytes(env, bl, float(counts.sum())),
+                               "it; latency-bound: VALU issue 0.33 of its SIMD cycles, 0.47 of the wave cycles "
+                               "waiting, DESIGN.md §3)", select_bytes(env, bl, float(counts.sum())),
                                phase_ms.get("rollout_select", float("nan")))
             out["roofline_select"] = sel
             with torch.no_grad():

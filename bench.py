@@ -219,10 +219,11 @@ def generic_residual_leg(env, log, cfg: str, reps: int = 10):
     kernels.TIMERS = None
     ref = env.last_residual.double() ** 2
     rel = float(((res2 - ref).abs() / ref).max())
-    bytes_a = a.idx.numel() * 4 + a.val.numel() * a.val.element_size()
+    av = kernels.narrow_values(a)  # fp64 A with fp32-exact values is read as fp32 (same numbers)
+    bytes_a = a.idx.numel() * 4 + av.numel() * av.element_size()
     bytes_m = n * W * (4 + m.element_size())
     name = "k_resid_shared" if W <= 7 else "k_resid_wide"
-    out = roofline_obj(f"{name}<{W},{a.width},{str(a.val.dtype)[6:]},{str(m.dtype)[6:]}> (||A M_b - I||_F^2 of "
+    out = roofline_obj(f"{name}<{W},{a.width},{str(av.dtype)[6:]},{str(m.dtype)[6:]}> (||A M_b - I||_F^2 of "
                        f"B={B} arbitrary sparse M_b: the step's LSQ fills with their own kept index sets; "
                        f"bytes = bytes(A) + B x bytes(M_b))", bytes_a + B * bytes_m, ms,
                        traffic=measured_traffic(cfg + "_residual", B))

@@ -84,6 +84,43 @@ __device__ __forceinline__ void gather_a_lines(const int (&k)[W], int wart, cons
   }
 }
 
+// <A_line p, A_line q> by index matching: an index occurs at most once per line, so entry s of
+// line p meets at most one entry of line q; a select chain in A's own precision (one compare +
+// one select per entry pair) finds its partner's value; padding (index -1, value 0) adds
+// nothing.  fp64 fma accumulation in slot order.
+template <int WA, typename TA>
+__device__ __forceinline__ double pair_dot(const int (&ip)[WA], const TA (&xp)[WA], const int (&iq)[WA],
+                                           const TA (&xq)[WA]) {
+  double g = 0.0;
+#pragma unroll
+  for (int s = 0; s < WA; ++s) {
+    TA m = (TA)0;
+#pragma unroll
+    for (int t = 0; t < WA; ++t) m = ip[s] == iq[t] ? xq[t] : m;
+    g = fma((double)xp[s], (double)m, g);
+  }
+  return g;
+}
+
+// The same with line p's values already widened to fp64 (identical products and order).
+template <int WA, typename TA>
+__device__ __forceinline__ double pair_dot_w(const int (&ip)[WA], const double (&xp)[WA], const int (&iq)[WA],
+                                             const TA (&xq)[WA]) {
+  // t outer, s inner: the WA independent select chains advance together, so consecutive
+  // compares are independent (their lane masks do not serialise on one SGPR pair)
+  TA m[WA];
+#pragma unroll
+  for (int s = 0; s < WA; ++s) m[s] = (TA)0;
+#pragma unroll
+  for (int t = 0; t < WA; ++t)
+#pragma unroll
+    for (int s = 0; s < WA; ++s) m[s] = ip[s] == iq[t] ? xq[t] : m[s];
+  double g = 0.0;
+#pragma unroll
+  for (int s = 0; s < WA; ++s) g = fma(xp[s], (double)m[s], g);
+  return g;
+}
+
 // Line Gram of M's slots against line j of A-product space:
 //   c_p = A_line(k_p)[j],  G_pp = ||A_line(k_p)||^2,  G_pq = <A_line(k_p), A_line(k_q)> (q > p).
 // An index occurs at most once per line: entry s of line p meets at most one entry of line q,
@@ -99,28 +136,19 @@ __device__ __forceinline__ void line_gram(const int (&ai)[W][WA], const TA (&av)
 #pragma unroll
     for (int s = 0; s < WA; ++s) {
       const double x = (double)av[p][s];
-      gpp += x * x;
+      gpp = fma(x, x, gpp);
       cp += (ai[p][s] == j) ? x : 0.0;
     }
     c[p] = cp;
     gd[p] = gpp;
 #pragma unroll
-    for (int q = p + 1; q < W; ++q) {
-      double g = 0.0;
-#pragma unroll
-      for (int s = 0; s < WA; ++s) {
-        TA m = (TA)0;
-#pragma unroll
-        for (int t = 0; t < WA; ++t) m = ai[p][s] == ai[q][t] ? av[q][t] : m;
-        g += (double)av[p][s] * (double)m;
-      }
-      go[o++] = g;
-    }
+    for (int q = p + 1; q < W; ++q) go[o++] = pair_dot<WA, TA>(ai[p], av[p], ai[q], av[q]);
   }
 }
 
-// ||sum_p v_p A_line(k_p) - e_j||^2 = 1 + sum_p v_p (v_p G_pp - 2 c_p + 2 sum_{q>p} v_q G_pq),
-// in this order (the same operations whichever kernel evaluates it).
+// ||sum_p v_p A_line(k_p) - e_j||^2 = 1 + sum_p v_p (v_p G_pp - 2 c_p + sum_{q>p} v_q (2 G_pq)),
+// as explicit fma in this order (every kernel evaluates a line with exactly these operations;
+// 2 G_pq is exact, so v_q (2 G_pq) is the product 2 v_q G_pq).
 template <int W>
 __device__ __forceinline__ double line_res2(const double (&v)[W], const double (&c)[W], const double (&gd)[W],
                                             const double (&go)[W * (W - 1) / 2]) {
@@ -128,10 +156,10 @@ __device__ __forceinline__ double line_res2(const double (&v)[W], const double (
   int o = 0;
 #pragma unroll
   for (int p = 0; p < W; ++p) {
-    double acc = v[p] * gd[p] - 2.0 * c[p];
+    double acc = fma(v[p], gd[p], -2.0 * c[p]);
 #pragma unroll
-    for (int q = p + 1; q < W; ++q) acc += 2.0 * v[q] * go[o++];
-    r2 += v[p] * acc;
+    for (int q = p + 1; q < W; ++q) acc = fma(v[q], 2.0 * go[o++], acc);
+    r2 = fma(v[p], acc, r2);
   }
   return r2;
 }
@@ -299,49 +327,56 @@ __global__ __launch_bounds__(kNT, WAVES) void k_resid_shared(int32_t line_begin,
                                             val_bstride, a_idx, a_val, partials, sred);
 }
 
-// Thread per line, chunks of kChunkW samples, W > 7 (C3's 13-wide lines): the samples' index
-// sets are read together; when they agree slot by slot (sub-patterns of one pattern) the A
-// lines of the union pattern are gathered once per chunk and every entry pair is matched ONCE
-// for the chunk: c_p and G_pp open each sample's row accumulator, each G_pq (q > p) is added
-// to it as soon as it is formed, and the row is closed into the sample's sum — exactly
+// Thread per line, chunks of C samples, W > 7 (C3's 13-wide lines): the samples' index sets
+// are read together; when they agree slot by slot (sub-patterns of one pattern) the A lines of
+// the union pattern are gathered once per chunk and every entry pair is matched ONCE for the
+// chunk: c_p and G_pp open each sample's row accumulator, each G_pq (q > p) is added to it as
+// soon as it is formed (pair_dot), and the row is closed into the sample's sum — exactly
 // line_res2's operations in line_res2's order, so a sample gets the same bits as on its own.
 // The Gram itself is never stored (91 + 26 fp64 values would not fit beside the A lines).
 // Lanes whose samples disagree evaluate each sample on its own index set (line_res2_any).
-// Index matching per line: once per chunk instead of once per sample.
-constexpr int kChunkW = 4;
-template <int W, int WA, bool FULL, typename TA, typename TV>
+// The index matching (49 compare + select per entry pair, 78 pairs per 13-wide line) is all of
+// the kernel's work, so the chunk is as large as the registers allow:
+//   TA = float (A's values exact in fp32: the caller passes them narrowed, widened back
+//   exactly here; 91 registers for the A lines' values): C = 8 — one matching per line for
+//   the usual batch of 8;
+//   TA = double: C = 4 (182 registers of A values).
+// One wave per SIMD either way (the chunk's 8 x 13 fp64 values, the A lines and the row
+// accumulators take ~450 registers).
+template <int W, int WA, int C, bool FULL, typename TA, typename TV>
 __device__ __forceinline__ void resid_wide_body(int32_t line_begin, int32_t line_end, int32_t wrt, int32_t wart,
                                                 int32_t B, int32_t nblk, const int32_t* __restrict__ m_idx,
                                                 int64_t idx_bstride, const TV* __restrict__ m_val,
                                                 int64_t val_bstride, const int32_t* __restrict__ a_idx,
                                                 const TA* __restrict__ a_val, double* __restrict__ partials,
-                                                double (&sred)[kChunkW][kNT / 64]) {
-  static_assert(kChunkW * W <= 64, "validity bits of a chunk in one u64");
+                                                double (&sred)[C][kNT / 64]) {
+  static_assert(W <= 32, "validity bits of a sample in one u32");
   const int blk = xcd_remap(blockIdx.x, gridDim.x);
   const int j = line_begin + blk * kNT + threadIdx.x;
   const bool valid = j < line_end;
   const int jj = valid ? j : line_begin;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll 1
-  for (int b0 = 0; b0 < B; b0 += kChunkW) {
-    const int nb = min(kChunkW, B - b0);
+  for (int b0 = 0; b0 < B; b0 += C) {
+    const int nb = min(C, B - b0);
     int kmax[W], kmin[W];
 #pragma unroll
     for (int p = 0; p < W; ++p) {
       kmax[p] = -1;
       kmin[p] = INT_MAX;
     }
-    uint64_t bits = 0;
+    uint32_t bits[C];  // bit p of bits[i]: slot p of sample b0 + i is valid
 #pragma unroll
-    for (int i = 0; i < kChunkW; ++i) {
+    for (int i = 0; i < C; ++i) {
       const int32_t* mi = m_idx + (int64_t)min(b0 + i, B - 1) * idx_bstride + (int64_t)jj * wrt;
       int k[W];
       load_slots<W, FULL, int>(mi, wrt, k);
+      bits[i] = 0u;
 #pragma unroll
       for (int p = 0; p < W; ++p) {
         const int kp = (valid && i < nb && p < wrt) ? k[p] : -1;
         if (kp >= 0) {
-          bits |= (uint64_t)1 << (i * W + p);
+          bits[i] |= 1u << p;
           kmax[p] = max(kmax[p], kp);
           kmin[p] = min(kmin[p], kp);
         }
@@ -350,53 +385,46 @@ __device__ __forceinline__ void resid_wide_body(int32_t line_begin, int32_t line
     bool shared = true;
 #pragma unroll
     for (int p = 0; p < W; ++p) shared = shared && (kmax[p] < 0 || kmin[p] == kmax[p]);
-    double r2s[kChunkW];
+    double r2s[C];
 #pragma unroll
-    for (int i = 0; i < kChunkW; ++i) r2s[i] = 0.0;
+    for (int i = 0; i < C; ++i) r2s[i] = 0.0;
     if (valid && shared) {
       int ai[W][WA];
       TA av[W][WA];
       gather_a_lines<W, WA, FULL, TA>(kmax, wart, a_idx, a_val, ai, av);
-      double v[kChunkW][W];
+      double v[C][W];
 #pragma unroll
-      for (int i = 0; i < kChunkW; ++i) {
+      for (int i = 0; i < C; ++i) {
         TV x[W];
         load_slots<W, FULL, TV>(m_val + (int64_t)min(b0 + i, B - 1) * val_bstride + (int64_t)jj * wrt, wrt, x);
 #pragma unroll
-        for (int p = 0; p < W; ++p) v[i][p] = ((bits >> (i * W + p)) & 1) ? (double)x[p] : 0.0;
+        for (int p = 0; p < W; ++p) v[i][p] = ((bits[i] >> p) & 1u) ? (double)x[p] : 0.0;
       }
 #pragma unroll
-      for (int i = 0; i < kChunkW; ++i) r2s[i] = 1.0;
+      for (int i = 0; i < C; ++i) r2s[i] = 1.0;
 #pragma unroll
       for (int p = 0; p < W; ++p) {
         double cp = 0.0, gpp = 0.0;  // line_gram's c_p and G_pp
 #pragma unroll
         for (int s = 0; s < WA; ++s) {
           const double x = (double)av[p][s];
-          gpp += x * x;
+          gpp = fma(x, x, gpp);
           cp += (ai[p][s] == j) ? x : 0.0;
         }
-        double acc[kChunkW];
+        double acc[C];
 #pragma unroll
-        for (int i = 0; i < kChunkW; ++i) acc[i] = v[i][p] * gpp - 2.0 * cp;
+        for (int i = 0; i < C; ++i) acc[i] = fma(v[i][p], gpp, -2.0 * cp);
 #pragma unroll
         for (int q = p + 1; q < W; ++q) {
-          double g = 0.0;  // line_gram's G_pq
+          const double g2 = 2.0 * pair_dot<WA, TA>(ai[p], av[p], ai[q], av[q]);  // line_gram's 2 G_pq
 #pragma unroll
-          for (int s = 0; s < WA; ++s) {
-            TA m = (TA)0;
-#pragma unroll
-            for (int t = 0; t < WA; ++t) m = ai[p][s] == ai[q][t] ? av[q][t] : m;
-            g += (double)av[p][s] * (double)m;
-          }
-#pragma unroll
-          for (int i = 0; i < kChunkW; ++i) acc[i] += 2.0 * v[i][q] * g;
+          for (int i = 0; i < C; ++i) acc[i] = fma(v[i][q], g2, acc[i]);
         }
 #pragma unroll
-        for (int i = 0; i < kChunkW; ++i) r2s[i] += v[i][p] * acc[i];
+        for (int i = 0; i < C; ++i) r2s[i] = fma(v[i][p], acc[i], r2s[i]);
       }
 #pragma unroll
-      for (int i = 0; i < kChunkW; ++i) r2s[i] = i < nb ? r2s[i] : 0.0;
+      for (int i = 0; i < C; ++i) r2s[i] = i < nb ? r2s[i] : 0.0;
     } else if (valid) {
 #pragma unroll 1
       for (int i = 0; i < nb; ++i) {  // one sample at a time on its own index set
@@ -405,21 +433,24 @@ __device__ __forceinline__ void resid_wide_body(int32_t line_begin, int32_t line
         int k[W], kp[W];
         TV x[W];
         double v[W];
+        uint32_t bi = 0u;
+#pragma unroll
+        for (int u = 0; u < C; ++u) bi = u == i ? bits[u] : bi;
         load_slots<W, FULL, int>(mi, wrt, kp);
         load_slots<W, FULL, TV>(mv, wrt, x);
 #pragma unroll
         for (int p = 0; p < W; ++p) {
-          const bool on = (bits >> (i * W + p)) & 1;
+          const bool on = (bi >> p) & 1u;
           k[p] = on ? kp[p] : -1;
           v[p] = on ? (double)x[p] : 0.0;
         }
         const double r2 = line_res2_any<W, WA, FULL, TA>(k, v, j, wart, a_idx, a_val);
 #pragma unroll
-        for (int u = 0; u < kChunkW; ++u) r2s[u] = u == i ? r2 : r2s[u];
+        for (int u = 0; u < C; ++u) r2s[u] = u == i ? r2 : r2s[u];
       }
     }
 #pragma unroll
-    for (int i = 0; i < kChunkW; ++i) {
+    for (int i = 0; i < C; ++i) {
       if (i < nb) {
         const double r2 = wave_sum_dpp(r2s[i]);
         if (lane == 0) sred[i][w] = r2;
@@ -436,19 +467,272 @@ __device__ __forceinline__ void resid_wide_body(int32_t line_begin, int32_t line
   }
 }
 
+template <typename TA>
+constexpr int wide_chunk() { return sizeof(TA) == 4 ? 8 : 4; }
+
 template <int W, int WA, typename TA, typename TV>
 __global__ __launch_bounds__(kNT) void k_resid_wide(int32_t line_begin, int32_t line_end, int32_t wrt, int32_t wart,
                                                     int32_t B, int32_t nblk, const int32_t* __restrict__ m_idx,
                                                     int64_t idx_bstride, const TV* __restrict__ m_val,
                                                     int64_t val_bstride, const int32_t* __restrict__ a_idx,
                                                     const TA* __restrict__ a_val, double* __restrict__ partials) {
-  __shared__ double sred[kChunkW][kNT / 64];
+  constexpr int C = wide_chunk<TA>();
+  __shared__ double sred[C][kNT / 64];
   if (wrt == W && wart == WA)
-    resid_wide_body<W, WA, true, TA, TV>(line_begin, line_end, wrt, wart, B, nblk, m_idx, idx_bstride, m_val,
-                                         val_bstride, a_idx, a_val, partials, sred);
+    resid_wide_body<W, WA, C, true, TA, TV>(line_begin, line_end, wrt, wart, B, nblk, m_idx, idx_bstride, m_val,
+                                            val_bstride, a_idx, a_val, partials, sred);
   else
-    resid_wide_body<W, WA, false, TA, TV>(line_begin, line_end, wrt, wart, B, nblk, m_idx, idx_bstride, m_val,
+    resid_wide_body<W, WA, C, false, TA, TV>(line_begin, line_end, wrt, wart, B, nblk, m_idx, idx_bstride, m_val,
+                                             val_bstride, a_idx, a_val, partials, sred);
+}
+
+// Wide lines (8 <= W <= 16, C3's 13-wide lines), SIXTEEN lanes per line: lane p of a 16-lane row
+// holds slot p only — the index and values of A line k_p (2 WA registers) and the chunk's 8
+// values v_ip — so a line's 78 entry-pair matchings are spread over its lanes at ~100 registers
+// per lane (4+ waves per SIMD) instead of one thread holding all 13 A lines at one wave per SIMD.
+// Round d = 1..8: every lane takes the slot data of lane p - d (mod 16) by DPP row_ror, matches
+// the pair (pair_dot) and adds v_iq * 2 G_pq (d = 8: both lanes of the pair meet, each adds
+// v_iq * G_pq) to its per-sample sum; every unordered pair is matched exactly once.  The lane's
+// row value v_ip (v_ip G_pp - 2 c_p + sum) is summed over the 16 lanes by a fixed DPP tree.
+// A block walks 16 groups of 16 consecutive lines (256 lines, the partials of k_resid_shared).
+// Rows whose samples disagree on a slot evaluate each sample on its own index set with the same
+// per-sample operations (a sample's value never depends on the other samples of its chunk:
+// bit-identical to the sample alone).  Explicit _rn arithmetic: no contraction differences
+// between the chunk and the single-sample instantiations.
+constexpr int kRowC = 8;  // samples per chunk of the row kernel
+// Round D of row_eval: the slot data of lane p - D (mod 16) by DPP row_ror:D, one pair matched.
+// (row_ror has a source lane for every lane: bound_ctrl, no "old" operand to preload)
+template <int kCtl>
+__device__ __forceinline__ int dpp_row_i(int x) {
+  return __builtin_amdgcn_mov_dpp(x, kCtl, 0xf, 0xf, true);
+}
+template <int kCtl>
+__device__ __forceinline__ double dpp_row_d(double x) {
+  const uint64_t u = __double_as_longlong(x);
+  const int lo = dpp_row_i<kCtl>((int)(uint32_t)u), hi = dpp_row_i<kCtl>((int)(uint32_t)(u >> 32));
+  return __longlong_as_double((long long)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo));
+}
+template <int D, int C, int WA, typename TA>
+__device__ __forceinline__ void row_round(const int (&ai)[WA], const TA (&av)[WA], const double (&xd)[WA],
+                                          const double (&v)[C], double (&acc)[C]) {
+  constexpr int kCtl = 0x120 + D;  // row_ror:D
+  int pi[WA];
+  TA pa[WA];
+#pragma unroll
+  for (int s = 0; s < WA; ++s) {
+    pi[s] = dpp_row_i<kCtl>(ai[s]);
+    if constexpr (sizeof(TA) == 4)
+      pa[s] = __int_as_float(dpp_row_i<kCtl>(__float_as_int(av[s])));
+    else
+      pa[s] = dpp_row_d<kCtl>(av[s]);
+  }
+  const double g = pair_dot_w<WA, TA>(ai, xd, pi, pa);
+  const double g2 = D < 8 ? 2.0 * g : g;  // D = 8: both lanes of the pair add it
+#pragma unroll
+  for (int i = 0; i < C; ++i) acc[i] = fma(dpp_row_d<kCtl>(v[i]), g2, acc[i]);
+}
+
+// A line k of the lane's slot (k < 0: empty, index -1 / value 0; clamped unconditional loads).
+template <int WA, bool FULL, typename TA>
+__device__ __forceinline__ void row_load(int k, int wart, const int32_t* __restrict__ a_idx,
+                                         const TA* __restrict__ a_val, int (&ai)[WA], TA (&av)[WA]) {
+  const int64_t base = (int64_t)max(k, 0) * wart;
+  load_slots<WA, FULL, int>(a_idx + base, wart, ai);
+  load_slots<WA, FULL, TA>(a_val + base, wart, av);
+#pragma unroll
+  for (int s = 0; s < WA; ++s) {
+    const bool on = k >= 0 && s < wart;
+    ai[s] = on ? ai[s] : -1;
+    av[s] = on ? av[s] : (TA)0;
+  }
+}
+
+// The row values v_ip (v_ip G_pp - 2 c_p + sum_q v_iq 2 G_pq) of C samples from the lane's A line.
+template <int C, int WA, typename TA>
+__device__ __forceinline__ void row_eval(const int (&ai)[WA], const TA (&av)[WA], int j, const double (&v)[C],
+                                         double (&row)[C]) {
+  double xd[WA];
+  double cp = 0.0, gpp = 0.0;
+#pragma unroll
+  for (int s = 0; s < WA; ++s) {
+    xd[s] = (double)av[s];
+    gpp = fma(xd[s], xd[s], gpp);
+    cp = __dadd_rn(cp, (ai[s] == j) ? xd[s] : 0.0);
+  }
+  double acc[C];
+#pragma unroll
+  for (int i = 0; i < C; ++i) acc[i] = 0.0;
+  row_round<1, C, WA, TA>(ai, av, xd, v, acc);
+  row_round<2, C, WA, TA>(ai, av, xd, v, acc);
+  row_round<3, C, WA, TA>(ai, av, xd, v, acc);
+  row_round<4, C, WA, TA>(ai, av, xd, v, acc);
+  row_round<5, C, WA, TA>(ai, av, xd, v, acc);
+  row_round<6, C, WA, TA>(ai, av, xd, v, acc);
+  row_round<7, C, WA, TA>(ai, av, xd, v, acc);
+  row_round<8, C, WA, TA>(ai, av, xd, v, acc);
+#pragma unroll
+  for (int i = 0; i < C; ++i) row[i] = __dmul_rn(v[i], __dadd_rn(fma(v[i], gpp, -2.0 * cp), acc[i]));
+}
+
+// Sum over the 16 lanes of a row, fixed tree (row_shr 1, 2, 4, 8): lane 15 of the row holds it.
+__device__ __forceinline__ double row16_sum(double x) {
+  x = __dadd_rn(x, dpp_d<0x111, 0xf>(x));
+  x = __dadd_rn(x, dpp_d<0x112, 0xf>(x));
+  x = __dadd_rn(x, dpp_d<0x114, 0xf>(x));
+  x = __dadd_rn(x, dpp_d<0x118, 0xf>(x));
+  return x;
+}
+
+template <int W, int WA, bool FULL, typename TA, typename TV>
+__device__ __forceinline__ void resid_row16_body(int32_t line_begin, int32_t line_end, int32_t wrt, int32_t wart,
+                                                 int32_t B, int32_t nblk, const int32_t* __restrict__ m_idx,
+                                                 int64_t idx_bstride, const TV* __restrict__ m_val,
+                                                 int64_t val_bstride, const int32_t* __restrict__ a_idx,
+                                                 const TA* __restrict__ a_val, double* __restrict__ partials,
+                                                 double (&sred)[kRowC][kNT / 16]) {
+  static_assert(W <= 16, "one slot per lane of a 16-lane row");
+  constexpr int kGroups = kNT / 16;
+  const int blk = xcd_remap(blockIdx.x, gridDim.x);
+  const int r = threadIdx.x >> 4, p = threadIdx.x & 15;
+  const int rw = (threadIdx.x & 63) >> 4;  // row inside the wave
+#pragma unroll 1
+  for (int b0 = 0; b0 < B; b0 += kRowC) {
+    const int nb = min(kRowC, B - b0);
+    double tot[kRowC];  // this row's sum over its 16 lines (valid in lane 15 of the row)
+#pragma unroll
+    for (int i = 0; i < kRowC; ++i) tot[i] = 0.0;
+    // Software pipeline over the block's 16 line groups: while group it is evaluated, the A
+    // lines of group it + 1 and the slot indices / values of group it + 2 are in flight, so the
+    // dependent gather (indices -> A lines) never stalls a wave.
+    int kn[kRowC];  // raw slot indices / values of the group being loaded
+    TV xn[kRowC];
+    auto load_group = [&](int it) {
+      const int j = line_begin + blk * kNT + it * 16 + r;
+      const int jj = j < line_end ? j : line_begin;
+      const int64_t o = (int64_t)jj * wrt + min(p, wrt - 1);
+      // sample bases recomputed here (opaque first sample): 8 x 2 loop-invariant 64-bit bases
+      // held across the loop would take 32 SGPRs, and the matching needs SGPR pairs for its masks
+      int bs = b0;
+      asm volatile("" : "+s"(bs));
+#pragma unroll
+      for (int i = 0; i < kRowC; ++i) {
+        const int b = min(bs + i, B - 1);
+        kn[i] = m_idx[(int64_t)b * idx_bstride + o];
+        xn[i] = m_val[(int64_t)b * val_bstride + o];
+      }
+    };
+    // a group's masked indices / values, its union index and whether its row is shared
+    auto take_group = [&](int it, int (&kk)[kRowC], double (&v)[kRowC], int& ku, bool& shared) {
+      const int j = line_begin + blk * kNT + it * 16 + r;
+      const bool slot = j < line_end && p < W && p < wrt;
+      int kmax = -1, kmin = INT_MAX;
+#pragma unroll
+      for (int i = 0; i < kRowC; ++i) {
+        const int k = kn[i];
+        const bool on = slot && i < nb && k >= 0;
+        kk[i] = on ? k : -1;
+        v[i] = on ? (double)xn[i] : 0.0;
+        if (on) {
+          kmax = max(kmax, k);
+          kmin = min(kmin, k);
+        }
+      }
+      // a row is on the shared path when every lane's valid indices agree across the chunk
+      const uint64_t bad = __ballot(!(kmax < 0 || kmin == kmax));
+      shared = ((bad >> (rw * 16)) & 0xFFFFull) == 0;
+      ku = kmax;
+    };
+    int kc[kRowC], kuc;
+    double vc[kRowC];
+    bool shc;
+    int aic[WA];
+    TA avc[WA];
+    load_group(0);
+    take_group(0, kc, vc, kuc, shc);
+    row_load<WA, FULL, TA>(kuc, wart, a_idx, a_val, aic, avc);
+    if (kGroups > 1) load_group(1);
+#pragma unroll 1
+    for (int it = 0; it < kGroups; ++it) {
+      int kx[kRowC], kux = -1;
+      double vx[kRowC];
+      bool shx = true;
+      int aix[WA];
+      TA avx[WA];
+      if (it + 1 < kGroups) {  // next group: its A lines into flight, then the slots of it + 2
+        take_group(it + 1, kx, vx, kux, shx);
+        row_load<WA, FULL, TA>(kux, wart, a_idx, a_val, aix, avx);
+        if (it + 2 < kGroups) load_group(it + 2);
+      }
+      const int j = line_begin + blk * kNT + it * 16 + r;
+      double row[kRowC];
+      if (shc) {
+        row_eval<kRowC, WA, TA>(aic, avc, j, vc, row);
+      } else {
+#pragma unroll 1
+        for (int i = 0; i < nb; ++i) {  // one sample at a time on its own index set
+          int ki = -1;
+          double vi[1] = {0.0}, ri[1];
+#pragma unroll
+          for (int u = 0; u < kRowC; ++u) {
+            ki = u == i ? kc[u] : ki;
+            vi[0] = u == i ? vc[u] : vi[0];
+          }
+          int ai1[WA];
+          TA av1[WA];
+          row_load<WA, FULL, TA>(ki, wart, a_idx, a_val, ai1, av1);
+          row_eval<1, WA, TA>(ai1, av1, j, vi, ri);
+#pragma unroll
+          for (int u = 0; u < kRowC; ++u) row[u] = u == i ? ri[0] : row[u];
+        }
+#pragma unroll
+        for (int u = 0; u < kRowC; ++u) row[u] = u < nb ? row[u] : 0.0;
+      }
+      const bool valid = j < line_end;
+#pragma unroll
+      for (int i = 0; i < kRowC; ++i) {
+        const double s = row16_sum(row[i]);
+        tot[i] = __dadd_rn(tot[i], valid ? __dadd_rn(1.0, s) : 0.0);
+      }
+#pragma unroll
+      for (int i = 0; i < kRowC; ++i) {
+        kc[i] = kx[i];
+        vc[i] = vx[i];
+      }
+#pragma unroll
+      for (int s = 0; s < WA; ++s) {
+        aic[s] = aix[s];
+        avc[s] = avx[s];
+      }
+      shc = shx;
+    }
+    if (p == 15) {
+#pragma unroll
+      for (int i = 0; i < kRowC; ++i) sred[i][r] = tot[i];
+    }
+    __syncthreads();
+    if (threadIdx.x < nb) {
+      double s = 0.0;
+#pragma unroll
+      for (int u = 0; u < kGroups; ++u) s = __dadd_rn(s, sred[threadIdx.x][u]);
+      partials[(int64_t)(b0 + threadIdx.x) * nblk + blk] = s;
+    }
+    __syncthreads();
+  }
+}
+
+template <int W, int WA, typename TA, typename TV>
+__global__ __launch_bounds__(kNT) void k_resid_row16(int32_t line_begin, int32_t line_end, int32_t wrt, int32_t wart,
+                                                     int32_t B, int32_t nblk, const int32_t* __restrict__ m_idx,
+                                                     int64_t idx_bstride, const TV* __restrict__ m_val,
+                                                     int64_t val_bstride, const int32_t* __restrict__ a_idx,
+                                                     const TA* __restrict__ a_val, double* __restrict__ partials) {
+  __shared__ double sred[kRowC][kNT / 16];
+  if (wart == WA)
+    resid_row16_body<W, WA, true, TA, TV>(line_begin, line_end, wrt, wart, B, nblk, m_idx, idx_bstride, m_val,
                                           val_bstride, a_idx, a_val, partials, sred);
+  else
+    resid_row16_body<W, WA, false, TA, TV>(line_begin, line_end, wrt, wart, B, nblk, m_idx, idx_bstride, m_val,
+                                           val_bstride, a_idx, a_val, partials, sred);
 }
 
 __global__ __launch_bounds__(kNT) void k_resid_reduce(const double* __restrict__ partials, int32_t nblk,
@@ -472,9 +756,12 @@ void launch_resid(int32_t lb, int32_t le, int32_t wrt, int32_t wart, int32_t B, 
   if constexpr (W <= 7)
     k_resid_shared<W, WA, TA, TV, kWaves><<<nblk, kNT, 0, s>>>(lb, le, wrt, wart, B, nblk, mi, ib, static_cast<const TV*>(mv),
                                                         vb, ai, static_cast<const TA*>(av), partials);
-  else
+  else if (getenv("SPAI_RESID_WIDE_OLD"))
     k_resid_wide<W, WA, TA, TV><<<nblk, kNT, 0, s>>>(lb, le, wrt, wart, B, nblk, mi, ib, static_cast<const TV*>(mv), vb,
                                                       ai, static_cast<const TA*>(av), partials);
+  else
+    k_resid_row16<W, WA, TA, TV><<<nblk, kNT, 0, s>>>(lb, le, wrt, wart, B, nblk, mi, ib, static_cast<const TV*>(mv), vb,
+                                                       ai, static_cast<const TA*>(av), partials);
 }
 
 struct ResidVariant {

@@ -197,6 +197,23 @@ def rollout_finish(lg, B, lmax, counts, ws, actions, fwd, part: int, nparts: int
     return t_dev
 
 
+def narrow_values(a_lines: Lines) -> torch.Tensor:
+    """A's values as the residual kernels read them: an fp64 A whose every value is exact in
+    fp32 (stencils, integer-valued matrices) is handed over as fp32 — the same numbers, widened
+    back exactly in the kernel, so every result keeps its bits — which halves the registers its
+    13-wide lines take and lets k_resid_wide match a line's entry pairs once for 8 samples
+    instead of 4.  Checked once per Lines object (one device->host sync) and cached on it."""
+    v = a_lines.val
+    if v.dtype != torch.float64:
+        return v
+    c = getattr(a_lines, "_narrow", None)
+    if c is None or c[0] is not v:
+        f = v.float()
+        c = (v, f if torch.equal(f.double(), v) else v)
+        a_lines._narrow = c
+    return c[1]
+
+
 def residual_lines(m_idx: torch.Tensor, m_val: torch.Tensor, a_lines: Lines, line_begin: int = 0,
                    line_end: int | None = None) -> torch.Tensor:
     """res2 [B] fp64 = sum over lines [begin, end) of ||sum_p M_b[l,p] A_line(idx_b[l,p]) - e_l||^2
@@ -215,13 +232,14 @@ def residual_lines(m_idx: torch.Tensor, m_val: torch.Tensor, a_lines: Lines, lin
     m_val = m_val.contiguous()
     if m_idx.shape[-2:] != (n, W) or (m_idx.dim() == 3 and m_idx.shape[0] != B):
         raise ValueError(f"m_idx shape {tuple(m_idx.shape)} does not match m_val {tuple(m_val.shape)}")
+    a_val = narrow_values(a_lines)
     res2 = torch.empty(B, dtype=torch.float64, device=m_val.device)
     nb = _l().spai_residual_workspace_bytes(max(line_end - line_begin, 0), B)
     ws = _lib.workspace(nb, m_val.device, "residual")
     with _timed("residual_lines"):
         st = _l().spai_residual_lines(n, line_begin, line_end, W, _lib.ptr(m_idx), n * W if m_idx.dim() == 3 else 0,
                                       _lib.ptr(m_val), _DT[m_val.dtype], n * W, a_lines.width, _lib.ptr(a_lines.idx),
-                                      _lib.ptr(a_lines.val), _DT[a_lines.val.dtype], B, _lib.ptr(res2),
+                                      _lib.ptr(a_val), _DT[a_val.dtype], B, _lib.ptr(res2),
                                       _lib.ptr(ws), ws.numel(), _lib.stream_ptr(m_val.device))
     _lib.check(st, "spai_residual_lines")
     return res2

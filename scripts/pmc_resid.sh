@@ -6,6 +6,7 @@ OUT=${OUT:-gpurun_out/pmc_resid}
 mkdir -p $OUT
 i=0
 for CTRS in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_WAIT_INST_ANY SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_LDS GRBM_GUI_ACTIVE" \
+            "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_INSTS_SALU SQ_WAVE_CYCLES GRBM_GUI_ACTIVE" \
             "TA_TA_BUSY_sum TD_TD_BUSY_sum TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum GRBM_GUI_ACTIVE" \
             "FETCH_SIZE"; do
   i=$((i+1))

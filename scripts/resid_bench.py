@@ -4,7 +4,9 @@ M_b = the candidate pattern (A's own lines) with an independent 25 % of the slot
 sample and random values (the GFlowNet candidates' structure); --distinct gives every sample
 random indices instead (the per-sample path).  Prints ms per launch and the fraction of the HBM
 roofline at bytes(A) + B x bytes(M_b).
-usage: python scripts/resid_bench.py [--config c4] [--batch 8] [--iters 20] [--distinct]
+--wide (C3): M on the 13-wide axial candidate pattern of the bench's C3 config with fp64 values
+(k_resid_row16), instead of A's own 7-wide pattern.
+usage: python scripts/resid_bench.py [--config c4] [--batch 8] [--iters 20] [--distinct] [--wide]
 """
 import argparse
 import json
@@ -17,7 +19,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 import bench  # noqa: E402
-from gflownet_spai_amd import PreconditionerEnv, kernels, poisson_2d, poisson_3d  # noqa: E402
+from gflownet_spai_amd import PreconditionerEnv, axial_pattern_3d, kernels, poisson_2d, poisson_3d  # noqa: E402
 
 
 def main():
@@ -26,6 +28,9 @@ def main():
     ap.add_argument("--batch", type=int, default=8)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--distinct", action="store_true")
+    ap.add_argument("--wide", action="store_true")
+    ap.add_argument("--dry", action="store_true", help="print the inputs, launch nothing")
+    ap.add_argument("--mf64", action="store_true", help="fp64 M values on A's own pattern")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     dims, grid, dtype, _ = bench.CONFIGS[args.config]
@@ -36,6 +41,10 @@ def main():
     B = args.batch
     g = torch.Generator(device=dev).manual_seed(0)
     pat = a.idx
+    mdt = torch.float64 if args.mf64 else torch.float32
+    if args.wide:  # the C3 candidate pattern (13-wide), fp64 M
+        env = PreconditionerEnv(n, axial_pattern_3d(grid, 2), A, side="AM", fill="copy", device=dev)
+        pat, mdt = env.pattern.idx, torch.float64
     W = pat.shape[1]
     if args.distinct:
         idx = torch.randint(0, n, (B, n, W), generator=g, device=dev, dtype=torch.int32)
@@ -47,15 +56,26 @@ def main():
         idx = pat.unsqueeze(0).repeat(B, 1, 1)
     idx[torch.rand(idx.shape, generator=g, device=dev) < 0.25] = -1
     idx = idx.contiguous()
-    m = torch.randn((B, n, W), generator=g, device=dev, dtype=torch.float32)
+    m = torch.randn((B, n, W), generator=g, device=dev, dtype=mdt)
+    if args.dry:
+        av = kernels.narrow_values(a)
+        print(json.dumps({"idx": [list(idx.shape), list(idx.stride()), str(idx.dtype), int(idx.min()), int(idx.max()),
+                                  idx.data_ptr() % 256],
+                          "m": [list(m.shape), list(m.stride()), str(m.dtype), m.data_ptr() % 256],
+                          "a_idx": [list(a.idx.shape), list(a.idx.stride()), int(a.idx.min()), int(a.idx.max()),
+                                    a.idx.data_ptr() % 256],
+                          "a_val": [list(av.shape), list(av.stride()), str(av.dtype), av.data_ptr() % 256],
+                          "n": n, "W": W, "B": B, "a_width": a.width}))
+        return
     kernels.residual_lines(idx, m, a)
     kernels.TIMERS = {}
     for _ in range(args.iters):
         kernels.residual_lines(idx, m, a)
     torch.cuda.synchronize()
     ms = sum(kernels.timer_ms("residual_lines")) / args.iters
-    nbytes = a.idx.numel() * 4 + a.val.numel() * a.val.element_size() + B * n * W * (4 + m.element_size())
-    print(json.dumps({"config": args.config, "B": B, "distinct": args.distinct, "ms": ms, "bytes": nbytes,
+    av = kernels.narrow_values(a)
+    nbytes = a.idx.numel() * 4 + av.numel() * av.element_size() + B * n * W * (4 + m.element_size())
+    print(json.dumps({"config": args.config, "B": B, "W": W, "distinct": args.distinct, "ms": ms, "bytes": nbytes,
                       "frac": nbytes / (ms * 1e-3) / 8e12}))
 
 

@@ -648,22 +648,34 @@ def test_stream_counter_and_graph_replay():
     assert not torch.equal(outs[0][2], outs[1][2])  # the fill ran again on the new removal sets
 
 
-@pytest.mark.parametrize("dims,W,adt,mdt,side", [(2, 5, np.float32, np.float32, "col"),
-                                                  (2, 7, np.float32, np.float64, "row"),
-                                                  (3, 7, np.float64, np.float64, "col"),
-                                                  (3, 13, np.float64, np.float32, "row")])
-def test_residual_lines_arbitrary_m_vs_scipy(dims, W, adt, mdt, side):
+def _inexact(v, rng):
+    """fp64 values that are NOT exact in fp32 (so the kernels read them as fp64, not narrowed)."""
+    return v * (1.0 + 2.0 ** -40 * rng.integers(1, 1000, v.shape))
+
+
+@pytest.mark.parametrize("dims,W,adt,mdt,side,exact", [(2, 5, np.float32, np.float32, "col", True),
+                                                        (2, 7, np.float32, np.float64, "row", True),
+                                                        (3, 7, np.float64, np.float64, "col", True),
+                                                        (3, 7, np.float64, np.float64, "col", False),
+                                                        (3, 13, np.float64, np.float32, "row", True),
+                                                        (3, 13, np.float64, np.float64, "col", True),
+                                                        (3, 13, np.float64, np.float64, "row", False)])
+def test_residual_lines_arbitrary_m_vs_scipy(dims, W, adt, mdt, side, exact):
     """The generic batched SpMM residual (spai_residual_lines) of B DISTINCT random sparse M
     (random indices anywhere in [0, n), random values, empty slots) against scipy's exact fp64
     ||M A - I||_F^2 (row lines) / ||A M - I||_F^2 (column lines), per sample; one shared index
-    set too (idx stride 0); line ranges sum to the whole."""
+    set too (idx stride 0); line ranges sum to the whole.  fp64 A with fp32-exact values runs
+    narrowed (kernels.narrow_values); `exact=False` keeps the fp64-A kernels covered."""
     from gflownet_spai_amd import kernels
     from gflownet_spai_amd.layout import build_lines
     r, c, v, n = (O.poisson2d(12, adt) if dims == 2 else O.poisson3d(6, adt))
+    if not exact:
+        v = _inexact(v, np.random.default_rng(1))
     A = sp.csr_matrix((v.astype(np.float64), (r, c)), shape=(n, n))
     a_lines = build_lines(torch.from_numpy(r), torch.from_numpy(c), torch.from_numpy(v), n, side, DEV)
+    assert (kernels.narrow_values(a_lines).dtype == torch.float32) == (exact or adt == np.float32)
     rng = np.random.default_rng(W)
-    B = 3
+    B = 3 if W < 13 else 11  # 13-wide: chunks of 8 (fp32-exact A) or 4 samples, and a partial chunk
     idx = rng.integers(0, n, (B, n, W)).astype(np.int32)
     idx[rng.random((B, n, W)) < 0.3] = -1
     for b in range(B):  # distinct indices inside a line (the ELL lines of a sparse matrix)
@@ -696,6 +708,36 @@ def test_residual_lines_arbitrary_m_vs_scipy(dims, W, adt, mdt, side):
     np.testing.assert_allclose(parts.cpu().numpy(), got, rtol=1e-13)
 
 
+@pytest.mark.parametrize("W,mdt", [(7, np.float64), (7, np.float32), (13, np.float64)])
+def test_residual_lines_multiblock_batch8(W, mdt):
+    """Many blocks and a full chunk: B = 8 samples of an fp64 3-D Laplacian's pattern (W = 7) or
+    the 13-wide axial pattern, 25 % of the slots removed per sample, random values, at
+    n = 16^3 (16 blocks of 256 lines) vs scipy's fp64 ||A M_b - I||_F^2."""
+    from gflownet_spai_amd import axial_pattern_3d, kernels
+    from gflownet_spai_amd.layout import build_lines
+    r, c, v, n = O.poisson3d(16, np.float64)
+    A = sp.csr_matrix((v, (r, c)), shape=(n, n))
+    a_lines = build_lines(torch.from_numpy(r), torch.from_numpy(c), torch.from_numpy(v), n, "col", DEV)
+    if W == 7:
+        pat = a_lines.idx.cpu().numpy()
+    else:
+        P = axial_pattern_3d(16, 2).coalesce()
+        pr, pc = P.indices()
+        pat = build_lines(pr, pc, P.values(), n, "col", DEV).idx.cpu().numpy()
+    rng = np.random.default_rng(11)
+    B = 8
+    idx = np.repeat(pat[None], B, 0).copy()
+    idx[rng.random(idx.shape) < 0.25] = -1
+    val = rng.standard_normal(idx.shape).astype(mdt)
+    got = kernels.residual_lines(torch.from_numpy(idx).to(DEV), torch.from_numpy(val).to(DEV), a_lines).cpu().numpy()
+    I = sp.identity(n, format="csr")
+    for b in range(B):
+        ok = idx[b] >= 0
+        lines, _ = np.nonzero(ok)
+        M = sp.csr_matrix((val[b][ok].astype(np.float64), (idx[b][ok], lines)), shape=(n, n))
+        assert got[b] == pytest.approx(sp.linalg.norm(A @ M - I) ** 2, rel=1e-12)
+
+
 def test_residual_lines_matches_fused_lsq_fill_residual():
     """||A M - I||_F^2 of the candidates' stored LSQ fills M (distinct kept index sets per
     sample) through the generic kernel equals the fused fill kernel's residual (which takes it
@@ -717,19 +759,21 @@ def test_residual_lines_matches_fused_lsq_fill_residual():
     np.testing.assert_allclose(got.cpu().numpy(), ref.cpu().numpy(), rtol=1e-6)
 
 
-@pytest.mark.parametrize("dims", [2, 3])
-def test_residual_lines_shared_pattern_and_conflicting_lanes(dims):
+@pytest.mark.parametrize("dims,exact", [(2, True), (3, True), (3, False)])
+def test_residual_lines_shared_pattern_and_conflicting_lanes(dims, exact):
     """k_resid_shared (2-D: A's own 5-wide pattern, fp32) and k_resid_wide (3-D: the 13-wide
-    axial C3 pattern, fp64): B = 9 samples that are sub-patterns of ONE line pattern (random
-    removals per sample: one index matching per line and chunk) except sample 3, which puts a
-    different valid index into one slot of ~10 % of the lines (those lanes evaluate every
-    sample of the chunk on its own index set).  Each sample vs scipy's exact fp64
-    ||A M_b - I||_F^2, and bit for bit vs the same sample evaluated alone (both paths apply the
-    same operations in the same order)."""
+    axial C3 pattern, fp64; fp32-exact A values: chunks of 8 samples, otherwise 4): B = 9
+    samples that are sub-patterns of ONE line pattern (random removals per sample: one index
+    matching per line and chunk) except sample 3, which puts a different valid index into one
+    slot of ~10 % of the lines (those lanes evaluate every sample of the chunk on its own index
+    set).  Each sample vs scipy's exact fp64 ||A M_b - I||_F^2, and bit for bit vs the same
+    sample evaluated alone (both paths apply the same operations in the same order)."""
     from gflownet_spai_amd import axial_pattern_3d, kernels
     from gflownet_spai_amd.layout import build_lines
     dt = np.float32 if dims == 2 else np.float64
     r, c, v, n = O.poisson2d(16, dt) if dims == 2 else O.poisson3d(7, dt)
+    if not exact:
+        v = _inexact(v, np.random.default_rng(2))
     A = sp.csr_matrix((v.astype(np.float64), (r, c)), shape=(n, n))
     a_lines = build_lines(torch.from_numpy(r), torch.from_numpy(c), torch.from_numpy(v), n, "col", DEV)
     if dims == 2:

@@ -18,10 +18,12 @@
 // algorithmic bytes per launch = bytes(A) + sum_b bytes(M_b) (SURVEY §8d with A shared by the
 // batch).  Consecutive line ranges run on one XCD (bijective XCD remap), so the A halo of
 // neighbouring blocks is served by that XCD's L2.
-// W = 13 (k_resid_wide): one thread per line for chunks of 4 samples; the line's index matching
-// runs once per chunk and each pair's product <A_line(k_p), A_line(k_q)> goes straight into the
-// chunk's quadratic forms (the 91-value Gram is never held); round 2's thread per (line,
-// sample) kernel matched every pair once per SAMPLE (C3: 1.76 ms -> 0.54 ms).
+// W = 13, A values exact in fp32 (k_resid_wide): one thread per line for chunks of 8 samples;
+// the line's index matching runs once per chunk and each pair's product
+// <A_line(k_p), A_line(k_q)> goes straight into the chunk's quadratic forms (the 91-value Gram
+// is never held).  W = 13 with fp64 A values (k_resid_row16): sixteen lanes per line, one slot
+// each, the pairs matched across lanes by DPP row rotations (C3: round 2's thread per (line,
+// sample) 1.76 ms -> chunks of 4 0.54 -> 0.21 ms; fp64 A 0.26 ms).
 // Per-block partial sums, then a fixed-order reduction per sample: the result is
 // bit-reproducible, and both kernels evaluate a line with the same operations in the same order.
 #include "spai_device.h"
@@ -46,7 +48,11 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
 template <int W, bool FULL, typename T>
 __device__ __forceinline__ void load_slots(const T* __restrict__ p, int n, T (&out)[W]) {
   constexpr int kPer = 16 / sizeof(T);
-  typedef T vec_t __attribute__((ext_vector_type(kPer)));
+  // the vector type carries the ELEMENT's alignment: a line starts at any multiple of
+  // sizeof(T), and a type that claimed 16-byte alignment let the compiler widen the scalar tail
+  // into a 16-byte load past the line (past the buffer's end on its last line: a fault when
+  // the allocation ends at a page)
+  typedef T vec_t __attribute__((ext_vector_type(kPer), aligned(sizeof(T))));
   if constexpr (FULL) {
 #pragma unroll
     for (int q = 0; q + kPer <= W; q += kPer) {
@@ -336,13 +342,12 @@ __global__ __launch_bounds__(kNT, WAVES) void k_resid_shared(int32_t line_begin,
 // The Gram itself is never stored (91 + 26 fp64 values would not fit beside the A lines).
 // Lanes whose samples disagree evaluate each sample on its own index set (line_res2_any).
 // The index matching (49 compare + select per entry pair, 78 pairs per 13-wide line) is all of
-// the kernel's work, so the chunk is as large as the registers allow:
-//   TA = float (A's values exact in fp32: the caller passes them narrowed, widened back
-//   exactly here; 91 registers for the A lines' values): C = 8 — one matching per line for
-//   the usual batch of 8;
-//   TA = double: C = 4 (182 registers of A values).
-// One wave per SIMD either way (the chunk's 8 x 13 fp64 values, the A lines and the row
-// accumulators take ~450 registers).
+// the kernel's work, so the chunk is as large as the registers allow: with A's values exact in
+// fp32 (the caller passes them narrowed, widened back exactly here; 91 registers for the A
+// lines' values) C = 8, one matching per line for the usual batch of 8, at one wave per SIMD
+// (the chunk's 8 x 13 fp64 values, the A lines and the row accumulators: ~480 registers).
+// fp64 A values would leave room for chunks of 4 only (182 registers of A values): those go to
+// k_resid_row16 instead (0.26 vs 0.47 ms at C3).
 template <int W, int WA, int C, bool FULL, typename TA, typename TV>
 __device__ __forceinline__ void resid_wide_body(int32_t line_begin, int32_t line_end, int32_t wrt, int32_t wart,
                                                 int32_t B, int32_t nblk, const int32_t* __restrict__ m_idx,
@@ -467,16 +472,14 @@ __device__ __forceinline__ void resid_wide_body(int32_t line_begin, int32_t line
   }
 }
 
-template <typename TA>
-constexpr int wide_chunk() { return sizeof(TA) == 4 ? 8 : 4; }
-
 template <int W, int WA, typename TA, typename TV>
 __global__ __launch_bounds__(kNT) void k_resid_wide(int32_t line_begin, int32_t line_end, int32_t wrt, int32_t wart,
                                                     int32_t B, int32_t nblk, const int32_t* __restrict__ m_idx,
                                                     int64_t idx_bstride, const TV* __restrict__ m_val,
                                                     int64_t val_bstride, const int32_t* __restrict__ a_idx,
                                                     const TA* __restrict__ a_val, double* __restrict__ partials) {
-  constexpr int C = wide_chunk<TA>();
+  static_assert(sizeof(TA) == 4, "fp64 A values: k_resid_row16");
+  constexpr int C = 8;
   __shared__ double sred[C][kNT / 64];
   if (wrt == W && wart == WA)
     resid_wide_body<W, WA, C, true, TA, TV>(line_begin, line_end, wrt, wart, B, nblk, m_idx, idx_bstride, m_val,
@@ -756,10 +759,10 @@ void launch_resid(int32_t lb, int32_t le, int32_t wrt, int32_t wart, int32_t B, 
   if constexpr (W <= 7)
     k_resid_shared<W, WA, TA, TV, kWaves><<<nblk, kNT, 0, s>>>(lb, le, wrt, wart, B, nblk, mi, ib, static_cast<const TV*>(mv),
                                                         vb, ai, static_cast<const TA*>(av), partials);
-  else if (getenv("SPAI_RESID_WIDE_OLD"))
+  else if constexpr (sizeof(TA) == 4)  // C3 exact-A: 0.21 ms vs 0.23 for k_resid_row16
     k_resid_wide<W, WA, TA, TV><<<nblk, kNT, 0, s>>>(lb, le, wrt, wart, B, nblk, mi, ib, static_cast<const TV*>(mv), vb,
                                                       ai, static_cast<const TA*>(av), partials);
-  else
+  else  // fp64 A: 0.26 ms vs 0.47 for k_resid_wide's chunks of 4 (C3, resid_bench.py --wide --inexact)
     k_resid_row16<W, WA, TA, TV><<<nblk, kNT, 0, s>>>(lb, le, wrt, wart, B, nblk, mi, ib, static_cast<const TV*>(mv), vb,
                                                        ai, static_cast<const TA*>(av), partials);
 }

@@ -31,10 +31,15 @@ def main():
     ap.add_argument("--wide", action="store_true")
     ap.add_argument("--dry", action="store_true", help="print the inputs, launch nothing")
     ap.add_argument("--mf64", action="store_true", help="fp64 M values on A's own pattern")
+    ap.add_argument("--pad", action="store_true", help="idx / M as views of larger buffers (overrun probe)")
+    ap.add_argument("--inexact", action="store_true", help="A values perturbed off fp32 (fp64-A kernels)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     dims, grid, dtype, _ = bench.CONFIGS[args.config]
     A = poisson_2d(grid, dtype) if dims == 2 else poisson_3d(grid, dtype)
+    if args.inexact:
+        A = A.coalesce()
+        A = torch.sparse_coo_tensor(A.indices(), A.values() * (1 + 2.0 ** -40 * torch.arange(A._nnz()) % 7), A.shape)
     n = A.shape[0]
     env = PreconditionerEnv(n, A, A, side="AM", fill="copy", device=dev)
     a = env.a_lines
@@ -57,6 +62,12 @@ def main():
     idx[torch.rand(idx.shape, generator=g, device=dev) < 0.25] = -1
     idx = idx.contiguous()
     m = torch.randn((B, n, W), generator=g, device=dev, dtype=mdt)
+    if args.pad:
+        bi = torch.full((B * n * W + 65536,), -1, dtype=idx.dtype, device=dev)
+        bi[: B * n * W] = idx.reshape(-1)
+        bm = torch.zeros(B * n * W + 65536, dtype=m.dtype, device=dev)
+        bm[: B * n * W] = m.reshape(-1)
+        idx, m = bi[: B * n * W].view(B, n, W), bm[: B * n * W].view(B, n, W)
     if args.dry:
         av = kernels.narrow_values(a)
         print(json.dumps({"idx": [list(idx.shape), list(idx.stride()), str(idx.dtype), int(idx.min()), int(idx.max()),

@@ -262,11 +262,11 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(W <= 5 ? FI
 // per sample (left-looking LDL^T, T = W(W+1)/2 doubles in registers), one wave per SIMD.
 // Masking and the per-pivot floor are those of k_gram_fill: a removed slot k only gets
 // 1/D_k := 0, so L[.][k] = 0 and m_k = 0.
-template <int W, typename TM, bool LSQ>
+template <int W, typename TM, bool LSQ, typename GT>
 __global__ __launch_bounds__(kNT) void k_gram_fill_wide(int32_t n, int32_t line_begin, int32_t line_end, int32_t wrt,
                                                         const int32_t* __restrict__ pat_act,
                                                         const float* __restrict__ pat_val,
-                                                        const double* __restrict__ gram, int32_t B,
+                                                        const GT* __restrict__ gram, int32_t B,
                                                         const uint32_t* __restrict__ removed, int32_t words,
                                                         int32_t word_base, TM* __restrict__ m_out,
                                                         double* __restrict__ partials) {
@@ -283,7 +283,7 @@ __global__ __launch_bounds__(kNT) void k_gram_fill_wide(int32_t n, int32_t line_
   const int jj = valid ? j : line_begin;
 #pragma unroll
   for (int p = 0; p < W; ++p) s_act[p][t] = (valid && p < wrt) ? pat_act[(int64_t)jj * wrt + p] : -1;
-  const double* gp = gram + (int64_t)(jj >> 6) * (T + W) * 64 + (jj & 63);
+  const GT* gp = gram + (int64_t)(jj >> 6) * (T + W) * 64 + (jj & 63);
   const int nvl = min(kNT, line_end - (line_begin + lb * kNT));
   // the slots' bitmap words of the next sample are loaded while the current one is solved
   uint32_t wd[W];
@@ -313,13 +313,13 @@ __global__ __launch_bounds__(kNT) void k_gram_fill_wide(int32_t n, int32_t line_
     // the samples and factors a second, working copy per sample (463 VGPRs, one wave per SIMD,
     // no spills).  Re-reading them per sample instead (an opaque address, 254 VGPRs, two waves
     // per SIMD) measured 286 vs 183 us at C3: the L2 re-reads cost more than the occupancy buys.
-    const double* gps = gp;
+    const GT* gps = gp;  // fp32 storage only when exact (spai_gram_compact): the same values
 #pragma unroll
-    for (int q = 0; q < T; ++q) a[q] = gps[q * 64];
+    for (int q = 0; q < T; ++q) a[q] = (double)gps[q * 64];
     double r2 = 1.0;
     if constexpr (LSQ) {
 #pragma unroll
-      for (int k = 0; k < W; ++k) y[k] = gps[(T + k) * 64];  // c, solved in place below
+      for (int k = 0; k < W; ++k) y[k] = (double)gps[(T + k) * 64];  // c, solved in place below
       // left-looking LDL^T in place (column k of the packed upper triangle at step k), so the
       // pivot test reads the ORIGINAL G_kk: the per-pivot floor 1e-13 G_kk of k_gram_fill and
       // fill.hip's k_line, with no extra registers.  Column k first becomes u_jk = G_jk -
@@ -366,7 +366,7 @@ __global__ __launch_bounds__(kNT) void k_gram_fill_wide(int32_t n, int32_t line_
         y[p] = ((keep >> p) & 1u) ? (double)pat_val[(int64_t)jj * wrt + (p < wrt ? p : 0)] : 0.0;
 #pragma unroll
       for (int p = 0; p < W; ++p) {
-        double acc = y[p] * a[gidx<W>(p, p)] - 2.0 * gps[(T + p) * 64];
+        double acc = y[p] * a[gidx<W>(p, p)] - 2.0 * (double)gps[(T + p) * 64];
 #pragma unroll
         for (int q = p + 1; q < W; ++q) acc += 2.0 * y[q] * a[gidx<W>(p, q)];
         r2 += y[p] * acc;
@@ -409,10 +409,14 @@ template <int W, typename TM, bool LSQ>
 hipError_t launch_fill(int32_t n, int32_t lb, int32_t le, int32_t wrt, const int32_t* pa, const float* pv,
                        const void* g, bool g32, int32_t B, const uint32_t* rm, int32_t words, int32_t wb,
                        void* mo, double* partials, int32_t nparts, hipStream_t s) {
-  if constexpr (W > 7)
-    k_gram_fill_wide<W, TM, LSQ><<<nparts, kNT, 0, s>>>(n, lb, le, wrt, pa, pv, static_cast<const double*>(g), B, rm,
-                                                       words, wb, static_cast<TM*>(mo), partials);
-  else if (g32)
+  if constexpr (W > 7) {
+    if (g32)
+      k_gram_fill_wide<W, TM, LSQ, float><<<nparts, kNT, 0, s>>>(n, lb, le, wrt, pa, pv, static_cast<const float*>(g),
+                                                                  B, rm, words, wb, static_cast<TM*>(mo), partials);
+    else
+      k_gram_fill_wide<W, TM, LSQ, double><<<nparts, kNT, 0, s>>>(n, lb, le, wrt, pa, pv, static_cast<const double*>(g),
+                                                                   B, rm, words, wb, static_cast<TM*>(mo), partials);
+  } else if (g32)
     k_gram_fill<W, TM, LSQ, float><<<nparts, kNT, 0, s>>>(n, lb, le, wrt, pa, pv, static_cast<const float*>(g), B, rm,
                                                            words, wb, static_cast<TM*>(mo), partials);
   else
@@ -514,8 +518,8 @@ extern "C" int spai_fill_lines_gram(int32_t fill_mode, int32_t n, int32_t line_b
     set_error("spai_fill_lines_gram: width W=%d above the compiled 13", W);
     return SPAI_ERR_UNSUPPORTED;
   }
-  SPAI_CHECK_ARG(gram_dtype == SPAI_DTYPE_F64 || (gram_dtype == SPAI_DTYPE_F32 && wc <= 7),
-                 "spai_fill_lines_gram: gram dtype %d (fp32 only for widths <= 7)", gram_dtype);
+  SPAI_CHECK_ARG(gram_dtype == SPAI_DTYPE_F64 || gram_dtype == SPAI_DTYPE_F32, "spai_fill_lines_gram: gram dtype %d",
+                 gram_dtype);
   const bool g32 = gram_dtype == SPAI_DTYPE_F32;
   const int32_t nparts = (nl + kNT - 1) / kNT;
   SPAI_CHECK_ARG(workspace_bytes >= sizeof(double) * (size_t)nparts * B, "spai_fill_lines_gram: workspace too small");

@@ -314,7 +314,7 @@ def gram_compact(gram: torch.Tensor, pattern: Lines):
     """fp32 copy of an fp64 Gram cache if every entry survives the round trip exactly (then the
     fill is bit-identical from it and streams half the Gram bytes), else None.  One host sync
     (once per env)."""
-    if pattern.width > 7:
+    if pattern.width > 13:
         return None
     g32 = torch.empty(gram.numel(), dtype=torch.float32, device=gram.device)
     exact = torch.ones(1, dtype=torch.int32, device=gram.device)

@@ -221,7 +221,7 @@ int spai_fill_residual(int32_t fill_mode, int32_t n, int32_t line_begin, int32_t
  * (use spai_fill_residual; its LSQ mode covers W <= 7).  Workspace: spai_fill_workspace_bytes(line_end - line_begin, B).
  * spai_gram_compact writes the same entries as fp32 (same blocked layout, half the bytes) and
  * clears *exact (caller sets it to 1) if any entry changes in the fp64 -> fp32 -> fp64 round
- * trip; only an exact copy may be used (gram_dtype SPAI_DTYPE_F32, widths W <= 7): the fill
+ * trip; only an exact copy may be used (gram_dtype SPAI_DTYPE_F32, widths W <= 13): the fill
  * then computes bit for bit what it computes from the fp64 cache (e.g. integer stencils,
  * whose G and c are small integers), with 80 instead of 160 bytes per 5-wide line. */
 size_t spai_gram_bytes(int32_t n, int32_t W);

@@ -112,15 +112,22 @@ def test_c4_lsq_fill_full_size_vs_oracle():
 
 def test_c3_lsq_fill_13_wide_fp64_vs_oracle():
     """C3 64^3 7-pt fp64 with the 13-wide axial candidate pattern (|J| <= 13,
-    |I| <= 37): one candidate's M over all 262,144 columns and ||AM - I||_F vs the oracle."""
-    from gflownet_spai_amd import PreconditionerEnv, axial_pattern_3d, poisson_3d
+    |I| <= 37): one candidate's M over all 262,144 columns and ||AM - I||_F vs the oracle.
+    The integer stencil's Gram cache round-trips through fp32, so the env streams it as fp32:
+    the fill from the fp64 cache gives the same bits."""
+    from gflownet_spai_amd import PreconditionerEnv, axial_pattern_3d, kernels, poisson_3d
     A = poisson_3d(64)
     P = axial_pattern_3d(64)
     n = A.shape[0]
     env = PreconditionerEnv(n, P, A, side="AM", fill="lsq", keep_m=True)
-    assert env.pattern.width == 13 and env.gram is not None and env.gram.dtype == torch.float64
-    removed, _ = _candidate(env, 77)
+    assert env.pattern.width == 13 and env.gram is not None and env.gram.dtype == torch.float32
+    removed, log = _candidate(env, 77)
     assert env.last_m.dtype == torch.float64
+    g64 = kernels.gram_build(env.pattern, env.a_lines)
+    res64, m64 = kernels.fill_residual_gram(env.pattern, g64, log.removed, True, store_m=True, m_dtype=torch.float64)
+    assert torch.equal(m64, env.last_m)
+    np.testing.assert_allclose(res64.double().sqrt().cpu().numpy(), env.last_residual.double().cpu().numpy(),
+                               rtol=1e-15)
     Ai, Pi = A.coalesce(), P.coalesce()
     A_sp = sp.csr_matrix((Ai.values().numpy(), tuple(Ai.indices().numpy())), shape=(n, n))
     P_sp = sp.coo_matrix((Pi.values().numpy(), tuple(Pi.indices().numpy())), shape=(n, n))

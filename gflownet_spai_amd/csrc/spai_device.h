@@ -277,9 +277,31 @@ __device__ __forceinline__ void write_reward(int b, double res2, const RewardArg
   if (ra.reward32) ra.reward32[b] = (float)rw;
 }
 
+// Wave-wide int64 sum by DPP (row shifts + row broadcasts, as wave_incl_scan; no LDS permutes),
+// valid in every lane.  Integer: any association gives the same bits.
+template <int kCtrl, int kRowMask>
+__device__ __forceinline__ int64_t dpp_add_i64(int64_t v) {
+  const uint64_t u = (uint64_t)v;
+  const int lo = dpp_i<kCtrl, kRowMask>(0, (int)(uint32_t)u), hi = dpp_i<kCtrl, kRowMask>(0, (int)(uint32_t)(u >> 32));
+  return v + (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+__device__ __forceinline__ int64_t wave_sum_i64(int64_t v) {
+  v = dpp_add_i64<0x111, 0xf>(v);
+  v = dpp_add_i64<0x112, 0xf>(v);
+  v = dpp_add_i64<0x114, 0xf>(v);
+  v = dpp_add_i64<0x118, 0xf>(v);
+  v = dpp_add_i64<0x142, 0xa>(v);
+  v = dpp_add_i64<0x143, 0xc>(v);
+  const uint64_t u = (uint64_t)v;
+  const int lo = __builtin_amdgcn_readlane((int)(uint32_t)u, 63), hi = __builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), 63);
+  return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+
 // res2_out[b] and/or limbs_out[b][kLimbSlots] from per-block fp64 partials [B][nparts], one block
 // per sample (the fill kernels' second half).  Every load of a round is issued before the
-// conversions (a dependent load per partial made this a 16 us latency chain at C4).
+// conversions (a dependent load per partial made this a 16 us latency chain at C4); DPP wave
+// sums of the limbs.  The conversions are the VALU chain: 1024 threads x 4 partials (C4's 4096
+// in one round); 256 threads x 16 took 13 us against 10.
 template <int NT>
 __global__ __launch_bounds__(NT) void k_fixed_reduce(const double* __restrict__ partials, int32_t nparts,
                                                      double* __restrict__ res2_out, int64_t* __restrict__ limbs_out,
@@ -301,7 +323,7 @@ __global__ __launch_bounds__(NT) void k_fixed_reduce(const double* __restrict__ 
     for (int j = 0; j < kPer; ++j) fixed_add(v[j], L);
   }
 #pragma unroll
-  for (int q = 0; q < 7; ++q) L[q] = wave_sum(L[q]);
+  for (int q = 0; q < 7; ++q) L[q] = wave_sum_i64(L[q]);
   if (lane == 0) {
 #pragma unroll
     for (int q = 0; q < 7; ++q) sred[wave][q] = L[q];

@@ -124,6 +124,19 @@ def _free_port():
     return p
 
 
+def _by_value(x, back=False):
+    """Tensors <-> numpy arrays through the result queue: numpy pickles by value, while CPU
+    tensors travel as shared-memory file descriptors that a rank which has already exited can no
+    longer hand over (a race that failed this test once)."""
+    if isinstance(x, dict):
+        return {k: _by_value(v, back) for k, v in x.items()}
+    if back and isinstance(x, np.ndarray):
+        return torch.from_numpy(x)
+    if not back and isinstance(x, torch.Tensor):
+        return x.numpy()
+    return x
+
+
 def _rank_main(rank, world, port, bl, q):
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -155,7 +168,7 @@ def _rank_main(rank, world, port, bl, q):
                 out["slices_guard"] = True  # the full log needs the explicit collective
             log.gather_parts()
             out["slices"] = dict(rewards=log.rewards.cpu(), actions=log.actions.cpu(), fwd=log.fwd_probs.cpu())
-        q.put((rank, out))
+        q.put((rank, _by_value(out)))
     finally:
         dist.destroy_process_group()
 
@@ -170,7 +183,7 @@ def test_two_processes_columns_and_slices_match_one_process():
     for p in procs:
         p.start()
     try:
-        res = dict(q.get(timeout=240) for _ in procs)
+        res = {r: _by_value(o, back=True) for r, o in (q.get(timeout=240) for _ in procs)}
     finally:
         for p in procs:
             p.join(timeout=60)

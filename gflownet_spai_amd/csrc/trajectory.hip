@@ -267,6 +267,39 @@ __device__ __forceinline__ uint64_t block_excl_scan_u64(uint64_t c, uint64_t* ld
   return base + incl - c;
 }
 
+#ifdef SPAI_PROF  // phase timing (variant builds only: make EXTRA=-DSPAI_PROF); slots 16*kernel + phase
+__device__ unsigned long long g_prof[64];
+__device__ __forceinline__ uint64_t prof_stamp() {
+  uint64_t t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+#define PROF_INIT uint64_t pf_t = prof_stamp(), pf_acc[16] = {};
+#define PROF(i)                          \
+  if (threadIdx.x == 0) {                \
+    const uint64_t pf_n = prof_stamp();   \
+    pf_acc[i] += pf_n - pf_t;            \
+    pf_t = pf_n;                         \
+  }
+#define PROF_END(base)     \
+  if (threadIdx.x == 0)    \
+    for (int q = 0; q < 16; ++q) atomicAdd(&g_prof[(base) + q], (unsigned long long)pf_acc[q]);
+extern "C" int spai_debug_prof(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_prof), sizeof(g_prof)) != hipSuccess) return 2;
+  if (reset) {
+    static const unsigned long long z[64] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, sizeof(z)) != hipSuccess) return 2;
+  }
+  return 0;
+}
+#else
+#define PROF_INIT
+#define PROF(i)
+#define PROF_END(base)
+#endif
+
 // ------------------------------------------------------------------ k_presample
 // Philox stream id of this rollout: the kernel argument, or the device counter when the caller
 // keeps one (graph replays draw fresh rollouts; k_bsum advances it at the end of the select phase).
@@ -369,6 +402,7 @@ __global__ __launch_bounds__(kSortNT) void k_splitters(int32_t E, int32_t M, int
     return;
   }
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  PROF_INIT
   __shared__ uint32_t s_smp[kSampCap];  // the sampled winner keys, compacted
   __shared__ int hist[kBins + 1];
   __shared__ int sblk[kMaxNsb + 1];
@@ -381,6 +415,7 @@ __global__ __launch_bounds__(kSortNT) void k_splitters(int32_t E, int32_t M, int
   if (tid == 0) sblk[nsb] = total;
   for (int i = tid; i <= kBins; i += kSortNT) hist[i] = 0;
   __syncthreads();
+  PROF(0)
   const int ns = min(total, kSampCap);
   const uint32_t* sb = samp + (int64_t)b * M;
   // the first ns sampled winners, compacted into LDS in two halves with every load of a half in
@@ -428,6 +463,7 @@ __global__ __launch_bounds__(kSortNT) void k_splitters(int32_t E, int32_t M, int
     s_mx[wave] = mx;
   }
   __syncthreads();
+  PROF(1)
   mn = 0xFFFFFFFFu;
   mx = 0u;
 #pragma unroll
@@ -440,6 +476,7 @@ __global__ __launch_bounds__(kSortNT) void k_splitters(int32_t E, int32_t M, int
   // histogram of the staged keys
   for (int p = tid; p < ns; p += kSortNT) atomicAdd(&hist[(s_smp[p] - mn) >> shift], 1);
   __syncthreads();
+  PROF(2)
   // exclusive scan of the bins (4 per thread), in place
   {
     int cv[4], loc = 0;
@@ -458,6 +495,7 @@ __global__ __launch_bounds__(kSortNT) void k_splitters(int32_t E, int32_t M, int
     if (tid == 0) hist[kBins] = t2;
   }
   __syncthreads();
+  PROF(3)
   // bucket count from the winner estimate: >= 16 sampled winners per bucket
   const double est = (double)total * (double)E / (double)M;
   int nb = (int)ceil(est / (double)kTarget);
@@ -479,6 +517,7 @@ __global__ __launch_bounds__(kSortNT) void k_splitters(int32_t E, int32_t M, int
     s_spl[j - 1] = sv;
   }
   __syncthreads();
+  PROF(4)
   // lookup table over the same bins: lut[bin] = #(splitters < start of bin); a key's bucket
   // count is then lut[bin] plus the few splitters inside its bin (bucket_lut)
   for (int bin = tid; bin < kBins; bin += kSortNT) {
@@ -496,40 +535,10 @@ __global__ __launch_bounds__(kSortNT) void k_splitters(int32_t E, int32_t M, int
     lut_base[2 * b] = mn;
     lut_base[2 * b + 1] = (uint32_t)shift;
   }
+  PROF(5)
+  PROF_END(16)
 }
 
-#ifdef SPAI_PROF  // phase timing (variant builds only: make EXTRA=-DSPAI_PROF); slots 16*kernel + phase
-__device__ unsigned long long g_prof[64];
-__device__ __forceinline__ uint64_t prof_stamp() {
-  uint64_t t;
-  __builtin_amdgcn_sched_barrier(0);
-  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-  __builtin_amdgcn_sched_barrier(0);
-  return t;
-}
-#define PROF_INIT uint64_t pf_t = prof_stamp(), pf_acc[16] = {};
-#define PROF(i)                          \
-  if (threadIdx.x == 0) {                \
-    const uint64_t pf_n = prof_stamp();   \
-    pf_acc[i] += pf_n - pf_t;            \
-    pf_t = pf_n;                         \
-  }
-#define PROF_END(base)     \
-  if (threadIdx.x == 0)    \
-    for (int q = 0; q < 16; ++q) atomicAdd(&g_prof[(base) + q], (unsigned long long)pf_acc[q]);
-extern "C" int spai_debug_prof(unsigned long long* out, int reset) {
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_prof), sizeof(g_prof)) != hipSuccess) return 2;
-  if (reset) {
-    static const unsigned long long z[64] = {};
-    if (hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, sizeof(z)) != hipSuccess) return 2;
-  }
-  return 0;
-}
-#else
-#define PROF_INIT
-#define PROF(i)
-#define PROF_END(base)
-#endif
 
 // w (fp32 in [0, 1]) as the fixed-point integer of k_tile's per-bucket sums: w * 2^47 for
 // w >= 2^-20, else w * 2^69, truncated — from the float's bits (mantissa shifted by its

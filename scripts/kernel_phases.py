@@ -1,4 +1,4 @@
-"""Per-phase wall-clock of k_sort2 and k_tile (variant build with -DSPAI_PROF):
+"""Per-phase wall-clock of k_sort2, k_tile and k_splitters' splitter blocks (variant build with -DSPAI_PROF):
   make -C gflownet_spai_amd/csrc BUILD=../../build/prof OUT=../../build/variants/libspai_prof.so EXTRA=-DSPAI_PROF
   SPAI_LIB_VARIANT=libspai_prof.so python scripts/kernel_phases.py
 Phase times are summed over the blocks of each kernel (thread 0's view, stamps after the
@@ -32,6 +32,7 @@ kern = {
     "k_sort2": (0, ["wait", "flush", "map", "mapbar", "issue", "minmax", "subcount", "subscan", "scatter", "rank", "place",
                  "wscan", "store"], ncu),
     "k_tile": (32, ["prologue", "keys", "atomics", "offsets", "win_place", "win_write", "list", "lut_rounds"], ncu),
+    "k_splitters": (16, ["counts", "keys", "hist", "scan", "splitters", "lut"], B),
 }
 for name, (base, phases, resident) in kern.items():
     tot = sum(buf[base + i] for i in range(len(phases)))

@@ -98,6 +98,7 @@ struct TrajWs {
   double* wrest;          // [B]
   double* bwsuf;          // [B][kMaxB]
   uint64_t* scratch;      // [B][E] oversized-bucket radix scratch
+  float* tE;              // [B] the terminal's arrival time (k_presample; k_tile reads it)
   size_t total_bytes;
 };
 
@@ -132,6 +133,7 @@ static void traj_ws(void* base, int32_t E, int32_t B, TrajWs* w) {
   w->wrest = c.take<double>(B);
   w->bwsuf = c.take<double>((size_t)B * kMaxB);
   w->scratch = c.take<uint64_t>((size_t)B * E);
+  w->tE = c.take<float>(B);
   w->total_bytes = c.off;
 }
 
@@ -352,7 +354,7 @@ __global__ __launch_bounds__(kSampNT) void k_presample(const float* __restrict__
                                                        uint32_t st0, uint32_t st1, const uint64_t* __restrict__ sctr,
                                                        int32_t sample_base,
                                                        uint32_t* __restrict__ samp, int32_t* __restrict__ samp_cnt,
-                                                       int32_t* __restrict__ ctl, int32_t nctl) {
+                                                       int32_t* __restrict__ ctl, int32_t nctl, float* __restrict__ tE_out) {
   const int tid = threadIdx.x;
   stream_words(sctr, st0, st1);
   {  // the rollout's control block (bucket totals, oversized-bucket list count, tdev) starts at 0;
@@ -365,7 +367,10 @@ __global__ __launch_bounds__(kSampNT) void k_presample(const float* __restrict__
   const uint32_t bg = (uint32_t)(sample_base + b);
   __shared__ float s_tk;
   __shared__ int s_wc[kSampNT / 64];
-  if (tid == 0) s_tk = terminal_t(E, bg, st0, st1, seed0, seed1);
+  if (tid == 0) {
+    s_tk = terminal_t(E, bg, st0, st1, seed0, seed1);
+    if (blk == 0) tE_out[b] = s_tk;  // for k_tile: one Philox call per sample instead of per thread
+  }
   __syncthreads();
   const int i = blk * kSampNT + tid;
   int win = 0;
@@ -575,7 +580,8 @@ void k_tile(const float* __restrict__ rr, const float* __restrict__ ww, int64_t 
             uint32_t* __restrict__ removed, int32_t words, const int32_t* __restrict__ nb_,
             const uint32_t* __restrict__ spl_, const uint16_t* __restrict__ lut_,
             const uint32_t* __restrict__ lut_base, uint32_t* __restrict__ staging,
-            uint32_t* __restrict__ runs, double* __restrict__ tbw, double* __restrict__ tile_wrest) {
+            uint32_t* __restrict__ runs, double* __restrict__ tbw, double* __restrict__ tile_wrest,
+            const float* __restrict__ tE_in) {
   // LDS regions (two blocks per CU: <= 80 KB per block):
   //   s_r0: the fixed-point bucket sums during the histogram, then the slot path's record window
   //   s_r1: the compacted winner list: keys, weights, tile-local ids (slot path: the window's
@@ -650,8 +656,9 @@ void k_tile(const float* __restrict__ rr, const float* __restrict__ ww, int64_t 
       for (int s = 0; s < 4; ++s) rvk[4 * g + s] = lvk[4 * g + s] = 0.0f;
     }
   }
-  // the terminal's arrival time, redundantly per thread (one Philox call) instead of a barrier
-  const float tE = terminal_t(E, bg, st0, st1, seed0, seed1);
+  // the terminal's arrival time, computed once per sample by k_presample (a scalar load issued
+  // with the block's other scalar loads, instead of a Philox call per thread on the critical path)
+  const float tE = tE_in[b];
   PROF(0)
   uint32_t ord[4 * kTileG];
   uint32_t win = 0;  // bit 4g + s: action a_t + g * 4 * kGrpNT + 4 * tid + s is a winner
@@ -1662,7 +1669,7 @@ extern "C" int spai_rollout_select(const float* logits, int64_t bstride, int32_t
   const int nwb = (int)((w.wstride + kRwChunk - 1) / kRwChunk);  // rate/weight blocks per logits row
   const int64_t rowsel = bstride ? 1 : 0;
   k_presample<<<nsb * B, kSampNT, 0, s>>>(logits, bstride, E, w.M, nsb, s0, s1, t0, t1, stream_ctr, sample_base,
-                                          w.samp, w.samp_cnt, w.ctl, 4);
+                                          w.samp, w.samp_cnt, w.ctl, 4, w.tE);
   SPAI_CHECK_LAUNCH();
   k_splitters<<<B + nwb * (bstride ? B : 1), kSortNT, 0, s>>>(E, w.M, nsb, w.samp, w.samp_cnt, w.nb, w.spl, w.lut,
                                                              w.lut_base, B, logits, bstride, lmax, w.rr, w.ww,
@@ -1670,7 +1677,7 @@ extern "C" int spai_rollout_select(const float* logits, int64_t bstride, int32_t
   SPAI_CHECK_LAUNCH();
   k_tile<<<w.ntiles * B, kGrpNT, 0, s>>>(w.rr, w.ww, w.wstride, rowsel, E, B, w.ntiles, s0, s1, t0, t1, stream_ctr,
                                          sample_base, part, nparts, removed, words, w.nb, w.spl, w.lut, w.lut_base,
-                                         w.staging, w.runs, w.tbw, w.tile_wrest);
+                                         w.staging, w.runs, w.tbw, w.tile_wrest, w.tE);
   SPAI_CHECK_LAUNCH();
   k_bsum<<<dim3(max_buckets(E) + 1, B), kBsumNT, 0, s>>>(w.ntiles, w.nb, w.runs, w.tbw, w.xch, stream_ctr, part,
                                                          nparts);

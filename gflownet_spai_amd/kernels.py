@@ -206,7 +206,7 @@ def narrow_values(a_lines: Lines) -> torch.Tensor:
     v = a_lines.val
     if v.dtype != torch.float64:
         return v
-    c = getattr(a_lines, "_narrow", None)
+    c = a_lines._narrow
     if c is None or c[0] is not v:
         f = v.float()
         c = (v, f if torch.equal(f.double(), v) else v)

@@ -14,7 +14,7 @@ is only its removal bitmap (and, for LSQ fill, its [n, W] values).
 """
 from __future__ import annotations
 
-from dataclasses import dataclass
+from dataclasses import dataclass, field
 
 import torch
 
@@ -27,6 +27,8 @@ class Lines:
     act: torch.Tensor  # [n, width] int32 action id (raw COO position), -1 = padding
     val: torch.Tensor  # [n, width] values (fp32 for a pattern, A's dtype for A lines)
     orient: str        # "row" | "col"
+    # kernels.narrow_values' cache: (val it was computed from, fp32 copy if exact else val)
+    _narrow: tuple | None = field(default=None, repr=False, compare=False)
 
     @property
     def nbytes(self) -> int:

@@ -78,3 +78,23 @@ def test_thermal_like_standin_structure():
     bw = np.abs(i[0] - i[1]).max()
     assert bw > n // 2  # numbering scattered: no band left
     assert np.all(np.linalg.eigvalsh(M.toarray()) > 0)
+
+
+def test_narrow_values_exact_only_and_cached():
+    """kernels.narrow_values hands A's fp64 values to the residual kernels as fp32 only when
+    every value survives the round trip (the same numbers), caches the copy on the Lines object
+    and recomputes it when the values tensor is replaced."""
+    from gflownet_spai_amd import kernels
+    from gflownet_spai_amd.layout import build_lines
+    r = torch.tensor([0, 0, 1, 1, 2])
+    c = torch.tensor([0, 1, 0, 1, 2])
+    exact = build_lines(r, c, torch.tensor([4.0, -1.0, -1.0, 4.0, 0.5], dtype=torch.float64), 3, "row", "cpu")
+    v32 = kernels.narrow_values(exact)
+    assert v32.dtype == torch.float32 and torch.equal(v32.double(), exact.val)
+    assert kernels.narrow_values(exact) is v32  # cached
+    inexact = build_lines(r, c, torch.tensor([4.0, -1.0, 0.1, 4.0, 0.5], dtype=torch.float64), 3, "row", "cpu")
+    assert kernels.narrow_values(inexact) is inexact.val  # 0.1 is not an fp32 number: stays fp64
+    exact.val = exact.val * (1 + 2.0 ** -40)
+    assert kernels.narrow_values(exact) is exact.val  # new values, checked again
+    f32 = build_lines(r, c, torch.ones(5), 3, "row", "cpu")
+    assert kernels.narrow_values(f32) is f32.val

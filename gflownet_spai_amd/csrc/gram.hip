@@ -272,8 +272,11 @@ __global__ __launch_bounds__(kNT) void k_gram_fill_wide(int32_t n, int32_t line_
                                                         double* __restrict__ partials) {
   constexpr int T = tri(W);
   static_assert(W <= 32, "keep mask is one 32-bit word");
-  __shared__ double s_r2[kNT];
-  __shared__ __attribute__((aligned(16))) TM s_m[kNT * W];
+  // per-sample line residuals of a chunk of kChunk samples (summed after the chunk: one barrier
+  // pair per chunk, not per sample) and M staged through two LDS buffers (sample b writes buffer
+  // b & 1 while sample b - 1's stores may still read the other)
+  __shared__ double s_r2[kChunk][kNT];
+  __shared__ __attribute__((aligned(16))) TM s_m[2][kNT * W];
   __shared__ int32_t s_act[W][kNT];  // action ids of the slots (LDS, not registers: G needs them)
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int lb = blockIdx.x;
@@ -372,11 +375,13 @@ __global__ __launch_bounds__(kNT) void k_gram_fill_wide(int32_t n, int32_t line_
         r2 += y[p] * acc;
       }
     }
+    s_r2[b % kChunk][t] = valid ? r2 : 0.0;
     if (m_out != nullptr) {
+      TM* sm = s_m[b & 1];
       if (valid) {
 #pragma unroll
         for (int p = 0; p < W; ++p)
-          if (p < wrt) s_m[t * wrt + p] = (TM)y[p];
+          if (p < wrt) sm[t * wrt + p] = (TM)y[p];
       }
       __syncthreads();
       TM* dst = m_out + ((int64_t)b * nloc + (int64_t)lb * kNT) * wrt;
@@ -385,21 +390,23 @@ __global__ __launch_bounds__(kNT) void k_gram_fill_wide(int32_t n, int32_t line_
       int e0 = 0;
       if ((reinterpret_cast<uintptr_t>(dst) & 15u) == 0) {
         for (int e = t; e < ne / V; e += kNT)
-          nt_store(reinterpret_cast<nt_u4*>(dst) + e, reinterpret_cast<const nt_u4*>(s_m)[e]);
+          nt_store(reinterpret_cast<nt_u4*>(dst) + e, reinterpret_cast<const nt_u4*>(sm)[e]);
         e0 = ne / V * V;
       }
-      for (int e = e0 + t; e < ne; e += kNT) nt_store(dst + e, s_m[e]);
+      for (int e = e0 + t; e < ne; e += kNT) nt_store(dst + e, sm[e]);
     }
-    s_r2[t] = valid ? r2 : 0.0;
-    __syncthreads();
-    if (wave == 0) {  // fixed-order block sum of this sample
-      double acc = 0.0;
+    if (b % kChunk == kChunk - 1 || b == B - 1) {  // the chunk's fixed-order block sums
+      const int c0 = b - b % kChunk, nb = b - c0 + 1;
+      __syncthreads();
+      for (int u = wave; u < nb; u += kNT / 64) {
+        double acc = 0.0;
 #pragma unroll
-      for (int q = 0; q < kNT / 64; ++q) acc += s_r2[q * 64 + lane];
-      acc = wave_sum(acc);
-      if (lane == 0) partials[(int64_t)b * gridDim.x + lb] = acc;
+        for (int q = 0; q < kNT / 64; ++q) acc += s_r2[u][q * 64 + lane];
+        acc = wave_sum(acc);
+        if (lane == 0) partials[(int64_t)(c0 + u) * gridDim.x + lb] = acc;
+      }
+      __syncthreads();
     }
-    __syncthreads();
   }
 }
 

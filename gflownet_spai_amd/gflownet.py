@@ -27,11 +27,11 @@ from .preconditioner import Data
 
 class GFlowNet(nn.Module):
     def __init__(self, forward_policy, backward_policy, env, *, mode: str = "parity", seed: int | None = None,
-                 sample_base: int = 0, shard: tuple | None = None, split: str = "columns"):
+                 sample_base: int = 0, shard: tuple | None = None, split: str | None = None):
         super().__init__()
         if mode not in ("parity", "throughput"):
             raise ValueError("mode must be 'parity' or 'throughput'")
-        if split not in ("columns", "slices"):
+        if split not in (None, "columns", "slices"):
             raise ValueError("split must be 'columns' or 'slices'")
         self.register_buffer("total_flow", torch.ones(1))
         self.forward_policy = forward_policy
@@ -52,15 +52,21 @@ class GFlowNet(nn.Module):
         #     P*len(s0) candidates, one all_reduce sums the exact residual limbs (distributed.py).
         #   split="slices": every rank draws the same B candidates and orders one slice of every
         #     trajectory; one all_reduce of the bucket sums + residual partials.
+        #   The two splits read s0 differently (this rank's candidates vs the whole batch), so a
+        #   sharded GFlowNet must name its split: an old slices-era call site fails loudly.
         self.shard = shard if shard is not None and shard[1] > 1 else None
+        if self.shard is not None and split is None:
+            raise ValueError("a sharded GFlowNet needs split='columns' (s0 = this rank's own candidates) or "
+                             "split='slices' (s0 = the whole batch on every rank); INTEGRATION.md §4")
         self.split = split if self.shard is not None else None
         if self.shard is not None:
             if mode != "throughput":
                 raise ValueError("a sharded GFlowNet needs mode='throughput'")
             from .distributed import LINE_ALIGN, shard_lines
             rank, world, _ = self.shard
-            align = LINE_ALIGN if split == "columns" else 1
-            self.lines = shard_lines(env.matrix_size, rank, world, align) if env is not None else None
+            # 256-line-aligned shards for both splits: the per-block fp64 partials of the fill
+            # start at the shard's first line, so only aligned shards sum to one GPU's bits
+            self.lines = shard_lines(env.matrix_size, rank, world, LINE_ALIGN) if env is not None else None
 
     @property
     def rollouts(self) -> int:
@@ -357,7 +363,12 @@ class GFlowNet(nn.Module):
         actions, fwd, t_dev = st["traj"]
         log = Log(st["s0"], self.backward_policy, self.total_flow, env)
         log._set_rollout(st["logits"], actions, fwd, t_dev, lmax=st["lmax"])
-        log.removed, log.counts = st["removed"], st["counts"]
+        removed, counts = st["removed"], st["counts"]
+        if not torch.cuda.is_current_stream_capturing():
+            # views into the persistent exchange buffer: copied, so a later step cannot overwrite
+            # this Log's bitmaps (a captured graph keeps the views: valid until the next replay)
+            removed, counts = removed.clone(), counts.clone()
+        log.removed, log.counts = removed, counts
         log.rewards = env.last_reward32[rank * bl:(rank + 1) * bl]
         log.rewards_all = rewards  # [P*bl] fp64, global sample order (the M lines of every one are here)
         st["log"] = log

@@ -135,7 +135,11 @@ class PreconditionerEnv(Env):
                                             line_end, **kw)
         if self.keep_m:
             self.last_m = m
-        self.last_removed = removed if word_base == 0 else None  # a window cannot be assembled
+        # only whole bitmaps over all lines can be assembled: a window (the columns split's
+        # all_to_all rows, whose last column is the removal count) or a line shard cannot
+        whole = (word_base == 0 and removed.shape[1] == (self.init_nnz + 31) // 32 and line_begin == 0
+                 and (line_end is None or line_end == self.matrix_size))
+        self.last_removed = removed if whole else None
         return res2
 
     def word_spans(self, world: int) -> list:

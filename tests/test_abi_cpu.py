@@ -52,3 +52,66 @@ def test_argument_validation_without_gpu():
         _lib.check(rc, "spai_rollout_select")
     assert lib.spai_fill_workspace_bytes(1000, 4) >= 1000 * 4 * 8
     assert lib.spai_logits_stats_workspace_bytes(10, 2) > 0
+
+
+def test_binding_signatures_match_header_parameter_lists():
+    """_lib.SIGNATURES (the package's ctypes binding) agrees with include/spai_hip.h argument for
+    argument: same count and, per position, the ctypes type the header's C type needs."""
+    from .abi_header import parse_header
+    hdr = parse_header()
+    assert sorted(hdr) == sorted(_lib.SIGNATURES)
+    for name, (res, args) in _lib.SIGNATURES.items():
+        h_res, h_args, h_names = hdr[name]
+        assert res is h_res, (name, res, h_res)
+        assert len(args) == len(h_args), (name, len(args), len(h_args))
+        for i, (a, h) in enumerate(zip(args, h_args)):
+            assert a is h, (name, h_names[i], a, h)
+
+
+def test_integration_stub_matches_header():
+    """The reference-side binding published in INTEGRATION.md binds every function it calls with
+    the header's parameter list (ABI 13), and calls each with that many arguments."""
+    import ast
+    from .abi_header import integration_stub, parse_header
+    hdr = parse_header()
+    src = integration_stub()
+    tree = ast.parse(src)
+    alias = {"_P": ctypes.c_void_p, "_I": ctypes.c_int32, "_L": ctypes.c_int64, "_Z": ctypes.c_size_t}
+    bound = {}
+    for node in ast.walk(tree):
+        if not isinstance(node, ast.Assign):
+            continue
+        targets = node.targets[0].elts if isinstance(node.targets[0], ast.Tuple) else [node.targets[0]]
+        values = node.value.elts if isinstance(node.value, ast.Tuple) and len(targets) > 1 else [node.value]
+        for t, v in zip(targets, values):
+            if isinstance(t, ast.Attribute) and t.attr == "argtypes" and isinstance(t.value, ast.Attribute):
+                bound[t.value.attr] = [alias[e.id] for e in v.elts]
+    assert {"spai_actions_to_removed", "spai_fill_residual", "spai_fill_workspace_bytes"} <= set(bound)
+    for name, args in bound.items():
+        h_args = hdr[name][1]
+        assert len(args) == len(h_args), (name, len(args), len(h_args))
+        assert all(a is h for a, h in zip(args, h_args)), name
+    calls = {}
+    for node in ast.walk(tree):
+        if isinstance(node, ast.Call) and isinstance(node.func, ast.Attribute) and node.func.attr.startswith("spai_"):
+            calls.setdefault(node.func.attr, []).append(len(node.args))
+    assert calls["spai_fill_residual"] == [23] and calls["spai_actions_to_removed"] == [10]
+    for name, ns in calls.items():
+        assert all(k == len(hdr[name][1]) for k in ns), name
+
+
+def test_sharded_gflownet_needs_an_explicit_split_and_aligned_lines():
+    """A sharded GFlowNet must name its split (the splits read s0 differently); both splits use
+    256-line-aligned shards (the exact residual sums are invariant only for aligned shards)."""
+    import types
+    from gflownet_spai_amd import GFlowNet
+    from gflownet_spai_amd.distributed import LINE_ALIGN
+    env = types.SimpleNamespace(matrix_size=96 * 96)
+    with pytest.raises(ValueError, match="split"):
+        GFlowNet(None, None, env, mode="throughput", shard=(0, 3, None))
+    GFlowNet(None, None, env, mode="throughput", shard=(0, 1, None))  # one rank: no split needed
+    for split in ("columns", "slices"):
+        rngs = [GFlowNet(None, None, env, mode="throughput", shard=(r, 3, None), split=split).lines for r in range(3)]
+        assert rngs[0][0] == 0 and rngs[-1][1] == env.matrix_size
+        assert all(rngs[i][1] == rngs[i + 1][0] for i in range(2))
+        assert all(b % LINE_ALIGN == 0 for b, _ in rngs)

@@ -117,6 +117,19 @@ def fill_bytes(env, B, store_m: bool = True) -> float:
     return line + B * per_sample
 
 
+def survey_fill_bytes(env, B, store_m: bool = True) -> float:
+    """SURVEY.md §8(d)'s algorithmic bytes of one LSQ fill + ||AM-I|| launch, with A counted as
+    A itself (not the Gram cache the kernel streams instead): bytes(A) = nnz_A (s_A + 4) + 4 (N + 1),
+    the pattern 4 nnz_P + 4 (N + 1), and per sample the removal bitmap + the M values s_M nnz_P."""
+    n = env.pattern.n
+    nnz_a = int((env.a_lines.idx >= 0).sum())
+    nnz_p = env.init_nnz
+    s_a = env.a_lines.val.element_size()
+    s_m = s_a if env.fill == "lsq" else 4
+    per_sample = math.ceil(nnz_p / 32) * 4 + (s_m * nnz_p if store_m else 0) + 8
+    return nnz_a * (s_a + 4) + 4 * (n + 1) + 4 * nnz_p + 4 * (n + 1) + B * per_sample
+
+
 def measured_traffic(cfg: str, B: int):
     """HBM bytes per launch of the roofline kernel from the committed PMC profile of this
     exact workload (profiles/fill_traffic.json, written by scripts/collect_profiles.py from
@@ -276,6 +289,8 @@ def main():
     ap.add_argument("--strong", action="store_true",
                     help="columns split: --batch is the GLOBAL batch (batch/P rollouts per GPU) instead of per GPU")
     ap.add_argument("--assemble", default="best", choices=["best", "all", "none"])
+    ap.add_argument("--fill", default="lsq", choices=["lsq", "qr"],
+                    help="least-squares fill: normal equations from the Gram cache (lsq) or Householder QR (qr)")
     ap.add_argument("--no-graph", action="store_true", help="time eager steps (host launches) instead of graph replays")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="process-group backend (nccl = RCCL over xGMI; gloo only to rehearse the flow)")
@@ -308,7 +323,7 @@ def main():
     dims, grid, dtype, text = CONFIGS[args.config]
     A, P = config_matrices(args.config)
     n = A.shape[0]
-    env = PreconditionerEnv(n, P, A, side="AM", fill="lsq", keep_m=True, device=dev)
+    env = PreconditionerEnv(n, P, A, side="AM", fill=args.fill, keep_m=True, device=dev)
     E = env.num_actions - 1
     shard = args.shard if world > 1 else "columns"  # one GPU: every split is the same one-GPU step
     if shard in ("samples", "slices") or (shard == "columns" and args.strong):
@@ -465,7 +480,8 @@ def main():
             "dtype": "f32 storage, f64 solve/accumulate" if dtype == torch.float32 else "f64",
             "data": "synthetic (random-init seeded ForwardPolicy GATv2x2+fc, hid=4, evaluated on the state graph in "
                     "every step; terminal fc bias set for 20% expected removal; matrix from its stencil)",
-            "config": {"workload": workload + ": ForwardPolicy logits + throughput rollout + LSQ fill + ||AM-I||_F",
+            "config": {"workload": workload + ": ForwardPolicy logits + throughput rollout + LSQ fill" +
+                                   (" (Householder QR)" if args.fill == "qr" else "") + " + ||AM-I||_F",
                        "N": n, "E": E, "global_batch": B, "rollouts_per_gpu": bl,
                        "parallelism": f"{shard} sharded x{world}"},
             "value_without_assembly": B * n / dt_noasm,
@@ -480,10 +496,23 @@ def main():
                                      f"reaches it through the env-constant Gram cache)", fb, fill_ms,
                                      measured_traffic(args.config, bl)),
         }
+        if args.fill == "qr":  # the Householder-QR fill reads A itself: SURVEY §8(d)'s bytes are its bytes
+            sbq = survey_fill_bytes(env, B if shard == "columns" else bl)
+            if split:
+                sbq *= (model.lines[1] - model.lines[0]) / n
+            out["roofline"] = roofline_obj(f"k_qr_fill<{env.pattern.width},rows {env.qr_rows}> (LSQ fill of M by "
+                                           f"Householder QR of each line's block A[I, J] + ||AM-I||^2)", sbq, fill_ms,
+                                           measured_traffic(args.config + "_qr", bl))
+        # the same launch at SURVEY §8(d)'s bytes (A counted as bytes(A), not as the Gram cache)
+        sb = survey_fill_bytes(env, B if shard == "columns" else bl)
+        if split:
+            sb *= (model.lines[1] - model.lines[0]) / n
+        out["roofline"]["bytes_survey_8d"] = sb
+        out["roofline"]["frac_survey_8d"] = sb / (fill_ms * 1e-3) / 1e9 / HBM_PEAK_GBS
         if world == 1:
             sel = roofline_obj("rollout_select phase: k_presample + k_splitters + k_tile + k_bsum (k_tile ~80 % of "
-                               "it; latency-bound: VALU issue 0.33 of its SIMD cycles, 0.47 of the wave cycles "
-                               "waiting, DESIGN.md §3)", select_bytes(env, bl, float(counts.sum())),
+                               "it; latency-bound, not bandwidth-bound: see the PMC profile in DESIGN.md §5)",
+                               select_bytes(env, bl, float(counts.sum())),
                                phase_ms.get("rollout_select", float("nan")))
             out["roofline_select"] = sel
             with torch.no_grad():

@@ -19,9 +19,9 @@ if os.environ.get("SPAI_LIB_VARIANT"):  # A/B timing of kernel variants built un
                             os.environ["SPAI_LIB_VARIANT"])
 
 SPAI_OK, SPAI_ERR_INVALID, SPAI_ERR_HIP, SPAI_ERR_UNSUPPORTED = 0, 1, 2, 3
-FILL_COPY, FILL_LSQ = 0, 1
+FILL_COPY, FILL_LSQ = 0, 1  # (the Householder-QR fill has its own entry point)
 DTYPE_F32, DTYPE_F64 = 0, 1
-ABI_VERSION = 13
+ABI_VERSION = 14
 RES2_LIMBS = 8  # SPAI_RES2_LIMBS
 
 _c_i32, _c_i64, _c_u64, _c_sz, _c_p = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_size_t, ctypes.c_void_p
@@ -89,6 +89,9 @@ SIGNATURES = {
                                           _c_i32, _c_i32, _c_p, _c_i32, _c_i32, _c_p, _c_i32, _c_p, _c_p, _c_p, _c_sz,
                                           _c_p]),
     "spai_res2_from_limbs": (ctypes.c_int, [_c_i32, _c_p, _c_p, _c_p]),
+    "spai_qr_max_rows": (ctypes.c_int, [_c_i32, _c_i32, _c_p, _c_i32, _c_p, _c_p, _c_p]),
+    "spai_fill_lines_qr": (ctypes.c_int, [_c_i32, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_i32, _c_p, _c_p, _c_i32,
+                                          _c_i32, _c_i32, _c_p, _c_i32, _c_i32, _c_p, _c_i32, _c_p, _c_sz, _c_p]),
 }
 
 _lib = None
@@ -107,11 +110,14 @@ def load():
         raise SpaiUnavailable(f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'` "
                               "or `make -C gflownet_spai_amd/csrc`")
     lib = ctypes.CDLL(LIB_PATH)
+    variant = bool(os.environ.get("SPAI_LIB_VARIANT"))  # an A/B build may predate newer entry points
     for name, (res, args) in SIGNATURES.items():
+        if variant and not hasattr(lib, name):
+            continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.spai_abi_version() != ABI_VERSION:
+    if lib.spai_abi_version() != ABI_VERSION and not variant:
         raise SpaiUnavailable(f"libspai_hip ABI {lib.spai_abi_version()} != expected {ABI_VERSION}")
     _lib = lib
     return lib

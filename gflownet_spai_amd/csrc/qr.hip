@@ -1,0 +1,389 @@
+// Least-squares fill of M by Householder QR, one small dense problem per (line, sample), for
+// gfx950.  The north star's per-column constrained least squares
+//     m_l = argmin || A[:, J] m - e_l ||_2 ,  J = the kept pattern slots of line l
+// solved the way it names: the line's dense block A[I, J] (I = the union of the rows the slots'
+// A lines touch) is staged in LDS once per line, and every sample's masked problem is factored by
+// Householder reflections on L lanes of a wavefront (a "group"), each lane holding RPL rows of the
+// block; the reflections' norms and dot products are group reductions on DPP lane swaps (quad_perm,
+// row_half_mirror, row_mirror) — no LDS traffic inside the factorisation.  No normal equations: the
+// conditioning is that of A[I, J] itself, not its square (the Gram-cached fill in
+// gram.hip is the normal-equations path).
+//
+// Per block: 256 consecutive lines (the exact-sum invariance unit, LINE_ALIGN), in rounds of NG
+// lines (one per group).  Per round:
+//   1. the W slots' A lines are staged in LDS and one lane per group merges them (they are sorted
+//      by row index) into the dense block D = A[I, slots] in ascending row order, with the column
+//      norms ||D[:, p]||^2 (pivot floor) and the position of row l in I (the right-hand side e_l);
+//   2. per sample: the kept-slot mask from the removal bitmap, then for p = 0 .. W-1 a reflection
+//      of column p onto the next pivot row if the slot is kept and its remaining norm exceeds
+//      1e-12 ||D[:, p]|| (numerical rank deficiency in fp64; the normal equations of gram.hip must
+//      already drop a column whose remaining norm is below ~3e-7 of its norm: 1e-13 of the squared
+//      norm), applied to the later columns and to e_l; the pivot rows (R and Q^T e) go through LDS to one lane that
+//      back-substitutes m; the line residual^2 is the norm^2 of Q^T e below the pivots (no
+//      cancellation), + 1 when row l is not in I.
+// Per-sample block sums in a fixed order (spai_fill_reduce / spai_fill_reduce_rewards sum them
+// exactly).  Deterministic: every group runs the same operation sequence, DPP reductions of
+// commutative pairs leave identical bits on every lane.
+#include "spai_device.h"
+#include "spai_status.h"
+
+namespace spai {
+namespace {
+
+constexpr int kQNT = 256;     // threads per block (k_qr_rows; the fill instances choose theirs)
+constexpr int kQLines = 256;  // lines per block (= distributed.LINE_ALIGN)
+constexpr int kQChunk = 8;    // samples per residual chunk
+
+// Sum over the L lanes of a group (L = 4, 8, 16, 32 consecutive lanes), valid on every lane of
+// the group with identical bits (each step adds a commutative pair).
+template <int L>
+__device__ __forceinline__ double group_sum(double v) {
+  v += dpp_d<0xB1, 0xf>(v);  // quad_perm [1, 0, 3, 2]
+  v += dpp_d<0x4E, 0xf>(v);  // quad_perm [2, 3, 0, 1]
+  if constexpr (L >= 8) v += dpp_d<0x141, 0xf>(v);  // row_half_mirror: quad 0 <-> quad 1
+  if constexpr (L >= 16) v += dpp_d<0x140, 0xf>(v);  // row_mirror: half-row 0 <-> 1
+  if constexpr (L >= 32) v += __shfl_xor(v, 16, kWave);
+  static_assert(L == 4 || L == 8 || L == 16 || L == 32, "group size");
+  return v;
+}
+
+// Union size of the rows the slots' A lines touch, per line (max over the lines -> *out).
+template <int W, int WA>
+__global__ __launch_bounds__(kQNT) void k_qr_rows(int32_t n, int32_t wrt, const int32_t* __restrict__ pat_idx,
+                                                  int32_t wart, const int32_t* __restrict__ a_idx,
+                                                  int32_t* __restrict__ out) {
+  const int l = blockIdx.x * kQNT + threadIdx.x;
+  int rows = 0;
+  if (l < n) {
+    int kp[W], h[W], cur[W];
+#pragma unroll
+    for (int p = 0; p < W; ++p) {
+      kp[p] = p < wrt ? pat_idx[(int64_t)l * wrt + p] : -1;
+      h[p] = 0;
+      const int a = kp[p] >= 0 ? a_idx[(int64_t)kp[p] * wart] : -1;
+      cur[p] = a >= 0 ? a : INT_MAX;
+    }
+#pragma unroll 1
+    for (int it = 0; it < W * WA; ++it) {
+      int r = INT_MAX;
+#pragma unroll
+      for (int p = 0; p < W; ++p) r = min(r, cur[p]);
+      if (r == INT_MAX) break;
+#pragma unroll
+      for (int p = 0; p < W; ++p)
+        if (cur[p] == r) {
+          ++h[p];
+          const int a = h[p] < wart ? a_idx[(int64_t)kp[p] * wart + h[p]] : -1;
+          cur[p] = a >= 0 ? a : INT_MAX;
+        }
+      ++rows;
+    }
+  }
+  rows = max(rows, (int)__shfl_xor(rows, 1, kWave));
+#pragma unroll
+  for (int o = 2; o < kWave; o <<= 1) rows = max(rows, (int)__shfl_xor(rows, o, kWave));
+  if ((threadIdx.x & 63) == 0 && rows > 0) atomicMax(out, rows);
+}
+
+template <int W, int WA, int L, int RPL, int NT, typename TA, typename TM>
+__global__ __launch_bounds__(NT) void k_qr_fill(int32_t n, int32_t line_begin, int32_t line_end, int32_t wrt,
+                                                  const int32_t* __restrict__ pat_idx,
+                                                  const int32_t* __restrict__ pat_act, int32_t wart,
+                                                  const int32_t* __restrict__ a_idx, const TA* __restrict__ a_val,
+                                                  int32_t B, const uint32_t* __restrict__ removed, int32_t words,
+                                                  int32_t word_base, TM* __restrict__ m_out,
+                                                  double* __restrict__ partials) {
+  constexpr int NG = NT / L, R = L * RPL, NR = kQLines / NG;  // groups, block rows, rounds
+  static_assert(kQLines % NG == 0 && W * WA <= 8 * 1024, "shapes");
+  __shared__ TA sD[NG][R][W];             // dense blocks A[I, slots] (rows of I ascending)
+  __shared__ int sAi[NG][W][WA];          // staged A lines of the slots
+  __shared__ TA sAv[NG][W][WA];
+  __shared__ double sCn[NG][W];           // ||D[:, p]||^2
+  __shared__ int sRowL[NG];               // position of row l in I; -1: not in I; -2: block overflow
+  __shared__ double sSol[NG][W][W + 1];   // pivot rows by slot: R[p][q > p], R[p][p], then (Q^T e)
+  __shared__ double sR2[kQChunk][kQLines];
+  const int t = threadIdx.x, g = t / L, j = t % L, lane = t & 63, wave = t >> 6;
+  const int lb = blockIdx.x;
+  const int64_t nloc = line_end - line_begin;
+  const int blk0 = line_begin + lb * kQLines;
+  const int nvl = min(kQLines, line_end - blk0);
+
+#pragma unroll 1
+  for (int b0 = 0; b0 < B; b0 += kQChunk) {
+    const int nb = min(kQChunk, B - b0);
+#pragma unroll 1
+    for (int r = 0; r < NR; ++r) {
+      const int li = r * NG + g;
+      const bool valid = li < nvl;
+      const int l = blk0 + (valid ? li : 0);
+      // ---- 1. stage the slots' A lines, zero the block
+      for (int e = j; e < W * WA; e += L) {
+        const int p = e / WA, s = e % WA;
+        const int kp = (valid && p < wrt) ? pat_idx[(int64_t)l * wrt + p] : -1;
+        const int a = (kp >= 0 && s < wart) ? a_idx[(int64_t)kp * wart + s] : -1;
+        sAi[g][p][s] = a;
+        sAv[g][p][s] = a >= 0 ? a_val[(int64_t)kp * wart + s] : (TA)0;
+      }
+      for (int e = j; e < R * W; e += L) (&sD[g][0][0])[e] = (TA)0;
+      __syncthreads();
+      if (j == 0) {  // merge the sorted A lines into the rows of I (ascending)
+        int h[W], cur[W];
+        double cn[W];
+#pragma unroll
+        for (int p = 0; p < W; ++p) {
+          h[p] = 0;
+          cn[p] = 0.0;
+          const int a = sAi[g][p][0];
+          cur[p] = a >= 0 ? a : INT_MAX;
+        }
+        int rowl = -1, rho = 0;
+#pragma unroll 1
+        for (int it = 0; it <= R; ++it) {
+          int rmin = INT_MAX;
+#pragma unroll
+          for (int p = 0; p < W; ++p) rmin = min(rmin, cur[p]);
+          if (rmin == INT_MAX) break;
+          if (rho == R) {  // more rows than the instance holds (the caller's max_rows was wrong)
+            rowl = -2;
+            break;
+          }
+#pragma unroll
+          for (int p = 0; p < W; ++p)
+            if (cur[p] == rmin) {
+              const TA v = sAv[g][p][h[p]];
+              sD[g][rho][p] = v;
+              cn[p] += (double)v * (double)v;
+              ++h[p];
+              const int a = h[p] < WA ? sAi[g][p][h[p]] : -1;
+              cur[p] = a >= 0 ? a : INT_MAX;
+            }
+          if (rmin == l) rowl = rho;
+          ++rho;
+        }
+#pragma unroll
+        for (int p = 0; p < W; ++p) sCn[g][p] = cn[p];
+        sRowL[g] = rowl;
+      }
+      __syncthreads();
+      // ---- 2. every sample of the chunk
+      int act[W], wofs[W];
+      double cn[W];
+#pragma unroll
+      for (int p = 0; p < W; ++p) {
+        act[p] = (valid && p < wrt && sAi[g][p][0] >= 0) ? pat_act[(int64_t)l * wrt + p] : -1;
+        wofs[p] = act[p] >= 0 ? (act[p] >> 5) - word_base : 0;
+        cn[p] = sCn[g][p];
+      }
+      const int rowl = sRowL[g];
+#pragma unroll 1
+      for (int s = 0; s < nb; ++s) {
+        const int b = b0 + s;
+        const uint32_t* rm = removed + (int64_t)b * words;
+        bool keep[W];
+#pragma unroll
+        for (int p = 0; p < W; ++p) keep[p] = act[p] >= 0 && !((rm[wofs[p]] >> (act[p] & 31)) & 1u);
+        double dv[RPL][W], rhs[RPL];
+#pragma unroll
+        for (int i = 0; i < RPL; ++i) {
+          const int rho = j + L * i;
+#pragma unroll
+          for (int p = 0; p < W; ++p) dv[i][p] = (double)sD[g][rho][p];
+          rhs[i] = rho == rowl ? 1.0 : 0.0;
+        }
+        int k = 0;  // next pivot row
+        double diag[W];
+#pragma unroll
+        for (int p = 0; p < W; ++p) {
+          double s1 = 0.0, xk = 0.0;
+#pragma unroll
+          for (int i = 0; i < RPL; ++i) {
+            const int rho = j + L * i;
+            const double x = dv[i][p];
+            s1 = fma(rho >= k ? x : 0.0, x, s1);
+            xk += rho == k ? x : 0.0;
+          }
+          const double sig = group_sum<L>(s1), xkk = group_sum<L>(xk);
+          const bool ok = keep[p] && sig > 1e-24 * cn[p];  // |R_kk| > 1e-12 ||D[:, p]||
+          const double sq = sqrt(sig);
+          const double alpha = xkk >= 0.0 ? -sq : sq;
+          const double tau = ok ? 1.0 / (sig - alpha * xkk) : 0.0;  // H = I - tau v v^T
+          double v[RPL];
+#pragma unroll
+          for (int i = 0; i < RPL; ++i) {
+            const int rho = j + L * i;
+            v[i] = rho >= k ? dv[i][p] - (rho == k ? alpha : 0.0) : 0.0;
+          }
+          double d[W + 1];  // v . column q (q > p), v . rhs
+#pragma unroll
+          for (int q = p + 1; q <= W; ++q) {
+            double a = 0.0;
+#pragma unroll
+            for (int i = 0; i < RPL; ++i) a = fma(v[i], q < W ? dv[i][q] : rhs[i], a);
+            d[q] = a;
+          }
+#pragma unroll
+          for (int q = p + 1; q <= W; ++q) d[q] = group_sum<L>(d[q]) * tau;
+#pragma unroll
+          for (int i = 0; i < RPL; ++i) {
+#pragma unroll
+            for (int q = p + 1; q < W; ++q) dv[i][q] = fma(-d[q], v[i], dv[i][q]);
+            rhs[i] = fma(-d[W], v[i], rhs[i]);
+          }
+          diag[p] = ok ? alpha : 0.0;
+          // pivot row k is final now (later reflections act on rows > k): its owner hands it on
+          if (ok && j == k % L) {
+            const int ks = k / L;
+#pragma unroll
+            for (int q = p + 1; q <= W; ++q) {
+              double x = 0.0;
+#pragma unroll
+              for (int i = 0; i < RPL; ++i) x = i == ks ? (q < W ? dv[i][q] : rhs[i]) : x;
+              sSol[g][p][q] = x;
+            }
+          }
+          k += ok ? 1 : 0;
+        }
+        // the line residual^2: Q^T e below the pivot rows (+1 when row l is outside I)
+        double rs = 0.0;
+#pragma unroll
+        for (int i = 0; i < RPL; ++i) rs = fma(j + L * i >= k ? rhs[i] : 0.0, rhs[i], rs);
+        rs = group_sum<L>(rs);
+        __syncthreads();  // the pivot rows in sSol
+        if (j == 0) {
+          double m[W];
+#pragma unroll
+          for (int p = W - 1; p >= 0; --p) {
+            double a = sSol[g][p][W];
+#pragma unroll
+            for (int q = p + 1; q < W; ++q) a = fma(-sSol[g][p][q], m[q], a);
+            m[p] = diag[p] != 0.0 ? a / diag[p] : 0.0;
+          }
+          if (valid) {
+            if (m_out != nullptr) {
+              TM* dst = m_out + ((int64_t)b * nloc + (l - line_begin)) * wrt;
+#pragma unroll
+              for (int p = 0; p < W; ++p)
+                if (p < wrt) dst[p] = (TM)m[p];
+            }
+            sR2[s][li] = rowl == -2 ? __builtin_nan("") : rs + (rowl < 0 ? 1.0 : 0.0);
+          }
+        }
+        __syncthreads();  // sSol reused by the next sample
+      }
+    }
+    // per-sample block sums in a fixed order (the k_gram_fill partial layout)
+    for (int s = wave; s < nb; s += NT / 64) {
+      double acc = 0.0;
+#pragma unroll
+      for (int q = 0; q < kQLines / 64; ++q) acc += (q * 64 + lane < nvl) ? sR2[s][q * 64 + lane] : 0.0;
+      acc = wave_sum(acc);
+      if (lane == 0) partials[(int64_t)(b0 + s) * gridDim.x + lb] = acc;
+    }
+    __syncthreads();
+  }
+}
+
+// (W class, A width class, rows) -> instance
+template <int W, int WA, int L, int RPL, int NT, typename TM>
+hipError_t launch_qr(bool a32, int32_t n, int32_t lb, int32_t le, int32_t wrt, const int32_t* pi, const int32_t* pa,
+                     int32_t wart, const int32_t* ai, const void* av, int32_t B, const uint32_t* rm, int32_t words,
+                     int32_t wb, void* mo, double* partials, int32_t nparts, hipStream_t s) {
+  if (a32)
+    k_qr_fill<W, WA, L, RPL, NT, float, TM><<<nparts, NT, 0, s>>>(n, lb, le, wrt, pi, pa, wart, ai,
+                                                                static_cast<const float*>(av), B, rm, words, wb,
+                                                                static_cast<TM*>(mo), partials);
+  else
+    k_qr_fill<W, WA, L, RPL, NT, double, TM><<<nparts, NT, 0, s>>>(n, lb, le, wrt, pi, pa, wart, ai,
+                                                                 static_cast<const double*>(av), B, rm, words, wb,
+                                                                 static_cast<TM*>(mo), partials);
+  return hipGetLastError();
+}
+
+template <typename TM>
+hipError_t dispatch_qr(int wc, int rows, bool a32, int32_t n, int32_t lb, int32_t le, int32_t wrt, const int32_t* pi,
+                       const int32_t* pa, int32_t wart, const int32_t* ai, const void* av, int32_t B,
+                       const uint32_t* rm, int32_t words, int32_t wb, void* mo, double* partials, int32_t nparts,
+                       hipStream_t s) {
+#define SPAI_QR_ARGS a32, n, lb, le, wrt, pi, pa, wart, ai, av, B, rm, words, wb, mo, partials, nparts, s
+  if (wc == 5) {
+    if (rows <= 16) return launch_qr<5, 5, 4, 4, 256, TM>(SPAI_QR_ARGS);
+    return launch_qr<5, 5, 8, 4, 256, TM>(SPAI_QR_ARGS);
+  }
+  if (wc == 7) {
+    if (rows <= 32) return launch_qr<7, 7, 8, 4, 256, TM>(SPAI_QR_ARGS);
+    return launch_qr<7, 7, 16, 4, 128, TM>(SPAI_QR_ARGS);
+  }
+  if (rows <= 64) return launch_qr<13, 7, 16, 4, 128, TM>(SPAI_QR_ARGS);
+  return launch_qr<13, 7, 32, 3, 128, TM>(SPAI_QR_ARGS);
+#undef SPAI_QR_ARGS
+}
+
+// width class of a (pattern, A) pair: 5 (W <= 5, WA <= 5), 7 (W <= 7, WA <= 7), 13 (W <= 13, WA <= 7)
+int qr_class(int32_t W, int32_t WA) {
+  if (W <= 5 && WA <= 5) return 5;
+  if (W <= 7 && WA <= 7) return 7;
+  if (W <= 13 && WA <= 7) return 13;
+  return 0;
+}
+int qr_rows_cap(int wc) { return wc == 5 ? 32 : (wc == 7 ? 64 : 96); }
+
+}  // namespace
+}  // namespace spai
+
+using namespace spai;
+
+extern "C" int spai_qr_max_rows(int32_t n, int32_t W, const int32_t* pat_idx, int32_t WA, const int32_t* a_idx,
+                                int32_t* max_rows, void* stream) {
+  SPAI_CHECK_ARG(n >= 1 && W >= 1 && WA >= 1 && pat_idx && a_idx && max_rows, "spai_qr_max_rows: bad arguments");
+  const int wc = qr_class(W, WA);
+  if (wc == 0) {
+    set_error("spai_qr_max_rows: widths W=%d WA=%d above the compiled 13 / 7", W, WA);
+    return SPAI_ERR_UNSUPPORTED;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  SPAI_CHECK_HIP(hipMemsetAsync(max_rows, 0, sizeof(int32_t), s));
+  const int grid = (n + kQNT - 1) / kQNT;
+  if (wc == 5)
+    k_qr_rows<5, 5><<<grid, kQNT, 0, s>>>(n, W, pat_idx, WA, a_idx, max_rows);
+  else if (wc == 7)
+    k_qr_rows<7, 7><<<grid, kQNT, 0, s>>>(n, W, pat_idx, WA, a_idx, max_rows);
+  else
+    k_qr_rows<13, 7><<<grid, kQNT, 0, s>>>(n, W, pat_idx, WA, a_idx, max_rows);
+  SPAI_CHECK_LAUNCH();
+  return SPAI_OK;
+}
+
+extern "C" int spai_fill_lines_qr(int32_t n, int32_t line_begin, int32_t line_end, int32_t W, const int32_t* pat_idx,
+                                  const int32_t* pat_act, int32_t WA, const int32_t* a_idx, const void* a_val,
+                                  int32_t a_dtype, int32_t max_rows, int32_t B, const uint32_t* removed, int32_t words,
+                                  int32_t word_base, void* m_out, int32_t m_dtype, void* workspace,
+                                  size_t workspace_bytes, void* stream) {
+  SPAI_CHECK_ARG(m_dtype == SPAI_DTYPE_F32 || m_dtype == SPAI_DTYPE_F64, "spai_fill_lines_qr: bad m_dtype");
+  SPAI_CHECK_ARG(a_dtype == SPAI_DTYPE_F32 || a_dtype == SPAI_DTYPE_F64, "spai_fill_lines_qr: bad a_dtype");
+  SPAI_CHECK_ARG(n >= 1 && line_begin >= 0 && line_end >= line_begin && line_end <= n && W >= 1 && WA >= 1 &&
+                     B >= 1 && words >= 1 && word_base >= 0 && max_rows >= 0,
+                 "spai_fill_lines_qr: bad shape");
+  SPAI_CHECK_ARG(workspace != nullptr, "spai_fill_lines_qr: null workspace");
+  const int32_t nl = line_end - line_begin;
+  if (nl == 0) return SPAI_OK;
+  SPAI_CHECK_ARG(pat_idx && pat_act && a_idx && a_val && removed, "spai_fill_lines_qr: null input");
+  const int wc = qr_class(W, WA);
+  if (wc == 0 || max_rows > qr_rows_cap(wc)) {
+    set_error("spai_fill_lines_qr: widths W=%d WA=%d / %d rows above the compiled 13 / 7 / %d", W, WA, max_rows,
+              wc ? qr_rows_cap(wc) : 0);
+    return SPAI_ERR_UNSUPPORTED;
+  }
+  const int32_t nparts = (nl + kQLines - 1) / kQLines;
+  SPAI_CHECK_ARG(workspace_bytes >= sizeof(double) * (size_t)nparts * B, "spai_fill_lines_qr: workspace too small");
+  double* partials = static_cast<double*>(workspace);
+  hipStream_t s = (hipStream_t)stream;
+  const bool a32 = a_dtype == SPAI_DTYPE_F32;
+  const hipError_t e =
+      m_dtype == SPAI_DTYPE_F64
+          ? dispatch_qr<double>(wc, max_rows, a32, n, line_begin, line_end, W, pat_idx, pat_act, WA, a_idx, a_val, B,
+                                removed, words, word_base, m_out, partials, nparts, s)
+          : dispatch_qr<float>(wc, max_rows, a32, n, line_begin, line_end, W, pat_idx, pat_act, WA, a_idx, a_val, B,
+                               removed, words, word_base, m_out, partials, nparts, s);
+  SPAI_CHECK_HIP(e);
+  return SPAI_OK;
+}

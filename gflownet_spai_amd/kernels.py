@@ -351,6 +351,49 @@ def fill_residual_gram(pattern: Lines, gram: torch.Tensor, removed: torch.Tensor
     return (lb if limbs else res2), m
 
 
+def qr_max_rows(pattern: Lines, a_lines: Lines) -> int:
+    """Largest row union |I| over the lines (the dense block A[I, slots] the QR fill factors);
+    one host sync (once per env).  spai_qr_max_rows."""
+    _lib.require_device(pattern.idx)
+    out = torch.empty(1, dtype=torch.int32, device=pattern.idx.device)
+    _lib.check(_l().spai_qr_max_rows(pattern.n, pattern.width, _lib.ptr(pattern.idx), a_lines.width,
+                                     _lib.ptr(a_lines.idx), _lib.ptr(out), _lib.stream_ptr(pattern.idx.device)),
+               "spai_qr_max_rows")
+    return int(out.item())
+
+
+def _fill_lines_qr(pattern: Lines, a_lines: Lines, max_rows: int, removed: torch.Tensor, line_begin: int,
+                   line_end: int, m, m_dtype, word_base: int, ws):
+    B, words = removed.shape
+    av = narrow_values(a_lines)  # fp32-exact A values are staged as fp32 (the same numbers)
+    with _timed("fill_residual"):  # the fill kernel alone
+        st = _l().spai_fill_lines_qr(pattern.n, line_begin, line_end, pattern.width, _lib.ptr(pattern.idx),
+                                     _lib.ptr(pattern.act), a_lines.width, _lib.ptr(a_lines.idx), _lib.ptr(av),
+                                     _DT[av.dtype], max_rows, B, _lib.ptr(removed), words, word_base, _lib.ptr(m),
+                                     _DT[m_dtype], _lib.ptr(ws), ws.numel(), _lib.stream_ptr(removed.device))
+    _lib.check(st, "spai_fill_lines_qr")
+
+
+def fill_residual_qr(pattern: Lines, a_lines: Lines, max_rows: int, removed: torch.Tensor, line_begin: int = 0,
+                     line_end: int | None = None, store_m: bool = False, m_dtype=torch.float64, word_base: int = 0,
+                     limbs: bool = False):
+    """The least-squares fill by Householder QR (spai_fill_lines_qr + spai_fill_reduce): same outputs
+    as fill_residual with lsq=True (res2 [B] or exact limbs, M or None)."""
+    _lib.require_device(removed)
+    if line_end is None:
+        line_end = pattern.n
+    removed = removed.contiguous()
+    B = removed.shape[0]
+    n_loc = line_end - line_begin
+    res2, lb = _fill_out(B, removed.device, limbs)
+    m = torch.empty(B, n_loc, pattern.width, dtype=m_dtype, device=removed.device) if store_m else None
+    ws = _lib.workspace(_l().spai_fill_workspace_bytes(max(n_loc, 1), B), removed.device, "fill")
+    _fill_lines_qr(pattern, a_lines, max_rows, removed, line_begin, line_end, m, m_dtype, word_base, ws)
+    _lib.check(_l().spai_fill_reduce(n_loc, B, _lib.ptr(ws), _lib.ptr(res2), _lib.ptr(lb),
+                                     _lib.stream_ptr(removed.device)), "spai_fill_reduce")
+    return (lb if limbs else res2), m
+
+
 def res2_from_limbs(limbs: torch.Tensor) -> torch.Tensor:
     """[B] fp64 squared residuals from exact sums [B, RES2_LIMBS] int64 (spai_res2_from_limbs)."""
     _lib.require_device(limbs)
@@ -402,14 +445,33 @@ def fill_rewards_gram(pattern: Lines, gram: torch.Tensor, removed: torch.Tensor,
                                        _lib.ptr(gram), _DT[gram.dtype], B, _lib.ptr(removed), words, 0, _lib.ptr(m),
                                        _DT[m_dtype], _lib.ptr(ws), ws.numel(), _lib.stream_ptr(removed.device))
     _lib.check(st, "spai_fill_lines_gram")
+    return _reduce_rewards(ws, n, B, counts, nnz0, r0, f0, alpha, removed.device) + (m,)
+
+
+def _reduce_rewards(ws, n, B, counts, nnz0, r0, f0, alpha, device):
+    """Exact residual sums of a whole-matrix fill's partials + the reward formula, one launch."""
     c, a = _reward_args(counts, alpha)
-    residual = torch.empty(B, dtype=torch.float64, device=removed.device)
-    reward = torch.empty(B, dtype=torch.float64, device=removed.device)
-    reward32 = torch.empty(B, dtype=torch.float32, device=removed.device)
+    residual = torch.empty(B, dtype=torch.float64, device=device)
+    reward = torch.empty(B, dtype=torch.float64, device=device)
+    reward32 = torch.empty(B, dtype=torch.float32, device=device)
     _lib.check(_l().spai_fill_reduce_rewards(n, B, _lib.ptr(ws), _lib.ptr(c), nnz0, n, float(r0), float(f0),
                                              _lib.ptr(a), _lib.ptr(residual), _lib.ptr(reward), _lib.ptr(reward32),
-                                             _lib.stream_ptr(removed.device)), "spai_fill_reduce_rewards")
-    return residual, reward, reward32, m
+                                             _lib.stream_ptr(device)), "spai_fill_reduce_rewards")
+    return residual, reward, reward32
+
+
+def fill_rewards_qr(pattern: Lines, a_lines: Lines, max_rows: int, removed: torch.Tensor, counts: torch.Tensor,
+                    nnz0: int, r0: float, f0: int, alpha: torch.Tensor, store_m: bool = False,
+                    m_dtype=torch.float64):
+    """fill_rewards_gram with the Householder-QR fill (spai_fill_lines_qr + spai_fill_reduce_rewards)."""
+    _lib.require_device(removed)
+    removed = removed.contiguous()
+    B = removed.shape[0]
+    n = pattern.n
+    m = torch.empty(B, n, pattern.width, dtype=m_dtype, device=removed.device) if store_m else None
+    ws = _lib.workspace(_l().spai_fill_workspace_bytes(n, B), removed.device, "fill")
+    _fill_lines_qr(pattern, a_lines, max_rows, removed, 0, n, m, m_dtype, 0, ws)
+    return _reduce_rewards(ws, n, B, counts, nnz0, r0, f0, alpha, removed.device) + (m,)
 
 
 def logp_grad(logits: torch.Tensor, lmax: torch.Tensor, actions_bt: torch.Tensor, probs_bt: torch.Tensor,

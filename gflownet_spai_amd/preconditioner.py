@@ -14,7 +14,9 @@ Same constructor, attributes and methods as the reference; the work behind
 
 Extensions (keyword-only, defaults = reference behaviour):
   side="MA" | "AM"    which residual: ||M A - I|| (reference) or ||A M - I|| (column SPAI)
-  fill="copy" | "lsq" M = copied pattern values (reference) or per-line least squares
+  fill="copy" | "lsq" | "qr"  M = copied pattern values (reference) or per-line least squares:
+                      "lsq" by the normal equations of the Gram cache (the bench path), "qr" by
+                      Householder QR of each line's dense block A[I, J] (spai_fill_lines_qr)
   keep_m=False        keep the last batch's M values (LSQ) in ``self.last_m``
 Documented deviations: alpha is taken from the ``alpha`` argument (the reference reads
 the never-set ``self.alpha``, preconditioner.py:163); fp64 original matrices are
@@ -54,10 +56,11 @@ class PreconditionerEnv(Env):
                  fill: str = "copy", keep_m: bool = False, device=None, compact_gram: bool = True):
         if side not in ("MA", "AM"):
             raise ValueError("side must be 'MA' or 'AM'")
-        if fill not in ("copy", "lsq"):
-            raise ValueError("fill must be 'copy' or 'lsq'")
+        if fill not in ("copy", "lsq", "qr"):
+            raise ValueError("fill must be 'copy', 'lsq' or 'qr'")
         self.device = torch.device(device) if device is not None else _default_device()
         self.side, self.fill, self.keep_m = side, fill, keep_m
+        self._lsq = fill in ("lsq", "qr")  # M holds fitted values (not the pattern's)
         self.matrix_size = matrix_size
         self.init_nnz = initial_matrix.coalesce().indices().size(1)
         self.state_dim = self.init_nnz
@@ -86,6 +89,8 @@ class PreconditionerEnv(Env):
         # wider patterns use the generic kernels)
         self.gram = (kernels.gram_build(self.pattern, self.a_lines)
                      if self.pattern.width <= 13 and self.a_lines.width <= 7 else None)
+        # the QR fill factors each line's dense block A[I, J]: its largest row union picks the kernel
+        self.qr_rows = kernels.qr_max_rows(self.pattern, self.a_lines) if fill == "qr" else None
         if self.gram is not None and compact_gram:
             # integer stencils (and any A whose G, c are fp32-exact): the same cache in fp32
             g32 = kernels.gram_compact(self.gram, self.pattern)
@@ -127,11 +132,14 @@ class PreconditionerEnv(Env):
         shards, spai_hip.h).  ``removed`` rows may be windows of the bitmaps starting at word
         ``word_base`` (the columns split's all_to_all delivers only a shard's words)."""
         kw = dict(store_m=self.keep_m, m_dtype=self.a_lines.val.dtype, word_base=word_base, limbs=limbs)
-        if self.gram is not None:
-            res2, m = kernels.fill_residual_gram(self.pattern, self.gram, removed, self.fill == "lsq", line_begin,
+        if self.fill == "qr":
+            res2, m = kernels.fill_residual_qr(self.pattern, self.a_lines, self.qr_rows, removed, line_begin, line_end,
+                                               **kw)
+        elif self.gram is not None:
+            res2, m = kernels.fill_residual_gram(self.pattern, self.gram, removed, self._lsq, line_begin,
                                                  line_end, **kw)
         else:
-            res2, m = kernels.fill_residual(self.pattern, self.a_lines, removed, self.fill == "lsq", line_begin,
+            res2, m = kernels.fill_residual(self.pattern, self.a_lines, removed, self._lsq, line_begin,
                                             line_end, **kw)
         if self.keep_m:
             self.last_m = m
@@ -163,13 +171,18 @@ class PreconditionerEnv(Env):
     def fill_rewards(self, removed: Tensor, counts: Tensor, alpha) -> Tensor:
         """fill_partial over ALL lines + rewards_from_res2 (one GPU): with the Gram cache the exact
         residual sums and the reward formula run in one launch (spai_fill_reduce_rewards)."""
-        if self.gram is None:
+        if self.gram is None and self.fill != "qr":
             return self.rewards_from_res2(self.fill_partial(removed), counts, alpha)
         if not torch.is_tensor(alpha):
             alpha = torch.tensor(float(alpha), dtype=torch.float32)
-        self.last_residual, reward, self.last_reward32, m = kernels.fill_rewards_gram(
-            self.pattern, self.gram, removed, self.fill == "lsq", counts, self.init_nnz, self._r0, self.orig_flops,
-            alpha, store_m=self.keep_m, m_dtype=self.a_lines.val.dtype)
+        if self.fill == "qr":
+            self.last_residual, reward, self.last_reward32, m = kernels.fill_rewards_qr(
+                self.pattern, self.a_lines, self.qr_rows, removed, counts, self.init_nnz, self._r0, self.orig_flops,
+                alpha, store_m=self.keep_m, m_dtype=self.a_lines.val.dtype)
+        else:
+            self.last_residual, reward, self.last_reward32, m = kernels.fill_rewards_gram(
+                self.pattern, self.gram, removed, self.fill == "lsq", counts, self.init_nnz, self._r0,
+                self.orig_flops, alpha, store_m=self.keep_m, m_dtype=self.a_lines.val.dtype)
         if self.keep_m:
             self.last_m = m
         self.last_removed = removed
@@ -241,11 +254,11 @@ class PreconditionerEnv(Env):
             removed = self.last_removed
         if removed is None:
             raise ValueError("no removal bitmaps: run update / rewards_from_removed first or pass removed")
-        if self.fill == "lsq" and self.last_m is None:
+        if self._lsq and self.last_m is None:
             raise ValueError("construct with keep_m=True to keep M")
         bits = removed[b].to(self.device)
         act = self.pattern.act.long()
         a = act.clamp(min=0)
         keep = (act >= 0) & (((bits[a >> 5] >> (a & 31)) & 1) == 0)
-        vals = self.last_m[b] if self.fill == "lsq" else self.pattern.val
+        vals = self.last_m[b] if self._lsq else self.pattern.val
         return lines_to_coo(self.pattern, vals, self.matrix_size, keep)

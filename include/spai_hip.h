@@ -248,6 +248,30 @@ int spai_fill_reduce_rewards(int32_t n_lines, int32_t B, const void* workspace, 
                              int64_t nnz0, int32_t n, double r0, double f0, const float* alpha, double* residual,
                              double* reward, float* reward32, void* stream);
 
+/* ---------------------------------------------------------------- least squares by Householder QR
+ * The LSQ fill of spai_fill_residual (m = argmin ||A_lines[J] m - e_l||, J = the kept slots of line
+ * l) solved by Householder QR of the line's dense block instead of the normal equations: per line
+ * the rows I the slots' A lines touch are merged (ascending) into D = A[I, slots] in LDS, and every
+ * sample's masked problem is factored on a group of lanes (reflection norms and dot products by DPP
+ * lane swaps); a slot is dropped when its remaining column norm is below 1e-12 of its full norm
+ * (fp64 rank deficiency; the normal-equations fill drops below 1e-13 of the SQUARED norm, i.e.
+ * ~3e-7 of the norm, so it loses nearly dependent columns the QR fill still resolves).  The line
+ * residual^2 is ||Q^T e_l||^2 below the pivots
+ * (+1 when l is not in I).  Same outputs and workspace as spai_fill_lines_gram: m_out (may be NULL)
+ * [B][line_end - line_begin][W] in m_dtype, per-block partials for spai_fill_reduce /
+ * spai_fill_reduce_rewards.  Pattern lines need pat_idx (other index) and pat_act; A lines a_idx /
+ * a_val [n][WA] (a_dtype F32 when every value is exact in fp32: the same numbers, staged in half
+ * the LDS).  Widths W <= 13 with WA <= 7 (W <= 5 needs WA <= 5, W <= 7 needs WA <= 7).
+ * max_rows: spai_qr_max_rows' result for this pattern and A (the largest |I|; it selects the group
+ * size: up to 16 / 32 / 64 / 96 rows); a line with more rows than the instance holds yields a NaN
+ * residual.  No reference counterpart (the reference copies the pattern values, utils.py:331-353). */
+int spai_qr_max_rows(int32_t n, int32_t W, const int32_t* pat_idx, int32_t WA, const int32_t* a_idx,
+                     int32_t* max_rows, void* stream);
+int spai_fill_lines_qr(int32_t n, int32_t line_begin, int32_t line_end, int32_t W, const int32_t* pat_idx,
+                       const int32_t* pat_act, int32_t WA, const int32_t* a_idx, const void* a_val, int32_t a_dtype,
+                       int32_t max_rows, int32_t B, const uint32_t* removed, int32_t words, int32_t word_base,
+                       void* m_out, int32_t m_dtype, void* workspace, size_t workspace_bytes, void* stream);
+
 /* ---------------------------------------------------------------- forward policy
  * logits[a] = fc(mean_pool(relu(GATv2_2(relu(GATv2_1(x))))))[a] for a < num_actions and
  * lmax[0..B-1] = max_a logits[a]: ForwardPolicy.forward up to the masked softmax

@@ -30,6 +30,7 @@ Usage:  python tests/golden/make_golden.py            (writes *.npz + meta.json)
         python tests/golden/make_golden.py g6         (C2/C4 parity rollouts, appended)
         python tests/golden/make_golden.py g7         (C1 assembled M of three removal sets, appended)
         python tests/golden/make_golden.py g8         (C2 long parity rollout, T > 1000, appended)
+        python tests/golden/make_golden.py g9         (C2 parity rollout with T >= 20000, appended)
 """
 import gc
 import json
@@ -324,6 +325,48 @@ def parity_rollout_long():
         json.dump(meta, f, indent=1)
 
 
+def parity_rollout_longer(terminal=3.8, seed=41, min_t=20000):
+    """G9: a C2 reference rollout at least ``min_t`` steps long (pin parity mode past
+    T = 2e4), stored like G8.  The terminal logit sets a per-step stop probability of ~7e-5; if
+    the draw is shorter than ``min_t`` the next seed is tried.  Appends to meta.json."""
+    preconditioner, policy, gfn_mod, ref_utils = _import_reference()
+    meta_path = os.path.join(HERE, "meta.json")
+    meta = json.load(open(meta_path))
+    tag, grid, logit_seed = "c2longer", 256, 21
+    A = poisson2d(grid)
+    order = np.lexsort((A.col, A.row))
+    rows, cols, vals = A.row[order].astype(np.int64), A.col[order].astype(np.int64), A.data[order].astype(np.float32)
+    n = grid * grid
+    A_t = to_torch_coo(rows, cols, vals, n)
+    env = make_env(preconditioner, A_t, n)
+    E = env.num_actions - 1
+    logits = torch.randn(E + 1, generator=torch.Generator().manual_seed(logit_seed))
+    logits[E] = terminal
+    B = 2
+    while True:
+        model = gfn_mod.GFlowNet(FixedLogitPolicy(logits), None, env)
+        s0 = [A_t.clone() for _ in range(B)]
+        torch.manual_seed(seed)
+        t0 = time.time()
+        lg = model.sample_states(s0, return_log=True)
+        dt = time.time() - t0
+        T = int(lg.actions.shape[0])
+        print(tag, "seed", seed, "T", T, "s", round(dt, 1), flush=True)
+        if T >= min_t:
+            break
+        seed += 1
+    np.savez_compressed(os.path.join(HERE, f"{tag}_rollout.npz"), grid=grid, logit_seed=logit_seed,
+                        terminal_logit=terminal, seed=seed, B=B, actions=lg.actions.numpy(),
+                        fwd_probs=lg.fwd_probs.detach().numpy(), rewards=lg.rewards.numpy())
+    meta["cases"][f"{tag}_rollout"] = {
+        "B": B, "T": T, "E": E, "grid": grid,
+        "logits": f"torch.randn(E + 1, generator=torch.Generator().manual_seed({logit_seed})); [E] = {terminal}",
+        "rollout_seed": f"torch.manual_seed({seed}) before sample_states", "seconds": round(dt, 3),
+        "cpu": torch.backends.cpu.get_cpu_capability()}
+    with open(meta_path, "w") as f:
+        json.dump(meta, f, indent=1)
+
+
 def assembled_m():
     """G7: the reference's M (update_edges_and_convert_to_sparse + resize_sparse_tensor,
     utils.py:295-356, 89-126) for three removal sets of the permuted-raw-order C1 pattern
@@ -358,5 +401,7 @@ if __name__ == "__main__":
         assembled_m()
     elif len(sys.argv) > 1 and sys.argv[1] == "g8":
         parity_rollout_long()
+    elif len(sys.argv) > 1 and sys.argv[1] == "g9":
+        parity_rollout_longer()
     else:
         main()

@@ -76,6 +76,14 @@ def softmax_bits(capability: str) -> np.ndarray:
     return np.load(out), cap.stdout.strip()
 
 
+def _per_entry(a, b):
+    r = a.astype(np.float64).ravel() / b.astype(np.float64).ravel()
+    dev = np.abs(r / np.median(r) - 1.0)
+    return {"per_entry_rel_dev_after_common_scale": {"p50": float(np.percentile(dev, 50)),
+                                                     "p99": float(np.percentile(dev, 99)), "max": float(dev.max()),
+                                                     "frac_below_6e-8": float(np.mean(dev < 6e-8))}}
+
+
 def main():
     steps_goal = int(sys.argv[1]) if len(sys.argv) > 1 else 100_000
     out_path = sys.argv[2] if len(sys.argv) > 2 else None
@@ -128,7 +136,9 @@ def main():
             "capabilities": [cap_def, cap_vec],
             "entries_differing": int((p_def.view(np.uint32) != p_vec.view(np.uint32)).sum()),
             "entries": int(p_def.size),
-            "max_rel_diff": float(np.max(np.abs(p_def.astype(np.float64) - p_vec) / p_vec))},
+            "max_rel_diff": float(np.max(np.abs(p_def.astype(np.float64) - p_vec) / p_vec)),
+            # the part that can change an argmax: per-entry deviation after the common scale
+            **_per_entry(p_def, p_vec)},
         "seconds": round(time.time() - t0, 1), "torch": torch.__version__,
     }
     print(json.dumps(res, indent=1))

@@ -39,8 +39,16 @@ def _logits(E, seed, terminal=1.5):
     return lg
 
 
+_ENVS = {}
+
+
 def _env(kind):
     from gflownet_spai_amd import PreconditionerEnv, axial_pattern_3d, poisson_2d, poisson_3d
+    if kind == "c4":  # BASELINE configs[3]: 1024^2 Poisson, fp32, ||AM - I||, LSQ fill (built once)
+        if kind not in _ENVS:
+            A = poisson_2d(1024)
+            _ENVS[kind] = (PreconditionerEnv(A.shape[0], A, A, side="AM", fill="lsq", keep_m=True), A, A)
+        return _ENVS[kind]
     if kind == "2d":
         A = poisson_2d(96)
         return PreconditionerEnv(A.shape[0], A, A, side="AM", fill="lsq", keep_m=True), A, A
@@ -49,8 +57,12 @@ def _env(kind):
     return PreconditionerEnv(A.shape[0], P, A, side="AM", fill="lsq", keep_m=True), P, A
 
 
-@pytest.mark.parametrize("kind,P,bl", [("2d", 2, 3), ("2d", 3, 2), ("2d", 8, 1), ("3d", 3, 2)])
+@pytest.mark.parametrize("kind,P,bl", [("2d", 2, 3), ("2d", 3, 2), ("2d", 8, 1), ("3d", 3, 2),
+                                       ("c4", 2, 1), ("c4", 4, 1), ("c4", 8, 1), ("c4", 3, 2)])
 def test_columns_split_in_process_bit_identical(kind, P, bl):
+    """P ranks in one process (C4 geometry included: 1024^2, E = 5,238,784, P = 2/4/8 with one
+    candidate per rank, and P = 3 whose shards are not equal): word spans, 256-line shards and the
+    all_to_all windows reproduce the one-process batch bit for bit."""
     from gflownet_spai_amd import kernels
     from gflownet_spai_amd.distributed import LINE_ALIGN, bitmap_pack_index, shard_lines
     env, _, _ = _env(kind)
@@ -73,6 +85,14 @@ def test_columns_split_in_process_bit_identical(kind, P, bl):
         rm, ct, _ = kernels.rollout_select(lg[: E + 1], bl, lmax[:bl], seed, stream, r * bl, out=sel, ws_tag=f"r{r}")
         assert torch.equal(rm, removed1[r * bl:(r + 1) * bl]) and torch.equal(ct, counts1[r * bl:(r + 1) * bl])
         sends.append(sel[bitmap_pack_index(spans, bl, words, DEV)])
+    # the spans are contiguous, cover every word, and a rank's window is ~1/P of a bitmap for the
+    # row-major stencil (the all_to_all volume DESIGN.md §6 assumes)
+    assert spans[0][0] == 0 and spans[-1][1] == words
+    assert all(spans[q][0] <= spans[q + 1][0] and spans[q][1] <= spans[q + 1][1] for q in range(P - 1))
+    if kind == "c4":  # lines [b, e) name the actions of rows b - 1024 .. e + 1024 (5 per row)
+        for q, (w0, w1) in enumerate(spans):
+            b, e = shard_lines(n, q, P, LINE_ALIGN)
+            assert w1 - w0 <= (e - b + 2 * 1024) * 5 // 32 + 2
     offs = np.cumsum([0] + [bl * (w1 - w0 + 1) for w0, w1 in spans])
     limbs, blocks = [], []
     for q in range(P):

@@ -18,9 +18,9 @@
 //      of column p onto the next pivot row if the slot is kept and its remaining norm exceeds
 //      1e-12 ||D[:, p]|| (numerical rank deficiency in fp64; the normal equations of gram.hip must
 //      already drop a column whose remaining norm is below ~3e-7 of its norm: 1e-13 of the squared
-//      norm), applied to the later columns and to e_l; the pivot rows (R and Q^T e) go through LDS to one lane that
-//      back-substitutes m; the line residual^2 is the norm^2 of Q^T e below the pivots (no
-//      cancellation), + 1 when row l is not in I.
+//      norm), applied to the later columns and to e_l; back-substitution on the group (each m_p
+//      from its pivot row's lane, broadcast by a DPP group sum); the line residual^2 is the norm^2
+//      of Q^T e below the pivots (no cancellation), + 1 when row l is not in I.
 // Per-sample block sums in a fixed order (spai_fill_reduce / spai_fill_reduce_rewards sum them
 // exactly).  Deterministic: every group runs the same operation sequence, DPP reductions of
 // commutative pairs leave identical bits on every lane.
@@ -85,8 +85,23 @@ __global__ __launch_bounds__(kQNT) void k_qr_rows(int32_t n, int32_t wrt, const 
   if ((threadIdx.x & 63) == 0 && rows > 0) atomicMax(out, rows);
 }
 
+// 1/x to ~1 ulp: hardware reciprocal + one Newton step (x finite, non-zero)
+__device__ __forceinline__ double qr_rcp(double x) {
+  const double r = __builtin_amdgcn_rcp(x);
+  return fma(r, fma(-x, r, 1.0), r);
+}
+
+// A group lives inside one wavefront, and a wave's LDS instructions execute in order: a hand-off
+// between the lanes of a group needs only that the compiler keeps the LDS accesses in program
+// order (no block barrier, so the waves of a block progress independently).
+__device__ __forceinline__ void group_sync() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+}
+
 template <int W, int WA, int L, int RPL, int NT, typename TA, typename TM>
-__global__ __launch_bounds__(NT) void k_qr_fill(int32_t n, int32_t line_begin, int32_t line_end, int32_t wrt,
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(W <= 5 ? 3 : 2))) void k_qr_fill(int32_t n, int32_t line_begin, int32_t line_end, int32_t wrt,
                                                   const int32_t* __restrict__ pat_idx,
                                                   const int32_t* __restrict__ pat_act, int32_t wart,
                                                   const int32_t* __restrict__ a_idx, const TA* __restrict__ a_val,
@@ -100,7 +115,6 @@ __global__ __launch_bounds__(NT) void k_qr_fill(int32_t n, int32_t line_begin, i
   __shared__ TA sAv[NG][W][WA];
   __shared__ double sCn[NG][W];           // ||D[:, p]||^2
   __shared__ int sRowL[NG];               // position of row l in I; -1: not in I; -2: block overflow
-  __shared__ double sSol[NG][W][W + 1];   // pivot rows by slot: R[p][q > p], R[p][p], then (Q^T e)
   __shared__ double sR2[kQChunk][kQLines];
   const int t = threadIdx.x, g = t / L, j = t % L, lane = t & 63, wave = t >> 6;
   const int lb = blockIdx.x;
@@ -125,7 +139,7 @@ __global__ __launch_bounds__(NT) void k_qr_fill(int32_t n, int32_t line_begin, i
         sAv[g][p][s] = a >= 0 ? a_val[(int64_t)kp * wart + s] : (TA)0;
       }
       for (int e = j; e < R * W; e += L) (&sD[g][0][0])[e] = (TA)0;
-      __syncthreads();
+      group_sync();
       if (j == 0) {  // merge the sorted A lines into the rows of I (ascending)
         int h[W], cur[W];
         double cn[W];
@@ -164,7 +178,7 @@ __global__ __launch_bounds__(NT) void k_qr_fill(int32_t n, int32_t line_begin, i
         for (int p = 0; p < W; ++p) sCn[g][p] = cn[p];
         sRowL[g] = rowl;
       }
-      __syncthreads();
+      group_sync();
       // ---- 2. every sample of the chunk
       int act[W], wofs[W];
       double cn[W];
@@ -191,7 +205,8 @@ __global__ __launch_bounds__(NT) void k_qr_fill(int32_t n, int32_t line_begin, i
           rhs[i] = rho == rowl ? 1.0 : 0.0;
         }
         int k = 0;  // next pivot row
-        double diag[W];
+        int krow[W];
+        double rdg[W];  // 1 / R_pp of the pivots (0: slot dropped)
 #pragma unroll
         for (int p = 0; p < W; ++p) {
           double s1 = 0.0, xk = 0.0;
@@ -206,7 +221,7 @@ __global__ __launch_bounds__(NT) void k_qr_fill(int32_t n, int32_t line_begin, i
           const bool ok = keep[p] && sig > 1e-24 * cn[p];  // |R_kk| > 1e-12 ||D[:, p]||
           const double sq = sqrt(sig);
           const double alpha = xkk >= 0.0 ? -sq : sq;
-          const double tau = ok ? 1.0 / (sig - alpha * xkk) : 0.0;  // H = I - tau v v^T
+          const double tau = ok ? qr_rcp(sig - alpha * xkk) : 0.0;  // H = I - tau v v^T
           double v[RPL];
 #pragma unroll
           for (int i = 0; i < RPL; ++i) {
@@ -229,18 +244,8 @@ __global__ __launch_bounds__(NT) void k_qr_fill(int32_t n, int32_t line_begin, i
             for (int q = p + 1; q < W; ++q) dv[i][q] = fma(-d[q], v[i], dv[i][q]);
             rhs[i] = fma(-d[W], v[i], rhs[i]);
           }
-          diag[p] = ok ? alpha : 0.0;
-          // pivot row k is final now (later reflections act on rows > k): its owner hands it on
-          if (ok && j == k % L) {
-            const int ks = k / L;
-#pragma unroll
-            for (int q = p + 1; q <= W; ++q) {
-              double x = 0.0;
-#pragma unroll
-              for (int i = 0; i < RPL; ++i) x = i == ks ? (q < W ? dv[i][q] : rhs[i]) : x;
-              sSol[g][p][q] = x;
-            }
-          }
+          krow[p] = k;  // row k is final now: later reflections act on rows > k
+          rdg[p] = ok ? qr_rcp(alpha) : 0.0;
           k += ok ? 1 : 0;
         }
         // the line residual^2: Q^T e below the pivot rows (+1 when row l is outside I)
@@ -248,30 +253,38 @@ __global__ __launch_bounds__(NT) void k_qr_fill(int32_t n, int32_t line_begin, i
 #pragma unroll
         for (int i = 0; i < RPL; ++i) rs = fma(j + L * i >= k ? rhs[i] : 0.0, rhs[i], rs);
         rs = group_sum<L>(rs);
-        __syncthreads();  // the pivot rows in sSol
-        if (j == 0) {
-          double m[W];
+        // back-substitution on the group: m_p from its pivot row (on lane krow % L), broadcast by a
+        // group sum to which only that lane contributes (x + 0 is exact)
+        double m[W];
 #pragma unroll
-          for (int p = W - 1; p >= 0; --p) {
-            double a = sSol[g][p][W];
+        for (int p = W - 1; p >= 0; --p) {
+          const int kr = krow[p], ks = kr / L;
+          double a = 0.0;
 #pragma unroll
-            for (int q = p + 1; q < W; ++q) a = fma(-sSol[g][p][q], m[q], a);
-            m[p] = diag[p] != 0.0 ? a / diag[p] : 0.0;
+          for (int i = 0; i < RPL; ++i) a = i == ks ? rhs[i] : a;
+#pragma unroll
+          for (int q = p + 1; q < W; ++q) {
+            double r = 0.0;
+#pragma unroll
+            for (int i = 0; i < RPL; ++i) r = i == ks ? dv[i][q] : r;
+            a = fma(-r, m[q], a);
           }
-          if (valid) {
-            if (m_out != nullptr) {
-              TM* dst = m_out + ((int64_t)b * nloc + (l - line_begin)) * wrt;
-#pragma unroll
-              for (int p = 0; p < W; ++p)
-                if (p < wrt) dst[p] = (TM)m[p];
-            }
-            sR2[s][li] = rowl == -2 ? __builtin_nan("") : rs + (rowl < 0 ? 1.0 : 0.0);
-          }
+          m[p] = group_sum<L>(rdg[p] != 0.0 && j == kr % L ? a * rdg[p] : 0.0);
         }
-        __syncthreads();  // sSol reused by the next sample
+        if (j == 0 && valid) {
+          if (m_out != nullptr) {
+            TM* dst = m_out + ((int64_t)b * nloc + (l - line_begin)) * wrt;
+#pragma unroll
+            for (int p = 0; p < W; ++p)
+              if (p < wrt) dst[p] = (TM)m[p];
+          }
+          sR2[s][li] = rowl == -2 ? __builtin_nan("") : rs + (rowl < 0 ? 1.0 : 0.0);
+        }
       }
+      group_sync();  // the group's block is re-staged by the next round
     }
     // per-sample block sums in a fixed order (the k_gram_fill partial layout)
+    __syncthreads();  // every group's line residuals are in sR2
     for (int s = wave; s < nb; s += NT / 64) {
       double acc = 0.0;
 #pragma unroll

@@ -11,19 +11,19 @@
 //
 // Per block: 256 consecutive lines (the exact-sum invariance unit, LINE_ALIGN), in rounds of NG
 // lines (one per group).  Per round:
-//   1. the W slots' A lines are staged in LDS and one lane per group merges them (they are sorted
-//      by row index) into the dense block D = A[I, slots] in ascending row order, with the column
-//      norms ||D[:, p]||^2 (pivot floor) and the position of row l in I (the right-hand side e_l);
-//   2. per sample: the kept-slot mask from the removal bitmap, then for p = 0 .. W-1 a reflection
-//      of column p onto the next pivot row if the slot is kept and its remaining norm exceeds
-//      1e-12 ||D[:, p]|| (numerical rank deficiency in fp64; the normal equations of gram.hip must
-//      already drop a column whose remaining norm is below ~3e-7 of its norm: 1e-13 of the squared
-//      norm), applied to the later columns and to e_l; back-substitution on the group (each m_p
-//      from its pivot row's lane, broadcast by a DPP group sum); the line residual^2 is the norm^2
-//      of Q^T e below the pivots (no cancellation), + 1 when row l is not in I.
-// Per-sample block sums in a fixed order (spai_fill_reduce / spai_fill_reduce_rewards sum them
-// exactly).  Deterministic: every group runs the same operation sequence, DPP reductions of
-// commutative pairs leave identical bits on every lane.
+//   1. per line, on its group of L lanes: the W slots' A lines are staged in LDS and one lane
+//      merges them (they are sorted by row index) into the dense block D = A[I, slots], rows of I
+//      ascending, with the column norms ||D[:, p]||^2 and the position of row l in I; then the
+//      FULL Householder QR of D (all slots, the sample-independent part): R (W x W), the first W
+//      entries of Q^T e_l and the tail ||(Q^T e_l)[W..]||^2 (+1 when l is not in I) go to LDS;
+//   2. per (line, sample), on ONE lane: the removal bitmap's kept slots J select the columns R_J
+//      of R (R_J = Q^T D_J: the same singular values as A[I, J], so the small problem
+//      min ||R_J m - Q^T e|| keeps the QR's accuracy, no normal equations), which are
+//      re-triangularised by Householder reflections of at most W rows; a slot is dropped when
+//      its remaining norm is below 1e-12 ||D[:, p]|| (numerical rank deficiency in fp64; the
+//      normal equations of gram.hip already drop a column whose remaining norm is below ~3e-7 of
+//      its norm: 1e-13 of the squared norm); back-substitution gives m, and the line residual^2
+//      is the tail + (Q^T e) below the pivots (sums of squares: no cancellation).
 #include "spai_device.h"
 #include "spai_status.h"
 
@@ -110,11 +110,15 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(W <= 5 ? 3 :
                                                   double* __restrict__ partials) {
   constexpr int NG = NT / L, R = L * RPL, NR = kQLines / NG;  // groups, block rows, rounds
   static_assert(kQLines % NG == 0 && W * WA <= 8 * 1024, "shapes");
+  constexpr int T = W * (W + 1) / 2;  // packed upper triangle of R (row-major: p <= q)
   __shared__ TA sD[NG][R][W];             // dense blocks A[I, slots] (rows of I ascending)
   __shared__ int sAi[NG][W][WA];          // staged A lines of the slots
   __shared__ TA sAv[NG][W][WA];
-  __shared__ double sCn[NG][W];           // ||D[:, p]||^2
+  __shared__ double sCn[NG][W];           // ||D[:, p]||^2 (the rank floor of the masked solves)
   __shared__ int sRowL[NG];               // position of row l in I; -1: not in I; -2: block overflow
+  __shared__ double sRf[NG][T];           // R of the full block (all slots)
+  __shared__ double sC[NG][W + 1];        // (Q^T e_l)[0..W), then the tail ||(Q^T e_l)[W..)||^2 (+1 if l not in I)
+  __shared__ int sAct[NG][W];             // action ids of the slots (-1: no slot / empty A line)
   __shared__ double sR2[kQChunk][kQLines];
   const int t = threadIdx.x, g = t / L, j = t % L, lane = t & 63, wave = t >> 6;
   const int lb = blockIdx.x;
@@ -127,75 +131,63 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(W <= 5 ? 3 :
     const int nb = min(kQChunk, B - b0);
 #pragma unroll 1
     for (int r = 0; r < NR; ++r) {
-      const int li = r * NG + g;
-      const bool valid = li < nvl;
-      const int l = blk0 + (valid ? li : 0);
-      // ---- 1. stage the slots' A lines, zero the block
-      for (int e = j; e < W * WA; e += L) {
-        const int p = e / WA, s = e % WA;
-        const int kp = (valid && p < wrt) ? pat_idx[(int64_t)l * wrt + p] : -1;
-        const int a = (kp >= 0 && s < wart) ? a_idx[(int64_t)kp * wart + s] : -1;
-        sAi[g][p][s] = a;
-        sAv[g][p][s] = a >= 0 ? a_val[(int64_t)kp * wart + s] : (TA)0;
-      }
-      for (int e = j; e < R * W; e += L) (&sD[g][0][0])[e] = (TA)0;
-      group_sync();
-      if (j == 0) {  // merge the sorted A lines into the rows of I (ascending)
-        int h[W], cur[W];
-        double cn[W];
-#pragma unroll
-        for (int p = 0; p < W; ++p) {
-          h[p] = 0;
-          cn[p] = 0.0;
-          const int a = sAi[g][p][0];
-          cur[p] = a >= 0 ? a : INT_MAX;
+      {
+        // ---- 1. per line (group g): the dense block, then its FULL Householder QR (all slots)
+        const int li = r * NG + g;
+        const bool valid = li < nvl;
+        const int l = blk0 + (valid ? li : 0);
+        for (int e = j; e < W * WA; e += L) {
+          const int p = e / WA, s = e % WA;
+          const int kp = (valid && p < wrt) ? pat_idx[(int64_t)l * wrt + p] : -1;
+          const int a = (kp >= 0 && s < wart) ? a_idx[(int64_t)kp * wart + s] : -1;
+          sAi[g][p][s] = a;
+          sAv[g][p][s] = a >= 0 ? a_val[(int64_t)kp * wart + s] : (TA)0;
         }
-        int rowl = -1, rho = 0;
-#pragma unroll 1
-        for (int it = 0; it <= R; ++it) {
-          int rmin = INT_MAX;
+        for (int e = j; e < R * W; e += L) (&sD[g][0][0])[e] = (TA)0;
+        group_sync();
+        if (j == 0) {  // merge the sorted A lines into the rows of I (ascending)
+          int h[W], cur[W];
+          double cn[W];
 #pragma unroll
-          for (int p = 0; p < W; ++p) rmin = min(rmin, cur[p]);
-          if (rmin == INT_MAX) break;
-          if (rho == R) {  // more rows than the instance holds (the caller's max_rows was wrong)
-            rowl = -2;
-            break;
+          for (int p = 0; p < W; ++p) {
+            h[p] = 0;
+            cn[p] = 0.0;
+            const int a = sAi[g][p][0];
+            cur[p] = a >= 0 ? a : INT_MAX;
+          }
+          int rowl = -1, rho = 0;
+#pragma unroll 1
+          for (int it = 0; it <= R; ++it) {
+            int rmin = INT_MAX;
+#pragma unroll
+            for (int p = 0; p < W; ++p) rmin = min(rmin, cur[p]);
+            if (rmin == INT_MAX) break;
+            if (rho == R) {  // more rows than the instance holds (the caller's max_rows was wrong)
+              rowl = -2;
+              break;
+            }
+#pragma unroll
+            for (int p = 0; p < W; ++p)
+              if (cur[p] == rmin) {
+                const TA v = sAv[g][p][h[p]];
+                sD[g][rho][p] = v;
+                cn[p] += (double)v * (double)v;
+                ++h[p];
+                const int a = h[p] < WA ? sAi[g][p][h[p]] : -1;
+                cur[p] = a >= 0 ? a : INT_MAX;
+              }
+            if (rmin == l) rowl = rho;
+            ++rho;
           }
 #pragma unroll
-          for (int p = 0; p < W; ++p)
-            if (cur[p] == rmin) {
-              const TA v = sAv[g][p][h[p]];
-              sD[g][rho][p] = v;
-              cn[p] += (double)v * (double)v;
-              ++h[p];
-              const int a = h[p] < WA ? sAi[g][p][h[p]] : -1;
-              cur[p] = a >= 0 ? a : INT_MAX;
-            }
-          if (rmin == l) rowl = rho;
-          ++rho;
+          for (int p = 0; p < W; ++p) {
+            sCn[g][p] = cn[p];
+            sAct[g][p] = (valid && p < wrt && sAi[g][p][0] >= 0) ? pat_act[(int64_t)l * wrt + p] : -1;
+          }
+          sRowL[g] = rowl;
         }
-#pragma unroll
-        for (int p = 0; p < W; ++p) sCn[g][p] = cn[p];
-        sRowL[g] = rowl;
-      }
-      group_sync();
-      // ---- 2. every sample of the chunk
-      int act[W], wofs[W];
-      double cn[W];
-#pragma unroll
-      for (int p = 0; p < W; ++p) {
-        act[p] = (valid && p < wrt && sAi[g][p][0] >= 0) ? pat_act[(int64_t)l * wrt + p] : -1;
-        wofs[p] = act[p] >= 0 ? (act[p] >> 5) - word_base : 0;
-        cn[p] = sCn[g][p];
-      }
-      const int rowl = sRowL[g];
-#pragma unroll 1
-      for (int s = 0; s < nb; ++s) {
-        const int b = b0 + s;
-        const uint32_t* rm = removed + (int64_t)b * words;
-        bool keep[W];
-#pragma unroll
-        for (int p = 0; p < W; ++p) keep[p] = act[p] >= 0 && !((rm[wofs[p]] >> (act[p] & 31)) & 1u);
+        group_sync();
+        const int rowl = sRowL[g];
         double dv[RPL][W], rhs[RPL];
 #pragma unroll
         for (int i = 0; i < RPL; ++i) {
@@ -204,9 +196,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(W <= 5 ? 3 :
           for (int p = 0; p < W; ++p) dv[i][p] = (double)sD[g][rho][p];
           rhs[i] = rho == rowl ? 1.0 : 0.0;
         }
-        int k = 0;  // next pivot row
-        int krow[W];
-        double rdg[W];  // 1 / R_pp of the pivots (0: slot dropped)
+        // reflection p maps column p onto row p (a column already zero below row p: none)
 #pragma unroll
         for (int p = 0; p < W; ++p) {
           double s1 = 0.0, xk = 0.0;
@@ -214,19 +204,18 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(W <= 5 ? 3 :
           for (int i = 0; i < RPL; ++i) {
             const int rho = j + L * i;
             const double x = dv[i][p];
-            s1 = fma(rho >= k ? x : 0.0, x, s1);
-            xk += rho == k ? x : 0.0;
+            s1 = fma(rho >= p ? x : 0.0, x, s1);
+            xk += rho == p ? x : 0.0;
           }
           const double sig = group_sum<L>(s1), xkk = group_sum<L>(xk);
-          const bool ok = keep[p] && sig > 1e-24 * cn[p];  // |R_kk| > 1e-12 ||D[:, p]||
           const double sq = sqrt(sig);
           const double alpha = xkk >= 0.0 ? -sq : sq;
-          const double tau = ok ? qr_rcp(sig - alpha * xkk) : 0.0;  // H = I - tau v v^T
+          const double tau = sig > 0.0 ? qr_rcp(sig - alpha * xkk) : 0.0;  // H = I - tau v v^T
           double v[RPL];
 #pragma unroll
           for (int i = 0; i < RPL; ++i) {
             const int rho = j + L * i;
-            v[i] = rho >= k ? dv[i][p] - (rho == k ? alpha : 0.0) : 0.0;
+            v[i] = rho >= p ? dv[i][p] - (rho == p ? alpha : 0.0) : 0.0;
           }
           double d[W + 1];  // v . column q (q > p), v . rhs
 #pragma unroll
@@ -244,47 +233,122 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(W <= 5 ? 3 :
             for (int q = p + 1; q < W; ++q) dv[i][q] = fma(-d[q], v[i], dv[i][q]);
             rhs[i] = fma(-d[W], v[i], rhs[i]);
           }
-          krow[p] = k;  // row k is final now: later reflections act on rows > k
-          rdg[p] = ok ? qr_rcp(alpha) : 0.0;
-          k += ok ? 1 : 0;
-        }
-        // the line residual^2: Q^T e below the pivot rows (+1 when row l is outside I)
-        double rs = 0.0;
+          // row p of R and (Q^T e)_p are final now (later reflections act on rows > p)
+          if (j == p % L) {
+            constexpr int kq0 = 0;
+            (void)kq0;
+            const int base = p * W - p * (p - 1) / 2;
+            sRf[g][base] = sig > 0.0 ? alpha : dv[p / L][p];
 #pragma unroll
-        for (int i = 0; i < RPL; ++i) rs = fma(j + L * i >= k ? rhs[i] : 0.0, rhs[i], rs);
-        rs = group_sum<L>(rs);
-        // back-substitution on the group: m_p from its pivot row (on lane krow % L), broadcast by a
-        // group sum to which only that lane contributes (x + 0 is exact)
-        double m[W];
-#pragma unroll
-        for (int p = W - 1; p >= 0; --p) {
-          const int kr = krow[p], ks = kr / L;
-          double a = 0.0;
-#pragma unroll
-          for (int i = 0; i < RPL; ++i) a = i == ks ? rhs[i] : a;
-#pragma unroll
-          for (int q = p + 1; q < W; ++q) {
-            double r = 0.0;
-#pragma unroll
-            for (int i = 0; i < RPL; ++i) r = i == ks ? dv[i][q] : r;
-            a = fma(-r, m[q], a);
+            for (int q = p + 1; q < W; ++q) sRf[g][base + (q - p)] = dv[p / L][q];
+            sC[g][p] = rhs[p / L];
           }
-          m[p] = group_sum<L>(rdg[p] != 0.0 && j == kr % L ? a * rdg[p] : 0.0);
         }
-        if (j == 0 && valid) {
-          if (m_out != nullptr) {
-            TM* dst = m_out + ((int64_t)b * nloc + (l - line_begin)) * wrt;
+        double tl = 0.0;  // the tail of Q^T e: rows >= W
 #pragma unroll
-            for (int p = 0; p < W; ++p)
-              if (p < wrt) dst[p] = (TM)m[p];
+        for (int i = 0; i < RPL; ++i) tl = fma(j + L * i >= W ? rhs[i] : 0.0, rhs[i], tl);
+        tl = group_sum<L>(tl);
+        if (j == 0) sC[g][W] = rowl == -2 ? __builtin_nan("") : tl + (rowl < 0 ? 1.0 : 0.0);
+      }
+      __syncthreads();  // R, Q^T e of the round's lines
+      // ---- 2. per (line, sample), one lane: QR of the masked columns of R (R_J has the singular
+      // values of A[I, J]: the small problem min ||R_J m - c|| keeps the QR's accuracy), the tail
+      // of Q^T e added to its residual
+      {
+        const int gl = t % NG;
+        const int li = r * NG + gl;
+        const bool valid = li < nvl;
+        const int l = blk0 + (valid ? li : 0);
+        int act[W], wofs[W];
+        double cn[W];
+#pragma unroll
+        for (int p = 0; p < W; ++p) {
+          act[p] = sAct[gl][p];
+          wofs[p] = act[p] >= 0 ? (act[p] >> 5) - word_base : 0;
+          cn[p] = sCn[gl][p];
+        }
+#pragma unroll 1
+        for (int s = t / NG; s < nb; s += NT / NG) {
+          const int b = b0 + s;
+          const uint32_t* rm = removed + (int64_t)b * words;
+          bool keep[W];
+#pragma unroll
+          for (int p = 0; p < W; ++p) keep[p] = act[p] >= 0 && !((rm[wofs[p]] >> (act[p] & 31)) & 1u);
+          double Rm[W][W], c[W];  // Rm[i][q], i <= q (the rest is never read)
+#pragma unroll
+          for (int i = 0; i < W; ++i) {
+#pragma unroll
+            for (int q = i; q < W; ++q) Rm[i][q] = sRf[gl][i * W - i * (i - 1) / 2 + (q - i)];
+            c[i] = sC[gl][i];
           }
-          sR2[s][li] = rowl == -2 ? __builtin_nan("") : rs + (rowl < 0 ? 1.0 : 0.0);
+          const double tail = sC[gl][W];
+          int k = 0, krow[W];
+          double rdg[W];
+#pragma unroll
+          for (int p = 0; p < W; ++p) {
+            // column p has rows 0..p; rows < k are earlier pivots: reflect rows k..p onto row k
+            double sig = 0.0, xk = 0.0;
+#pragma unroll
+            for (int i = 0; i <= p; ++i) {
+              sig = fma(i >= k ? Rm[i][p] : 0.0, Rm[i][p], sig);
+              xk = i == k ? Rm[i][p] : xk;
+            }
+            const bool ok = keep[p] && sig > 1e-24 * cn[p];  // |R_kk| > 1e-12 ||D[:, p]||
+            const double sq = sqrt(sig);
+            const double alpha = xk >= 0.0 ? -sq : sq;
+            const double tau = ok ? qr_rcp(sig - alpha * xk) : 0.0;
+            double v[W];
+#pragma unroll
+            for (int i = 0; i <= p; ++i) v[i] = i >= k ? Rm[i][p] - (i == k ? alpha : 0.0) : 0.0;
+#pragma unroll
+            for (int q = p + 1; q <= W; ++q) {
+              double a = 0.0;
+#pragma unroll
+              for (int i = 0; i <= p; ++i) a = fma(v[i], q < W ? Rm[i][q] : c[i], a);
+              a *= tau;
+#pragma unroll
+              for (int i = 0; i <= p; ++i) {
+                if (q < W) Rm[i][q] = fma(-a, v[i], Rm[i][q]);
+                else c[i] = fma(-a, v[i], c[i]);
+              }
+            }
+            krow[p] = k;
+            rdg[p] = ok ? qr_rcp(alpha) : 0.0;
+            k += ok ? 1 : 0;
+          }
+          double rs = tail;  // + (Q^T e) below the pivots within R's rows
+#pragma unroll
+          for (int i = 0; i < W; ++i) rs = fma(i >= k ? c[i] : 0.0, c[i], rs);
+          double m[W];
+#pragma unroll
+          for (int p = W - 1; p >= 0; --p) {
+            const int kr = krow[p];
+            double a = 0.0;
+#pragma unroll
+            for (int i = 0; i <= p; ++i) a = i == kr ? c[i] : a;
+#pragma unroll
+            for (int q = p + 1; q < W; ++q) {
+              double x = 0.0;
+#pragma unroll
+              for (int i = 0; i <= p; ++i) x = i == kr ? Rm[i][q] : x;
+              a = fma(-x, m[q], a);
+            }
+            m[p] = a * rdg[p];  // 0 for a dropped slot
+          }
+          if (valid) {
+            if (m_out != nullptr) {
+              TM* dst = m_out + ((int64_t)b * nloc + (l - line_begin)) * wrt;
+#pragma unroll
+              for (int p = 0; p < W; ++p)
+                if (p < wrt) dst[p] = (TM)m[p];
+            }
+            sR2[s][li] = rs;
+          }
         }
       }
-      group_sync();  // the group's block is re-staged by the next round
+      __syncthreads();  // the round's LDS is reused by the next round
     }
     // per-sample block sums in a fixed order (the k_gram_fill partial layout)
-    __syncthreads();  // every group's line residuals are in sR2
     for (int s = wave; s < nb; s += NT / 64) {
       double acc = 0.0;
 #pragma unroll

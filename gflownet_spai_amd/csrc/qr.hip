@@ -1,13 +1,13 @@
-// Least-squares fill of M by Householder QR, one small dense problem per (line, sample), for
-// gfx950.  The north star's per-column constrained least squares
+// Least-squares fill of M by Householder QR for gfx950.  The north star's per-column constrained
+// least squares
 //     m_l = argmin || A[:, J] m - e_l ||_2 ,  J = the kept pattern slots of line l
-// solved the way it names: the line's dense block A[I, J] (I = the union of the rows the slots'
-// A lines touch) is staged in LDS once per line, and every sample's masked problem is factored by
-// Householder reflections on L lanes of a wavefront (a "group"), each lane holding RPL rows of the
-// block; the reflections' norms and dot products are group reductions on DPP lane swaps (quad_perm,
-// row_half_mirror, row_mirror) — no LDS traffic inside the factorisation.  No normal equations: the
-// conditioning is that of A[I, J] itself, not its square (the Gram-cached fill in
-// gram.hip is the normal-equations path).
+// solved the way it names: the line's dense block A[I, slots] (I = the union of the rows the
+// slots' A lines touch) is staged in LDS once per line and factored by Householder reflections on
+// L lanes of a wavefront (a "group"), each lane holding RPL rows of the block; the reflections'
+// norms and dot products are group reductions on DPP lane swaps (quad_perm, row_half_mirror,
+// row_mirror) — no LDS traffic inside the factorisation.  No normal equations: the conditioning
+// is that of A[I, J] itself, not its square (the Gram-cached fill in gram.hip is the
+// normal-equations path).
 //
 // Per block: 256 consecutive lines (the exact-sum invariance unit, LINE_ALIGN), in rounds of NG
 // lines (one per group).  Per round:

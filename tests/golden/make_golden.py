@@ -325,7 +325,7 @@ def parity_rollout_long():
         json.dump(meta, f, indent=1)
 
 
-def parity_rollout_longer(terminal=3.8, seed=41, min_t=20000):
+def parity_rollout_longer(terminal=3.0, seed=41, min_t=20000):
     """G9: a C2 reference rollout at least ``min_t`` steps long (pin parity mode past
     T = 2e4), stored like G8.  The terminal logit sets a per-step stop probability of ~7e-5; if
     the draw is shorter than ``min_t`` the next seed is tried.  Appends to meta.json."""
@@ -348,7 +348,8 @@ def parity_rollout_longer(terminal=3.8, seed=41, min_t=20000):
         s0 = [A_t.clone() for _ in range(B)]
         torch.manual_seed(seed)
         t0 = time.time()
-        lg = model.sample_states(s0, return_log=True)
+        with torch.no_grad():  # values only: without it every step's autograd graph ([B, E+1] tensors) is kept
+            lg = model.sample_states(s0, return_log=True)
         dt = time.time() - t0
         T = int(lg.actions.shape[0])
         print(tag, "seed", seed, "T", T, "s", round(dt, 1), flush=True)

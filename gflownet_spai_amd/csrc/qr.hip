@@ -101,7 +101,7 @@ __device__ __forceinline__ void group_sync() {
 }
 
 template <int W, int WA, int L, int RPL, int NT, typename TA, typename TM>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(W <= 5 ? 3 : 2))) void k_qr_fill(int32_t n, int32_t line_begin, int32_t line_end, int32_t wrt,
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(W <= 5 ? 4 : 2))) void k_qr_fill(int32_t n, int32_t line_begin, int32_t line_end, int32_t wrt,
                                                   const int32_t* __restrict__ pat_idx,
                                                   const int32_t* __restrict__ pat_act, int32_t wart,
                                                   const int32_t* __restrict__ a_idx, const TA* __restrict__ a_val,
@@ -119,7 +119,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(W <= 5 ? 3 :
   __shared__ double sRf[NG][T];           // R of the full block (all slots)
   __shared__ double sC[NG][W + 1];        // (Q^T e_l)[0..W), then the tail ||(Q^T e_l)[W..)||^2 (+1 if l not in I)
   __shared__ int sAct[NG][W];             // action ids of the slots (-1: no slot / empty A line)
-  __shared__ double sR2[kQChunk][kQLines];
+  __shared__ double sR2[kQChunk][NG];       // per (sample, group line): the sum over the rounds
   const int t = threadIdx.x, g = t / L, j = t % L, lane = t & 63, wave = t >> 6;
   const int lb = blockIdx.x;
   const int64_t nloc = line_end - line_begin;
@@ -129,6 +129,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(W <= 5 ? 3 :
 #pragma unroll 1
   for (int b0 = 0; b0 < B; b0 += kQChunk) {
     const int nb = min(kQChunk, B - b0);
+    for (int i = t; i < kQChunk * NG; i += NT) (&sR2[0][0])[i] = 0.0;  // ordered by the first barrier
 #pragma unroll 1
     for (int r = 0; r < NR; ++r) {
       {
@@ -342,17 +343,16 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(W <= 5 ? 3 :
               for (int p = 0; p < W; ++p)
                 if (p < wrt) dst[p] = (TM)m[p];
             }
-            sR2[s][li] = rs;
+            sR2[s][gl] += rs;  // one thread per (s, gl): the rounds in order
           }
         }
       }
       __syncthreads();  // the round's LDS is reused by the next round
     }
     // per-sample block sums in a fixed order (the k_gram_fill partial layout)
+    static_assert(NG <= 64, "one wave sums a sample's group lines");
     for (int s = wave; s < nb; s += NT / 64) {
-      double acc = 0.0;
-#pragma unroll
-      for (int q = 0; q < kQLines / 64; ++q) acc += (q * 64 + lane < nvl) ? sR2[s][q * 64 + lane] : 0.0;
+      double acc = lane < NG ? sR2[s][lane] : 0.0;
       acc = wave_sum(acc);
       if (lane == 0) partials[(int64_t)(b0 + s) * gridDim.x + lb] = acc;
     }

@@ -53,11 +53,17 @@ static_assert(kTile <= 65535, "run offsets and counts are packed in 16 bits (k_t
 constexpr int kGrpNT = KGRPNT;             // threads of a k_tile block (16 actions each)
 constexpr int kWin = 2048;                 // records per LDS output window of k_tile's slot path
 constexpr int kList = 4000;                // compacted winners per k_tile block (<= 49 % of the tile; denser: slot path)
-constexpr int kSampM = 65536;              // subset size (power of two, capped by E)
+#ifndef KSAMPM
+#define KSAMPM 65536
+#endif
+constexpr int kSampM = KSAMPM;             // subset size (power of two, capped by E)
 constexpr int kSampNT = 256;
 constexpr int kSampCap = 32768;            // sampled winners behind the splitters
 constexpr int kMaxNsb = kSampM / kSampNT;  // presample blocks per sample (256)
-constexpr int kTarget = 4096;              // winners per bucket (target)
+#ifndef KTARGET
+#define KTARGET 4096
+#endif
+constexpr int kTarget = KTARGET;            // winners per bucket (target)
 constexpr int kMaxB = 1024;                // buckets per sample (11 bits in the LDS record)
 constexpr int kCap2 = 8192;               // LDS capacity of k_sort2 (records per bucket)
 constexpr int kMaxSub = 4096;              // value sub-buckets per bucket in k_sort2
@@ -427,7 +433,8 @@ __global__ __launch_bounds__(kSortNT) void k_splitters(int32_t E, int32_t M, int
   // flight at once: wave w reads presample blocks w*kBPW .. w*kBPW + kBPW - 1 (kSampNT keys
   // each, kLPB per lane); the key range comes from the registers
   constexpr int kBPW = kMaxNsb / (kSortNT / 64), kLPB = kSampNT / 64, kHalf = kBPW / 2;
-  static_assert(kMaxNsb % (kSortNT / 64) == 0 && kSampNT % 64 == 0 && kBPW % 2 == 0, "k_splitters staging");
+  static_assert(kMaxNsb % (kSortNT / 64) == 0 && kSampNT % 64 == 0 && kBPW % 2 == 0 && kHalf * kLPB <= 32,
+                "k_splitters staging (the 32-bit validity mask of a half)");
   uint32_t mn = 0xFFFFFFFFu, mx = 0u;
 #pragma unroll 1
   for (int h = 0; h < 2; ++h) {

@@ -257,6 +257,54 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(W <= 5 ? FI
   }
 }
 
+// The masked LDL^T solve of one wide line and sample, in place: a = G (packed upper triangle),
+// y = c on entry; y = m on exit (0 on removed slots); returns the line residual^2 1 - c^T m.
+template <int W>
+__device__ __forceinline__ double wide_lsq_solve(double (&a)[tri(W)], double (&y)[W], uint32_t keep) {
+  double r2 = 1.0;
+  // left-looking LDL^T in place (column k of the packed upper triangle at step k), so the
+  // pivot test reads the ORIGINAL G_kk: the per-pivot floor 1e-13 G_kk of k_gram_fill and
+  // fill.hip's k_line, with no extra registers.  Column k first becomes u_jk = G_jk -
+  // sum_{q<j} l_qj u_qk (j < k), then l_qk = u_qk / D_q; the diagonal slot ends as 1/D_k
+  // (0 for a removed or singular pivot: l_k. = 0 and m_k = 0, as in k_gram_fill).
+#pragma unroll
+  for (int k = 0; k < W; ++k) {
+#pragma unroll
+    for (int j = 1; j < k; ++j) {
+      double u = a[gidx<W>(j, k)];
+#pragma unroll
+      for (int q = 0; q < j; ++q) u -= a[gidx<W>(q, j)] * a[gidx<W>(q, k)];
+      a[gidx<W>(j, k)] = u;
+    }
+    const double gkk = a[gidx<W>(k, k)];
+    double d = gkk;
+#pragma unroll
+    for (int q = 0; q < k; ++q) {
+      const double l = a[gidx<W>(q, k)] * a[gidx<W>(q, q)];  // u_qk / D_q
+      d -= l * a[gidx<W>(q, k)];
+      a[gidx<W>(q, k)] = l;
+    }
+    a[gidx<W>(k, k)] = (((keep >> k) & 1u) && d > 1e-13 * gkk) ? fast_rcp(d) : 0.0;
+  }
+#pragma unroll
+  for (int k = 0; k < W; ++k) {  // forward substitution in place (y[q < k] are final)
+    double v = y[k];
+#pragma unroll
+    for (int q = 0; q < k; ++q) v -= a[gidx<W>(q, k)] * y[q];
+    y[k] = v;
+  }
+#pragma unroll
+  for (int k = 0; k < W; ++k) r2 -= y[k] * y[k] * a[gidx<W>(k, k)];
+#pragma unroll
+  for (int k = W - 1; k >= 0; --k) {  // back substitution in place: y[q > k] already hold m_q
+    double v = y[k] * a[gidx<W>(k, k)];
+#pragma unroll
+    for (int q = k + 1; q < W; ++q) v -= a[gidx<W>(k, q)] * y[q];
+    y[k] = v;
+  }
+  return r2;
+}
+
 // Wide lines (8 <= W <= 13, e.g. the 13-point 3-D star of config C3): the same stream and
 // outputs as k_gram_fill, but the factorisation runs in place on one packed working copy of G
 // per sample (left-looking LDL^T, T = W(W+1)/2 doubles in registers), one wave per SIMD.
@@ -323,46 +371,7 @@ __global__ __launch_bounds__(kNT) void k_gram_fill_wide(int32_t n, int32_t line_
     if constexpr (LSQ) {
 #pragma unroll
       for (int k = 0; k < W; ++k) y[k] = (double)gps[(T + k) * 64];  // c, solved in place below
-      // left-looking LDL^T in place (column k of the packed upper triangle at step k), so the
-      // pivot test reads the ORIGINAL G_kk: the per-pivot floor 1e-13 G_kk of k_gram_fill and
-      // fill.hip's k_line, with no extra registers.  Column k first becomes u_jk = G_jk -
-      // sum_{q<j} l_qj u_qk (j < k), then l_qk = u_qk / D_q; the diagonal slot ends as 1/D_k
-      // (0 for a removed or singular pivot: l_k. = 0 and m_k = 0, as in k_gram_fill).
-#pragma unroll
-      for (int k = 0; k < W; ++k) {
-#pragma unroll
-        for (int j = 1; j < k; ++j) {
-          double u = a[gidx<W>(j, k)];
-#pragma unroll
-          for (int q = 0; q < j; ++q) u -= a[gidx<W>(q, j)] * a[gidx<W>(q, k)];
-          a[gidx<W>(j, k)] = u;
-        }
-        const double gkk = a[gidx<W>(k, k)];
-        double d = gkk;
-#pragma unroll
-        for (int q = 0; q < k; ++q) {
-          const double l = a[gidx<W>(q, k)] * a[gidx<W>(q, q)];  // u_qk / D_q
-          d -= l * a[gidx<W>(q, k)];
-          a[gidx<W>(q, k)] = l;
-        }
-        a[gidx<W>(k, k)] = (((keep >> k) & 1u) && d > 1e-13 * gkk) ? fast_rcp(d) : 0.0;
-      }
-#pragma unroll
-      for (int k = 0; k < W; ++k) {  // forward substitution in place (y[q < k] are final)
-        double v = y[k];
-#pragma unroll
-        for (int q = 0; q < k; ++q) v -= a[gidx<W>(q, k)] * y[q];
-        y[k] = v;
-      }
-#pragma unroll
-      for (int k = 0; k < W; ++k) r2 -= y[k] * y[k] * a[gidx<W>(k, k)];
-#pragma unroll
-      for (int k = W - 1; k >= 0; --k) {  // back substitution in place: y[q > k] already hold m_q
-        double v = y[k] * a[gidx<W>(k, k)];
-#pragma unroll
-        for (int q = k + 1; q < W; ++q) v -= a[gidx<W>(k, q)] * y[q];
-        y[k] = v;
-      }
+      r2 = wide_lsq_solve<W>(a, y, keep);
     } else {
 #pragma unroll
       for (int p = 0; p < W; ++p)
@@ -410,6 +419,134 @@ __global__ __launch_bounds__(kNT) void k_gram_fill_wide(int32_t n, int32_t line_
   }
 }
 
+// The bench form of the wide LSQ fill (fp32 Gram cache): the same per-line arithmetic
+// (wide_lsq_solve) and the same partials as k_gram_fill_wide, restructured so that HBM overlaps
+// the fp64 solves at one wave per SIMD.  Persistent: one block per CU walks 256-line blocks; a
+// block's Gram values (256 x (T + W) fp32, contiguous in the blocked layout) are loaded with
+// 16-byte loads into registers DURING the previous line block's solves, then parked in LDS, from
+// where each sample's working copy is read (each thread reads only its own line's column).  The
+// removal-bitmap words of a chunk of samples are gathered before the next block's Gram prefetch
+// is issued, so waiting for them never waits for the prefetch (vmcnt counts in order).
+template <int W, typename TM>
+__global__ __launch_bounds__(kNT) void k_gram_fill_wide_pf(int32_t line_begin, int32_t line_end, int32_t wrt,
+                                                           const int32_t* __restrict__ pat_act,
+                                                           const float* __restrict__ gram, int32_t B,
+                                                           const uint32_t* __restrict__ removed, int32_t words,
+                                                           int32_t word_base, TM* __restrict__ m_out,
+                                                           double* __restrict__ partials, int32_t nparts) {
+  constexpr int T = tri(W), TG = T + W;
+  constexpr int kRegion = kNT * TG / 4;  // 16-byte words of a line block's Gram values
+  constexpr int kPf = (kRegion + kNT - 1) / kNT;
+  static_assert(W <= 32 && kNT % 64 == 0, "shapes");
+  __shared__ __attribute__((aligned(16))) float sG[kNT / 64][TG][64];  // the blocked layout, as in HBM
+  __shared__ double s_r2[kChunk][kNT];
+  constexpr int kMBuf = sizeof(TM) == 4 ? 2 : 1;  // M staging buffers (fp64 M: one, LDS)
+  __shared__ __attribute__((aligned(16))) TM s_m[kMBuf][kNT * W];
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int64_t nloc = line_end - line_begin;
+  f4 pf[kPf];
+  auto prefetch = [&](int lb) {
+    // line block lb covers the 64-line Gram blocks (line_begin + lb*kNT) / 64 .. + 3; the last
+    // block of the range may be partial: its loads stay inside the cache (spai_gram_bytes pads to
+    // 64 lines), and lines past line_end are never used
+    const int64_t g0 = (int64_t)(line_begin + lb * kNT) >> 6;
+    const int64_t gend = ((int64_t)line_end + 63) >> 6;
+    const f4* src = reinterpret_cast<const f4*>(gram + g0 * TG * 64);
+    const int64_t lim = (gend - g0) * TG * 16;  // 16-byte words inside the cache for this block
+#pragma unroll
+    for (int i = 0; i < kPf; ++i) {
+      const int w = i * kNT + t;
+      pf[i] = (w < kRegion && w < lim) ? src[w] : f4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  int lb = blockIdx.x;
+  if (lb < nparts) prefetch(lb);
+#pragma unroll 1
+  for (; lb < nparts; lb += gridDim.x) {
+    const int j = line_begin + lb * kNT + t;
+    const bool valid = j < line_end;
+    const int jj = valid ? j : line_begin;
+    const int nvl = min(kNT, line_end - (line_begin + lb * kNT));
+    __syncthreads();  // every thread is done with the previous block's sG
+#pragma unroll
+    for (int i = 0; i < kPf; ++i) {
+      const int w = i * kNT + t;
+      if (w < kRegion) reinterpret_cast<f4*>(&sG[0][0][0])[w] = pf[i];
+    }
+    __syncthreads();
+    int act[W];
+#pragma unroll
+    for (int p = 0; p < W; ++p) act[p] = (valid && p < wrt) ? pat_act[(int64_t)jj * wrt + p] : -1;
+#pragma unroll 1
+    for (int b0 = 0; b0 < B; b0 += kChunk) {
+      const int nb = min(kChunk, B - b0);
+      uint32_t keepm[kChunk];
+      {
+        uint32_t wd[kChunk][W];
+#pragma unroll
+        for (int s = 0; s < kChunk; ++s) {
+          const uint32_t* rb = removed + (int64_t)min(b0 + s, B - 1) * words;
+#pragma unroll
+          for (int p = 0; p < W; ++p) wd[s][p] = act[p] >= 0 ? rb[(act[p] >> 5) - word_base] : 0u;
+        }
+#pragma unroll
+        for (int s = 0; s < kChunk; ++s) {
+          uint32_t k = 0;
+#pragma unroll
+          for (int p = 0; p < W; ++p)
+            if (act[p] >= 0 && !((wd[s][p] >> (act[p] & 31)) & 1u)) k |= 1u << p;
+          keepm[s] = k;
+        }
+      }
+      // the next line block's Gram values fly during this block's solves (issued after the
+      // bitmap words above have been consumed)
+      if (b0 == 0 && lb + (int)gridDim.x < nparts) prefetch(lb + gridDim.x);
+      const float* gcol = &sG[t >> 6][0][t & 63];
+#pragma unroll 1
+      for (int s = 0; s < nb; ++s) {
+        const int b = b0 + s;
+        double a[T], y[W];
+#pragma unroll
+        for (int q = 0; q < T; ++q) a[q] = (double)gcol[q * 64];
+#pragma unroll
+        for (int k = 0; k < W; ++k) y[k] = (double)gcol[(T + k) * 64];
+        const double r2 = wide_lsq_solve<W>(a, y, keepm[s]);
+        s_r2[s][t] = valid ? r2 : 0.0;
+        if (m_out != nullptr) {
+          TM* sm = s_m[b % kMBuf];
+          if constexpr (kMBuf == 1) __syncthreads();  // the previous sample's stores have read it
+          if (valid) {
+#pragma unroll
+            for (int p = 0; p < W; ++p)
+              if (p < wrt) sm[t * wrt + p] = (TM)y[p];
+          }
+          __syncthreads();
+          TM* dst = m_out + ((int64_t)b * nloc + (int64_t)lb * kNT) * wrt;
+          const int ne = nvl * wrt;
+          constexpr int V = 16 / sizeof(TM);
+          int e0 = 0;
+          if ((reinterpret_cast<uintptr_t>(dst) & 15u) == 0) {
+            for (int e = t; e < ne / V; e += kNT)
+              nt_store(reinterpret_cast<nt_u4*>(dst) + e, reinterpret_cast<const nt_u4*>(sm)[e]);
+            e0 = ne / V * V;
+          }
+          for (int e = e0 + t; e < ne; e += kNT) nt_store(dst + e, sm[e]);
+        }
+      }
+      __syncthreads();
+      for (int u = wave; u < nb; u += kNT / 64) {  // the chunk's fixed-order block sums (k_gram_fill_wide's)
+        double acc = 0.0;
+#pragma unroll
+        for (int q = 0; q < kNT / 64; ++q) acc += s_r2[u][q * 64 + lane];
+        acc = wave_sum(acc);
+        if (lane == 0) partials[(int64_t)(b0 + u) * nparts + lb] = acc;
+      }
+      __syncthreads();
+    }
+  }
+}
+
 static int gram_width(int32_t W) { return W <= 5 ? 5 : (W <= 7 ? 7 : (W <= 13 ? 13 : 0)); }
 
 template <int W, typename TM, bool LSQ>
@@ -417,7 +554,10 @@ hipError_t launch_fill(int32_t n, int32_t lb, int32_t le, int32_t wrt, const int
                        const void* g, bool g32, int32_t B, const uint32_t* rm, int32_t words, int32_t wb,
                        void* mo, double* partials, int32_t nparts, hipStream_t s) {
   if constexpr (W > 7) {
-    if (g32)
+    if (g32 && LSQ)  // the bench form: persistent, one block per CU (LDS)
+      k_gram_fill_wide_pf<W, TM><<<std::min(nparts, device_cus()), kNT, 0, s>>>(
+          lb, le, wrt, pa, static_cast<const float*>(g), B, rm, words, wb, static_cast<TM*>(mo), partials, nparts);
+    else if (g32)
       k_gram_fill_wide<W, TM, LSQ, float><<<nparts, kNT, 0, s>>>(n, lb, le, wrt, pa, pv, static_cast<const float*>(g),
                                                                   B, rm, words, wb, static_cast<TM*>(mo), partials);
     else
@@ -529,8 +669,10 @@ extern "C" int spai_fill_lines_gram(int32_t fill_mode, int32_t n, int32_t line_b
                  gram_dtype);
   const bool g32 = gram_dtype == SPAI_DTYPE_F32;
   const int32_t nparts = (nl + kNT - 1) / kNT;
-  SPAI_CHECK_ARG(workspace_bytes >= sizeof(double) * (size_t)nparts * B, "spai_fill_lines_gram: workspace too small");
-  double* partials = static_cast<double*>(workspace);
+  SPAI_CHECK_ARG(workspace_bytes >= fill_ws_carve(nullptr, nparts, B, nullptr), "spai_fill_lines_gram: workspace too small");
+  FillWs fw;
+  fill_ws_carve(workspace, nparts, B, &fw);
+  double* partials = fw.partials;
   const uint32_t* rm = removed;
   const int32_t wb = word_base;
   hipError_t e;
@@ -563,9 +705,8 @@ extern "C" int spai_fill_reduce(int32_t n_lines, int32_t B, const void* workspac
     if (limbs_out) SPAI_CHECK_HIP(hipMemsetAsync(limbs_out, 0, sizeof(int64_t) * kLimbSlots * B, s));
     return SPAI_OK;
   }
-  k_fixed_reduce<1024><<<B, 1024, 0, s>>>(static_cast<const double*>(workspace), (n_lines + kNT - 1) / kNT, res2_out,
-                                          limbs_out, RewardArgs{});
-  SPAI_CHECK_LAUNCH();
+  SPAI_CHECK_HIP(launch_fixed_reduce(const_cast<void*>(workspace), (n_lines + kNT - 1) / kNT, B, res2_out, limbs_out,
+                                     RewardArgs{}, s));
   return SPAI_OK;
 }
 
@@ -579,9 +720,8 @@ extern "C" int spai_fill_reduce_rewards(int32_t n_lines, int32_t B, const void* 
                      nnz0 >= 0,
                  "spai_fill_reduce_rewards: bad arguments");
   const RewardArgs ra{removed_counts, nnz0, n, r0, f0, alpha, residual, reward, reward32};
-  k_fixed_reduce<1024><<<B, 1024, 0, (hipStream_t)stream>>>(static_cast<const double*>(workspace),
-                                                            (n_lines + kNT - 1) / kNT, nullptr, nullptr, ra);
-  SPAI_CHECK_LAUNCH();
+  SPAI_CHECK_HIP(launch_fixed_reduce(const_cast<void*>(workspace), (n_lines + kNT - 1) / kNT, B, nullptr, nullptr, ra,
+                                     (hipStream_t)stream));
   return SPAI_OK;
 }
 

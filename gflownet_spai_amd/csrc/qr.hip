@@ -451,8 +451,10 @@ extern "C" int spai_fill_lines_qr(int32_t n, int32_t line_begin, int32_t line_en
     return SPAI_ERR_UNSUPPORTED;
   }
   const int32_t nparts = (nl + kQLines - 1) / kQLines;
-  SPAI_CHECK_ARG(workspace_bytes >= sizeof(double) * (size_t)nparts * B, "spai_fill_lines_qr: workspace too small");
-  double* partials = static_cast<double*>(workspace);
+  SPAI_CHECK_ARG(workspace_bytes >= fill_ws_carve(nullptr, nparts, B, nullptr), "spai_fill_lines_qr: workspace too small");
+  FillWs fw;
+  fill_ws_carve(workspace, nparts, B, &fw);
+  double* partials = fw.partials;
   hipStream_t s = (hipStream_t)stream;
   const bool a32 = a_dtype == SPAI_DTYPE_F32;
   const hipError_t e =

@@ -134,6 +134,40 @@ def test_c3_lsq_fill_13_wide_fp64_vs_oracle():
     _lsq_vs_oracle(env, A_sp, P_sp, removed, tol=1e-11)
 
 
+@pytest.mark.parametrize("m_dtype", [torch.float32, torch.float64])
+def test_c3_wide_prefetch_fill_bit_identical_to_generic_wide_kernel(m_dtype):
+    """C3's fp32-Gram LSQ fill runs k_gram_fill_wide_pf (persistent, one block per CU walking
+    1,024 line blocks, the next block's Gram values prefetched during the solves); the fp64 Gram
+    cache of the same integer stencil runs k_gram_fill_wide.  Same per-line arithmetic, so: M
+    and the residuals bit-identical, for fp32 and fp64 M, over the whole matrix and over
+    256-line-aligned shards (partial last blocks, line_begin > 0) whose exact limbs sum to the
+    one-launch bits."""
+    from gflownet_spai_amd import PreconditionerEnv, axial_pattern_3d, kernels, poisson_3d
+    from gflownet_spai_amd.distributed import LINE_ALIGN, shard_lines
+    A = poisson_3d(64)
+    P = axial_pattern_3d(64)
+    n = A.shape[0]
+    env = PreconditionerEnv(n, P, A, side="AM", fill="lsq")
+    assert env.gram.dtype == torch.float32
+    g64 = kernels.gram_build(env.pattern, env.a_lines)
+    E = env.init_nnz
+    rng = np.random.default_rng(91)
+    rem = rng.random((10, E)) < rng.uniform(0.05, 0.5, (10, 1))
+    bits = torch.cat([removal_bits(r) for r in rem])  # B = 10: two chunks of samples
+    r32, m32 = kernels.fill_residual_gram(env.pattern, env.gram, bits, True, store_m=True, m_dtype=m_dtype)
+    r64, m64 = kernels.fill_residual_gram(env.pattern, g64, bits, True, store_m=True, m_dtype=m_dtype)
+    assert torch.equal(m32, m64) and torch.equal(r32, r64)
+    for nparts in (3, 7):
+        lb = 0
+        for q in range(nparts):
+            b, e = shard_lines(n, q, nparts, LINE_ALIGN)
+            limbs, ms = kernels.fill_residual_gram(env.pattern, env.gram, bits, True, b, e, store_m=True,
+                                                   m_dtype=m_dtype, limbs=True)
+            assert torch.equal(ms, m64[:, b:e])
+            lb = lb + limbs
+        assert torch.equal(kernels.res2_from_limbs(lb), r64)
+
+
 def test_c5_standin_lsq_fill_full_size_vs_oracle():
     """C5 stand-in (utils.thermal_like(1108): 1,227,664 unknowns, 8,584,786 nnz, 7 per row,
     lognormal conductivities, permuted numbering, fp64; thermal2 itself is not in the

@@ -21,7 +21,7 @@ if os.environ.get("SPAI_LIB_VARIANT"):  # A/B timing of kernel variants built un
 SPAI_OK, SPAI_ERR_INVALID, SPAI_ERR_HIP, SPAI_ERR_UNSUPPORTED = 0, 1, 2, 3
 FILL_COPY, FILL_LSQ = 0, 1  # (the Householder-QR fill has its own entry point)
 DTYPE_F32, DTYPE_F64 = 0, 1
-ABI_VERSION = 15
+ABI_VERSION = 14
 RES2_LIMBS = 8  # SPAI_RES2_LIMBS
 
 _c_i32, _c_i64, _c_u64, _c_sz, _c_p = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_size_t, ctypes.c_void_p
@@ -152,12 +152,10 @@ _ws_cache: dict = {}
 
 def workspace(nbytes: int, device, tag: str) -> torch.Tensor:
     """Caller-owned workspace (a byte tensor from torch's caching allocator), reused per
-    (tag, device, current stream) so concurrent streams never share one.  Zero-filled when
-    allocated: the arrival counters some calls keep in their workspace start at zero and every
-    call leaves them there (include/spai_hip.h, "Workspaces")."""
+    (tag, device, current stream) so concurrent streams never share one."""
     key = (tag, str(device), torch.cuda.current_stream(device).cuda_stream)
     ws = _ws_cache.get(key)
     if ws is None or ws.numel() < nbytes:
-        ws = torch.zeros(max(int(nbytes), 256), dtype=torch.uint8, device=device)
+        ws = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
         _ws_cache[key] = ws
     return ws

@@ -291,7 +291,9 @@ using namespace spai;
 
 extern "C" size_t spai_fill_workspace_bytes(int32_t n_lines, int32_t B) {
   const int64_t nparts = std::max(n_lines, 1);  // one partial per line (hash variant) or per block
-  return fill_ws_carve(nullptr, nparts, std::max(B, 1), nullptr);
+  Carve c(nullptr);
+  c.take<double>((size_t)nparts * std::max(B, 1));
+  return c.off;
 }
 
 extern "C" int spai_fill_residual(int32_t fill_mode, int32_t n, int32_t line_begin, int32_t line_end, int32_t W,
@@ -331,16 +333,15 @@ extern "C" int spai_fill_residual(int32_t fill_mode, int32_t n, int32_t line_beg
     const int64_t bound = std::min<int64_t>((int64_t)W * WA + 1, (int64_t)n);
     if (fill_mode == SPAI_FILL_COPY && bound < kHashMaxEntries) {
       const int32_t tb = (int32_t)std::min<int64_t>(kHashMaxEntries, std::max<int64_t>(64, 2 * bound));
-      FillWs fw;
-      fill_ws_carve(workspace, nl, B, &fw);
-      double* partials = fw.partials;
+      double* partials = static_cast<double*>(workspace);
       hipError_t e = a_dtype == SPAI_DTYPE_F32
                          ? launch_hash<float>(line_begin, line_end, W, WA, pat_idx, pat_act, pat_val, a_idx, a_val, B,
                                               removed, words, word_base, m_out, partials, tb, s)
                          : launch_hash<double>(line_begin, line_end, W, WA, pat_idx, pat_act, pat_val, a_idx, a_val,
                                                B, removed, words, word_base, m_out, partials, tb, s);
       SPAI_CHECK_HIP(e);
-      SPAI_CHECK_HIP(launch_fixed_reduce(workspace, nl, B, res2_out, limbs_out, RewardArgs{}, s));
+      k_fixed_reduce<1024><<<B, 1024, 0, s>>>(partials, nl, res2_out, limbs_out, RewardArgs{});
+      SPAI_CHECK_LAUNCH();
       return SPAI_OK;
     }
     set_error("spai_fill_residual: no compiled kernel for W=%d WA=%d a_dtype=%d m_dtype=%d mode=%d", W, WA, a_dtype,
@@ -348,12 +349,11 @@ extern "C" int spai_fill_residual(int32_t fill_mode, int32_t n, int32_t line_beg
     return SPAI_ERR_UNSUPPORTED;
   }
   const int32_t nparts = (nl + kNT - 1) / kNT;
-  FillWs fw;
-  fill_ws_carve(workspace, nparts, B, &fw);
-  double* partials = fw.partials;
+  double* partials = static_cast<double*>(workspace);
   SPAI_CHECK_HIP(v->fn(line_begin, line_end, W, WA, pat_idx, pat_act, pat_val, a_idx, a_val, B, removed, words,
                        word_base, m_out, partials, nparts, s));
-  SPAI_CHECK_HIP(launch_fixed_reduce(workspace, nparts, B, res2_out, limbs_out, RewardArgs{}, s));
+  k_fixed_reduce<1024><<<B, 1024, 0, s>>>(partials, nparts, res2_out, limbs_out, RewardArgs{});
+  SPAI_CHECK_LAUNCH();
   return SPAI_OK;
 }
 

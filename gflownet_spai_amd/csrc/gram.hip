@@ -43,6 +43,44 @@ __device__ __forceinline__ double fast_rcp(double x) {
   return fma(r, e, r);
 }
 
+constexpr int kNtAux = 2;              // buffer-store cache policy: nt (streaming output, gfx950)
+constexpr int kBufWord3 = 0x00020000;  // buffer resource dword 3 (raw byte addressing)
+typedef unsigned int u2v __attribute__((ext_vector_type(2)));
+typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+
+// One sample's M block of a line block (ne = nvl * wrt values, contiguous at dst) from its LDS
+// staging copy sm, with a FIXED number of buffer stores per thread: 16-byte stores over the whole
+// 16-byte chunks, then one element store for the tail.  Stores past the block — all of them when
+// dst is null (no M requested) — fall outside the buffer's bound and are dropped.  No branch skips
+// a store, so the compiler's wait for the next sample's bitmap words (loaded before these stores;
+// vmcnt counts in order) is vmcnt(stores), not vmcnt(0): at one wave per SIMD a drain of the M
+// stores per sample was an HBM write latency per sample.
+template <int W, typename TM>
+__device__ __forceinline__ void store_m_block(TM* dst, const TM* sm, int ne) {
+  constexpr int kV = 16 / (int)sizeof(TM), kChunks = kNT * W / kV;
+  constexpr int kSt = (kChunks + kNT - 1) / kNT;
+  static_assert(kNT * W % kV == 0, "whole 16-byte chunks in the staging buffer");
+  const int t = threadIdx.x, nfull = ne / kV;
+  const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(dst, 0, dst ? nfull * 16 : 0, kBufWord3);
+  const __amdgpu_buffer_rsrc_t re =
+      __builtin_amdgcn_make_buffer_rsrc(dst, 0, dst ? ne * (int)sizeof(TM) : 0, kBufWord3);
+#pragma unroll
+  for (int i = 0; i < kSt; ++i) {
+    const int c = i * kNT + t;
+    const u4v v = reinterpret_cast<const u4v*>(sm)[min(c, kChunks - 1)];
+    __builtin_amdgcn_raw_buffer_store_b128(v, rv, c * 16, 0, kNtAux);
+  }
+  const int e = nfull * kV + min(t, kV - 1);  // the tail (< kV values): threads 0 .. kV - 1
+  const int off = t < kV ? e * (int)sizeof(TM) : 0x7ffffff0;
+  const TM x = sm[min(e, kNT * W - 1)];
+  if constexpr (sizeof(TM) == 4)
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x), re, off, 0, kNtAux);
+  else {
+    const uint64_t u = (uint64_t)__double_as_longlong(x);
+    __builtin_amdgcn_raw_buffer_store_b64((u2v){(uint32_t)u, (uint32_t)(u >> 32)}, re, off, 0, kNtAux);
+  }
+}
+
 template <int W, int WA, typename TA>
 __global__ __launch_bounds__(kNT) void k_gram_build(int32_t n, int32_t wrt, int32_t wart,
                                                     const int32_t* __restrict__ pat_idx,
@@ -332,8 +370,13 @@ __global__ __launch_bounds__(kNT) void k_gram_fill_wide(int32_t n, int32_t line_
   const bool valid = j < line_end;
   const int64_t nloc = line_end - line_begin;
   const int jj = valid ? j : line_begin;
+  {
+    int av[W];  // every load issued before any is used (no branch per slot)
 #pragma unroll
-  for (int p = 0; p < W; ++p) s_act[p][t] = (valid && p < wrt) ? pat_act[(int64_t)jj * wrt + p] : -1;
+    for (int p = 0; p < W; ++p) av[p] = pat_act[(int64_t)jj * wrt + min(p, wrt - 1)];
+#pragma unroll
+    for (int p = 0; p < W; ++p) s_act[p][t] = (valid && p < wrt) ? av[p] : -1;
+  }
   const GT* gp = gram + (int64_t)(jj >> 6) * (T + W) * 64 + (jj & 63);
   const int nvl = min(kNT, line_end - (line_begin + lb * kNT));
   // the slots' bitmap words of the next sample are loaded while the current one is solved
@@ -341,7 +384,7 @@ __global__ __launch_bounds__(kNT) void k_gram_fill_wide(int32_t n, int32_t line_
 #pragma unroll
   for (int p = 0; p < W; ++p) {
     const int ap = s_act[p][t];
-    wd[p] = ap >= 0 ? removed[(ap >> 5) - word_base] : 0u;
+    wd[p] = removed[ap >= 0 ? (ap >> 5) - word_base : 0];  // unconditional (masked at use): no branch per slot
   }
 #pragma unroll 1
   for (int b = 0; b < B; ++b) {
@@ -349,14 +392,14 @@ __global__ __launch_bounds__(kNT) void k_gram_fill_wide(int32_t n, int32_t line_
 #pragma unroll
     for (int p = 0; p < W; ++p) {
       const int ap = s_act[p][t];
-      if (ap >= 0 && !((wd[p] >> (ap & 31)) & 1u)) keep |= 1u << p;
+      keep |= (uint32_t)((ap >= 0) & !((wd[p] >> (ap & 31)) & 1u)) << p;
     }
     if (b + 1 < B) {
       const uint32_t* rn = removed + (int64_t)(b + 1) * words;
 #pragma unroll
       for (int p = 0; p < W; ++p) {
         const int ap = s_act[p][t];
-        wd[p] = ap >= 0 ? rn[(ap >> 5) - word_base] : 0u;
+        wd[p] = rn[ap >= 0 ? (ap >> 5) - word_base : 0];
       }
     }
     double a[T], y[W];
@@ -385,7 +428,7 @@ __global__ __launch_bounds__(kNT) void k_gram_fill_wide(int32_t n, int32_t line_
       }
     }
     s_r2[b % kChunk][t] = valid ? r2 : 0.0;
-    if (m_out != nullptr) {
+    {  // M (no branch on m_out: store_m_block drops every store when it is null)
       TM* sm = s_m[b & 1];
       if (valid) {
 #pragma unroll
@@ -393,16 +436,7 @@ __global__ __launch_bounds__(kNT) void k_gram_fill_wide(int32_t n, int32_t line_
           if (p < wrt) sm[t * wrt + p] = (TM)y[p];
       }
       __syncthreads();
-      TM* dst = m_out + ((int64_t)b * nloc + (int64_t)lb * kNT) * wrt;
-      const int ne = nvl * wrt;
-      constexpr int V = 16 / sizeof(TM);
-      int e0 = 0;
-      if ((reinterpret_cast<uintptr_t>(dst) & 15u) == 0) {
-        for (int e = t; e < ne / V; e += kNT)
-          nt_store(reinterpret_cast<nt_u4*>(dst) + e, reinterpret_cast<const nt_u4*>(sm)[e]);
-        e0 = ne / V * V;
-      }
-      for (int e = e0 + t; e < ne; e += kNT) nt_store(dst + e, sm[e]);
+      store_m_block<W, TM>(m_out ? m_out + ((int64_t)b * nloc + (int64_t)lb * kNT) * wrt : nullptr, sm, nvl * wrt);
     }
     if (b % kChunk == kChunk - 1 || b == B - 1) {  // the chunk's fixed-order block sums
       const int c0 = b - b % kChunk, nb = b - c0 + 1;
@@ -457,7 +491,7 @@ __global__ __launch_bounds__(kNT) void k_gram_fill_wide_pf(int32_t line_begin, i
 #pragma unroll
     for (int i = 0; i < kPf; ++i) {
       const int w = i * kNT + t;
-      pf[i] = (w < kRegion && w < lim) ? src[w] : f4{0.f, 0.f, 0.f, 0.f};
+      pf[i] = src[min((int64_t)min(w, kRegion - 1), lim - 1)];  // unconditional (clamped): no branch per load
     }
   };
   int lb = blockIdx.x;
@@ -477,7 +511,9 @@ __global__ __launch_bounds__(kNT) void k_gram_fill_wide_pf(int32_t line_begin, i
     __syncthreads();
     int act[W];
 #pragma unroll
-    for (int p = 0; p < W; ++p) act[p] = (valid && p < wrt) ? pat_act[(int64_t)jj * wrt + p] : -1;
+    for (int p = 0; p < W; ++p) act[p] = pat_act[(int64_t)jj * wrt + min(p, wrt - 1)];
+#pragma unroll
+    for (int p = 0; p < W; ++p) act[p] = (valid && p < wrt) ? act[p] : -1;
 #pragma unroll 1
     for (int b0 = 0; b0 < B; b0 += kChunk) {
       const int nb = min(kChunk, B - b0);
@@ -488,14 +524,14 @@ __global__ __launch_bounds__(kNT) void k_gram_fill_wide_pf(int32_t line_begin, i
         for (int s = 0; s < kChunk; ++s) {
           const uint32_t* rb = removed + (int64_t)min(b0 + s, B - 1) * words;
 #pragma unroll
-          for (int p = 0; p < W; ++p) wd[s][p] = act[p] >= 0 ? rb[(act[p] >> 5) - word_base] : 0u;
+          for (int p = 0; p < W; ++p) wd[s][p] = rb[act[p] >= 0 ? (act[p] >> 5) - word_base : 0];
         }
 #pragma unroll
         for (int s = 0; s < kChunk; ++s) {
           uint32_t k = 0;
 #pragma unroll
           for (int p = 0; p < W; ++p)
-            if (act[p] >= 0 && !((wd[s][p] >> (act[p] & 31)) & 1u)) k |= 1u << p;
+            k |= (uint32_t)((act[p] >= 0) & !((wd[s][p] >> (act[p] & 31)) & 1u)) << p;  // no branch: the load stays put
           keepm[s] = k;
         }
       }
@@ -513,7 +549,7 @@ __global__ __launch_bounds__(kNT) void k_gram_fill_wide_pf(int32_t line_begin, i
         for (int k = 0; k < W; ++k) y[k] = (double)gcol[(T + k) * 64];
         const double r2 = wide_lsq_solve<W>(a, y, keepm[s]);
         s_r2[s][t] = valid ? r2 : 0.0;
-        if (m_out != nullptr) {
+        {  // M (no branch on m_out: store_m_block drops every store when it is null)
           TM* sm = s_m[b % kMBuf];
           if constexpr (kMBuf == 1) __syncthreads();  // the previous sample's stores have read it
           if (valid) {
@@ -522,16 +558,8 @@ __global__ __launch_bounds__(kNT) void k_gram_fill_wide_pf(int32_t line_begin, i
               if (p < wrt) sm[t * wrt + p] = (TM)y[p];
           }
           __syncthreads();
-          TM* dst = m_out + ((int64_t)b * nloc + (int64_t)lb * kNT) * wrt;
-          const int ne = nvl * wrt;
-          constexpr int V = 16 / sizeof(TM);
-          int e0 = 0;
-          if ((reinterpret_cast<uintptr_t>(dst) & 15u) == 0) {
-            for (int e = t; e < ne / V; e += kNT)
-              nt_store(reinterpret_cast<nt_u4*>(dst) + e, reinterpret_cast<const nt_u4*>(sm)[e]);
-            e0 = ne / V * V;
-          }
-          for (int e = e0 + t; e < ne; e += kNT) nt_store(dst + e, sm[e]);
+          store_m_block<W, TM>(m_out ? m_out + ((int64_t)b * nloc + (int64_t)lb * kNT) * wrt : nullptr, sm,
+                               nvl * wrt);
         }
       }
       __syncthreads();
@@ -554,7 +582,11 @@ hipError_t launch_fill(int32_t n, int32_t lb, int32_t le, int32_t wrt, const int
                        const void* g, bool g32, int32_t B, const uint32_t* rm, int32_t words, int32_t wb,
                        void* mo, double* partials, int32_t nparts, hipStream_t s) {
   if constexpr (W > 7) {
+#ifdef WIDE_NO_PF  // A/B: the generic wide kernel for every cache type
+    if (false)
+#else
     if (g32 && LSQ)  // the bench form: persistent, one block per CU (LDS)
+#endif
       k_gram_fill_wide_pf<W, TM><<<std::min(nparts, device_cus()), kNT, 0, s>>>(
           lb, le, wrt, pa, static_cast<const float*>(g), B, rm, words, wb, static_cast<TM*>(mo), partials, nparts);
     else if (g32)
@@ -669,10 +701,8 @@ extern "C" int spai_fill_lines_gram(int32_t fill_mode, int32_t n, int32_t line_b
                  gram_dtype);
   const bool g32 = gram_dtype == SPAI_DTYPE_F32;
   const int32_t nparts = (nl + kNT - 1) / kNT;
-  SPAI_CHECK_ARG(workspace_bytes >= fill_ws_carve(nullptr, nparts, B, nullptr), "spai_fill_lines_gram: workspace too small");
-  FillWs fw;
-  fill_ws_carve(workspace, nparts, B, &fw);
-  double* partials = fw.partials;
+  SPAI_CHECK_ARG(workspace_bytes >= sizeof(double) * (size_t)nparts * B, "spai_fill_lines_gram: workspace too small");
+  double* partials = static_cast<double*>(workspace);
   const uint32_t* rm = removed;
   const int32_t wb = word_base;
   hipError_t e;
@@ -705,8 +735,9 @@ extern "C" int spai_fill_reduce(int32_t n_lines, int32_t B, const void* workspac
     if (limbs_out) SPAI_CHECK_HIP(hipMemsetAsync(limbs_out, 0, sizeof(int64_t) * kLimbSlots * B, s));
     return SPAI_OK;
   }
-  SPAI_CHECK_HIP(launch_fixed_reduce(const_cast<void*>(workspace), (n_lines + kNT - 1) / kNT, B, res2_out, limbs_out,
-                                     RewardArgs{}, s));
+  k_fixed_reduce<1024><<<B, 1024, 0, s>>>(static_cast<const double*>(workspace), (n_lines + kNT - 1) / kNT, res2_out,
+                                          limbs_out, RewardArgs{});
+  SPAI_CHECK_LAUNCH();
   return SPAI_OK;
 }
 
@@ -720,8 +751,9 @@ extern "C" int spai_fill_reduce_rewards(int32_t n_lines, int32_t B, const void* 
                      nnz0 >= 0,
                  "spai_fill_reduce_rewards: bad arguments");
   const RewardArgs ra{removed_counts, nnz0, n, r0, f0, alpha, residual, reward, reward32};
-  SPAI_CHECK_HIP(launch_fixed_reduce(const_cast<void*>(workspace), (n_lines + kNT - 1) / kNT, B, nullptr, nullptr, ra,
-                                     (hipStream_t)stream));
+  k_fixed_reduce<1024><<<B, 1024, 0, (hipStream_t)stream>>>(static_cast<const double*>(workspace),
+                                                            (n_lines + kNT - 1) / kNT, nullptr, nullptr, ra);
+  SPAI_CHECK_LAUNCH();
   return SPAI_OK;
 }
 

@@ -18,11 +18,9 @@
 //           relu + the block's fp64 pooled sum.  k_pool sums the block partials in block
 //           order (deterministic) into h = mean.
 //   k_fc    one thread per action: logit_a = b_a + W_a . h (W row-major [actions][hid],
-//           16-byte loads), the block max; the last block to finish (an arrival counter in
-//           the workspace) writes lmax.
-// The pooled sum is a separate one-block kernel (k_pool): a device-scope fence per block
-// writes back the XCD's L2, which k_fc's one fence per 1024 actions amortises and k_gat2's
-// one per 256 nodes would not.
+//           16-byte loads), the block max; k_max writes lmax.
+// Cross-block reductions are separate one-block kernels, not last-block-done counters: on
+// gfx950 a device-scope fence writes back the XCD's L2, which costs far more than a launch.
 // Every kernel is bound by HBM / L2 gathers; the only products are hid-wide dot products
 // per node or action (K <= 128, M = 1 for the fc), so there is no MFMA tile to fill.
 #include "spai_device.h"
@@ -386,8 +384,7 @@ template <int F, int C, bool kConst>
 __global__ __launch_bounds__(kNT) void k_fc(int32_t na, const float* __restrict__ W, const float* __restrict__ b,
                                             const float* __restrict__ hpool, const float* __restrict__ x0,
                                             const float* __restrict__ p1, const float* __restrict__ p2,
-                                            float* __restrict__ logits, float* __restrict__ pmax,
-                                            float* __restrict__ lmax, int32_t B, uint32_t* __restrict__ done) {
+                                            float* __restrict__ logits, float* __restrict__ pmax) {
   typedef float f4v __attribute__((ext_vector_type(4)));
   float hv[C];
   if constexpr (kConst) {
@@ -433,23 +430,24 @@ __global__ __launch_bounds__(kNT) void k_fc(int32_t na, const float* __restrict_
     float v = sm[0];
 #pragma unroll
     for (int k = 1; k < kNT / 64; ++k) v = fmaxf(v, sm[k]);
-    handoff_store(pmax + blockIdx.x, v);
+    pmax[blockIdx.x] = v;
   }
-  if (!handoff_arrive(done, gridDim.x)) return;
-  // the last block to finish: lmax[0..B-1] = max of the block maxima (a max: any order), and
-  // the arrival counter back to 0 for the next launch (the workspace contract: zero on first use)
-  float m = -INFINITY;
-  for (int k = threadIdx.x; k < (int)gridDim.x; k += kNT) m = fmaxf(m, handoff_load(pmax + k));
+}
+
+// lmax[0..B-1] = max of the k_fc block maxima (a max: independent of the order)
+__global__ __launch_bounds__(kRedNT) void k_max(int32_t nblk, const float* __restrict__ pmax,
+                                                float* __restrict__ lmax, int32_t B) {
+  __shared__ float sm[kRedNT / 64];
+  float v = -INFINITY;
+  for (int k = threadIdx.x; k < nblk; k += kRedNT) v = fmaxf(v, pmax[k]);
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, kWave));
-  __syncthreads();
-  if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = m;
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, kWave));
+  if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = v;
   __syncthreads();
   float r = sm[0];
 #pragma unroll
-  for (int k = 1; k < kNT / 64; ++k) r = fmaxf(r, sm[k]);
-  for (int bb = threadIdx.x; bb < B; bb += kNT) lmax[bb] = r;
-  handoff_reset(done);
+  for (int k = 1; k < kRedNT / 64; ++k) r = fmaxf(r, sm[k]);
+  for (int bb = threadIdx.x; bb < B; bb += kRedNT) lmax[bb] = r;
 }
 
 // ------------------------------------------------------------------ constant node features
@@ -471,7 +469,6 @@ __global__ __launch_bounds__(kNT) void k_rows_const(int32_t n, int32_t F, const 
 }
 
 struct PolicyWs {
-  uint32_t* done;  // k_fc blocks finished (first in the carve: zero on first use, left at zero)
   float* xlr2;
   double* part;
   float* hpool;
@@ -483,7 +480,6 @@ int fc_blocks(int32_t na) { return (na + kNT * kFcPer - 1) / (kNT * kFcPer); }
 size_t policy_ws(int32_t n, int32_t hid, int32_t na, void* base, PolicyWs* w) {
   Carve c(base);
   const int g2 = (n + kNT - 1) / kNT;
-  w->done = c.take<uint32_t>(1);
   w->xlr2 = c.take<float>((size_t)n * 2 * hid);
   w->part = c.take<double>((size_t)g2 * hid);
   w->hpool = c.take<float>(hid);
@@ -499,13 +495,14 @@ void launch_policy(int32_t n, const float* x, const int32_t* rp, const int32_t* 
   const int64_t t1 = (int64_t)n * (kH1 / HPT);
   const int g2 = (n + kNT - 1) / kNT, gf = fc_blocks(na);
   if (const_rows) {  // the pooled embedding is computed inside k_fc (const_pool)
-    k_fc<F, C, true><<<gf, kNT, 0, s>>>(na, fw, fb, w.hpool, x, p1, p2, logits, w.pmax, lmax, B, w.done);
+    k_fc<F, C, true><<<gf, kNT, 0, s>>>(na, fw, fb, w.hpool, x, p1, p2, logits, w.pmax);
   } else {
     k_gat1<F, C, HPT><<<(int)((t1 + kNT - 1) / kNT), kNT, 0, s>>>(n, x, rp, src, ea, p1, p2, w.xlr2);
     k_gat2<C><<<g2, kNT, 0, s>>>(n, rp, src, ea, p2, w.xlr2, w.part);
     k_pool<C><<<1, kRedNT, 0, s>>>(n, g2, w.part, w.hpool);
-    k_fc<F, C, false><<<gf, kNT, 0, s>>>(na, fw, fb, w.hpool, x, p1, p2, logits, w.pmax, lmax, B, w.done);
+    k_fc<F, C, false><<<gf, kNT, 0, s>>>(na, fw, fb, w.hpool, x, p1, p2, logits, w.pmax);
   }
+  k_max<<<1, kRedNT, 0, s>>>(gf, w.pmax, lmax, B);
 }
 
 template <int F>

@@ -100,8 +100,11 @@ __device__ __forceinline__ void group_sync() {
   asm volatile("" ::: "memory");
 }
 
+#ifndef QR_WPE
+#define QR_WPE 2  // waves per SIMD of the 5-wide fill instances (175 VGPRs: 2 is what they reach)
+#endif
 template <int W, int WA, int L, int RPL, int NT, typename TA, typename TM>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(W <= 5 ? 4 : 2))) void k_qr_fill(int32_t n, int32_t line_begin, int32_t line_end, int32_t wrt,
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(W <= 5 ? QR_WPE : 2))) void k_qr_fill(int32_t n, int32_t line_begin, int32_t line_end, int32_t wrt,
                                                   const int32_t* __restrict__ pat_idx,
                                                   const int32_t* __restrict__ pat_act, int32_t wart,
                                                   const int32_t* __restrict__ a_idx, const TA* __restrict__ a_val,
@@ -451,10 +454,8 @@ extern "C" int spai_fill_lines_qr(int32_t n, int32_t line_begin, int32_t line_en
     return SPAI_ERR_UNSUPPORTED;
   }
   const int32_t nparts = (nl + kQLines - 1) / kQLines;
-  SPAI_CHECK_ARG(workspace_bytes >= fill_ws_carve(nullptr, nparts, B, nullptr), "spai_fill_lines_qr: workspace too small");
-  FillWs fw;
-  fill_ws_carve(workspace, nparts, B, &fw);
-  double* partials = fw.partials;
+  SPAI_CHECK_ARG(workspace_bytes >= sizeof(double) * (size_t)nparts * B, "spai_fill_lines_qr: workspace too small");
+  double* partials = static_cast<double*>(workspace);
   hipStream_t s = (hipStream_t)stream;
   const bool a32 = a_dtype == SPAI_DTYPE_F32;
   const hipError_t e =

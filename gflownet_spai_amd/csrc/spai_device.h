@@ -297,107 +297,30 @@ __device__ __forceinline__ int64_t wave_sum_i64(int64_t v) {
   return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
 }
 
-// ---- last-block-done hand-off: a grid's blocks store their results, arrive on a counter, and
-// the last block to arrive finishes the reduction in the same launch.  The handed-off values are
-// stored at agent scope (gfx950: a write-through `sc1` store) and each storing wave waits for its
-// stores to complete before the block arrives; the last block reads them with agent-scope loads
-// (never a stale L1/L2 line).  A release/acquire fence pair would instead write back and
-// invalidate the whole XCD L2 once per block.  (-DSPAI_HANDOFF_FENCE: the fence form, for A/B.)
-template <typename T>
-__device__ __forceinline__ void handoff_store(T* p, T v) {
-#ifdef SPAI_HANDOFF_FENCE
-  *p = v;
-#else
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#endif
-}
-template <typename T>
-__device__ __forceinline__ T handoff_load(const T* p) {
-#ifdef SPAI_HANDOFF_FENCE
-  return *p;
-#else
-  return __hip_atomic_load(const_cast<T*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#endif
-}
-// Every thread of the block calls it after its hand-off stores; true in every thread of the
-// block that arrives last (of `total`), which then reads the others' values with handoff_load.
-// The counter is back at zero when that block returns (handoff_reset).
-__device__ __forceinline__ bool handoff_arrive(uint32_t* ctr, uint32_t total) {
-  __shared__ bool s_last;
-#ifdef SPAI_HANDOFF_FENCE
-  __threadfence();
-#else
-  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's hand-off stores have completed
-#endif
-  __syncthreads();
-  if (threadIdx.x == 0)
-    s_last = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == total - 1;
-  __syncthreads();
-#ifdef SPAI_HANDOFF_FENCE
-  if (s_last) __threadfence();
-#endif
-  return s_last;
-}
-__device__ __forceinline__ void handoff_reset(uint32_t* ctr) {
-  if (threadIdx.x == 0) __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// ---- fill workspaces (spai_fill_workspace_bytes): [0, 256) the reduce's arrival counter (zero
-// on first use, left at zero), then the fp64 partials [B][nparts], then the slice limbs
-// [B][slices][kLimbSlots] of k_fixed_reduce.
-constexpr int kFixNT = 256;       // threads of a k_fixed_reduce block
-constexpr int kFixPer = 2;        // partials per thread and round (all loads before the conversions)
-constexpr int kFixSlice = 512;    // partials per k_fixed_reduce block (one round at kFixNT x kFixPer)
-constexpr int kFixMaxSlices = 64;
-__host__ __device__ inline int fix_slices(int nparts) {
-  const int s = (nparts + kFixSlice - 1) / kFixSlice;
-  return s < 1 ? 1 : (s > kFixMaxSlices ? kFixMaxSlices : s);
-}
-struct FillWs {
-  uint32_t* done;
-  double* partials;
-  int64_t* slimbs;
-};
-__host__ __device__ inline size_t fill_ws_carve(void* base, int64_t nparts, int32_t B, FillWs* w) {
-  char* p = static_cast<char*>(base);
-  const size_t pb = ((size_t)nparts * (size_t)B * sizeof(double) + 255) & ~(size_t)255;
-  const size_t lb = (size_t)B * kFixMaxSlices * kLimbSlots * sizeof(int64_t);
-  if (w) {
-    w->done = reinterpret_cast<uint32_t*>(p);
-    w->partials = reinterpret_cast<double*>(p + 256);
-    w->slimbs = reinterpret_cast<int64_t*>(p + 256 + pb);
-  }
-  return 256 + pb + lb;
-}
-
-// res2_out[b] and/or limbs_out[b][kLimbSlots] from per-block fp64 partials [B][nparts] (the fill
-// kernels' second half).  Grid (slices, B): each block converts one slice of a sample's
-// partials to exact limbs (every load of a round issued before the conversions; DPP wave sums)
-// and stores the slice's limbs; the last block to arrive (the workspace counter) adds the
-// slices of every sample — integers, so any order gives the same bits — and writes the outputs
-// (and the fused reward).  One block per sample converting all 4096 partials of C4 was a
-// 9 us VALU chain on 8 CUs.
-template <int NT = kFixNT>  // (a template: one definition per program, like the header's other kernels)
+// res2_out[b] and/or limbs_out[b][kLimbSlots] from per-block fp64 partials [B][nparts], one block
+// per sample (the fill kernels' second half).  Every load of a round is issued before the
+// conversions (a dependent load per partial made this a 16 us latency chain at C4); DPP wave
+// sums of the limbs.  The conversions are the VALU chain: 1024 threads x 4 partials (C4's 4096
+// in one round); 256 threads x 16 took 13 us against 10.
+template <int NT>
 __global__ __launch_bounds__(NT) void k_fixed_reduce(const double* __restrict__ partials, int32_t nparts,
-                                                         int64_t* __restrict__ slimbs, uint32_t* __restrict__ done,
-                                                         double* __restrict__ res2_out,
-                                                         int64_t* __restrict__ limbs_out, RewardArgs ra) {
+                                                     double* __restrict__ res2_out, int64_t* __restrict__ limbs_out,
+                                                     RewardArgs ra) {
+  constexpr int kPer = 4;
   __shared__ int64_t sred[NT / 64][kLimbSlots];
-  const int sl = blockIdx.x, b = blockIdx.y, S = gridDim.x, B = gridDim.y;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int per = (nparts + S - 1) / S, i_lo = sl * per, i_hi = min(i_lo + per, nparts);
+  const int b = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const double* p = partials + (int64_t)b * nparts;
   int64_t L[kLimbSlots] = {0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll 1
-  for (int i0 = i_lo; i0 < i_hi; i0 += kFixPer * NT) {
-    double v[kFixPer];
+  for (int i0 = 0; i0 < nparts; i0 += kPer * NT) {
+    double v[kPer];
 #pragma unroll
-    for (int j = 0; j < kFixPer; ++j) {
+    for (int j = 0; j < kPer; ++j) {
       const int i = i0 + j * NT + (int)threadIdx.x;
-      v[j] = i < i_hi ? p[i] : 0.0;
+      v[j] = i < nparts ? p[i] : 0.0;
     }
 #pragma unroll
-    for (int j = 0; j < kFixPer; ++j) fixed_add(v[j], L);
+    for (int j = 0; j < kPer; ++j) fixed_add(v[j], L);
   }
 #pragma unroll
   for (int q = 0; q < 7; ++q) L[q] = wave_sum_i64(L[q]);
@@ -406,39 +329,20 @@ __global__ __launch_bounds__(NT) void k_fixed_reduce(const double* __restrict__ 
     for (int q = 0; q < 7; ++q) sred[wave][q] = L[q];
   }
   __syncthreads();
-  if (threadIdx.x < 7) {
-    int64_t t = 0;
-#pragma unroll
-    for (int w = 0; w < NT / 64; ++w) t += sred[w][threadIdx.x];
-    handoff_store(slimbs + ((int64_t)b * S + sl) * kLimbSlots + threadIdx.x, t);
-  }
-  if (!handoff_arrive(done, (uint32_t)(S * B))) return;
-  for (int bb = threadIdx.x; bb < B; bb += NT) {
+  if (threadIdx.x == 0) {
     int64_t T[kLimbSlots] = {0, 0, 0, 0, 0, 0, 0, 0};
-    const int64_t* src = slimbs + (int64_t)bb * S * kLimbSlots;
-#pragma unroll 1
-    for (int k = 0; k < S; ++k)
 #pragma unroll
-      for (int q = 0; q < 7; ++q) T[q] += handoff_load(src + k * kLimbSlots + q);
+    for (int w = 0; w < NT / 64; ++w)
+#pragma unroll
+      for (int q = 0; q < 7; ++q) T[q] += sred[w][q];
     if (limbs_out) {
 #pragma unroll
-      for (int q = 0; q < kLimbSlots; ++q) limbs_out[(int64_t)bb * kLimbSlots + q] = T[q];
+      for (int q = 0; q < kLimbSlots; ++q) limbs_out[(int64_t)b * kLimbSlots + q] = T[q];
     }
     const double r2 = fixed_value(T);
-    if (res2_out) res2_out[bb] = r2;
-    if (ra.reward) write_reward(bb, r2, ra);  // fused reward (one GPU: the sums are complete here)
+    if (res2_out) res2_out[b] = r2;
+    if (ra.reward) write_reward(b, r2, ra);  // fused reward (one GPU: the sums are complete here)
   }
-  handoff_reset(done);
-}
-
-// Launch of k_fixed_reduce over a fill workspace carved for (nparts, B).
-inline hipError_t launch_fixed_reduce(void* workspace, int32_t nparts, int32_t B, double* res2_out,
-                                      int64_t* limbs_out, const RewardArgs& ra, hipStream_t s) {
-  FillWs w;
-  fill_ws_carve(workspace, nparts, B, &w);
-  k_fixed_reduce<kFixNT><<<dim3(fix_slices(nparts), B), kFixNT, 0, s>>>(w.partials, nparts, w.slimbs, w.done, res2_out,
-                                                                limbs_out, ra);
-  return hipGetLastError();
 }
 
 }  // namespace spai

@@ -81,12 +81,10 @@ constexpr int kBins = 4096;                // splitter histogram / bucket lookup
 
 struct TrajWs {
   int32_t ntiles, M;
-  int32_t* ctl;           // zeroed per rollout: bigcnt | tdev | lastbig | pad | bdone[B]
+  int32_t* ctl;           // zeroed per rollout: bigcnt | tdev | lastbig | pad
   int32_t* bigcnt;        // number of oversized buckets k_sort2 met (k_pad moves it to lastbig, then 0)
   int32_t* tdev;
   int32_t* lastbig;       // bigcnt of the last sort (kept for tests / diagnostics)
-  uint32_t* bdone;        // [B] k_bsum blocks finished per sample (the last one runs the bucket scan)
-  int32_t nctl;           // int32 words of ctl
   double* xch;            // exchange array: [B][2][kMaxB] bucket weight sums | winner counts, then
                           // [B][8] caller slots (the residual limbs); a part fills its own buckets
   int32_t* samp_cnt;      // [B][M / kSampNT] winners per presample block
@@ -119,12 +117,10 @@ static void traj_ws(void* base, int32_t E, int32_t B, TrajWs* w) {
   while (M * 2 <= E && M * 2 <= kSampM) M *= 2;
   w->M = M;
   const int nsb = (M + kSampNT - 1) / kSampNT;
-  w->nctl = 4 + B;
-  w->ctl = c.take<int32_t>(w->nctl);
+  w->ctl = c.take<int32_t>(4);
   w->bigcnt = w->ctl;
   w->tdev = w->ctl + 1;
   w->lastbig = w->ctl + 2;
-  w->bdone = reinterpret_cast<uint32_t*>(w->ctl + 4);
   w->xch = c.take<double>(xch_doubles(B));
   w->samp_cnt = c.take<int32_t>((size_t)B * nsb);
   w->samp = c.take<uint32_t>((size_t)B * M);
@@ -904,77 +900,6 @@ void k_tile(const float* __restrict__ rr, const float* __restrict__ ww, int64_t 
   PROF_END(32)
 }
 
-// ------------------------------------------------------------------ bucket scan
-// Per sample, once the exchange array holds every part's buckets: bucket starts (trajectory
-// positions), winner count, T, the untouched mass W_rest (terminal included) and the mass of
-// all later buckets per bucket (fixed-order suffix).  One block of NT threads; the one-part
-// rollout runs it in the last k_bsum block of the sample, the multi-part merge in k_bscan —
-// the same NT, so the same summation order and bits either way.
-constexpr int kBsumNT = 256;
-template <int NT>
-__device__ __forceinline__ void bscan_sample(int b, int32_t E, int32_t ntiles, const float* __restrict__ ww,
-                                             int64_t wrow_stride, const int32_t* __restrict__ nb_,
-                                             const double* xch, const double* __restrict__ tile_wrest,
-                                             int32_t* __restrict__ bstart, int32_t* __restrict__ counts,
-                                             double* __restrict__ wrest, int32_t* __restrict__ tdev,
-                                             double* __restrict__ bwsuf) {
-  constexpr int kPer = kMaxB / NT;  // buckets per thread of the count scan (contiguous)
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  __shared__ int s_wc[NT / 64];
-  __shared__ double s_wr[NT / 64], s_wd[NT / 64];
-  const int nb = nb_[b];
-  double wr = 0.0;
-  for (int t = tid; t < ntiles; t += NT) wr += tile_wrest[(int64_t)b * ntiles + t];
-  wr = wave_sum(wr);
-  if (lane == 0) s_wr[wave] = wr;
-  const double* xw = xch + (int64_t)b * 2 * kMaxB;
-  const double* xc = xw + kMaxB;
-  int h[kPer], hs = 0;
-#pragma unroll
-  for (int j = 0; j < kPer; ++j) {
-    const int k = kPer * tid + j;
-    h[j] = k < nb ? (int)handoff_load(xc + k) : 0;
-    hs += h[j];
-  }
-  int tot;
-  int ex = block_excl_scan<NT>(hs, s_wc, &tot);
-  int32_t* bs = bstart + (int64_t)b * (kMaxB + 1);
-#pragma unroll
-  for (int j = 0; j < kPer; ++j) {
-    const int k = kPer * tid + j;
-    if (k < nb) bs[k] = ex;
-    ex += h[j];
-  }
-  if (tid == 0) {
-    bs[nb] = tot;
-    double t = (double)ww[(int64_t)b * wrow_stride + E];  // the terminal stays available
-#pragma unroll
-    for (int w = 0; w < NT / 64; ++w) t += s_wr[w];
-    wrest[b] = t;
-    counts[b] = tot;
-    atomicMax(tdev, tot + 1);
-  }
-  // bwsuf[k] = sum of the weights of all buckets after k: thread t owns the t-th chunk counted
-  // from the end (contiguous, fixed order)
-  const int per = (nb + NT - 1) / NT;
-  const int hi_ = nb - min(tid * per, nb), lo_ = max(hi_ - per, 0);
-  double xv[kPer];  // per <= kPer buckets (nb <= kMaxB)
-  static_assert(kMaxB % NT == 0, "bucket chunks");
-#pragma unroll
-  for (int q = 0; q < kPer; ++q) xv[q] = hi_ - 1 - q >= lo_ ? handoff_load(xw + hi_ - 1 - q) : 0.0;
-  double loc = 0.0;
-#pragma unroll
-  for (int q = 0; q < kPer; ++q) loc += xv[q];  // the chunk from its end (zeros past lo_)
-  double total;
-  double run = block_excl_scan_d<NT>(loc, s_wd, &total);
-  double* wp = bwsuf + (int64_t)b * kMaxB;
-#pragma unroll
-  for (int q = 0; q < kPer; ++q) {
-    if (hi_ - 1 - q >= lo_) wp[hi_ - 1 - q] = run;
-    run += xv[q];
-  }
-}
-
 // ------------------------------------------------------------------ k_bsum
 // Per (sample, bucket) of this part, one block: the winner count and the weight sum over the
 // tiles (thread t adds tiles t, t + kBsumNT, ... in order, then a fixed butterfly per wave and
@@ -982,82 +907,102 @@ __device__ __forceinline__ void bscan_sample(int b, int32_t E, int32_t ntiles, c
 // array xch[b][0][k] (weights) / xch[b][1][k] (counts); the other buckets are zeroed, so the
 // sum of the parts' arrays is the one-part array.  Also advances the device stream counter:
 // every k_presample / k_tile block has read it.
-// kScan (one part): every block of a sample then arrives on bdone[b] (zeroed by k_presample) and
-// the last one runs the sample's bucket scan — no separate k_bscan launch.
-struct BscanArgs {
-  int32_t E;
-  const float* ww;
-  int64_t wrow_stride;
-  const double* tile_wrest;
-  int32_t* bstart;
-  int32_t* counts;
-  double* wrest;
-  int32_t* tdev;
-  double* bwsuf;
-  uint32_t* bdone;
-};
-template <bool kScan>
+constexpr int kBsumNT = 256;
 __global__ __launch_bounds__(kBsumNT) void k_bsum(int32_t ntiles, const int32_t* __restrict__ nb_,
                                                   const uint32_t* __restrict__ runs, const double* __restrict__ tbw,
                                                   double* __restrict__ xch, uint64_t* __restrict__ sctr,
-                                                  int32_t part, int32_t nparts, BscanArgs sa) {
+                                                  int32_t part, int32_t nparts) {
   const int b = blockIdx.y, k = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   if (sctr && b == 0 && k == 0 && tid == 0) *sctr += 1;
   const int nb = nb_[b];
   double* xw = xch + (int64_t)b * 2 * kMaxB;
   if (k >= nb) {  // beyond this sample's buckets: zero the rest of its rows (one block does it)
     if (k == nb)
-      for (int j = nb + tid; j < kMaxB; j += kBsumNT) {
-        handoff_store(xw + j, 0.0);
-        handoff_store(xw + kMaxB + j, 0.0);
-      }
-  } else if (k < part_lo(nb, part, nparts) || k >= part_lo(nb, part + 1, nparts)) {
-    if (tid == 0) {
-      handoff_store(xw + k, 0.0);
-      handoff_store(xw + kMaxB + k, 0.0);
-    }
-  } else {
-    __shared__ double s_d[kBsumNT / 64];
-    __shared__ int s_c[kBsumNT / 64];
-    const int64_t row = ((int64_t)b * kMaxB + k) * ntiles;
-    double s = 0.0;
-    int c = 0;
-    for (int t = tid; t < ntiles; t += kBsumNT) {  // coalesced over the tiles, in order per thread
-      s += tbw[row + t];
-      c += (int)(runs[row + t] & 0xFFFFu);
-    }
-    s = wave_sum(s);
-    c = wave_sum(c);
-    if (lane == 0) {
-      s_d[wave] = s;
-      s_c[wave] = c;
-    }
-    __syncthreads();
-    if (tid == 0) {
-      double t = 0.0;
-      int ct = 0;
-#pragma unroll
-      for (int w = 0; w < kBsumNT / 64; ++w) {
-        t += s_d[w];
-        ct += s_c[w];
-      }
-      handoff_store(xw + k, t);
-      handoff_store(xw + kMaxB + k, (double)ct);
-    }
+      for (int j = nb + tid; j < kMaxB; j += kBsumNT) xw[j] = xw[kMaxB + j] = 0.0;
+    return;
   }
-  if constexpr (kScan) {
-    if (handoff_arrive(sa.bdone + b, gridDim.x)) {  // bdone: zeroed by k_presample
-      bscan_sample<kBsumNT>(b, sa.E, ntiles, sa.ww, sa.wrow_stride, nb_, xch, sa.tile_wrest, sa.bstart, sa.counts,
-                            sa.wrest, sa.tdev, sa.bwsuf);
+  if (k < part_lo(nb, part, nparts) || k >= part_lo(nb, part + 1, nparts)) {
+    if (tid == 0) xw[k] = xw[kMaxB + k] = 0.0;
+    return;
+  }
+  __shared__ double s_d[kBsumNT / 64];
+  __shared__ int s_c[kBsumNT / 64];
+  const int64_t row = ((int64_t)b * kMaxB + k) * ntiles;
+  double s = 0.0;
+  int c = 0;
+  for (int t = tid; t < ntiles; t += kBsumNT) {  // coalesced over the tiles, in order per thread
+    s += tbw[row + t];
+    c += (int)(runs[row + t] & 0xFFFFu);
+  }
+  s = wave_sum(s);
+  c = wave_sum(c);
+  if (lane == 0) {
+    s_d[wave] = s;
+    s_c[wave] = c;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    double t = 0.0;
+    int ct = 0;
+#pragma unroll
+    for (int w = 0; w < kBsumNT / 64; ++w) {
+      t += s_d[w];
+      ct += s_c[w];
     }
+    xw[k] = t;
+    xw[kMaxB + k] = (double)ct;
   }
 }
 
-// Multi-part merge: the bucket scan once the parts' exchange arrays are summed.
-__global__ __launch_bounds__(kBsumNT) void k_bscan(int32_t ntiles, const int32_t* __restrict__ nb_,
-                                                   const double* __restrict__ xch, BscanArgs sa) {
-  bscan_sample<kBsumNT>(blockIdx.x, sa.E, ntiles, sa.ww, sa.wrow_stride, nb_, xch, sa.tile_wrest, sa.bstart,
-                        sa.counts, sa.wrest, sa.tdev, sa.bwsuf);
+// ------------------------------------------------------------------ k_bscan
+// Per sample, once the exchange array holds every part's buckets: bucket starts (trajectory
+// positions), winner count, T, the untouched mass W_rest (terminal included) and the mass of
+// all later buckets per bucket (fixed-order suffix).
+__global__ __launch_bounds__(1024) void k_bscan(int32_t E, int32_t ntiles, const float* __restrict__ ww,
+                                                int64_t wrow_stride, const int32_t* __restrict__ nb_,
+                                                const double* __restrict__ xch, const double* __restrict__ tile_wrest,
+                                                int32_t* __restrict__ bstart, int32_t* __restrict__ counts,
+                                                double* __restrict__ wrest, int32_t* __restrict__ tdev,
+                                                double* __restrict__ bwsuf) {
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  __shared__ int s_wc[16];
+  __shared__ double s_wr[16], s_wd[16];
+  const int nb = nb_[b];
+  double wr = 0.0;
+  for (int t = tid; t < ntiles; t += 1024) wr += tile_wrest[(int64_t)b * ntiles + t];
+  wr = wave_sum(wr);
+  if (lane == 0) s_wr[wave] = wr;
+  const double* xw = xch + (int64_t)b * 2 * kMaxB;
+  const double* xc = xw + kMaxB;
+  const int k0 = 2 * tid, k1 = 2 * tid + 1;
+  const int h0 = k0 < nb ? (int)xc[k0] : 0, h1 = k1 < nb ? (int)xc[k1] : 0;
+  int tot;
+  const int ex = block_excl_scan<1024>(h0 + h1, s_wc, &tot);
+  int32_t* bs = bstart + (int64_t)b * (kMaxB + 1);
+  if (k0 < nb) bs[k0] = ex;
+  if (k1 < nb) bs[k1] = ex + h0;
+  if (tid == 0) {
+    bs[nb] = tot;
+    double t = (double)ww[(int64_t)b * wrow_stride + E];  // the terminal stays available
+#pragma unroll
+    for (int w = 0; w < 16; ++w) t += s_wr[w];
+    wrest[b] = t;
+    counts[b] = tot;
+    atomicMax(tdev, tot + 1);
+  }
+  // bwsuf[k] = sum of the weights of all buckets after k: thread t owns the t-th chunk counted
+  // from the end (contiguous, fixed order)
+  const int per = (nb + 1023) / 1024;
+  const int hi_ = nb - min(tid * per, nb), lo_ = max(hi_ - per, 0);
+  double loc = 0.0;
+  for (int k = hi_ - 1; k >= lo_; --k) loc += xw[k];
+  double total;
+  double run = block_excl_scan_d<1024>(loc, s_wd, &total);
+  double* wp = bwsuf + (int64_t)b * kMaxB;
+  for (int k = hi_ - 1; k >= lo_; --k) {
+    wp[k] = run;
+    run += xw[k];
+  }
 }
 
 // In-block exact sort of an oversized bucket (n > kCap2) in global memory: 1-bit LSD radix
@@ -1709,12 +1654,9 @@ static int select_args(const float* logits, const float* lmax, int32_t E, int32_
   return SPAI_OK;
 }
 
-static BscanArgs bscan_args(const TrajWs& w, int32_t E, int64_t bstride, int32_t* counts) {
-  return BscanArgs{E, w.ww, bstride ? w.wstride : 0, w.tile_wrest, w.bstart, counts, w.wrest, w.tdev, w.bwsuf, w.bdone};
-}
-
 static void launch_merge(const TrajWs& w, int32_t E, int32_t B, int64_t bstride, int32_t* counts, hipStream_t s) {
-  k_bscan<<<B, kBsumNT, 0, s>>>(w.ntiles, w.nb, w.xch, bscan_args(w, E, bstride, counts));
+  k_bscan<<<B, 1024, 0, s>>>(E, w.ntiles, w.ww, bstride ? w.wstride : 0, w.nb, w.xch, w.tile_wrest, w.bstart,
+                             counts, w.wrest, w.tdev, w.bwsuf);
 }
 
 extern "C" int spai_rollout_select(const float* logits, int64_t bstride, int32_t E, int32_t B, const float* lmax,
@@ -1734,7 +1676,7 @@ extern "C" int spai_rollout_select(const float* logits, int64_t bstride, int32_t
   const int nwb = (int)((w.wstride + kRwChunk - 1) / kRwChunk);  // rate/weight blocks per logits row
   const int64_t rowsel = bstride ? 1 : 0;
   k_presample<<<nsb * B, kSampNT, 0, s>>>(logits, bstride, E, w.M, nsb, s0, s1, t0, t1, stream_ctr, sample_base,
-                                          w.samp, w.samp_cnt, w.ctl, w.nctl, w.tE);
+                                          w.samp, w.samp_cnt, w.ctl, 4, w.tE);
   SPAI_CHECK_LAUNCH();
   k_splitters<<<B + nwb * (bstride ? B : 1), kSortNT, 0, s>>>(E, w.M, nsb, w.samp, w.samp_cnt, w.nb, w.spl, w.lut,
                                                              w.lut_base, B, logits, bstride, lmax, w.rr, w.ww,
@@ -1744,14 +1686,13 @@ extern "C" int spai_rollout_select(const float* logits, int64_t bstride, int32_t
                                          sample_base, part, nparts, removed, words, w.nb, w.spl, w.lut, w.lut_base,
                                          w.staging, w.runs, w.tbw, w.tile_wrest, w.tE);
   SPAI_CHECK_LAUNCH();
-  const dim3 gb(max_buckets(E) + 1, B);
-  if (nparts == 1)  // the bucket scan runs in the last k_bsum block of each sample
-    k_bsum<true><<<gb, kBsumNT, 0, s>>>(w.ntiles, w.nb, w.runs, w.tbw, w.xch, stream_ctr, part, nparts,
-                                        bscan_args(w, E, bstride, counts));
-  else
-    k_bsum<false><<<gb, kBsumNT, 0, s>>>(w.ntiles, w.nb, w.runs, w.tbw, w.xch, stream_ctr, part, nparts,
-                                         bscan_args(w, E, bstride, counts));
+  k_bsum<<<dim3(max_buckets(E) + 1, B), kBsumNT, 0, s>>>(w.ntiles, w.nb, w.runs, w.tbw, w.xch, stream_ctr, part,
+                                                         nparts);
   SPAI_CHECK_LAUNCH();
+  if (nparts == 1) {
+    launch_merge(w, E, B, bstride, counts, s);
+    SPAI_CHECK_LAUNCH();
+  }
   return SPAI_OK;
 }
 

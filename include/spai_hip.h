@@ -16,10 +16,6 @@
  * Conventions
  *   - Every pointer argument is a DEVICE pointer owned by the caller, unless noted.
  *     No allocation crosses the ABI; the library uses only the caller's workspace.
- *   - Workspaces are zero-filled by the caller before their first use.  Calls that finish
- *     with a last-block-done reduction (spai_policy_logits, the fill / reduce calls) keep an
- *     arrival counter at the start of their workspace and leave it at zero, so a workspace can
- *     be reused by any later call of the same family (and replayed in a HIP graph) as is.
  *   - `stream` is a hipStream_t passed as void*; all calls are stream-ordered and
  *     asynchronous (no host synchronisation inside any call).
  *   - Return value: SPAI_OK (0) or an error code; spai_last_error() returns a

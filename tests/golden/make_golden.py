@@ -30,7 +30,7 @@ Usage:  python tests/golden/make_golden.py            (writes *.npz + meta.json)
         python tests/golden/make_golden.py g6         (C2/C4 parity rollouts, appended)
         python tests/golden/make_golden.py g7         (C1 assembled M of three removal sets, appended)
         python tests/golden/make_golden.py g8         (C2 long parity rollout, T > 1000, appended)
-        python tests/golden/make_golden.py g9         (C2 parity rollout with T >= 20000, appended)
+        python tests/golden/make_golden.py g9         (72^2 parity rollout with T >= 20000, appended)
 """
 import gc
 import json
@@ -325,14 +325,18 @@ def parity_rollout_long():
         json.dump(meta, f, indent=1)
 
 
-def parity_rollout_longer(terminal=3.0, seed=41, min_t=20000):
-    """G9: a C2 reference rollout at least ``min_t`` steps long (pin parity mode past
-    T = 2e4), stored like G8.  The terminal logit sets a per-step stop probability of ~7e-5; if
-    the draw is shorter than ``min_t`` the next seed is tried.  Appends to meta.json."""
+def parity_rollout_longer(terminal=-6.0, seed=41, min_t=20000, grid=72, B=2):
+    """G9: a reference rollout at least ``min_t`` steps long (pin parity mode past
+    T = 2e4), stored like G8.  On C2 (256^2, E = 326,656) the reference keeps every step's state
+    and evaluates the residual per step: the first attempt held 15.5 GB after 2 h without
+    finishing a draw (T = 2e4 would need ~80 GB), so the long draw runs on the 72^2 Poisson
+    matrix (E = 25,632) with the terminal logit at -6, which removes most of the actions before
+    it stops.  If the draw is shorter than ``min_t`` the next seed is tried.  Appends to
+    meta.json."""
     preconditioner, policy, gfn_mod, ref_utils = _import_reference()
     meta_path = os.path.join(HERE, "meta.json")
     meta = json.load(open(meta_path))
-    tag, grid, logit_seed = "c2longer", 256, 21
+    tag, logit_seed = "longer", 21
     A = poisson2d(grid)
     order = np.lexsort((A.col, A.row))
     rows, cols, vals = A.row[order].astype(np.int64), A.col[order].astype(np.int64), A.data[order].astype(np.float32)
@@ -342,7 +346,6 @@ def parity_rollout_longer(terminal=3.0, seed=41, min_t=20000):
     E = env.num_actions - 1
     logits = torch.randn(E + 1, generator=torch.Generator().manual_seed(logit_seed))
     logits[E] = terminal
-    B = 2
     while True:
         model = gfn_mod.GFlowNet(FixedLogitPolicy(logits), None, env)
         s0 = [A_t.clone() for _ in range(B)]

@@ -453,128 +453,6 @@ __global__ __launch_bounds__(kNT) void k_gram_fill_wide(int32_t n, int32_t line_
   }
 }
 
-// The bench form of the wide LSQ fill (fp32 Gram cache): the same per-line arithmetic
-// (wide_lsq_solve) and the same partials as k_gram_fill_wide, restructured so that HBM overlaps
-// the fp64 solves at one wave per SIMD.  Persistent: one block per CU walks 256-line blocks; a
-// block's Gram values (256 x (T + W) fp32, contiguous in the blocked layout) are loaded with
-// 16-byte loads into registers DURING the previous line block's solves, then parked in LDS, from
-// where each sample's working copy is read (each thread reads only its own line's column).  The
-// removal-bitmap words of a chunk of samples are gathered before the next block's Gram prefetch
-// is issued, so waiting for them never waits for the prefetch (vmcnt counts in order).
-template <int W, typename TM>
-__global__ __launch_bounds__(kNT) void k_gram_fill_wide_pf(int32_t line_begin, int32_t line_end, int32_t wrt,
-                                                           const int32_t* __restrict__ pat_act,
-                                                           const float* __restrict__ gram, int32_t B,
-                                                           const uint32_t* __restrict__ removed, int32_t words,
-                                                           int32_t word_base, TM* __restrict__ m_out,
-                                                           double* __restrict__ partials, int32_t nparts) {
-  constexpr int T = tri(W), TG = T + W;
-  constexpr int kRegion = kNT * TG / 4;  // 16-byte words of a line block's Gram values
-  constexpr int kPf = (kRegion + kNT - 1) / kNT;
-  static_assert(W <= 32 && kNT % 64 == 0, "shapes");
-  __shared__ __attribute__((aligned(16))) float sG[kNT / 64][TG][64];  // the blocked layout, as in HBM
-  __shared__ double s_r2[kChunk][kNT];
-  constexpr int kMBuf = sizeof(TM) == 4 ? 2 : 1;  // M staging buffers (fp64 M: one, LDS)
-  __shared__ __attribute__((aligned(16))) TM s_m[kMBuf][kNT * W];
-  typedef float f4 __attribute__((ext_vector_type(4)));
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const int64_t nloc = line_end - line_begin;
-  f4 pf[kPf];
-  auto prefetch = [&](int lb) {
-    // line block lb covers the 64-line Gram blocks (line_begin + lb*kNT) / 64 .. + 3; the last
-    // block of the range may be partial: its loads stay inside the cache (spai_gram_bytes pads to
-    // 64 lines), and lines past line_end are never used
-    const int64_t g0 = (int64_t)(line_begin + lb * kNT) >> 6;
-    const int64_t gend = ((int64_t)line_end + 63) >> 6;
-    const f4* src = reinterpret_cast<const f4*>(gram + g0 * TG * 64);
-    const int64_t lim = (gend - g0) * TG * 16;  // 16-byte words inside the cache for this block
-#pragma unroll
-    for (int i = 0; i < kPf; ++i) {
-      const int w = i * kNT + t;
-      pf[i] = src[min((int64_t)min(w, kRegion - 1), lim - 1)];  // unconditional (clamped): no branch per load
-    }
-  };
-  int lb = blockIdx.x;
-  if (lb < nparts) prefetch(lb);
-#pragma unroll 1
-  for (; lb < nparts; lb += gridDim.x) {
-    const int j = line_begin + lb * kNT + t;
-    const bool valid = j < line_end;
-    const int jj = valid ? j : line_begin;
-    const int nvl = min(kNT, line_end - (line_begin + lb * kNT));
-    __syncthreads();  // every thread is done with the previous block's sG
-#pragma unroll
-    for (int i = 0; i < kPf; ++i) {
-      const int w = i * kNT + t;
-      if (w < kRegion) reinterpret_cast<f4*>(&sG[0][0][0])[w] = pf[i];
-    }
-    __syncthreads();
-    int act[W];
-#pragma unroll
-    for (int p = 0; p < W; ++p) act[p] = pat_act[(int64_t)jj * wrt + min(p, wrt - 1)];
-#pragma unroll
-    for (int p = 0; p < W; ++p) act[p] = (valid && p < wrt) ? act[p] : -1;
-#pragma unroll 1
-    for (int b0 = 0; b0 < B; b0 += kChunk) {
-      const int nb = min(kChunk, B - b0);
-      uint32_t keepm[kChunk];
-      {
-        uint32_t wd[kChunk][W];
-#pragma unroll
-        for (int s = 0; s < kChunk; ++s) {
-          const uint32_t* rb = removed + (int64_t)min(b0 + s, B - 1) * words;
-#pragma unroll
-          for (int p = 0; p < W; ++p) wd[s][p] = rb[act[p] >= 0 ? (act[p] >> 5) - word_base : 0];
-        }
-#pragma unroll
-        for (int s = 0; s < kChunk; ++s) {
-          uint32_t k = 0;
-#pragma unroll
-          for (int p = 0; p < W; ++p)
-            k |= (uint32_t)((act[p] >= 0) & !((wd[s][p] >> (act[p] & 31)) & 1u)) << p;  // no branch: the load stays put
-          keepm[s] = k;
-        }
-      }
-      // the next line block's Gram values fly during this block's solves (issued after the
-      // bitmap words above have been consumed)
-      if (b0 == 0 && lb + (int)gridDim.x < nparts) prefetch(lb + gridDim.x);
-      const float* gcol = &sG[t >> 6][0][t & 63];
-#pragma unroll 1
-      for (int s = 0; s < nb; ++s) {
-        const int b = b0 + s;
-        double a[T], y[W];
-#pragma unroll
-        for (int q = 0; q < T; ++q) a[q] = (double)gcol[q * 64];
-#pragma unroll
-        for (int k = 0; k < W; ++k) y[k] = (double)gcol[(T + k) * 64];
-        const double r2 = wide_lsq_solve<W>(a, y, keepm[s]);
-        s_r2[s][t] = valid ? r2 : 0.0;
-        {  // M (no branch on m_out: store_m_block drops every store when it is null)
-          TM* sm = s_m[b % kMBuf];
-          if constexpr (kMBuf == 1) __syncthreads();  // the previous sample's stores have read it
-          if (valid) {
-#pragma unroll
-            for (int p = 0; p < W; ++p)
-              if (p < wrt) sm[t * wrt + p] = (TM)y[p];
-          }
-          __syncthreads();
-          store_m_block<W, TM>(m_out ? m_out + ((int64_t)b * nloc + (int64_t)lb * kNT) * wrt : nullptr, sm,
-                               nvl * wrt);
-        }
-      }
-      __syncthreads();
-      for (int u = wave; u < nb; u += kNT / 64) {  // the chunk's fixed-order block sums (k_gram_fill_wide's)
-        double acc = 0.0;
-#pragma unroll
-        for (int q = 0; q < kNT / 64; ++q) acc += s_r2[u][q * 64 + lane];
-        acc = wave_sum(acc);
-        if (lane == 0) partials[(int64_t)(b0 + u) * nparts + lb] = acc;
-      }
-      __syncthreads();
-    }
-  }
-}
-
 static int gram_width(int32_t W) { return W <= 5 ? 5 : (W <= 7 ? 7 : (W <= 13 ? 13 : 0)); }
 
 template <int W, typename TM, bool LSQ>
@@ -582,14 +460,7 @@ hipError_t launch_fill(int32_t n, int32_t lb, int32_t le, int32_t wrt, const int
                        const void* g, bool g32, int32_t B, const uint32_t* rm, int32_t words, int32_t wb,
                        void* mo, double* partials, int32_t nparts, hipStream_t s) {
   if constexpr (W > 7) {
-#ifdef WIDE_NO_PF  // A/B: the generic wide kernel for every cache type
-    if (false)
-#else
-    if (g32 && LSQ)  // the bench form: persistent, one block per CU (LDS)
-#endif
-      k_gram_fill_wide_pf<W, TM><<<std::min(nparts, device_cus()), kNT, 0, s>>>(
-          lb, le, wrt, pa, static_cast<const float*>(g), B, rm, words, wb, static_cast<TM*>(mo), partials, nparts);
-    else if (g32)
+    if (g32)
       k_gram_fill_wide<W, TM, LSQ, float><<<nparts, kNT, 0, s>>>(n, lb, le, wrt, pa, pv, static_cast<const float*>(g),
                                                                   B, rm, words, wb, static_cast<TM*>(mo), partials);
     else

@@ -13,18 +13,6 @@ void set_error(const char* fmt, ...);
 
 inline size_t align_up(size_t x, size_t a = 256) { return (x + a - 1) / a * a; }
 
-// Compute units of the current device (persistent grids), cached per process.
-inline int device_cus() {
-  static int n = 0;
-  if (n == 0) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
-      n = 256;
-  }
-  return n;
-}
-
 // Bump allocator over the caller's workspace.
 struct Carve {
   char* base;

@@ -135,13 +135,12 @@ def test_c3_lsq_fill_13_wide_fp64_vs_oracle():
 
 
 @pytest.mark.parametrize("m_dtype", [torch.float32, torch.float64])
-def test_c3_wide_prefetch_fill_bit_identical_to_generic_wide_kernel(m_dtype):
-    """C3's fp32-Gram LSQ fill runs k_gram_fill_wide_pf (persistent, one block per CU walking
-    1,024 line blocks, the next block's Gram values prefetched during the solves); the fp64 Gram
-    cache of the same integer stencil runs k_gram_fill_wide.  Same per-line arithmetic, so: M
-    and the residuals bit-identical, for fp32 and fp64 M, over the whole matrix and over
-    256-line-aligned shards (partial last blocks, line_begin > 0) whose exact limbs sum to the
-    one-launch bits."""
+def test_c3_wide_fill_fp32_and_fp64_gram_caches_bit_identical_over_shards(m_dtype):
+    """C3's 13-wide LSQ fill (k_gram_fill_wide: fixed-count buffer stores of M, B = 10 = two
+    sample chunks) from the env's fp32 Gram cache and from the fp64 cache of the same integer
+    stencil: M and the residuals bit-identical, for fp32 and fp64 M, over the whole matrix and
+    over 256-line-aligned shards (partial last blocks, line_begin > 0, M blocks that end inside a
+    16-byte store) whose exact limbs sum to the one-launch bits."""
     from gflownet_spai_amd import PreconditionerEnv, axial_pattern_3d, kernels, poisson_3d
     from gflownet_spai_amd.distributed import LINE_ALIGN, shard_lines
     A = poisson_3d(64)

@@ -1,4 +1,6 @@
 """Isolated timing of spai_fill_residual (LSQ / COPY) at C4 for several batch sizes.
+--path line times the fill that forms each line's Gram from A in the launch (fill.hip k_line,
+spai_fill_residual) instead of reading the env's Gram cache (gram.hip, the bench's path).
 
 Working sets at B >= 16 exceed the 256 MiB Infinity Cache, so the GB/s figure there is an
 HBM figure.  usage: python scripts/fill_bench.py [--config c4] [--batches 8,32] [--iters 20]
@@ -22,6 +24,7 @@ def main():
     ap.add_argument("--config", default="c4")
     ap.add_argument("--batches", default="8,32")
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--path", default="gram", choices=["gram", "line"])
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     dims, grid, dtype, _ = bench.CONFIGS[args.config]
@@ -38,6 +41,10 @@ def main():
             lgs, lmax, _ = kernels.logits_stats(lg, B)
             removed, counts, _ = kernels.rollout_select(lgs, B, lmax, 7, 0)
             def run():
+                if args.path == "line":
+                    return kernels.fill_residual(env.pattern, env.a_lines, removed, fill == "lsq",
+                                                 store_m=os.environ.get("NO_STORE") is None,
+                                                 m_dtype=env.a_lines.val.dtype)
                 return kernels.fill_residual_gram(env.pattern, env.gram, removed, fill == "lsq",
                                                   store_m=os.environ.get("NO_STORE") is None,
                                                   m_dtype=env.a_lines.val.dtype)
@@ -52,7 +59,7 @@ def main():
             torch.cuda.synchronize()
             ms = s.elapsed_time(e) / args.iters
             fb = bench.fill_bytes(env, B, store_m=os.environ.get("NO_STORE") is None)
-            rec = {"fill": fill, "B": B, "ms": ms, "bytes": fb, "GBps": fb / ms / 1e6,
+            rec = {"path": args.path, "fill": fill, "B": B, "ms": ms, "bytes": fb, "GBps": fb / ms / 1e6,
                    "frac": fb / ms / 1e6 / bench.HBM_PEAK_GBS, "columns_per_s": B * n / ms * 1e3}
             out.append(rec)
             print(json.dumps(rec), flush=True)

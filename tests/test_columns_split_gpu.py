@@ -157,6 +157,54 @@ def _by_value(x, back=False):
     return x
 
 
+def _rccl_world1_main(port, q):
+    """RCCL (backend "nccl") with one rank: the device-tensor branch of every collective the splits
+    use (no host staging), on the dtypes and shapes they send."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1")
+    import torch.distributed as dist
+    from gflownet_spai_amd.distributed import (LINE_ALIGN, all_reduce_, allgather_lines, exchange_bitmaps,
+                                               select_best_samples)
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", device_id=dev)
+    out = {"backend": dist.get_backend()}
+    try:
+        bl, w0, w1 = 3, 5, 40
+        send = torch.arange(bl * (w1 - w0 + 1), dtype=torch.int32, device=dev)
+        recv = torch.empty(bl, w1 - w0 + 1, dtype=torch.int32, device=dev)
+        exchange_bitmaps(send, recv, [(w0, w1)], bl, 0, async_op=True).wait()
+        out["a2a"] = bool(torch.equal(recv.view(-1), send))
+        limbs = torch.arange(8 * bl, dtype=torch.int64, device=dev).view(bl, 8) * (1 << 40)
+        ref = limbs.clone()
+        all_reduce_(limbs)
+        out["allreduce"] = bool(torch.equal(limbs, ref))
+        n = 1000
+        m = torch.randn(bl, n, 5, device=dev)
+        out["allgather"] = bool(torch.equal(allgather_lines(m, n, align=LINE_ALIGN), m))
+        rw = torch.tensor([0.5, 2.0, 1.0], dtype=torch.float64, device=dev)
+        r, best, mb = select_best_samples(rw, m)
+        out["best"] = bool(torch.equal(r, rw) and int(best) == 1 and torch.equal(mb, m[1]))
+        torch.cuda.synchronize()
+    finally:
+        dist.destroy_process_group()
+    q.put(out)
+
+
+def test_rccl_one_rank_collectives():
+    """The RCCL branch of the split collectives (all_to_all_single with uneven splits, int64
+    all_reduce, all_gather_into_tensor, the samples split's all_gather + reduce) executed on the
+    GPU with one rank: two ranks cannot share one GPU under RCCL (duplicate-GPU check), so the
+    multi-rank tests above run gloo; this is the device-tensor path they skip."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_world1_main, args=(_free_port(), q))
+    p.start()
+    out = q.get(timeout=240)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    assert out == {"backend": "nccl", "a2a": True, "allreduce": True, "allgather": True, "best": True}, out
+
+
 def _rank_main(rank, world, port, bl, q):
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"

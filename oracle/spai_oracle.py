@@ -93,8 +93,10 @@ def poisson3d(grid, dtype=np.float64):
 # --------------------------------------------------------------------------------------
 
 
-def parity_rollout(logits, B, generator=None):
-    """Sequential rollout with exactly the reference's torch ops and noise stream.
+def parity_rollout(logits, B, generator=None, max_steps=None):
+    """Sequential rollout with exactly the reference's torch ops and noise stream
+    (``max_steps``: stop after that many steps — the prefix of the full rollout, for long golden
+    trajectories whose O(T^2) history masking would take minutes here).
 
     Per step: each sample's probs = softmax(logits masked by its history)
     (policy.py:65-73) -> stack [B,1,E+1] -> row renormalisation when B > 1
@@ -108,7 +110,7 @@ def parity_rollout(logits, B, generator=None):
     done = torch.zeros(B, dtype=torch.bool)
     hist = []  # list of [B] int64 (log._actions)
     fwd = []
-    while not bool(done.all()):
+    while not bool(done.all()) and (max_steps is None or len(hist) < max_steps):
         a_all, probs_all = reference_step(logits, B, hist, generator)
         mask_active = ~done
         fp = torch.ones(B)

@@ -83,10 +83,12 @@ def test_parity_rollout_bit_exact_vs_reference(seed):
     np.testing.assert_allclose(pol.l.grad.view(-1).numpy(), gref, rtol=2e-4, atol=2e-6 * np.abs(gref).max())
 
 
-@pytest.mark.parametrize("name", ["c2_rollout.npz", "c4_rollout.npz", "c2long_rollout.npz"])
+@pytest.mark.parametrize("name", ["c2_rollout.npz", "c4_rollout.npz", "c2long_rollout.npz", "longer_rollout.npz"])
 def test_parity_rollout_bit_exact_vs_reference_large(name):
-    """C2 (E = 326,656) and C4 (E = 5,238,784) reference rollouts (G6, make_golden.py g6) and a
-    LONG C2 rollout (G8: T = 4,605 steps, make_golden.py g8): the HIP parity step reproduces the
+    """C2 (E = 326,656) and C4 (E = 5,238,784) reference rollouts (G6, make_golden.py g6), a
+    LONG C2 rollout (G8: T = 4,605 steps, make_golden.py g8) and a 25,633-step rollout of the 72^2
+    matrix (G9, make_golden.py g9: both samples remove all 25,632 actions, then the terminal —
+    every step of the remaining-mass chain down to the last action): the HIP parity step reproduces the
     reference's actions from the same torch seed, its fwd_probs within 1e-6 and its rewards
     (copy fill, ||MA - I||).  The kernel ranks w_a / q_a with w_a = e^(l_a - lmax) instead of the
     reference's renormalised fp32 softmax p_a (a flip needs the two best ratios

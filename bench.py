@@ -318,7 +318,7 @@ def main():
             dist.init_process_group(args.backend)
 
     from gflownet_spai_amd import GFlowNet, PreconditionerEnv, kernels
-    from gflownet_spai_amd.distributed import LINE_ALIGN, allgather_lines
+    from gflownet_spai_amd.distributed import LINE_ALIGN
 
     dims, grid, dtype, text = CONFIGS[args.config]
     A, P = config_matrices(args.config)
@@ -339,6 +339,10 @@ def main():
     s0 = [P] * bl
     assembled = {}
     do_assemble = [args.assemble != "none" and world > 1 and shard != "candidates"]
+    # the M all_gather of a step runs asynchronously and overlaps the next step's rollout; the
+    # timed region still ends after the last one (gather.wait() before the closing barrier)
+    from gflownet_spai_amd.distributed import LineGather
+    gather = LineGather(n, align=LINE_ALIGN if shard == "columns" else 1) if do_assemble[0] else None
 
     def assemble(log):
         if not do_assemble[0]:
@@ -350,7 +354,7 @@ def main():
         m = env.last_m  # columns: [B, this shard's lines, W] of EVERY candidate; slices: the same B on every rank
         if args.assemble == "best":  # the candidate with the highest reward: the preconditioner kept
             m = m.index_select(0, torch.argmax(log.rewards_all).view(1))
-        assembled["m"] = allgather_lines(m, n, align=LINE_ALIGN if shard == "columns" else 1)
+        gather.start(m)
 
     phases = model.rollout_phases()
 
@@ -427,6 +431,8 @@ def main():
         t0 = time.perf_counter()
         for _ in range(args.steps):
             log = step()
+        if gather is not None:
+            gather.wait()
         barrier()
         dt = (time.perf_counter() - t0) / args.steps
         dt_noasm = dt

@@ -59,19 +59,21 @@ def all_reduce_(t: torch.Tensor, group=None) -> torch.Tensor:
     return t
 
 
-def all_gather_into_(out: torch.Tensor, inp: torch.Tensor, group=None) -> torch.Tensor:
+class _Done:
+    def wait(self):
+        return None
+
+
+def all_gather_into_(out: torch.Tensor, inp: torch.Tensor, group=None, async_op: bool = False):
+    """all_gather_into_tensor (host-staged and synchronous on gloo).  Returns ``out``, or with
+    ``async_op`` a work handle whose ``wait()`` orders the current stream after the gather."""
     if _host_staged(inp, group):
         h = torch.empty(out.shape, dtype=out.dtype)
         dist.all_gather_into_tensor(h, inp.cpu(), group=group)
         out.copy_(h)
-    else:
-        dist.all_gather_into_tensor(out, inp, group=group)
-    return out
-
-
-class _Done:
-    def wait(self):
-        return None
+        return _Done() if async_op else out
+    w = dist.all_gather_into_tensor(out, inp, group=group, async_op=async_op)
+    return w if async_op else out
 
 
 def all_to_all_(out: torch.Tensor, inp: torch.Tensor, out_splits: list, in_splits: list, group=None,
@@ -112,6 +114,45 @@ def allgather_lines(m_local: torch.Tensor, n: int, group=None, align: int = 1) -
     if all(e - b == chunk for b, e in rng):
         return out.permute(1, 0, 2, 3).reshape(B, world * chunk, W)
     return torch.cat([out[r, :, : e - b] for r, (b, e) in enumerate(rng)], dim=1)
+
+
+class LineGather:
+    """``allgather_lines`` pipelined across steps: ``start(m_local)`` copies the rank's block into
+    a persistent send buffer and launches the all_gather asynchronously (RCCL runs it on its own
+    stream, so it overlaps whatever the current stream does next — the next step's rollout); the
+    next ``start`` (or ``result`` / ``wait``) first orders the current stream after the previous
+    gather, so the buffers are reused only once it has finished.  ``result()`` is the [B, n, W]
+    assembly of the last started gather."""
+
+    def __init__(self, n: int, group=None, align: int = 1):
+        self.n, self.group, self.align = n, group, align
+        self.work = None
+        self.buf = self.out = None
+
+    def wait(self) -> None:
+        if self.work is not None:
+            self.work.wait()
+            self.work = None
+
+    def start(self, m_local: torch.Tensor) -> "LineGather":
+        world = dist.get_world_size(self.group)
+        B, n_loc, W = m_local.shape
+        self.rng = [shard_lines(self.n, r, world, self.align) for r in range(world)]
+        chunk = max(e - b for b, e in self.rng)
+        self.wait()  # the previous gather has read buf and written out
+        if self.buf is None or self.buf.shape != (B, chunk, W) or self.buf.dtype != m_local.dtype:
+            self.buf = torch.zeros(B, chunk, W, dtype=m_local.dtype, device=m_local.device)  # padding rows stay 0
+            self.out = torch.empty(world, B, chunk, W, dtype=m_local.dtype, device=m_local.device)
+        self.buf[:, :n_loc].copy_(m_local)
+        self.work = all_gather_into_(self.out.view(-1), self.buf.view(-1), self.group, async_op=True)
+        return self
+
+    def result(self) -> torch.Tensor:
+        self.wait()
+        world, B, chunk, W = self.out.shape
+        if all(e - b == chunk for b, e in self.rng):
+            return self.out.permute(1, 0, 2, 3).reshape(B, world * chunk, W)
+        return torch.cat([self.out[r, :, : e - b] for r, (b, e) in enumerate(self.rng)], dim=1)
 
 
 # ---------------------------------------------------------------- columns split: bitmap exchange

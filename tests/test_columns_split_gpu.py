@@ -162,8 +162,8 @@ def _rccl_world1_main(port, q):
     use (no host staging), on the dtypes and shapes they send."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1")
     import torch.distributed as dist
-    from gflownet_spai_amd.distributed import (LINE_ALIGN, all_reduce_, allgather_lines, exchange_bitmaps,
-                                               select_best_samples)
+    from gflownet_spai_amd.distributed import (LINE_ALIGN, LineGather, all_reduce_, allgather_lines,
+                                               exchange_bitmaps, select_best_samples)
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     dist.init_process_group("nccl", device_id=dev)
@@ -180,7 +180,11 @@ def _rccl_world1_main(port, q):
         out["allreduce"] = bool(torch.equal(limbs, ref))
         n = 1000
         m = torch.randn(bl, n, 5, device=dev)
-        out["allgather"] = bool(torch.equal(allgather_lines(m, n, align=LINE_ALIGN), m))
+        lg = LineGather(n, align=LINE_ALIGN)
+        lg.start(m)
+        lg.start(m * 2)  # the second waits for the first before reusing its buffers
+        out["allgather"] = bool(torch.equal(allgather_lines(m, n, align=LINE_ALIGN), m)
+                                and torch.equal(lg.result(), m * 2))
         rw = torch.tensor([0.5, 2.0, 1.0], dtype=torch.float64, device=dev)
         r, best, mb = select_best_samples(rw, m)
         out["best"] = bool(torch.equal(r, rw) and int(best) == 1 and torch.equal(mb, m[1]))

@@ -13,7 +13,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from gflownet_spai_amd.distributed import (LINE_ALIGN, allgather_lines, allreduce_res2, bitmap_pack_index,
+from gflownet_spai_amd.distributed import (LINE_ALIGN, LineGather, allgather_lines, allreduce_res2, bitmap_pack_index,
                                            exchange_bitmaps, exchange_parts, gather_rewards, gather_slices,
                                            select_best_samples, shard_lines, word_spans)
 from oracle import spai_oracle as O
@@ -60,6 +60,13 @@ def _worker(rank, world, port, q):
         full_m = allgather_lines(m_loc, n)
         out["res2"] = res2.numpy()
         out["m"] = full_m.numpy()
+        # the pipelined form (bench.py's per-step assembly): two gathers through the same buffers
+        lgth = LineGather(n, align=LINE_ALIGN)
+        b0a, b1a = shard_lines(n, rank, world, LINE_ALIGN)
+        ma = torch.arange(2 * (b1a - b0a) * 5, dtype=torch.float32).view(2, b1a - b0a, 5) + 1000 * rank
+        lgth.start(ma)
+        lgth.start(ma + 1)
+        out["m_pipe"] = lgth.result().numpy()
         out["rewards"] = gather_rewards(torch.arange(B, dtype=torch.float64) + 10 * rank).numpy()
         # the slices split's exchange: each part fills the bucket weight sums and winner counts
         # of its own bucket range (zero elsewhere, the exchange array's [B][2][kMaxB] layout)
@@ -184,6 +191,12 @@ def test_world2_column_sharded_reward_and_assembly():
             assert res[rank]["res2"][b] == pytest.approx(full, rel=1e-12)
             np.testing.assert_allclose(res[rank]["m"][b], m, rtol=1e-12, atol=1e-15)
     np.testing.assert_array_equal(res[0]["rewards"], [0, 1, 2, 10, 11, 12])
+    blocks = []
+    for q_ in (0, 1):
+        b0a, b1a = shard_lines(n, q_, 2, LINE_ALIGN)
+        blocks.append(torch.arange(2 * (b1a - b0a) * 5, dtype=torch.float32).view(2, b1a - b0a, 5) + 1000 * q_ + 1)
+    for rank in (0, 1):  # the second of two pipelined gathers, on every rank
+        assert np.array_equal(res[rank]["m_pipe"], torch.cat(blocks, 1).numpy())
     full_bs, partials = _split_fixture()
     acts, fwd, _, _ = _slices_fixture()
     env, words, bits, counts = _columns_fixture(2, 3)

@@ -100,6 +100,40 @@ __device__ __forceinline__ void group_sync() {
   asm volatile("" ::: "memory");
 }
 
+// LDS row strides chosen against bank conflicts (64 banks of 4 bytes).  The dense blocks: group
+// g's block starts at g * qr_group_stride words, and the two access shapes are lane (g, j)
+// reading row j (+ L i) of its group's block and the 64 / L group leaders writing during the
+// merge; the smallest padding that minimises the worse of the two (e.g. W = 5, R = 16, L = 4:
+// 80 -> 84 words per group, 4-way -> conflict-free).  Per-line fp64 rows read by consecutive
+// lines in phase 2 get an odd stride in doubles (conflict-free over a half-wave).
+__host__ __device__ constexpr int qr_ways(int gs, int rw, int L) {
+  int worst = 0;
+  for (int b = 0; b < 64; ++b) {
+    int n1 = 0, n2 = 0;
+    for (int g = 0; g < 64 / L; ++g) {
+      n2 += (gs * g) % 64 == b;
+      for (int j = 0; j < L; ++j) n1 += (gs * g + rw * j) % 64 == b;
+    }
+    worst = n1 > worst ? n1 : worst;
+    worst = n2 > worst ? n2 : worst;
+  }
+  return worst;
+}
+template <int R, int W, int L, typename TA>
+__host__ __device__ constexpr int qr_group_stride() {  // in elements of TA
+  constexpr int ew = (int)(sizeof(TA) / 4), base = R * W;
+  int best = base, bw = 1 << 30;
+  for (int pad = 0; pad < 16; ++pad) {
+    const int w = qr_ways((base + pad) * ew, W * ew, L);
+    if (w < bw) {
+      bw = w;
+      best = base + pad;
+    }
+  }
+  return best;
+}
+__host__ __device__ constexpr int odd_up(int x) { return x | 1; }
+
 #ifndef QR_WPE
 #define QR_WPE 2  // waves per SIMD of the 5-wide fill instances (175 VGPRs: 2 is what they reach)
 #endif
@@ -114,13 +148,15 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(W <= 5 ? QR_
   constexpr int NG = NT / L, R = L * RPL, NR = kQLines / NG;  // groups, block rows, rounds
   static_assert(kQLines % NG == 0 && W * WA <= 8 * 1024, "shapes");
   constexpr int T = W * (W + 1) / 2;  // packed upper triangle of R (row-major: p <= q)
-  __shared__ TA sD[NG][R][W];             // dense blocks A[I, slots] (rows of I ascending)
+  constexpr int GS = qr_group_stride<R, W, L, TA>();
+  __shared__ TA sDb[NG * GS];             // dense blocks A[I, slots] (rows of I ascending), GS per group
+#define SD(g_, r_, p_) sDb[(g_) * GS + (r_) * W + (p_)]
   __shared__ int sAi[NG][W][WA];          // staged A lines of the slots
   __shared__ TA sAv[NG][W][WA];
   __shared__ double sCn[NG][W];           // ||D[:, p]||^2 (the rank floor of the masked solves)
   __shared__ int sRowL[NG];               // position of row l in I; -1: not in I; -2: block overflow
-  __shared__ double sRf[NG][T];           // R of the full block (all slots)
-  __shared__ double sC[NG][W + 1];        // (Q^T e_l)[0..W), then the tail ||(Q^T e_l)[W..)||^2 (+1 if l not in I)
+  __shared__ double sRf[NG][odd_up(T)];   // R of the full block (all slots)
+  __shared__ double sC[NG][odd_up(W + 1)];  // (Q^T e_l)[0..W), then the tail ||(Q^T e_l)[W..)||^2 (+1 if l not in I)
   __shared__ int sAct[NG][W];             // action ids of the slots (-1: no slot / empty A line)
   __shared__ double sR2[kQChunk][NG];       // per (sample, group line): the sum over the rounds
   const int t = threadIdx.x, g = t / L, j = t % L, lane = t & 63, wave = t >> 6;
@@ -147,7 +183,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(W <= 5 ? QR_
           sAi[g][p][s] = a;
           sAv[g][p][s] = a >= 0 ? a_val[(int64_t)kp * wart + s] : (TA)0;
         }
-        for (int e = j; e < R * W; e += L) (&sD[g][0][0])[e] = (TA)0;
+        for (int e = j; e < R * W; e += L) sDb[g * GS + e] = (TA)0;
         group_sync();
         if (j == 0) {  // merge the sorted A lines into the rows of I (ascending)
           int h[W], cur[W];
@@ -174,7 +210,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(W <= 5 ? QR_
             for (int p = 0; p < W; ++p)
               if (cur[p] == rmin) {
                 const TA v = sAv[g][p][h[p]];
-                sD[g][rho][p] = v;
+                SD(g, rho, p) = v;
                 cn[p] += (double)v * (double)v;
                 ++h[p];
                 const int a = h[p] < WA ? sAi[g][p][h[p]] : -1;
@@ -197,7 +233,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(W <= 5 ? QR_
         for (int i = 0; i < RPL; ++i) {
           const int rho = j + L * i;
 #pragma unroll
-          for (int p = 0; p < W; ++p) dv[i][p] = (double)sD[g][rho][p];
+          for (int p = 0; p < W; ++p) dv[i][p] = (double)SD(g, rho, p);
           rhs[i] = rho == rowl ? 1.0 : 0.0;
         }
         // reflection p maps column p onto row p (a column already zero below row p: none)
@@ -362,6 +398,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(W <= 5 ? QR_
     __syncthreads();
   }
 }
+#undef SD
 
 // (W class, A width class, rows) -> instance
 template <int W, int WA, int L, int RPL, int NT, typename TM>

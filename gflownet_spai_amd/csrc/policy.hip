@@ -350,7 +350,10 @@ __global__ __launch_bounds__(kRedNT) void k_pool(int32_t n, int32_t nblk, const 
   }
 }
 
-constexpr int kFcPer = 4;  // actions per thread of k_fc (strided by kNT inside a block)
+#ifndef KFCPER
+#define KFCPER 4
+#endif
+constexpr int kFcPer = KFCPER;  // actions per thread of k_fc (strided by kNT inside a block)
 
 // The pooled embedding of the constant-row closed form (k_const_pool's arithmetic, same fmaf
 // order): h1 = relu(W_l1 x0 + b_l1 + bias1), h = relu(W_l2 h1 + b_l2 + bias2).  Uniform loads

@@ -107,9 +107,11 @@ def fill_bytes(env, B, store_m: bool = True) -> float:
     Gram values (T + Wc, fp32 when the cache round-trips exactly, else fp64), per sample the
     removal bitmap and the stored values of M."""
     n, W = env.pattern.n, env.pattern.width
-    s = env.a_lines.val.element_size() if env.fill == "lsq" else 4
+    s = env.a_lines.val.element_size() if env._lsq else 4
     per_sample = math.ceil(env.init_nnz / 32) * 4 + (n * W * s if store_m else 0) + 8
-    if getattr(env, "gram", None) is not None:
+    if getattr(env, "rcache", None) is not None:  # QR fill: the action ids + the env-constant R cache
+        line = n * W * 4 + env.rcache.numel() * env.rcache.element_size()
+    elif getattr(env, "gram", None) is not None:
         line = n * W * 4 + env.gram.numel() * env.gram.element_size() + (n * W * 4 if env.fill == "copy" else 0)
     else:
         sa = env.a_lines.val.element_size()
@@ -125,7 +127,7 @@ def survey_fill_bytes(env, B, store_m: bool = True) -> float:
     nnz_a = int((env.a_lines.idx >= 0).sum())
     nnz_p = env.init_nnz
     s_a = env.a_lines.val.element_size()
-    s_m = s_a if env.fill == "lsq" else 4
+    s_m = s_a if env._lsq else 4
     per_sample = math.ceil(nnz_p / 32) * 4 + (s_m * nnz_p if store_m else 0) + 8
     return nnz_a * (s_a + 4) + 4 * (n + 1) + 4 * nnz_p + 4 * (n + 1) + B * per_sample
 
@@ -143,7 +145,7 @@ def measured_traffic(cfg: str, B: int):
         rec = {rec["config"]: rec}
     rec = rec.get(cfg, {})
     if rec.get("batch") == B:
-        return float(rec["hbm_bytes_per_launch"])
+        return float(rec["hbm_bytes_per_launch"]), rec.get("source", "profiles/fill_traffic.json")
     return None
 
 
@@ -254,9 +256,13 @@ def select_bytes(env, B: int, winners: float) -> float:
 
 
 def roofline_obj(kernel, nbytes, ms, traffic=None):
+    """traffic: (HBM bytes per launch, source) from a committed PMC pass of the same workload
+    (measured_traffic: NOT measured in this run; `traffic_source` names the file), or None."""
     achieved = nbytes / (ms * 1e-3) / 1e9
+    tb, src = traffic if traffic is not None else (None, None)
     return {"kernel": kernel, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "bytes_per_launch": nbytes, "avg_launch_ms": ms}
+            "frac": achieved / HBM_PEAK_GBS, "traffic": tb, "traffic_source": src, "bytes_per_launch": nbytes,
+            "avg_launch_ms": ms}
 
 
 def launch_ranks(n: int) -> int:
@@ -292,10 +298,19 @@ def main():
     ap.add_argument("--fill", default="lsq", choices=["lsq", "qr"],
                     help="least-squares fill: normal equations from the Gram cache (lsq) or Householder QR (qr)")
     ap.add_argument("--no-graph", action="store_true", help="time eager steps (host launches) instead of graph replays")
+    ap.add_argument("--no-overlap", action="store_true",
+                    help="one GPU: run the fill + rewards after the trajectory sort on one stream instead of beside it")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="process-group backend (nccl = RCCL over xGMI; gloo only to rehearse the flow)")
     ap.add_argument("--share-gpu", action="store_true",
                     help="every rank on GPU 0 (rehearsal of the multi-rank flow on a one-GPU box, with --backend gloo)")
+    ap.add_argument("--dist", action="store_true",
+                    help="initialise the process group and run the --shard split's multi-GPU step even at one rank "
+                         "(--gpus 1 --backend nccl: the columns split's graph segments, all_to_all and pipelined M "
+                         "all_gather through a one-rank RCCL group)")
+    ap.add_argument("--dump", default=None,
+                    help="write the last assembled step (Philox stream id, rewards of every candidate, the assembled "
+                         "M) to this .pt file (rank 0; tests/test_bench_dist_gpu.py)")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -310,7 +325,8 @@ def main():
         local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    dist_on = world > 1 or args.dist
+    if dist_on:
         import torch.distributed as dist
         if args.backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
@@ -325,7 +341,7 @@ def main():
     n = A.shape[0]
     env = PreconditionerEnv(n, P, A, side="AM", fill=args.fill, keep_m=True, device=dev)
     E = env.num_actions - 1
-    shard = args.shard if world > 1 else "columns"  # one GPU: every split is the same one-GPU step
+    shard = args.shard if dist_on else "columns"  # one GPU: every split is the same one-GPU step
     if shard in ("samples", "slices") or (shard == "columns" and args.strong):
         if args.batch % world:
             sys.exit(f"bench.py: --shard {shard} needs the batch ({args.batch}) divisible by the GPU count ({world})")
@@ -333,16 +349,18 @@ def main():
     else:  # columns (weak: --batch rollouts per GPU, fill of every candidate by column shard) / candidates
         B, bl, strong = args.batch * world, args.batch, False
     base = {"samples": rank * bl, "candidates": rank * bl}.get(shard, 0)
-    split = {"columns": "columns", "slices": "slices"}.get(shard) if world > 1 else None
+    split = {"columns": "columns", "slices": "slices"}.get(shard) if dist_on else None
     model = GFlowNet(make_policy(env, P, dev), None, env, mode="throughput", seed=1234, sample_base=base,
-                     shard=(rank, world, None) if split else None, split=split or "columns")
+                     shard=(rank, world, None) if split else None, split=split or "columns",
+                     overlap=not args.no_overlap)
     s0 = [P] * bl
     assembled = {}
-    do_assemble = [args.assemble != "none" and world > 1 and shard != "candidates"]
+    do_assemble = [args.assemble != "none" and dist_on and shard != "candidates"]
     # the M all_gather of a step runs asynchronously and overlaps the next step's rollout; the
-    # timed region still ends after the last one (gather.wait() before the closing barrier)
+    # timed region still ends after the last one (gather.wait() before the closing barrier).
+    # GFlowNet gives both splits 256-line-aligned shards (its .lines): the gather uses the same
     from gflownet_spai_amd.distributed import LineGather
-    gather = LineGather(n, align=LINE_ALIGN if shard == "columns" else 1) if do_assemble[0] else None
+    gather = LineGather(n, align=LINE_ALIGN) if do_assemble[0] else None
 
     def assemble(log):
         if not do_assemble[0]:
@@ -368,7 +386,7 @@ def main():
         return st["log"]
 
     def barrier():
-        if world > 1:
+        if dist_on:
             torch.distributed.barrier()
         torch.cuda.synchronize()
 
@@ -389,6 +407,8 @@ def main():
 
         use_graph = not args.no_graph
         if use_graph:
+            if gather is not None:
+                gather.wait()  # no RCCL gather in flight while a graph is captured
             # capture every maximal run of collective-free phases as one HIP graph (one GPU: the
             # whole step is one graph); the collectives run eagerly between the replays
             side = torch.cuda.Stream(dev)
@@ -436,6 +456,12 @@ def main():
         barrier()
         dt = (time.perf_counter() - t0) / args.steps
         dt_noasm = dt
+        if args.dump and rank == 0:  # the last timed step: its stream id, every candidate's reward, M
+            dump = {"stream_id": model.rollouts - 1, "rewards_all": log.rewards_all.double().cpu(),
+                    "residual": env.last_residual.double().cpu(), "shard": shard, "world": world}
+            if gather is not None and args.assemble != "none":
+                dump["m_assembled"] = gather.result().cpu()
+            torch.save(dump, args.dump)
         if do_assemble[0]:  # the same steps without the M all_gather (reported apart)
             do_assemble[0] = False
             barrier()
@@ -445,7 +471,7 @@ def main():
             barrier()
             dt_noasm = (time.perf_counter() - t0) / args.steps
             do_assemble[0] = True
-    if world > 1:
+    if dist_on:
         t = torch.tensor([dt, dt_eager, dt_noasm], device=dev, dtype=torch.float64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         dt, dt_eager, dt_noasm = float(t[0]), float(t[1]), float(t[2])
@@ -506,16 +532,22 @@ def main():
             sbq = survey_fill_bytes(env, B if shard == "columns" else bl)
             if split:
                 sbq *= (model.lines[1] - model.lines[0]) / n
-            out["roofline"] = roofline_obj(f"k_qr_fill<{env.pattern.width},rows {env.qr_rows}> (LSQ fill of M by "
-                                           f"Householder QR of each line's block A[I, J] + ||AM-I||^2)", sbq, fill_ms,
-                                           measured_traffic(args.config + "_qr", bl))
+            if env.rcache is not None:  # phase 2 from the R cache: its bytes are the cache + the per-sample stream
+                out["roofline"] = roofline_obj(
+                    f"k_qr_solve<{env.pattern.width}> (LSQ fill of M by Householder QR: masked re-triangularisation of "
+                    f"each line's cached R (the full block A[I, slots] factored once per env, rows {env.qr_rows}) + "
+                    f"||AM-I||^2)", fb, fill_ms, measured_traffic(args.config + "_qr", bl))
+            else:
+                out["roofline"] = roofline_obj(f"k_qr_fill<{env.pattern.width},rows {env.qr_rows}> (LSQ fill of M by "
+                                               f"Householder QR of each line's block A[I, J] + ||AM-I||^2)", sbq,
+                                               fill_ms, measured_traffic(args.config + "_qr", bl))
         # the same launch at SURVEY §8(d)'s bytes (A counted as bytes(A), not as the Gram cache)
         sb = survey_fill_bytes(env, B if shard == "columns" else bl)
         if split:
             sb *= (model.lines[1] - model.lines[0]) / n
         out["roofline"]["bytes_survey_8d"] = sb
         out["roofline"]["frac_survey_8d"] = sb / (fill_ms * 1e-3) / 1e9 / HBM_PEAK_GBS
-        if world == 1:
+        if not dist_on:
             sel = roofline_obj("rollout_select phase: k_presample + k_splitters + k_tile + k_bsum (k_tile ~80 % of "
                                "it; latency-bound, not bandwidth-bound: see the PMC profile in DESIGN.md §5)",
                                select_bytes(env, bl, float(counts.sum())),
@@ -523,12 +555,12 @@ def main():
             out["roofline_select"] = sel
             with torch.no_grad():
                 out["roofline_residual"] = generic_residual_leg(env, log, args.config)
-        if not args.no_cpu_baseline and world == 1:
+        if not args.no_cpu_baseline and not dist_on:
             with torch.no_grad():
                 lg_host = model.forward_policy.logits(model.state_to_data(s0[:1])[0])[0].reshape(-1).cpu().numpy()
             out["cpu_baseline"] = cpu_baseline(args.config, B, args.cpu_budget, lg_host, float(counts.mean()) + 1)
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist_on:
         torch.distributed.destroy_process_group()
 
 

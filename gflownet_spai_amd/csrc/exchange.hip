@@ -1,0 +1,67 @@
+// The columns split's bitmap exchange for gfx950 (distributed.py).
+//
+// Rank q fills the lines of its 256-line-aligned column shard for every candidate, so it needs,
+// per candidate, the removal bits of exactly the actions its lines hold.  Action ids are raw COO
+// positions (preconditioner.py:23-25), so for a matrix whose raw order is not banded (thermal2's
+// file order, any permuted numbering) those bits are scattered over the whole bitmap.  The send
+// buffer is therefore built by gathering, per destination q, the bits of q's action ids in
+// LINE-MAJOR order (the order q's fill visits them) and packing them 32 to a word: every rank
+// receives exactly nnz(shard) bits per candidate whatever the numbering; the receiving fill reads
+// them through a shard-local action table (the same line-major positions).
+#include "spai_device.h"
+#include "spai_status.h"
+
+namespace spai {
+namespace {
+
+constexpr int kPackNT = 256;
+
+// One thread per packed bit j of destination q (blockIdx.y); a wave's 64 bits are two whole
+// words (j0 is a multiple of 64), formed by one ballot per candidate.  Layout of q's block at
+// out + out_off[q]: [bl][wq + 1] words = the wq packed words, then the candidate's removal count.
+__global__ __launch_bounds__(kPackNT) void k_bitmap_pack(int32_t bl, const uint32_t* __restrict__ removed,
+                                                         int32_t words, const int32_t* __restrict__ counts,
+                                                         const int32_t* __restrict__ ids,
+                                                         const int64_t* __restrict__ seg,
+                                                         const int64_t* __restrict__ out_off,
+                                                         uint32_t* __restrict__ out) {
+  const int q = blockIdx.y, lane = threadIdx.x & 63;
+  const int64_t s0 = seg[q], m = seg[q + 1] - s0, wq = (m + 31) / 32;
+  const int64_t j = (int64_t)blockIdx.x * kPackNT + threadIdx.x;
+  if ((int64_t)blockIdx.x * kPackNT >= m && blockIdx.x != 0) return;  // block-uniform
+  uint32_t* o = out + out_off[q];
+  const int a = j < m ? ids[s0 + j] : -1;
+  const int64_t w = (j - lane) >> 5;  // the wave's first word
+  const uint32_t* rw = removed + (a >= 0 ? (a >> 5) : 0);
+  const uint32_t sh = (uint32_t)a & 31u;
+#pragma unroll 1
+  for (int b = 0; b < bl; ++b) {
+    const bool bit = a >= 0 && ((rw[(int64_t)b * words] >> sh) & 1u);
+    const uint64_t mask = __ballot(bit);
+    uint32_t* ob = o + (int64_t)b * (wq + 1);
+    if (lane == 0 && w < wq) ob[w] = (uint32_t)mask;
+    if (lane == 32 && w + 1 < wq) ob[w + 1] = (uint32_t)(mask >> 32);
+  }
+  if (j == 0)
+    for (int b = 0; b < bl; ++b) o[(int64_t)b * (wq + 1) + wq] = (uint32_t)counts[b];
+}
+
+}  // namespace
+}  // namespace spai
+
+using namespace spai;
+
+extern "C" int spai_bitmap_pack(int32_t P, int32_t bl, const uint32_t* removed, int32_t words, const int32_t* counts,
+                                const int32_t* ids, const int64_t* seg, const int64_t* out_off, int64_t max_seg,
+                                uint32_t* out, void* stream) {
+  SPAI_CHECK_ARG(P >= 1 && bl >= 1 && words >= 1 && max_seg >= 0 && removed && counts && seg && out_off && out &&
+                     (ids || max_seg == 0),
+                 "spai_bitmap_pack: bad arguments");
+  SPAI_CHECK_ARG(P <= 65535, "spai_bitmap_pack: P=%d above 65535", P);
+  const int64_t gx = (max_seg + kPackNT - 1) / kPackNT;
+  SPAI_CHECK_ARG(gx <= 0x7fffffff, "spai_bitmap_pack: segment too long");
+  dim3 grid((unsigned)(gx > 0 ? gx : 1), (unsigned)P);
+  k_bitmap_pack<<<grid, kPackNT, 0, (hipStream_t)stream>>>(bl, removed, words, counts, ids, seg, out_off, out);
+  SPAI_CHECK_LAUNCH();
+  return SPAI_OK;
+}

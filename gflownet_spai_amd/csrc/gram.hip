@@ -43,44 +43,6 @@ __device__ __forceinline__ double fast_rcp(double x) {
   return fma(r, e, r);
 }
 
-constexpr int kNtAux = 2;              // buffer-store cache policy: nt (streaming output, gfx950)
-constexpr int kBufWord3 = 0x00020000;  // buffer resource dword 3 (raw byte addressing)
-typedef unsigned int u2v __attribute__((ext_vector_type(2)));
-typedef unsigned int u4v __attribute__((ext_vector_type(4)));
-
-// One sample's M block of a line block (ne = nvl * wrt values, contiguous at dst) from its LDS
-// staging copy sm, with a FIXED number of buffer stores per thread: 16-byte stores over the whole
-// 16-byte chunks, then one element store for the tail.  Stores past the block — all of them when
-// dst is null (no M requested) — fall outside the buffer's bound and are dropped.  No branch skips
-// a store, so the compiler's wait for the next sample's bitmap words (loaded before these stores;
-// vmcnt counts in order) is vmcnt(stores), not vmcnt(0): at one wave per SIMD a drain of the M
-// stores per sample was an HBM write latency per sample.
-template <int W, typename TM>
-__device__ __forceinline__ void store_m_block(TM* dst, const TM* sm, int ne) {
-  constexpr int kV = 16 / (int)sizeof(TM), kChunks = kNT * W / kV;
-  constexpr int kSt = (kChunks + kNT - 1) / kNT;
-  static_assert(kNT * W % kV == 0, "whole 16-byte chunks in the staging buffer");
-  const int t = threadIdx.x, nfull = ne / kV;
-  const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(dst, 0, dst ? nfull * 16 : 0, kBufWord3);
-  const __amdgpu_buffer_rsrc_t re =
-      __builtin_amdgcn_make_buffer_rsrc(dst, 0, dst ? ne * (int)sizeof(TM) : 0, kBufWord3);
-#pragma unroll
-  for (int i = 0; i < kSt; ++i) {
-    const int c = i * kNT + t;
-    const u4v v = reinterpret_cast<const u4v*>(sm)[min(c, kChunks - 1)];
-    __builtin_amdgcn_raw_buffer_store_b128(v, rv, c * 16, 0, kNtAux);
-  }
-  const int e = nfull * kV + min(t, kV - 1);  // the tail (< kV values): threads 0 .. kV - 1
-  const int off = t < kV ? e * (int)sizeof(TM) : 0x7ffffff0;
-  const TM x = sm[min(e, kNT * W - 1)];
-  if constexpr (sizeof(TM) == 4)
-    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x), re, off, 0, kNtAux);
-  else {
-    const uint64_t u = (uint64_t)__double_as_longlong(x);
-    __builtin_amdgcn_raw_buffer_store_b64((u2v){(uint32_t)u, (uint32_t)(u >> 32)}, re, off, 0, kNtAux);
-  }
-}
-
 template <int W, int WA, typename TA>
 __global__ __launch_bounds__(kNT) void k_gram_build(int32_t n, int32_t wrt, int32_t wart,
                                                     const int32_t* __restrict__ pat_idx,
@@ -436,7 +398,7 @@ __global__ __launch_bounds__(kNT) void k_gram_fill_wide(int32_t n, int32_t line_
           if (p < wrt) sm[t * wrt + p] = (TM)y[p];
       }
       __syncthreads();
-      store_m_block<W, TM>(m_out ? m_out + ((int64_t)b * nloc + (int64_t)lb * kNT) * wrt : nullptr, sm, nvl * wrt);
+      store_m_block<kNT, W, TM>(m_out ? m_out + ((int64_t)b * nloc + (int64_t)lb * kNT) * wrt : nullptr, sm, nvl * wrt);
     }
     if (b % kChunk == kChunk - 1 || b == B - 1) {  // the chunk's fixed-order block sums
       const int c0 = b - b % kChunk, nb = b - c0 + 1;

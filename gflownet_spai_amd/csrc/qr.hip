@@ -137,6 +137,216 @@ __host__ __device__ constexpr int odd_up(int x) { return x | 1; }
 #ifndef QR_WPE
 #define QR_WPE 2  // waves per SIMD of the 5-wide fill instances (175 VGPRs: 2 is what they reach)
 #endif
+
+// LDS of the per-line factorisation (phase 1) for NT / L groups of L lanes.
+template <int W, int WA, int L, int RPL, int NT, typename TA>
+struct QrStage {
+  static constexpr int NG = NT / L, R = L * RPL, T = W * (W + 1) / 2;
+  static constexpr int GS = qr_group_stride<R, W, L, TA>();
+  TA sDb[NG * GS];                 // dense blocks A[I, slots] (rows of I ascending), GS per group
+  int sAi[NG][W][WA];              // staged A lines of the slots
+  TA sAv[NG][W][WA];
+  double sCn[NG][W];               // ||D[:, p]||^2 (the rank floor of the masked solves)
+  int sRowL[NG];                   // position of row l in I; -1: not in I; -2: block overflow
+  double sRf[NG][odd_up(T)];       // R of the full block (all slots), packed upper triangle
+  double sC[NG][odd_up(W + 1)];    // (Q^T e_l)[0..W), then the tail ||(Q^T e_l)[W..)||^2 (+1 if l not in I)
+  int sAct[NG][W];                 // action ids of the slots (-1: no slot / empty A line)
+};
+
+// Phase 1 for line l on group g (lane j of L): the slots' A lines staged and merged (one lane;
+// they are sorted by row index) into D = A[I, slots], then the FULL Householder QR of D on the
+// group -> S.sRf[g], S.sC[g], S.sCn[g], S.sAct[g].  Sample-independent: it depends on A and the
+// pattern only.  Ends with the group's LDS writes issued (the caller orders them by a barrier).
+template <int W, int WA, int L, int RPL, int NT, typename TA>
+__device__ __forceinline__ void qr_factor_line(QrStage<W, WA, L, RPL, NT, TA>& S, int g, int j, bool valid, int l,
+                                               int32_t wrt, const int32_t* __restrict__ pat_idx,
+                                               const int32_t* __restrict__ pat_act, int32_t wart,
+                                               const int32_t* __restrict__ a_idx, const TA* __restrict__ a_val) {
+  using St = QrStage<W, WA, L, RPL, NT, TA>;
+  constexpr int R = St::R, GS = St::GS;
+#define SD(g_, r_, p_) S.sDb[(g_) * GS + (r_) * W + (p_)]
+  for (int e = j; e < W * WA; e += L) {
+    const int p = e / WA, s = e % WA;
+    const int kp = (valid && p < wrt) ? pat_idx[(int64_t)l * wrt + p] : -1;
+    const int a = (kp >= 0 && s < wart) ? a_idx[(int64_t)kp * wart + s] : -1;
+    S.sAi[g][p][s] = a;
+    S.sAv[g][p][s] = a >= 0 ? a_val[(int64_t)kp * wart + s] : (TA)0;
+  }
+  for (int e = j; e < R * W; e += L) S.sDb[g * GS + e] = (TA)0;
+  group_sync();
+  if (j == 0) {  // merge the sorted A lines into the rows of I (ascending)
+    int h[W], cur[W];
+    double cn[W];
+#pragma unroll
+    for (int p = 0; p < W; ++p) {
+      h[p] = 0;
+      cn[p] = 0.0;
+      const int a = S.sAi[g][p][0];
+      cur[p] = a >= 0 ? a : INT_MAX;
+    }
+    int rowl = -1, rho = 0;
+#pragma unroll 1
+    for (int it = 0; it <= R; ++it) {
+      int rmin = INT_MAX;
+#pragma unroll
+      for (int p = 0; p < W; ++p) rmin = min(rmin, cur[p]);
+      if (rmin == INT_MAX) break;
+      if (rho == R) {  // more rows than the instance holds (the caller's max_rows was wrong)
+        rowl = -2;
+        break;
+      }
+#pragma unroll
+      for (int p = 0; p < W; ++p)
+        if (cur[p] == rmin) {
+          const TA v = S.sAv[g][p][h[p]];
+          SD(g, rho, p) = v;
+          cn[p] += (double)v * (double)v;
+          ++h[p];
+          const int a = h[p] < WA ? S.sAi[g][p][h[p]] : -1;
+          cur[p] = a >= 0 ? a : INT_MAX;
+        }
+      if (rmin == l) rowl = rho;
+      ++rho;
+    }
+#pragma unroll
+    for (int p = 0; p < W; ++p) {
+      S.sCn[g][p] = cn[p];
+      S.sAct[g][p] = (valid && p < wrt && S.sAi[g][p][0] >= 0) ? pat_act[(int64_t)l * wrt + p] : -1;
+    }
+    S.sRowL[g] = rowl;
+  }
+  group_sync();
+  const int rowl = S.sRowL[g];
+  double dv[RPL][W], rhs[RPL];
+#pragma unroll
+  for (int i = 0; i < RPL; ++i) {
+    const int rho = j + L * i;
+#pragma unroll
+    for (int p = 0; p < W; ++p) dv[i][p] = (double)SD(g, rho, p);
+    rhs[i] = rho == rowl ? 1.0 : 0.0;
+  }
+  // reflection p maps column p onto row p (a column already zero below row p: none)
+#pragma unroll
+  for (int p = 0; p < W; ++p) {
+    double s1 = 0.0, xk = 0.0;
+#pragma unroll
+    for (int i = 0; i < RPL; ++i) {
+      const int rho = j + L * i;
+      const double x = dv[i][p];
+      s1 = fma(rho >= p ? x : 0.0, x, s1);
+      xk += rho == p ? x : 0.0;
+    }
+    const double sig = group_sum<L>(s1), xkk = group_sum<L>(xk);
+    const double sq = sqrt(sig);
+    const double alpha = xkk >= 0.0 ? -sq : sq;
+    const double tau = sig > 0.0 ? qr_rcp(sig - alpha * xkk) : 0.0;  // H = I - tau v v^T
+    double v[RPL];
+#pragma unroll
+    for (int i = 0; i < RPL; ++i) {
+      const int rho = j + L * i;
+      v[i] = rho >= p ? dv[i][p] - (rho == p ? alpha : 0.0) : 0.0;
+    }
+    double d[W + 1];  // v . column q (q > p), v . rhs
+#pragma unroll
+    for (int q = p + 1; q <= W; ++q) {
+      double a = 0.0;
+#pragma unroll
+      for (int i = 0; i < RPL; ++i) a = fma(v[i], q < W ? dv[i][q] : rhs[i], a);
+      d[q] = a;
+    }
+#pragma unroll
+    for (int q = p + 1; q <= W; ++q) d[q] = group_sum<L>(d[q]) * tau;
+#pragma unroll
+    for (int i = 0; i < RPL; ++i) {
+#pragma unroll
+      for (int q = p + 1; q < W; ++q) dv[i][q] = fma(-d[q], v[i], dv[i][q]);
+      rhs[i] = fma(-d[W], v[i], rhs[i]);
+    }
+    // row p of R and (Q^T e)_p are final now (later reflections act on rows > p)
+    if (j == p % L) {
+      const int base = p * W - p * (p - 1) / 2;
+      S.sRf[g][base] = sig > 0.0 ? alpha : dv[p / L][p];
+#pragma unroll
+      for (int q = p + 1; q < W; ++q) S.sRf[g][base + (q - p)] = dv[p / L][q];
+      S.sC[g][p] = rhs[p / L];
+    }
+  }
+  double tl = 0.0;  // the tail of Q^T e: rows >= W
+#pragma unroll
+  for (int i = 0; i < RPL; ++i) tl = fma(j + L * i >= W ? rhs[i] : 0.0, rhs[i], tl);
+  tl = group_sum<L>(tl);
+  if (j == 0) S.sC[g][W] = rowl == -2 ? __builtin_nan("") : tl + (rowl < 0 ? 1.0 : 0.0);
+#undef SD
+}
+
+// 1/sqrt(t) to ~1 ulp: hardware reciprocal square root + one Newton step (t > 0, normal)
+__device__ __forceinline__ double qr_rsq(double t) {
+  const double r = __builtin_amdgcn_rsq(t);
+  const double e = fma(-t * r, r, 1.0);  // 1 - t r^2
+  return fma(0.5 * r, e, r);
+}
+
+// Phase 2 for one (line, sample) on ONE lane: min ||R_J m - c|| over the kept columns J of the
+// line's full-block R (R_J = Q^T D_J has the singular values of A[I, J], so the small problem
+// keeps the QR's accuracy: no normal equations).  The pivot of a kept column p stays in row p:
+// the rows whose own column was removed (or rank-dropped) are "free", and at column p ONE
+// Householder reflection over {free rows < p} u {row p} maps column p onto row p (the pivot rows
+// < p take no part: their entries of v are 0, so they are left exactly as they are).  Only which
+// rows are free depends on the mask — no data-dependent row index anywhere, so the back-
+// substitution is the plain triangular one.  Column p pivots when it is kept and its norm outside
+// the pivot rows exceeds 1e-12 ||D[:, p]|| (cn[p] = ||D[:, p]||^2: fp64 rank deficiency), else
+// m_p = 0 and row p becomes free (no reflection).  Rm (Rm[i][q], i <= q; the rest is never read)
+// and c are worked in place; m gets the solution; returns the line residual^2 = tail + sum of
+// (Q^T e)^2 over the free rows (sums of squares: no cancellation).
+template <int W>
+__device__ __forceinline__ double qr_masked_solve(double (&Rm)[W][W], double (&c)[W], double tail,
+                                                  const double (&cn)[W], const bool (&keep)[W], double (&m)[W]) {
+  bool piv[W];
+  double rd[W];
+#pragma unroll
+  for (int p = 0; p < W; ++p) {
+    double v[W];  // the reflection vector over rows 0..p (0 on the pivot rows)
+    const double xp = Rm[p][p];
+    double sig = xp * xp;
+#pragma unroll
+    for (int i = 0; i < p; ++i) {
+      v[i] = piv[i] ? 0.0 : Rm[i][p];
+      sig = fma(v[i], v[i], sig);
+    }
+    piv[p] = keep[p] && sig > 1e-24 * cn[p];  // |R_pp| after the reflection > 1e-12 ||D[:, p]||
+    const double rs = qr_rsq(piv[p] ? sig : 1.0);
+    const double sq = sig * rs;                                 // sqrt(sig)
+    const double alpha = __builtin_copysign(sq, -xp);           // the new R_pp (sign opposite to x_p)
+    const double tau = piv[p] ? qr_rcp(fma(sq, __builtin_fabs(xp), sig)) : 0.0;  // 1 / (sig - alpha x_p)
+    v[p] = xp - alpha;
+    rd[p] = piv[p] ? __builtin_copysign(rs, -xp) : 0.0;         // 1 / alpha
+#pragma unroll
+    for (int q = p + 1; q <= W; ++q) {
+      double a = v[p] * (q < W ? Rm[p][q] : c[p]);
+#pragma unroll
+      for (int i = 0; i < p; ++i) a = fma(v[i], q < W ? Rm[i][q] : c[i], a);
+      a *= tau;
+#pragma unroll
+      for (int i = 0; i <= p; ++i) {
+        if (q < W) Rm[i][q] = fma(-a, v[i], Rm[i][q]);
+        else c[i] = fma(-a, v[i], c[i]);
+      }
+    }
+  }
+  double rsum = tail;  // + (Q^T e) over the free rows
+#pragma unroll
+  for (int i = 0; i < W; ++i) rsum = fma(piv[i] ? 0.0 : c[i], c[i], rsum);
+#pragma unroll
+  for (int p = W - 1; p >= 0; --p) {
+    double a = c[p];
+#pragma unroll
+    for (int q = p + 1; q < W; ++q) a = fma(-Rm[p][q], m[q], a);  // m_q = 0 for a non-pivot q
+    m[p] = a * rd[p];  // 0 for a dropped slot
+  }
+  return rsum;
+}
+
+// The fused fill: phase 1 and phase 2 in one launch, A read every call (no cache).
 template <int W, int WA, int L, int RPL, int NT, typename TA, typename TM>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(W <= 5 ? QR_WPE : 2))) void k_qr_fill(int32_t n, int32_t line_begin, int32_t line_end, int32_t wrt,
                                                   const int32_t* __restrict__ pat_idx,
@@ -145,19 +355,10 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(W <= 5 ? QR_
                                                   int32_t B, const uint32_t* __restrict__ removed, int32_t words,
                                                   int32_t word_base, TM* __restrict__ m_out,
                                                   double* __restrict__ partials) {
-  constexpr int NG = NT / L, R = L * RPL, NR = kQLines / NG;  // groups, block rows, rounds
+  using St = QrStage<W, WA, L, RPL, NT, TA>;
+  constexpr int NG = St::NG, NR = kQLines / NG;  // groups, rounds
   static_assert(kQLines % NG == 0 && W * WA <= 8 * 1024, "shapes");
-  constexpr int T = W * (W + 1) / 2;  // packed upper triangle of R (row-major: p <= q)
-  constexpr int GS = qr_group_stride<R, W, L, TA>();
-  __shared__ TA sDb[NG * GS];             // dense blocks A[I, slots] (rows of I ascending), GS per group
-#define SD(g_, r_, p_) sDb[(g_) * GS + (r_) * W + (p_)]
-  __shared__ int sAi[NG][W][WA];          // staged A lines of the slots
-  __shared__ TA sAv[NG][W][WA];
-  __shared__ double sCn[NG][W];           // ||D[:, p]||^2 (the rank floor of the masked solves)
-  __shared__ int sRowL[NG];               // position of row l in I; -1: not in I; -2: block overflow
-  __shared__ double sRf[NG][odd_up(T)];   // R of the full block (all slots)
-  __shared__ double sC[NG][odd_up(W + 1)];  // (Q^T e_l)[0..W), then the tail ||(Q^T e_l)[W..)||^2 (+1 if l not in I)
-  __shared__ int sAct[NG][W];             // action ids of the slots (-1: no slot / empty A line)
+  __shared__ St S;
   __shared__ double sR2[kQChunk][NG];       // per (sample, group line): the sum over the rounds
   const int t = threadIdx.x, g = t / L, j = t % L, lane = t & 63, wave = t >> 6;
   const int lb = blockIdx.x;
@@ -172,128 +373,12 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(W <= 5 ? QR_
 #pragma unroll 1
     for (int r = 0; r < NR; ++r) {
       {
-        // ---- 1. per line (group g): the dense block, then its FULL Householder QR (all slots)
         const int li = r * NG + g;
         const bool valid = li < nvl;
-        const int l = blk0 + (valid ? li : 0);
-        for (int e = j; e < W * WA; e += L) {
-          const int p = e / WA, s = e % WA;
-          const int kp = (valid && p < wrt) ? pat_idx[(int64_t)l * wrt + p] : -1;
-          const int a = (kp >= 0 && s < wart) ? a_idx[(int64_t)kp * wart + s] : -1;
-          sAi[g][p][s] = a;
-          sAv[g][p][s] = a >= 0 ? a_val[(int64_t)kp * wart + s] : (TA)0;
-        }
-        for (int e = j; e < R * W; e += L) sDb[g * GS + e] = (TA)0;
-        group_sync();
-        if (j == 0) {  // merge the sorted A lines into the rows of I (ascending)
-          int h[W], cur[W];
-          double cn[W];
-#pragma unroll
-          for (int p = 0; p < W; ++p) {
-            h[p] = 0;
-            cn[p] = 0.0;
-            const int a = sAi[g][p][0];
-            cur[p] = a >= 0 ? a : INT_MAX;
-          }
-          int rowl = -1, rho = 0;
-#pragma unroll 1
-          for (int it = 0; it <= R; ++it) {
-            int rmin = INT_MAX;
-#pragma unroll
-            for (int p = 0; p < W; ++p) rmin = min(rmin, cur[p]);
-            if (rmin == INT_MAX) break;
-            if (rho == R) {  // more rows than the instance holds (the caller's max_rows was wrong)
-              rowl = -2;
-              break;
-            }
-#pragma unroll
-            for (int p = 0; p < W; ++p)
-              if (cur[p] == rmin) {
-                const TA v = sAv[g][p][h[p]];
-                SD(g, rho, p) = v;
-                cn[p] += (double)v * (double)v;
-                ++h[p];
-                const int a = h[p] < WA ? sAi[g][p][h[p]] : -1;
-                cur[p] = a >= 0 ? a : INT_MAX;
-              }
-            if (rmin == l) rowl = rho;
-            ++rho;
-          }
-#pragma unroll
-          for (int p = 0; p < W; ++p) {
-            sCn[g][p] = cn[p];
-            sAct[g][p] = (valid && p < wrt && sAi[g][p][0] >= 0) ? pat_act[(int64_t)l * wrt + p] : -1;
-          }
-          sRowL[g] = rowl;
-        }
-        group_sync();
-        const int rowl = sRowL[g];
-        double dv[RPL][W], rhs[RPL];
-#pragma unroll
-        for (int i = 0; i < RPL; ++i) {
-          const int rho = j + L * i;
-#pragma unroll
-          for (int p = 0; p < W; ++p) dv[i][p] = (double)SD(g, rho, p);
-          rhs[i] = rho == rowl ? 1.0 : 0.0;
-        }
-        // reflection p maps column p onto row p (a column already zero below row p: none)
-#pragma unroll
-        for (int p = 0; p < W; ++p) {
-          double s1 = 0.0, xk = 0.0;
-#pragma unroll
-          for (int i = 0; i < RPL; ++i) {
-            const int rho = j + L * i;
-            const double x = dv[i][p];
-            s1 = fma(rho >= p ? x : 0.0, x, s1);
-            xk += rho == p ? x : 0.0;
-          }
-          const double sig = group_sum<L>(s1), xkk = group_sum<L>(xk);
-          const double sq = sqrt(sig);
-          const double alpha = xkk >= 0.0 ? -sq : sq;
-          const double tau = sig > 0.0 ? qr_rcp(sig - alpha * xkk) : 0.0;  // H = I - tau v v^T
-          double v[RPL];
-#pragma unroll
-          for (int i = 0; i < RPL; ++i) {
-            const int rho = j + L * i;
-            v[i] = rho >= p ? dv[i][p] - (rho == p ? alpha : 0.0) : 0.0;
-          }
-          double d[W + 1];  // v . column q (q > p), v . rhs
-#pragma unroll
-          for (int q = p + 1; q <= W; ++q) {
-            double a = 0.0;
-#pragma unroll
-            for (int i = 0; i < RPL; ++i) a = fma(v[i], q < W ? dv[i][q] : rhs[i], a);
-            d[q] = a;
-          }
-#pragma unroll
-          for (int q = p + 1; q <= W; ++q) d[q] = group_sum<L>(d[q]) * tau;
-#pragma unroll
-          for (int i = 0; i < RPL; ++i) {
-#pragma unroll
-            for (int q = p + 1; q < W; ++q) dv[i][q] = fma(-d[q], v[i], dv[i][q]);
-            rhs[i] = fma(-d[W], v[i], rhs[i]);
-          }
-          // row p of R and (Q^T e)_p are final now (later reflections act on rows > p)
-          if (j == p % L) {
-            constexpr int kq0 = 0;
-            (void)kq0;
-            const int base = p * W - p * (p - 1) / 2;
-            sRf[g][base] = sig > 0.0 ? alpha : dv[p / L][p];
-#pragma unroll
-            for (int q = p + 1; q < W; ++q) sRf[g][base + (q - p)] = dv[p / L][q];
-            sC[g][p] = rhs[p / L];
-          }
-        }
-        double tl = 0.0;  // the tail of Q^T e: rows >= W
-#pragma unroll
-        for (int i = 0; i < RPL; ++i) tl = fma(j + L * i >= W ? rhs[i] : 0.0, rhs[i], tl);
-        tl = group_sum<L>(tl);
-        if (j == 0) sC[g][W] = rowl == -2 ? __builtin_nan("") : tl + (rowl < 0 ? 1.0 : 0.0);
+        qr_factor_line<W, WA, L, RPL, NT, TA>(S, g, j, valid, blk0 + (valid ? li : 0), wrt, pat_idx, pat_act, wart,
+                                              a_idx, a_val);
       }
       __syncthreads();  // R, Q^T e of the round's lines
-      // ---- 2. per (line, sample), one lane: QR of the masked columns of R (R_J has the singular
-      // values of A[I, J]: the small problem min ||R_J m - c|| keeps the QR's accuracy), the tail
-      // of Q^T e added to its residual
       {
         const int gl = t % NG;
         const int li = r * NG + gl;
@@ -303,9 +388,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(W <= 5 ? QR_
         double cn[W];
 #pragma unroll
         for (int p = 0; p < W; ++p) {
-          act[p] = sAct[gl][p];
+          act[p] = S.sAct[gl][p];
           wofs[p] = act[p] >= 0 ? (act[p] >> 5) - word_base : 0;
-          cn[p] = sCn[gl][p];
+          cn[p] = S.sCn[gl][p];
         }
 #pragma unroll 1
         for (int s = t / NG; s < nb; s += NT / NG) {
@@ -314,67 +399,14 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(W <= 5 ? QR_
           bool keep[W];
 #pragma unroll
           for (int p = 0; p < W; ++p) keep[p] = act[p] >= 0 && !((rm[wofs[p]] >> (act[p] & 31)) & 1u);
-          double Rm[W][W], c[W];  // Rm[i][q], i <= q (the rest is never read)
+          double Rm[W][W], c[W], m[W];
 #pragma unroll
           for (int i = 0; i < W; ++i) {
 #pragma unroll
-            for (int q = i; q < W; ++q) Rm[i][q] = sRf[gl][i * W - i * (i - 1) / 2 + (q - i)];
-            c[i] = sC[gl][i];
+            for (int q = i; q < W; ++q) Rm[i][q] = S.sRf[gl][i * W - i * (i - 1) / 2 + (q - i)];
+            c[i] = S.sC[gl][i];
           }
-          const double tail = sC[gl][W];
-          int k = 0, krow[W];
-          double rdg[W];
-#pragma unroll
-          for (int p = 0; p < W; ++p) {
-            // column p has rows 0..p; rows < k are earlier pivots: reflect rows k..p onto row k
-            double sig = 0.0, xk = 0.0;
-#pragma unroll
-            for (int i = 0; i <= p; ++i) {
-              sig = fma(i >= k ? Rm[i][p] : 0.0, Rm[i][p], sig);
-              xk = i == k ? Rm[i][p] : xk;
-            }
-            const bool ok = keep[p] && sig > 1e-24 * cn[p];  // |R_kk| > 1e-12 ||D[:, p]||
-            const double sq = sqrt(sig);
-            const double alpha = xk >= 0.0 ? -sq : sq;
-            const double tau = ok ? qr_rcp(sig - alpha * xk) : 0.0;
-            double v[W];
-#pragma unroll
-            for (int i = 0; i <= p; ++i) v[i] = i >= k ? Rm[i][p] - (i == k ? alpha : 0.0) : 0.0;
-#pragma unroll
-            for (int q = p + 1; q <= W; ++q) {
-              double a = 0.0;
-#pragma unroll
-              for (int i = 0; i <= p; ++i) a = fma(v[i], q < W ? Rm[i][q] : c[i], a);
-              a *= tau;
-#pragma unroll
-              for (int i = 0; i <= p; ++i) {
-                if (q < W) Rm[i][q] = fma(-a, v[i], Rm[i][q]);
-                else c[i] = fma(-a, v[i], c[i]);
-              }
-            }
-            krow[p] = k;
-            rdg[p] = ok ? qr_rcp(alpha) : 0.0;
-            k += ok ? 1 : 0;
-          }
-          double rs = tail;  // + (Q^T e) below the pivots within R's rows
-#pragma unroll
-          for (int i = 0; i < W; ++i) rs = fma(i >= k ? c[i] : 0.0, c[i], rs);
-          double m[W];
-#pragma unroll
-          for (int p = W - 1; p >= 0; --p) {
-            const int kr = krow[p];
-            double a = 0.0;
-#pragma unroll
-            for (int i = 0; i <= p; ++i) a = i == kr ? c[i] : a;
-#pragma unroll
-            for (int q = p + 1; q < W; ++q) {
-              double x = 0.0;
-#pragma unroll
-              for (int i = 0; i <= p; ++i) x = i == kr ? Rm[i][q] : x;
-              a = fma(-x, m[q], a);
-            }
-            m[p] = a * rdg[p];  // 0 for a dropped slot
-          }
+          const double rs = qr_masked_solve<W>(Rm, c, S.sC[gl][W], cn, keep, m);
           if (valid) {
             if (m_out != nullptr) {
               TM* dst = m_out + ((int64_t)b * nloc + (l - line_begin)) * wrt;
@@ -398,7 +430,144 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(W <= 5 ? QR_
     __syncthreads();
   }
 }
-#undef SD
+
+// ---- the R cache: phase 1 once per env (A and the pattern are constant for an env's lifetime,
+// preconditioner.py:23-25), phase 2 per rollout from the cache.
+// Layout (blocks of 64 lines, structure of arrays as the Gram cache): rcache[l / 64][q][l % 64],
+// q < T: R packed upper triangle (row-major, p <= q); T + p: (Q^T e_l)_p; T + W: the tail.
+__host__ __device__ constexpr int qr_cache_q(int W) { return W * (W + 1) / 2 + W + 1; }
+
+template <int W, int WA, int L, int RPL, int NT, typename TA>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2))) void k_qr_factor(int32_t n, int32_t wrt,
+                                                  const int32_t* __restrict__ pat_idx,
+                                                  const int32_t* __restrict__ pat_act, int32_t wart,
+                                                  const int32_t* __restrict__ a_idx, const TA* __restrict__ a_val,
+                                                  double* __restrict__ rcache) {
+  using St = QrStage<W, WA, L, RPL, NT, TA>;
+  constexpr int NG = St::NG, NR = kQLines / NG, T = St::T, NQ = qr_cache_q(W);
+  __shared__ St S;
+  const int t = threadIdx.x, g = t / L, j = t % L;
+  const int blk0 = blockIdx.x * kQLines;
+  const int nvl = min(kQLines, n - blk0);
+#pragma unroll 1
+  for (int r = 0; r < NR; ++r) {
+    const int li = r * NG + g;
+    const bool valid = li < nvl;
+    qr_factor_line<W, WA, L, RPL, NT, TA>(S, g, j, valid, blk0 + (valid ? li : 0), wrt, pat_idx, pat_act, wart,
+                                          a_idx, a_val);
+    __syncthreads();
+    for (int e = t; e < NG * NQ; e += NT) {  // consecutive threads: consecutive lines of one entry
+      const int gl = e % NG, q = e / NG, li2 = r * NG + gl;
+      if (li2 >= nvl) continue;
+      const int l = blk0 + li2;
+      const double v = q < T ? S.sRf[gl][q] : S.sC[gl][q - T];
+      rcache[(int64_t)(l >> 6) * NQ * 64 + q * 64 + (l & 63)] = v;
+    }
+    __syncthreads();
+  }
+}
+
+// Phase 2 from the R cache, one thread per line (the k_gram_fill stream): per line the W action
+// ids and the NQ cached values once, the column norms ||D[:, p]||^2 = sum_i R_ip^2 recomputed
+// (they only set the rank floor), then per sample W mask bits, the masked re-triangularisation and
+// back-substitution (qr_masked_solve), M staged through LDS and written with 16-byte `nt` buffer
+// stores, the line residuals summed per sample in a fixed order (the k_gram_fill partial layout:
+// 256-line blocks, so 256-line-aligned shards sum to one launch's bits).
+#ifndef QRS_WPE
+#define QRS_WPE 3
+#endif
+template <int W, typename TM>
+__global__ __launch_bounds__(kQNT) __attribute__((amdgpu_waves_per_eu(W <= 5 ? QRS_WPE : 2))) void k_qr_solve(
+    int32_t line_begin, int32_t line_end, int32_t wrt, const int32_t* __restrict__ pat_act,
+    const double* __restrict__ rcache, int32_t B, const uint32_t* __restrict__ removed, int32_t words,
+    int32_t word_base, TM* __restrict__ m_out, double* __restrict__ partials) {
+  constexpr int T = W * (W + 1) / 2, NQ = qr_cache_q(W);
+  static_assert(kQNT == kQLines, "one thread per line of a 256-line block");
+  __shared__ double s_r2[kQChunk][kQNT];
+  __shared__ __attribute__((aligned(16))) TM s_m[2][kQNT * W];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int lb = blockIdx.x;
+  const int j = line_begin + lb * kQNT + t;
+  const bool valid = j < line_end;
+  const int64_t nloc = line_end - line_begin;
+  const int jj = valid ? j : line_begin;  // clamped: loads stay in bounds
+  const int nvl = min(kQNT, line_end - (line_begin + lb * kQNT));
+
+  int act[W];
+  {
+    int av[W];  // every load issued before any is used
+#pragma unroll
+    for (int p = 0; p < W; ++p) av[p] = pat_act[(int64_t)jj * wrt + min(p, wrt - 1)];
+#pragma unroll
+    for (int p = 0; p < W; ++p) act[p] = (valid && p < wrt) ? av[p] : -1;
+  }
+  double R0[T], c0[W], tail, cn[W];
+  const double* rp = rcache + (int64_t)(jj >> 6) * NQ * 64 + (jj & 63);
+#pragma unroll
+  for (int q = 0; q < T; ++q) R0[q] = rp[q * 64];
+#pragma unroll
+  for (int p = 0; p < W; ++p) c0[p] = rp[(T + p) * 64];
+  tail = rp[(T + W) * 64];
+#pragma unroll
+  for (int p = 0; p < W; ++p) {
+    double s = 0.0;
+#pragma unroll
+    for (int i = 0; i <= p; ++i) {
+      const double x = R0[i * W - i * (i - 1) / 2 + (p - i)];
+      s = fma(x, x, s);
+    }
+    cn[p] = s;
+  }
+  int wofs[W];
+#pragma unroll
+  for (int p = 0; p < W; ++p) wofs[p] = act[p] >= 0 ? (act[p] >> 5) - word_base : 0;
+  uint32_t wd[W];  // the slots' bitmap words of the next sample are loaded while the current one is solved
+#pragma unroll
+  for (int p = 0; p < W; ++p) wd[p] = removed[wofs[p]];
+#pragma unroll 1
+  for (int b = 0; b < B; ++b) {
+    bool keep[W];
+#pragma unroll
+    for (int p = 0; p < W; ++p) keep[p] = act[p] >= 0 && !((wd[p] >> (act[p] & 31)) & 1u);
+    if (b + 1 < B) {
+      const uint32_t* rn = removed + (int64_t)(b + 1) * words;
+#pragma unroll
+      for (int p = 0; p < W; ++p) wd[p] = rn[wofs[p]];
+    }
+    double Rm[W][W], c[W], m[W];
+#pragma unroll
+    for (int i = 0; i < W; ++i) {
+#pragma unroll
+      for (int q = i; q < W; ++q) Rm[i][q] = R0[i * W - i * (i - 1) / 2 + (q - i)];
+      c[i] = c0[i];
+    }
+    const double rs = qr_masked_solve<W>(Rm, c, tail, cn, keep, m);
+    s_r2[b % kQChunk][t] = valid ? rs : 0.0;
+    {  // M (no branch on m_out: store_m_block drops every store when it is null)
+      TM* sm = s_m[b & 1];
+      if (valid) {
+#pragma unroll
+        for (int p = 0; p < W; ++p)
+          if (p < wrt) sm[t * wrt + p] = (TM)m[p];
+      }
+      __syncthreads();
+      store_m_block<kQNT, W, TM>(m_out ? m_out + ((int64_t)b * nloc + (int64_t)lb * kQNT) * wrt : nullptr, sm,
+                                 nvl * wrt);
+    }
+    if (b % kQChunk == kQChunk - 1 || b == B - 1) {  // the chunk's fixed-order block sums
+      const int c0b = b - b % kQChunk, nb = b - c0b + 1;
+      __syncthreads();
+      for (int u = wave; u < nb; u += kQNT / 64) {
+        double acc = 0.0;
+#pragma unroll
+        for (int q = 0; q < kQNT / 64; ++q) acc += s_r2[u][q * 64 + lane];
+        acc = wave_sum(acc);
+        if (lane == 0) partials[(int64_t)(c0b + u) * gridDim.x + lb] = acc;
+      }
+      __syncthreads();
+    }
+  }
+}
 
 // (W class, A width class, rows) -> instance
 template <int W, int WA, int L, int RPL, int NT, typename TM>
@@ -433,6 +602,48 @@ hipError_t dispatch_qr(int wc, int rows, bool a32, int32_t n, int32_t lb, int32_
   if (rows <= 64) return launch_qr<13, 7, 16, 4, 128, TM>(SPAI_QR_ARGS);
   return launch_qr<13, 7, 32, 3, 128, TM>(SPAI_QR_ARGS);
 #undef SPAI_QR_ARGS
+}
+
+// the R cache build: the same (W class, rows) -> instance choice as the fused fill
+template <int W, int WA, int L, int RPL, int NT>
+hipError_t launch_factor(bool a32, int32_t n, int32_t wrt, const int32_t* pi, const int32_t* pa, int32_t wart,
+                         const int32_t* ai, const void* av, double* rc, hipStream_t s) {
+  const int grid = (n + kQLines - 1) / kQLines;
+  if (a32)
+    k_qr_factor<W, WA, L, RPL, NT, float><<<grid, NT, 0, s>>>(n, wrt, pi, pa, wart, ai, static_cast<const float*>(av),
+                                                             rc);
+  else
+    k_qr_factor<W, WA, L, RPL, NT, double><<<grid, NT, 0, s>>>(n, wrt, pi, pa, wart, ai,
+                                                              static_cast<const double*>(av), rc);
+  return hipGetLastError();
+}
+hipError_t dispatch_factor(int wc, int rows, bool a32, int32_t n, int32_t wrt, const int32_t* pi, const int32_t* pa,
+                           int32_t wart, const int32_t* ai, const void* av, double* rc, hipStream_t s) {
+#define SPAI_QF_ARGS a32, n, wrt, pi, pa, wart, ai, av, rc, s
+  if (wc == 5) {
+    if (rows <= 16) return launch_factor<5, 5, 4, 4, 256>(SPAI_QF_ARGS);
+    return launch_factor<5, 5, 8, 4, 256>(SPAI_QF_ARGS);
+  }
+  if (wc == 7) {
+    if (rows <= 32) return launch_factor<7, 7, 8, 4, 256>(SPAI_QF_ARGS);
+    return launch_factor<7, 7, 16, 4, 128>(SPAI_QF_ARGS);
+  }
+  if (rows <= 64) return launch_factor<13, 7, 16, 4, 128>(SPAI_QF_ARGS);
+  return launch_factor<13, 7, 32, 3, 128>(SPAI_QF_ARGS);
+#undef SPAI_QF_ARGS
+}
+
+template <int W>
+hipError_t launch_solve(bool f64, int32_t lb, int32_t le, int32_t wrt, const int32_t* pa, const double* rc, int32_t B,
+                        const uint32_t* rm, int32_t words, int32_t wb, void* mo, double* partials, int32_t nparts,
+                        hipStream_t s) {
+  if (f64)
+    k_qr_solve<W, double><<<nparts, kQNT, 0, s>>>(lb, le, wrt, pa, rc, B, rm, words, wb, static_cast<double*>(mo),
+                                                  partials);
+  else
+    k_qr_solve<W, float><<<nparts, kQNT, 0, s>>>(lb, le, wrt, pa, rc, B, rm, words, wb, static_cast<float*>(mo),
+                                                 partials);
+  return hipGetLastError();
 }
 
 // width class of a (pattern, A) pair: 5 (W <= 5, WA <= 5), 7 (W <= 7, WA <= 7), 13 (W <= 13, WA <= 7)
@@ -501,6 +712,66 @@ extern "C" int spai_fill_lines_qr(int32_t n, int32_t line_begin, int32_t line_en
                                 removed, words, word_base, m_out, partials, nparts, s)
           : dispatch_qr<float>(wc, max_rows, a32, n, line_begin, line_end, W, pat_idx, pat_act, WA, a_idx, a_val, B,
                                removed, words, word_base, m_out, partials, nparts, s);
+  SPAI_CHECK_HIP(e);
+  return SPAI_OK;
+}
+
+// ---- the R cache (phase 1 once per env) and the per-rollout solve from it
+static int qr_cache_class(int32_t W, int32_t WA) { return qr_class(W, WA); }
+
+extern "C" size_t spai_qr_cache_bytes(int32_t n, int32_t W, int32_t WA) {
+  const int wc = qr_cache_class(W, WA);
+  if (n <= 0 || wc == 0) return 0;
+  return sizeof(double) * (size_t)qr_cache_q(wc) * (size_t)((n + 63) / 64 * 64);
+}
+
+extern "C" int spai_qr_factor(int32_t n, int32_t W, const int32_t* pat_idx, const int32_t* pat_act, int32_t WA,
+                              const int32_t* a_idx, const void* a_val, int32_t a_dtype, int32_t max_rows,
+                              double* rcache, size_t rcache_bytes, void* stream) {
+  SPAI_CHECK_ARG(n >= 1 && W >= 1 && WA >= 1 && max_rows >= 0 && pat_idx && pat_act && a_idx && a_val && rcache,
+                 "spai_qr_factor: bad arguments");
+  SPAI_CHECK_ARG(a_dtype == SPAI_DTYPE_F32 || a_dtype == SPAI_DTYPE_F64, "spai_qr_factor: bad a_dtype");
+  const int wc = qr_cache_class(W, WA);
+  if (wc == 0 || max_rows > qr_rows_cap(wc)) {
+    set_error("spai_qr_factor: widths W=%d WA=%d / %d rows above the compiled 13 / 7 / %d", W, WA, max_rows,
+              wc ? qr_rows_cap(wc) : 0);
+    return SPAI_ERR_UNSUPPORTED;
+  }
+  SPAI_CHECK_ARG(rcache_bytes >= spai_qr_cache_bytes(n, W, WA), "spai_qr_factor: rcache too small");
+  SPAI_CHECK_HIP(dispatch_factor(wc, max_rows, a_dtype == SPAI_DTYPE_F32, n, W, pat_idx, pat_act, WA, a_idx, a_val,
+                                 rcache, (hipStream_t)stream));
+  return SPAI_OK;
+}
+
+extern "C" int spai_fill_lines_qr_cached(int32_t n, int32_t line_begin, int32_t line_end, int32_t W, int32_t WA,
+                                         const int32_t* pat_act, const double* rcache, int32_t B,
+                                         const uint32_t* removed, int32_t words, int32_t word_base, void* m_out,
+                                         int32_t m_dtype, void* workspace, size_t workspace_bytes, void* stream) {
+  SPAI_CHECK_ARG(m_dtype == SPAI_DTYPE_F32 || m_dtype == SPAI_DTYPE_F64, "spai_fill_lines_qr_cached: bad m_dtype");
+  SPAI_CHECK_ARG(n >= 1 && line_begin >= 0 && line_end >= line_begin && line_end <= n && W >= 1 && WA >= 1 &&
+                     B >= 1 && words >= 1 && word_base >= 0,
+                 "spai_fill_lines_qr_cached: bad shape");
+  SPAI_CHECK_ARG(workspace != nullptr, "spai_fill_lines_qr_cached: null workspace");
+  const int32_t nl = line_end - line_begin;
+  if (nl == 0) return SPAI_OK;
+  SPAI_CHECK_ARG(pat_act && rcache && removed, "spai_fill_lines_qr_cached: null input");
+  const int wc = qr_cache_class(W, WA);
+  if (wc != 5 && wc != 7) {
+    set_error("spai_fill_lines_qr_cached: width class %d (W=%d WA=%d): the cached solve is compiled for 5 and 7", wc,
+              W, WA);
+    return SPAI_ERR_UNSUPPORTED;
+  }
+  const int32_t nparts = (nl + kQNT - 1) / kQNT;
+  SPAI_CHECK_ARG(workspace_bytes >= sizeof(double) * (size_t)nparts * B,
+                 "spai_fill_lines_qr_cached: workspace too small");
+  double* partials = static_cast<double*>(workspace);
+  hipStream_t s = (hipStream_t)stream;
+  const bool f64 = m_dtype == SPAI_DTYPE_F64;
+  const hipError_t e =
+      wc == 5 ? launch_solve<5>(f64, line_begin, line_end, W, pat_act, rcache, B, removed, words, word_base, m_out,
+                                partials, nparts, s)
+              : launch_solve<7>(f64, line_begin, line_end, W, pat_act, rcache, B, removed, words, word_base, m_out,
+                                partials, nparts, s);
   SPAI_CHECK_HIP(e);
   return SPAI_OK;
 }

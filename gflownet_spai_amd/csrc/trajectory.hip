@@ -72,11 +72,10 @@ constexpr int kSortNT = 1024;
 constexpr int kMaxTiles = 2048;            // E <= kMaxTiles * kTile actions
 constexpr int kFinNT = 256;
 constexpr int kMaxSamples = 1024;          // B per rollout call
-constexpr int kBufWord3 = 0x00020000;      // buffer resource dword 3 (raw byte addressing, gfx9 family)
 typedef unsigned int spai_u2 __attribute__((ext_vector_type(2)));
 typedef unsigned int spai_u3 __attribute__((ext_vector_type(3)));
 typedef unsigned int spai_u4 __attribute__((ext_vector_type(4)));
-constexpr int kNtAux = 2;                 // buffer-store cache policy: nt (streaming output, gfx950)
+// (kBufWord3, kNtAux: spai_device.h)
 constexpr int kBins = 4096;                // splitter histogram / bucket lookup table bins
 
 struct TrajWs {

@@ -5,9 +5,10 @@ Three ways to spread the work; ``GFlowNet(shard=(rank, world, gr
   * columns (bench.py's default for --gpus > 1; the north star's "columns of M shard across the
     GPUs, one all-gather assembles M"): rank r rolls out ITS candidates (global sample ids
     r*Bl .. r*Bl + Bl - 1: the same Philox draws as a one-GPU batch of P*Bl), then
-      1. one all_to_all of the removal bitmaps: rank q receives, for every candidate, only the
-         bitmap words its lines' action ids span, plus the candidate's removal count
-         (``bitmap_pack_index`` / ``exchange_bitmaps``);
+      1. one all_to_all of the removal bits: rank q receives, for every candidate, exactly the
+         bits of its lines' action ids packed in line-major order, plus the candidate's removal
+         count, whatever the matrix numbering (``PackPlan`` / spai_bitmap_pack /
+         ``exchange_packed``);
       2. every rank fills lines ``shard_lines(n, r, P, align=256)`` of ALL P*Bl candidates;
       3. one all_reduce of the exact (integer-limb) squared-residual sums [P*Bl] — bit-identical
          to one GPU whatever P, because the shards are 256-line aligned and integer sums are
@@ -158,9 +159,11 @@ class LineGather:
 # ---------------------------------------------------------------- columns split: bitmap exchange
 def word_spans(env, world: int) -> list:
     """[(w0, w1)] per rank: the bitmap words the action ids of rank q's lines span (one host
-    sync, once per model).  For stencil matrices in row-major raw order a column shard's action
-    ids are one contiguous range (its rows +- the stencil's reach), so a rank needs ~1/P of every
-    bitmap; a randomly numbered matrix degrades to whole bitmaps (an all_gather's volume)."""
+    sync).  For stencil matrices in row-major raw order a column shard's action ids are one
+    contiguous range (its rows +- the stencil's reach), so a rank needs ~1/P of every bitmap; a
+    randomly numbered matrix degrades to whole bitmaps (an all_gather's volume) — the product
+    path exchanges line-major packed bits instead (``PackPlan``); the windows remain as a
+    diagnostic of a numbering's locality."""
     act = env.pattern.act
     spans = []
     for q in range(world):
@@ -173,6 +176,90 @@ def word_spans(env, world: int) -> list:
         lo, hi = int(a.min()) >> 5, (int(a.max()) >> 5) + 1
         spans.append((lo, hi))
     return spans
+
+
+class PackPlan:
+    """The columns split's bitmap exchange plan for ``world`` ranks (built once per env and world,
+    one host sync): per rank q the LINE-MAJOR action ids of its 256-line shard (``ids`` =
+    all shards one after the other, ``seg`` [P+1] their bounds) and the packed word count
+    ``wq[q]`` = ceil(nnz(shard q) / 32).  The send buffer of a rank with ``bl`` candidates is, per
+    destination q, [bl][wq[q] + 1] words (q's bits packed in that order, then the removal count:
+    spai_hip.h spai_bitmap_pack); rank r receives [P * bl, wq[r] + 1] and its fill reads the bits
+    through ``local_pattern(env, r)``: the pattern with each of r's action ids replaced by its
+    position in r's segment.  Every rank receives exactly nnz(shard) bits per candidate for any
+    numbering of the matrix (action ids are raw COO positions, preconditioner.py:23-25)."""
+
+    def __init__(self, env, world: int):
+        act = env.pattern.act
+        dev = act.device
+        self.world = world
+        ids, seg, self.wq, self.lines = [], [0], [], []
+        for q in range(world):
+            b, e = shard_lines(env.matrix_size, q, world, LINE_ALIGN)
+            a = act[b:e].reshape(-1)
+            a = a[a >= 0]
+            ids.append(a)
+            seg.append(seg[-1] + a.numel())
+            self.wq.append((a.numel() + 31) // 32)
+            self.lines.append((b, e))
+        self.ids = torch.cat(ids).to(torch.int32).contiguous()
+        self.seg = torch.tensor(seg, dtype=torch.int64, device=dev)
+        self.max_seg = max(seg[q + 1] - seg[q] for q in range(world))
+        self._off = {}
+        self._local = {}
+
+    def out_off(self, bl: int) -> torch.Tensor:
+        """[P] int64 word offsets of the destinations' blocks in a send buffer of bl candidates."""
+        if bl not in self._off:
+            o = [0]
+            for w in self.wq[:-1]:
+                o.append(o[-1] + bl * (w + 1))
+            self._off[bl] = (torch.tensor(o, dtype=torch.int64, device=self.seg.device), o[-1] + bl * (self.wq[-1] + 1))
+        return self._off[bl]
+
+    def send_words(self, bl: int) -> int:
+        return self.out_off(bl)[1]
+
+    def local_pattern(self, env, rank: int):
+        """env.pattern with rank's action ids renumbered 0 .. nnz(shard) - 1 in line-major order
+        (the bit positions of its received packed rows); other lines are left as they are."""
+        if rank not in self._local:
+            import dataclasses
+            b, e = self.lines[rank]
+            act = env.pattern.act.clone()
+            blk = act[b:e]
+            ok = blk >= 0
+            loc = torch.cumsum(ok.reshape(-1).to(torch.int64), 0).view_as(blk) - 1
+            act[b:e] = torch.where(ok, loc.to(torch.int32), blk)
+            self._local[rank] = dataclasses.replace(env.pattern, act=act)
+        return self._local[rank]
+
+
+def pack_bits_reference(removed: torch.Tensor, counts: torch.Tensor, plan: "PackPlan", bl: int) -> torch.Tensor:
+    """torch restatement of spai_bitmap_pack (test infrastructure: the CPU gloo tests build the
+    send buffer with it; the GPU tests check the kernel against it)."""
+    out = []
+    seg = plan.seg.tolist()
+    for q in range(plan.world):
+        a = plan.ids[seg[q]:seg[q + 1]].long().to(removed.device)
+        words = plan.wq[q]
+        bits = ((removed.view(torch.int32)[:, a >> 5].long() >> (a & 31)) & 1).to(torch.int64)  # [bl, m]
+        pad = torch.zeros(bl, words * 32, dtype=torch.int64, device=removed.device)
+        pad[:, :a.numel()] = bits
+        w = (pad.view(bl, words, 32) << torch.arange(32, device=removed.device)).sum(2)
+        w = torch.where(w >= 2 ** 31, w - 2 ** 32, w).to(torch.int32)
+        out.append(torch.cat([w, counts.view(bl, 1).to(torch.int32)], 1).reshape(-1))
+    return torch.cat(out)
+
+
+def exchange_packed(send: torch.Tensor, recv: torch.Tensor, plan: "PackPlan", bl: int, rank: int, group=None,
+                    async_op: bool = False):
+    """The columns split's all_to_all of packed rows: ``send`` [plan.send_words(bl)] int32 ->
+    ``recv`` [P * bl, wq[rank] + 1] int32 (every candidate's packed bits of this rank's shard, then
+    its removal count; global sample order: rank q's candidates are rows q*bl ..)."""
+    in_splits = [bl * (w + 1) for w in plan.wq]
+    out_splits = [bl * (plan.wq[rank] + 1)] * plan.world
+    return all_to_all_(recv.view(-1), send, out_splits, in_splits, group, async_op)
 
 
 def bitmap_pack_index(spans: list, bl: int, words: int, device) -> torch.Tensor:

@@ -27,7 +27,7 @@ from .preconditioner import Data
 
 class GFlowNet(nn.Module):
     def __init__(self, forward_policy, backward_policy, env, *, mode: str = "parity", seed: int | None = None,
-                 sample_base: int = 0, shard: tuple | None = None, split: str | None = None):
+                 sample_base: int = 0, shard: tuple | None = None, split: str | None = None, overlap: bool = True):
         super().__init__()
         if mode not in ("parity", "throughput"):
             raise ValueError("mode must be 'parity' or 'throughput'")
@@ -45,6 +45,10 @@ class GFlowNet(nn.Module):
         self._ctr = None     # the stream id on the device (advanced by the select phase itself)
         self._data_cache = {}
         self._bufs = {}      # persistent exchange buffers of the columns split (graph-replay safe)
+        # one GPU, throughput mode: run the fill + rewards on a second stream beside the trajectory
+        # sort (the two chains share only the select phase's outputs)
+        self.overlap = overlap
+        self._side = None
         # (rank, world, group): the multi-GPU split of DESIGN.md §6 (throughput mode)
         #   split="columns": rank r rolls out its own len(s0) candidates (global sample ids
         #     sample_base + r*len(s0) ..), one all_to_all ships each rank the bitmap words of its
@@ -54,7 +58,9 @@ class GFlowNet(nn.Module):
         #     trajectory; one all_reduce of the bucket sums + residual partials.
         #   The two splits read s0 differently (this rank's candidates vs the whole batch), so a
         #   sharded GFlowNet must name its split: an old slices-era call site fails loudly.
-        self.shard = shard if shard is not None and shard[1] > 1 else None
+        # a one-rank shard is dropped (the one-GPU step) unless a split is named explicitly: then
+        # the split's phases run with their collectives on a one-rank group (bench.py --dist)
+        self.shard = shard if shard is not None and (shard[1] > 1 or split is not None) else None
         if self.shard is not None and split is None:
             raise ValueError("a sharded GFlowNet needs split='columns' (s0 = this rank's own candidates) or "
                              "split='slices' (s0 = the whole batch on every rank); INTEGRATION.md §4")
@@ -238,6 +244,11 @@ class GFlowNet(nn.Module):
             return [(self._begin, False), (self.rollout_exchange, True), (self._end, False)]
         return [(self._begin, False), (self.rollout_exchange, False), (self._end, False)]
 
+    def _side_stream(self, dev):
+        if self._side is None or self._side.device != dev:
+            self._side = torch.cuda.Stream(dev)
+        return self._side
+
     def _counter(self, dev):
         if self._ctr is None or self._ctr.device != dev:
             self._ctr = torch.tensor([self._rollouts0], dtype=torch.int64, device=dev)
@@ -266,7 +277,18 @@ class GFlowNet(nn.Module):
         st.update(B=B, E=E, logits=logits, alpha=alpha, lg=lg, lmax=lmax, removed=removed, counts=counts, ws=ws,
                   part=(rank, world, group))
         if world == 1:  # all lines here: fill, exact sums and rewards (one launch after the fill)
-            st["rewards"] = env.fill_rewards(removed, counts, alpha)
+            if self.overlap:
+                # the fill needs only the removal bitmaps and the sort only the staged records: the
+                # fill + rewards run on a second stream beside rollout_sort / rollout_finish (under
+                # HIP-graph capture: two parallel branches), joined in _end
+                main = torch.cuda.current_stream(lg.device)
+                side = self._side_stream(lg.device)
+                side.wait_stream(main)
+                with torch.cuda.stream(side):
+                    st["rewards"] = env.fill_rewards(removed, counts, alpha)
+                st["join"] = side
+            else:
+                st["rewards"] = env.fill_rewards(removed, counts, alpha)
         else:  # a split sums exact limbs of its lines
             st["res2_part"] = env.fill_partial(removed, *self.lines, limbs=True)
 
@@ -294,6 +316,8 @@ class GFlowNet(nn.Module):
             kernels.rollout_merge(lg, B, lmax, ws, rank, world, counts)
         actions, fwd = kernels.rollout_sort(lg, B, lmax, ws, rank, world)
         t_dev = kernels.rollout_finish(lg, B, lmax, counts, ws, actions, fwd, rank, world)
+        if "join" in st:  # the fill's stream (rollout_begin) rejoins before anything reads its outputs
+            torch.cuda.current_stream(lg.device).wait_stream(st.pop("join"))
         rewards = st["rewards"] if world == 1 else env.rewards_from_res2(st["res2"], counts, st["alpha"])
         log = Log(st["s0"], self.backward_policy, self.total_flow, env)
         log._set_rollout(st["logits"], actions, fwd, t_dev, lmax=lmax)
@@ -316,23 +340,17 @@ class GFlowNet(nn.Module):
         sel = self._buf("select", (bl * words + bl,), torch.int32, dev)
         removed, counts, ws = kernels.rollout_select(lg, bl, lmax, self.seed, 0, self.sample_base + rank * bl,
                                                      self._counter(dev), out=sel)
-        spans = env.word_spans(world)
-        key = ("pack", bl, words)
-        idx = self._bufs.get(key)
-        if idx is None:
-            from .distributed import bitmap_pack_index
-            idx = self._bufs[key] = bitmap_pack_index(spans, bl, words, dev)
-        send = self._buf("send", (idx.numel(),), torch.int32, dev)
-        torch.index_select(sel, 0, idx, out=send)
-        w0, w1 = spans[rank]
-        recv = self._buf("recv", (world * bl, w1 - w0 + 1), torch.int32, dev)
+        plan = env.pack_plan(world)
+        send = self._buf("send", (plan.send_words(bl),), torch.int32, dev)
+        kernels.bitmap_pack(removed, counts, plan, out=send)  # line-major packed bits per destination
+        recv = self._buf("recv", (world * bl, plan.wq[rank] + 1), torch.int32, dev)
         st.update(B=bl, E=E, logits=logits, alpha=alpha, lg=lg, lmax=lmax, removed=removed, counts=counts, ws=ws,
-                  send=send, recv=recv, spans=spans, part=(rank, world, group))
+                  send=send, recv=recv, plan=plan, part=(rank, world, group))
 
     def _c_send(self, st: dict) -> None:
-        from .distributed import exchange_bitmaps
+        from .distributed import exchange_packed
         rank, _, group = st["part"]
-        st["a2a"] = exchange_bitmaps(st["send"], st["recv"], st["spans"], st["B"], rank, group, async_op=True)
+        st["a2a"] = exchange_packed(st["send"], st["recv"], st["plan"], st["B"], rank, group, async_op=True)
 
     def _c_order(self, st: dict) -> None:
         # this rank's own trajectories, while the bitmaps are in flight
@@ -345,10 +363,9 @@ class GFlowNet(nn.Module):
 
     def _c_fill(self, st: dict) -> None:
         rank = st["part"][0]
-        w0, w1 = st["spans"][rank]
-        recv = st["recv"]
-        st["limbs"] = self.env.fill_partial(recv, *self.lines, word_base=w0, limbs=True)
-        st["counts_all"] = recv[:, w1 - w0].contiguous()
+        plan, recv = st["plan"], st["recv"]
+        st["limbs"] = self.env.fill_partial(recv, *self.lines, limbs=True, pattern=plan.local_pattern(self.env, rank))
+        st["counts_all"] = recv[:, plan.wq[rank]].contiguous()
 
     def _c_reduce(self, st: dict) -> None:
         from .distributed import all_reduce_

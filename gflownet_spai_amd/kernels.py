@@ -362,9 +362,34 @@ def qr_max_rows(pattern: Lines, a_lines: Lines) -> int:
     return int(out.item())
 
 
+def qr_cache(pattern: Lines, a_lines: Lines, max_rows: int):
+    """The R cache of the QR fill (spai_qr_factor): per line the Householder R of its full block
+    A[I, slots], Q^T e_l and the tail, fp64, built once per env.  None for width classes the
+    cached solve is not compiled for (13-wide lines: the fused spai_fill_lines_qr runs instead)."""
+    _lib.require_device(pattern.idx)
+    lib = _l()
+    nb = lib.spai_qr_cache_bytes(pattern.n, pattern.width, a_lines.width)
+    if nb == 0 or not (pattern.width <= 7 and a_lines.width <= 7):
+        return None
+    rc = torch.zeros(nb // 8, dtype=torch.float64, device=pattern.idx.device)
+    av = narrow_values(a_lines)
+    _lib.check(lib.spai_qr_factor(pattern.n, pattern.width, _lib.ptr(pattern.idx), _lib.ptr(pattern.act),
+                                  a_lines.width, _lib.ptr(a_lines.idx), _lib.ptr(av), _DT[av.dtype], max_rows,
+                                  _lib.ptr(rc), nb, _lib.stream_ptr(pattern.idx.device)), "spai_qr_factor")
+    return rc
+
+
 def _fill_lines_qr(pattern: Lines, a_lines: Lines, max_rows: int, removed: torch.Tensor, line_begin: int,
-                   line_end: int, m, m_dtype, word_base: int, ws):
+                   line_end: int, m, m_dtype, word_base: int, ws, rcache: torch.Tensor | None = None):
     B, words = removed.shape
+    if rcache is not None:  # phase 2 only, from the env's R cache
+        with _timed("fill_residual"):  # the fill kernel alone
+            st = _l().spai_fill_lines_qr_cached(pattern.n, line_begin, line_end, pattern.width, a_lines.width,
+                                                _lib.ptr(pattern.act), _lib.ptr(rcache), B, _lib.ptr(removed), words,
+                                                word_base, _lib.ptr(m), _DT[m_dtype], _lib.ptr(ws), ws.numel(),
+                                                _lib.stream_ptr(removed.device))
+        _lib.check(st, "spai_fill_lines_qr_cached")
+        return
     av = narrow_values(a_lines)  # fp32-exact A values are staged as fp32 (the same numbers)
     with _timed("fill_residual"):  # the fill kernel alone
         st = _l().spai_fill_lines_qr(pattern.n, line_begin, line_end, pattern.width, _lib.ptr(pattern.idx),
@@ -376,9 +401,10 @@ def _fill_lines_qr(pattern: Lines, a_lines: Lines, max_rows: int, removed: torch
 
 def fill_residual_qr(pattern: Lines, a_lines: Lines, max_rows: int, removed: torch.Tensor, line_begin: int = 0,
                      line_end: int | None = None, store_m: bool = False, m_dtype=torch.float64, word_base: int = 0,
-                     limbs: bool = False):
-    """The least-squares fill by Householder QR (spai_fill_lines_qr + spai_fill_reduce): same outputs
-    as fill_residual with lsq=True (res2 [B] or exact limbs, M or None)."""
+                     limbs: bool = False, rcache: torch.Tensor | None = None):
+    """The least-squares fill by Householder QR (spai_fill_lines_qr, or spai_fill_lines_qr_cached from
+    an R cache, + spai_fill_reduce): same outputs as fill_residual with lsq=True (res2 [B] or exact
+    limbs, M or None)."""
     _lib.require_device(removed)
     if line_end is None:
         line_end = pattern.n
@@ -388,10 +414,31 @@ def fill_residual_qr(pattern: Lines, a_lines: Lines, max_rows: int, removed: tor
     res2, lb = _fill_out(B, removed.device, limbs)
     m = torch.empty(B, n_loc, pattern.width, dtype=m_dtype, device=removed.device) if store_m else None
     ws = _lib.workspace(_l().spai_fill_workspace_bytes(max(n_loc, 1), B), removed.device, "fill")
-    _fill_lines_qr(pattern, a_lines, max_rows, removed, line_begin, line_end, m, m_dtype, word_base, ws)
+    _fill_lines_qr(pattern, a_lines, max_rows, removed, line_begin, line_end, m, m_dtype, word_base, ws, rcache)
     _lib.check(_l().spai_fill_reduce(n_loc, B, _lib.ptr(ws), _lib.ptr(res2), _lib.ptr(lb),
                                      _lib.stream_ptr(removed.device)), "spai_fill_reduce")
     return (lb if limbs else res2), m
+
+
+def bitmap_pack(removed: torch.Tensor, counts: torch.Tensor, plan, out: torch.Tensor | None = None) -> torch.Tensor:
+    """The columns split's all_to_all send buffer (spai_bitmap_pack): per destination q of
+    ``plan`` (distributed.PackPlan) and candidate b, b's removal bits of q's line-major action ids
+    packed 32 per word, then counts[b]; int32 [plan.send_words(bl)]."""
+    _lib.require_device(removed)
+    bl, words = removed.shape
+    off, total = plan.out_off(bl)
+    if out is None:
+        out = torch.empty(total, dtype=torch.int32, device=removed.device)
+    if out.numel() != total or out.dtype != torch.int32 or not out.is_contiguous():
+        raise ValueError(f"out must be a contiguous int32 buffer of {total} words")
+    if removed.stride(1) != 1 or counts.dtype != torch.int32:
+        raise ValueError("removed rows must be contiguous and counts int32")
+    with _timed("bitmap_pack"):
+        st = _l().spai_bitmap_pack(plan.world, bl, _lib.ptr(removed), removed.stride(0), _lib.ptr(counts),
+                                   _lib.ptr(plan.ids), _lib.ptr(plan.seg), _lib.ptr(off), plan.max_seg,
+                                   _lib.ptr(out), _lib.stream_ptr(removed.device))
+    _lib.check(st, "spai_bitmap_pack")
+    return out
 
 
 def res2_from_limbs(limbs: torch.Tensor) -> torch.Tensor:
@@ -462,15 +509,15 @@ def _reduce_rewards(ws, n, B, counts, nnz0, r0, f0, alpha, device):
 
 def fill_rewards_qr(pattern: Lines, a_lines: Lines, max_rows: int, removed: torch.Tensor, counts: torch.Tensor,
                     nnz0: int, r0: float, f0: int, alpha: torch.Tensor, store_m: bool = False,
-                    m_dtype=torch.float64):
-    """fill_rewards_gram with the Householder-QR fill (spai_fill_lines_qr + spai_fill_reduce_rewards)."""
+                    m_dtype=torch.float64, rcache: torch.Tensor | None = None):
+    """fill_rewards_gram with the Householder-QR fill (spai_fill_lines_qr[_cached] + spai_fill_reduce_rewards)."""
     _lib.require_device(removed)
     removed = removed.contiguous()
     B = removed.shape[0]
     n = pattern.n
     m = torch.empty(B, n, pattern.width, dtype=m_dtype, device=removed.device) if store_m else None
     ws = _lib.workspace(_l().spai_fill_workspace_bytes(n, B), removed.device, "fill")
-    _fill_lines_qr(pattern, a_lines, max_rows, removed, 0, n, m, m_dtype, 0, ws)
+    _fill_lines_qr(pattern, a_lines, max_rows, removed, 0, n, m, m_dtype, 0, ws, rcache)
     return _reduce_rewards(ws, n, B, counts, nnz0, r0, f0, alpha, removed.device) + (m,)
 
 

@@ -18,6 +18,9 @@ Extensions (keyword-only, defaults = reference behaviour):
                       "lsq" by the normal equations of the Gram cache (the bench path), "qr" by
                       Householder QR of each line's dense block A[I, J] (spai_fill_lines_qr)
   keep_m=False        keep the last batch's M values (LSQ) in ``self.last_m``
+  rcache=True         fill="qr": factor every line's full block once per env (spai_qr_factor) and
+                      solve each rollout's masked problems from that R cache; False: the fused
+                      kernel refactors every call
 Documented deviations: alpha is taken from the ``alpha`` argument (the reference reads
 the never-set ``self.alpha``, preconditioner.py:163); fp64 original matrices are
 accepted (the reference raises in torch.mm, utils.py:350); a raw COO pattern with
@@ -53,7 +56,8 @@ def _default_device():
 
 class PreconditionerEnv(Env):
     def __init__(self, matrix_size: int, initial_matrix: Tensor, original_matrix: Tensor, *, side: str = "MA",
-                 fill: str = "copy", keep_m: bool = False, device=None, compact_gram: bool = True):
+                 fill: str = "copy", keep_m: bool = False, device=None, compact_gram: bool = True,
+                 rcache: bool = True):
         if side not in ("MA", "AM"):
             raise ValueError("side must be 'MA' or 'AM'")
         if fill not in ("copy", "lsq", "qr"):
@@ -87,10 +91,15 @@ class PreconditionerEnv(Env):
         # Gram cache of the fixed pattern (G = A_J^T A_J, c = A[l, J] per line): the per-rollout
         # fill then streams it instead of re-gathering A (pattern widths <= 13, A widths <= 7;
         # wider patterns use the generic kernels)
+        # (not for fill="qr", which never reads it)
         self.gram = (kernels.gram_build(self.pattern, self.a_lines)
-                     if self.pattern.width <= 13 and self.a_lines.width <= 7 else None)
-        # the QR fill factors each line's dense block A[I, J]: its largest row union picks the kernel
+                     if self.pattern.width <= 13 and self.a_lines.width <= 7 and fill != "qr" else None)
+        # the QR fill factors each line's dense block A[I, J]: its largest row union picks the kernel;
+        # the factorisation of the FULL block is sample-independent, so it is done once here into the
+        # R cache (rcache=False: refactor every call, the fused kernel)
         self.qr_rows = kernels.qr_max_rows(self.pattern, self.a_lines) if fill == "qr" else None
+        self.rcache = (kernels.qr_cache(self.pattern, self.a_lines, self.qr_rows)
+                       if fill == "qr" and rcache else None)
         if self.gram is not None and compact_gram:
             # integer stencils (and any A whose G, c are fp32-exact): the same cache in fp32
             g32 = kernels.gram_compact(self.gram, self.pattern)
@@ -125,30 +134,39 @@ class PreconditionerEnv(Env):
         return self.rewards_from_res2(kernels.res2_from_limbs(limbs), counts, alpha)
 
     def fill_partial(self, removed: Tensor, line_begin: int = 0, line_end: int | None = None, word_base: int = 0,
-                     limbs: bool = False) -> Tensor:
+                     limbs: bool = False, pattern: Lines | None = None) -> Tensor:
         """Fill lines [line_begin, line_end) of M for every sample and return the per-sample
         squared residual norms of those lines, [B] fp64 (kept in ``last_m`` / ``last_removed``);
         with ``limbs`` their exact sums [B, RES2_LIMBS] int64 instead (summable across line
         shards, spai_hip.h).  ``removed`` rows may be windows of the bitmaps starting at word
-        ``word_base`` (the columns split's all_to_all delivers only a shard's words)."""
+        ``word_base``, or packed rows read through ``pattern`` (the pattern with the shard's
+        action ids renumbered: distributed.PackPlan.local_pattern, the columns split's exchange)."""
         kw = dict(store_m=self.keep_m, m_dtype=self.a_lines.val.dtype, word_base=word_base, limbs=limbs)
+        pat = self.pattern if pattern is None else pattern
         if self.fill == "qr":
-            res2, m = kernels.fill_residual_qr(self.pattern, self.a_lines, self.qr_rows, removed, line_begin, line_end,
-                                               **kw)
+            res2, m = kernels.fill_residual_qr(pat, self.a_lines, self.qr_rows, removed, line_begin, line_end,
+                                               rcache=self.rcache, **kw)
         elif self.gram is not None:
-            res2, m = kernels.fill_residual_gram(self.pattern, self.gram, removed, self._lsq, line_begin,
-                                                 line_end, **kw)
+            res2, m = kernels.fill_residual_gram(pat, self.gram, removed, self._lsq, line_begin, line_end, **kw)
         else:
-            res2, m = kernels.fill_residual(self.pattern, self.a_lines, removed, self._lsq, line_begin,
-                                            line_end, **kw)
+            res2, m = kernels.fill_residual(pat, self.a_lines, removed, self._lsq, line_begin, line_end, **kw)
         if self.keep_m:
             self.last_m = m
         # only whole bitmaps over all lines can be assembled: a window (the columns split's
         # all_to_all rows, whose last column is the removal count) or a line shard cannot
-        whole = (word_base == 0 and removed.shape[1] == (self.init_nnz + 31) // 32 and line_begin == 0
-                 and (line_end is None or line_end == self.matrix_size))
+        whole = (pattern is None and word_base == 0 and removed.shape[1] == (self.init_nnz + 31) // 32
+                 and line_begin == 0 and (line_end is None or line_end == self.matrix_size))
         self.last_removed = removed if whole else None
         return res2
+
+    def pack_plan(self, world: int):
+        """The columns split's bitmap exchange plan for ``world`` ranks (distributed.PackPlan; one
+        host sync per world size, cached)."""
+        plans = self.__dict__.setdefault("_pack_plans", {})
+        if world not in plans:
+            from .distributed import PackPlan
+            plans[world] = PackPlan(self, world)
+        return plans[world]
 
     def word_spans(self, world: int) -> list:
         """Bitmap word span [(w0, w1)] of each of ``world`` 256-line-aligned column shards
@@ -178,7 +196,7 @@ class PreconditionerEnv(Env):
         if self.fill == "qr":
             self.last_residual, reward, self.last_reward32, m = kernels.fill_rewards_qr(
                 self.pattern, self.a_lines, self.qr_rows, removed, counts, self.init_nnz, self._r0, self.orig_flops,
-                alpha, store_m=self.keep_m, m_dtype=self.a_lines.val.dtype)
+                alpha, store_m=self.keep_m, m_dtype=self.a_lines.val.dtype, rcache=self.rcache)
         else:
             self.last_residual, reward, self.last_reward32, m = kernels.fill_rewards_gram(
                 self.pattern, self.gram, removed, self.fill == "lsq", counts, self.init_nnz, self._r0,

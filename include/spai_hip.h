@@ -271,6 +271,39 @@ int spai_fill_lines_qr(int32_t n, int32_t line_begin, int32_t line_end, int32_t 
                        const int32_t* pat_act, int32_t WA, const int32_t* a_idx, const void* a_val, int32_t a_dtype,
                        int32_t max_rows, int32_t B, const uint32_t* removed, int32_t words, int32_t word_base,
                        void* m_out, int32_t m_dtype, void* workspace, size_t workspace_bytes, void* stream);
+/* The same fill split at its sample-independent boundary.  The per-line Householder QR of the
+ * full block D = A[I, slots] depends on A and the pattern only, both fixed for an env's lifetime
+ * (preconditioner.py:23-25), so it runs ONCE per env (spai_qr_factor) into an R cache: per line the
+ * packed R (W(W+1)/2), Q^T e_l (W) and the tail ||(Q^T e_l)[W..]||^2 (+1 when l is not in I), fp64,
+ * blocks of 64 lines structure-of-arrays (spai_qr_cache_bytes; W = the width class 5 / 7 / 13 of
+ * (W, WA) as spai_fill_lines_qr).  Per rollout, spai_fill_lines_qr_cached reads the cache and the
+ * pattern's action ids, one thread per line: the kept columns R_J re-triangularised by Householder
+ * reflections of at most W rows (R_J has the singular values of A[I, J]: no normal equations),
+ * back-substitution, the same rank floor (the column norms are recomputed as sum_i R_ip^2) and the
+ * same outputs / workspace / partial layout as spai_fill_lines_qr (width classes 5 and 7; 13 ->
+ * SPAI_ERR_UNSUPPORTED, use spai_fill_lines_qr).  No reference counterpart (utils.py:331-353 copies). */
+size_t spai_qr_cache_bytes(int32_t n, int32_t W, int32_t WA);
+int spai_qr_factor(int32_t n, int32_t W, const int32_t* pat_idx, const int32_t* pat_act, int32_t WA,
+                   const int32_t* a_idx, const void* a_val, int32_t a_dtype, int32_t max_rows, double* rcache,
+                   size_t rcache_bytes, void* stream);
+int spai_fill_lines_qr_cached(int32_t n, int32_t line_begin, int32_t line_end, int32_t W, int32_t WA,
+                              const int32_t* pat_act, const double* rcache, int32_t B, const uint32_t* removed,
+                              int32_t words, int32_t word_base, void* m_out, int32_t m_dtype, void* workspace,
+                              size_t workspace_bytes, void* stream);
+
+/* ---------------------------------------------------------------- multi-GPU bitmap exchange
+ * The columns split's all_to_all send buffer (gflownet_spai_amd/distributed.py; the reference has
+ * no parallelism, its per-sample loop is preconditioner.py:37-51).  For destination q < P and
+ * candidate b < bl: the removal bits removed[b] (row stride `words`) of the action ids
+ * ids[seg[q] .. seg[q+1]) — q's line-major action ids — packed 32 per word (bit j of the segment
+ * -> word j / 32, bit j % 32), then counts[b].  q's block starts at out + out_off[q] and is
+ * [bl][wq + 1] words, wq = ceil((seg[q+1] - seg[q]) / 32).  max_seg = the longest segment.  The
+ * receiver reads the packed rows through shard-local action ids (0 .. seg length - 1 in the same
+ * line-major order), so every rank receives nnz(shard) bits per candidate for ANY numbering of
+ * the matrix (raw COO order defines the action ids, preconditioner.py:23-25). */
+int spai_bitmap_pack(int32_t P, int32_t bl, const uint32_t* removed, int32_t words, const int32_t* counts,
+                     const int32_t* ids, const int64_t* seg, const int64_t* out_off, int64_t max_seg, uint32_t* out,
+                     void* stream);
 
 /* ---------------------------------------------------------------- forward policy
  * logits[a] = fc(mean_pool(relu(GATv2_2(relu(GATv2_1(x))))))[a] for a < num_actions and

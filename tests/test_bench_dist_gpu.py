@@ -1,0 +1,50 @@
+"""The multi-GPU columns step as bench.py runs it, through RCCL, on the one GPU of the box.
+
+Two ranks cannot share one GPU under RCCL (its duplicate-GPU check), so the
+multi-rank exchange itself first runs on the driver's 8-GPU node.  What one GPU can run is the
+WHOLE columns-split step of bench.py on a one-rank RCCL group (``--gpus 1 --dist --backend
+nccl``): the line-major packed bitmap all_to_all issued asynchronously beside rollout_sort, the
+graph segments captured between the eager collectives, the exact limb all_reduce, and the
+pipelined M all_gather (LineGather) still in flight when the next step's graph replays.  The bench
+is launched as a fresh child process (its own HIP context and process group) and dumps its last
+step; this test recomputes that step with the one-GPU product path (same seed, same Philox
+stream id) and requires the rewards of every candidate and the assembled M bit for bit.
+Reference loops being split: gflownet/gflownet.py:135-183, preconditioner.py:37-51.
+"""
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.parametrize("fill", ["qr", "lsq"])
+def test_bench_columns_step_under_rccl_matches_one_gpu(tmp_path, fill):
+    dump = tmp_path / f"dist_{fill}.pt"
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--config", "c2", "--gpus", "1", "--dist", "--backend",
+           "nccl", "--fill", fill, "--steps", "3", "--warmup", "1", "--no-cpu-baseline", "--dump", str(dump)]
+    r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=400)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = torch.load(dump, weights_only=True)
+    assert d["shard"] == "columns" and d["world"] == 1 and "m_assembled" in d
+
+    sys.path.insert(0, ROOT)
+    import bench
+    from gflownet_spai_amd import GFlowNet, PreconditionerEnv
+    A, P = bench.config_matrices("c2")
+    n = A.shape[0]
+    dev = torch.device("cuda", 0)
+    genv = PreconditionerEnv(n, P, A, side="AM", fill=fill, keep_m=True, device=dev)
+    with torch.no_grad():
+        model = GFlowNet(bench.make_policy(genv, P, dev), None, genv, mode="throughput", seed=1234)
+        model.rollouts = int(d["stream_id"])
+        log = model.sample_states([P] * 8, return_log=True)
+    assert torch.equal(log.rewards_all.double().cpu(), d["rewards_all"])
+    assert torch.equal(genv.last_residual.double().cpu(), d["residual"])
+    best = int(torch.argmax(log.rewards_all))
+    assert torch.equal(genv.last_m[best].cpu(), d["m_assembled"][0])

@@ -52,19 +52,27 @@ def _env(kind):
     if kind == "2d":
         A = poisson_2d(96)
         return PreconditionerEnv(A.shape[0], A, A, side="AM", fill="lsq", keep_m=True), A, A
+    if kind == "thermal":  # the C5 stand-in's randomly permuted numbering (fp64, 7 per line), QR fill
+        from gflownet_spai_amd import thermal_like
+        A = thermal_like(160, 0, torch.float64)
+        return PreconditionerEnv(A.shape[0], A, A, side="AM", fill="qr", keep_m=True), A, A
     A = poisson_3d(12)
     P = axial_pattern_3d(12, 2, torch.float64)
     return PreconditionerEnv(A.shape[0], P, A, side="AM", fill="lsq", keep_m=True), P, A
 
 
 @pytest.mark.parametrize("kind,P,bl", [("2d", 2, 3), ("2d", 3, 2), ("2d", 8, 1), ("3d", 3, 2),
-                                       ("c4", 2, 1), ("c4", 4, 1), ("c4", 8, 1), ("c4", 3, 2)])
+                                       ("c4", 2, 1), ("c4", 4, 1), ("c4", 8, 1), ("c4", 3, 2),
+                                       ("thermal", 8, 1), ("thermal", 3, 2)])
 def test_columns_split_in_process_bit_identical(kind, P, bl):
     """P ranks in one process (C4 geometry included: 1024^2, E = 5,238,784, P = 2/4/8 with one
-    candidate per rank, and P = 3 whose shards are not equal): word spans, 256-line shards and the
-    all_to_all windows reproduce the one-process batch bit for bit."""
+    candidate per rank, and P = 3 whose shards are not equal; and the C5 stand-in's randomly
+    PERMUTED numbering, whose action ids scatter every shard over the whole bitmap): the packed
+    line-major exchange (spai_bitmap_pack == its torch restatement), 256-line shards and the
+    shard-local action tables reproduce the one-process batch bit for bit, and every rank receives
+    exactly nnz(shard) bits per candidate (~1/P of a bitmap) whatever the numbering."""
     from gflownet_spai_amd import kernels
-    from gflownet_spai_amd.distributed import LINE_ALIGN, bitmap_pack_index, shard_lines
+    from gflownet_spai_amd.distributed import LINE_ALIGN, pack_bits_reference, shard_lines, word_spans
     env, _, _ = _env(kind)
     n, E = env.matrix_size, env.num_actions - 1
     words = (E + 31) // 32
@@ -77,33 +85,35 @@ def test_columns_split_in_process_bit_identical(kind, P, bl):
     m1 = env.last_m.clone()
     alpha = torch.tensor(0.4)
     rw1 = env.rewards_from_res2(res2_1, counts1, alpha)
-    # P ranks: own candidates, then the all_to_all of bitmap windows + counts
-    spans = env.word_spans(P)
+    # P ranks: own candidates, then the all_to_all of packed rows + counts
+    plan = env.pack_plan(P)
     sends = []
     for r in range(P):
         sel = torch.empty(bl * words + bl, dtype=torch.int32, device=DEV)
         rm, ct, _ = kernels.rollout_select(lg[: E + 1], bl, lmax[:bl], seed, stream, r * bl, out=sel, ws_tag=f"r{r}")
         assert torch.equal(rm, removed1[r * bl:(r + 1) * bl]) and torch.equal(ct, counts1[r * bl:(r + 1) * bl])
-        sends.append(sel[bitmap_pack_index(spans, bl, words, DEV)])
-    # the spans are contiguous, cover every word, and a rank's window is ~1/P of a bitmap for the
-    # row-major stencil (the all_to_all volume DESIGN.md §6 assumes)
-    assert spans[0][0] == 0 and spans[-1][1] == words
-    assert all(spans[q][0] <= spans[q + 1][0] and spans[q][1] <= spans[q + 1][1] for q in range(P - 1))
-    if kind == "c4":  # lines [b, e) name the actions of rows b - 1024 .. e + 1024 (5 per row)
-        for q, (w0, w1) in enumerate(spans):
-            b, e = shard_lines(n, q, P, LINE_ALIGN)
-            assert w1 - w0 <= (e - b + 2 * 1024) * 5 // 32 + 2
-    offs = np.cumsum([0] + [bl * (w1 - w0 + 1) for w0, w1 in spans])
+        send = kernels.bitmap_pack(rm, ct, plan)
+        assert torch.equal(send, pack_bits_reference(rm, ct, plan, bl))
+        sends.append(send)
+    nnz = [int(plan.seg[q + 1] - plan.seg[q]) for q in range(P)]
+    assert sum(nnz) == E
+    for q in range(P):  # exactly the shard's bits: ~1/P of a bitmap per candidate
+        b, e = shard_lines(n, q, P, LINE_ALIGN)
+        assert plan.wq[q] == -(-nnz[q] // 32) and nnz[q] == int((env.pattern.act[b:e] >= 0).sum())
+    if kind == "thermal":  # the word windows of this numbering would be whole bitmaps
+        spans = word_spans(env, P)
+        assert all(w1 - w0 > 0.95 * words for w0, w1 in spans)
+        assert max(plan.wq) <= words // P + 64
+    offs = np.cumsum([0] + [bl * (w + 1) for w in plan.wq])
     limbs, blocks = [], []
     for q in range(P):
-        w0, w1 = spans[q]
-        recv = torch.cat([sends[r][offs[q]:offs[q + 1]] for r in range(P)]).view(B, w1 - w0 + 1)
-        assert torch.equal(recv[:, w1 - w0], counts1)
+        recv = torch.cat([sends[r][offs[q]:offs[q + 1]] for r in range(P)]).view(B, plan.wq[q] + 1)
+        assert torch.equal(recv[:, plan.wq[q]], counts1)
         b, e = shard_lines(n, q, P, LINE_ALIGN)
-        limbs.append(env.fill_partial(recv, b, e, word_base=w0, limbs=True))
+        limbs.append(env.fill_partial(recv, b, e, limbs=True, pattern=plan.local_pattern(env, q)))
         blocks.append(env.last_m.clone())
     res2 = kernels.res2_from_limbs(sum(limbs))
-    assert torch.equal(res2, res2_1)  # bit for bit, whatever P
+    assert torch.equal(res2, res2_1)  # bit for bit, whatever P and the numbering
     assert torch.equal(torch.cat(blocks, 1), m1)
     assert torch.equal(env.rewards_from_res2(res2, counts1, alpha), rw1)
 

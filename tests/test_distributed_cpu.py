@@ -13,9 +13,9 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from gflownet_spai_amd.distributed import (LINE_ALIGN, LineGather, allgather_lines, allreduce_res2, bitmap_pack_index,
-                                           exchange_bitmaps, exchange_parts, gather_rewards, gather_slices,
-                                           select_best_samples, shard_lines, word_spans)
+from gflownet_spai_amd.distributed import (LINE_ALIGN, LineGather, PackPlan, allgather_lines, allreduce_res2,
+                                           exchange_packed, exchange_parts, gather_rewards, gather_slices,
+                                           pack_bits_reference, select_best_samples, shard_lines, word_spans)
 from oracle import spai_oracle as O
 
 
@@ -114,17 +114,22 @@ def _split_fixture():
 
 
 class _Pattern:
-    """The attributes distributed.word_spans reads from a PreconditionerEnv (CPU stand-in)."""
+    """The attributes distributed.PackPlan / word_spans read from a PreconditionerEnv (CPU
+    stand-in); ``perm_seed``: the raw COO entries shuffled, i.e. a numbering whose action ids are
+    scattered over the whole bitmap (thermal2's file order, BASELINE C5)."""
 
-    def __init__(self, grid):
+    def __init__(self, grid, perm_seed=None):
         r, c, v, n = O.poisson2d(grid)
+        if perm_seed is not None:
+            o = np.random.default_rng(perm_seed).permutation(len(r))
+            r, c, v = r[o], c[o], v[o]
         idx, act, _ = O.lines_from_coo(r, c, v, n, "col")
         self.matrix_size, self.E = n, len(r)
         self.pattern = type("P", (), {"act": torch.from_numpy(act), "idx": torch.from_numpy(idx)})()
 
 
-def _columns_fixture(world, bl):
-    env = _Pattern(24)  # 576 lines: 256-line blocks split 2 + 1 over two ranks
+def _columns_fixture(world, bl, perm_seed=None):
+    env = _Pattern(24, perm_seed)  # 576 lines: 256-line blocks split 2 + 1 over two ranks
     words = (env.E + 31) // 32
     rng = np.random.default_rng(7)
     bits = rng.integers(0, 2 ** 32, size=(world * bl, words), dtype=np.uint64).astype(np.uint32).view(np.int32)
@@ -132,19 +137,31 @@ def _columns_fixture(world, bl):
     return env, words, torch.from_numpy(bits), torch.from_numpy(counts)
 
 
-def _columns_exchange(rank, world, bl=3):
-    """The columns split's all_to_all: rank r holds candidates r*bl .. (its bitmaps + counts in
-    one buffer, as rollout_select(out=) writes them) and receives every candidate's window of
-    the words its 256-line shard spans, plus the counts."""
-    env, words, bits, counts = _columns_fixture(world, bl)
-    spans = word_spans(env, world)
+def _columns_exchange(rank, world, bl=3, perm_seed=None):
+    """The columns split's all_to_all: rank r holds candidates r*bl .. and sends every rank q the
+    bits of q's line-major action ids packed 32 per word, plus the counts (spai_bitmap_pack,
+    restated in torch); it receives every candidate's packed row of its own shard."""
+    env, words, bits, counts = _columns_fixture(world, bl, perm_seed)
+    plan = PackPlan(env, world)
     mine = slice(rank * bl, (rank + 1) * bl)
-    buf = torch.cat([bits[mine].reshape(-1), counts[mine]])
-    send = buf[bitmap_pack_index(spans, bl, words, "cpu")]
-    w0, w1 = spans[rank]
-    recv = torch.full((world * bl, w1 - w0 + 1), -7, dtype=torch.int32)
-    exchange_bitmaps(send, recv, spans, bl, rank).wait()
-    return spans, recv.numpy()
+    send = pack_bits_reference(bits[mine], counts[mine], plan, bl)
+    assert send.numel() == plan.send_words(bl)
+    recv = torch.full((world * bl, plan.wq[rank] + 1), -7, dtype=torch.int32)
+    exchange_packed(send, recv, plan, bl, rank).wait()
+    return plan.wq, recv.numpy()
+
+
+def _unpack_expected(env, bits, lines):
+    """[B, m] removal bits of the line-major action ids of lines [b, e) (the receiver's view)."""
+    b, e = lines
+    a = env.pattern.act[b:e].reshape(-1)
+    a = a[a >= 0].long()
+    return ((bits[:, a >> 5].long() >> (a & 31)) & 1).numpy()
+
+
+def _unpack(recv, m):
+    w = recv[:, :-1].astype(np.uint32)
+    return ((w[:, :, None] >> np.arange(32, dtype=np.uint32)) & 1).reshape(len(recv), -1)[:, :m]
 
 
 def _slices_fixture():
@@ -206,13 +223,13 @@ def test_world2_column_sharded_reward_and_assembly():
         assert np.array_equal(res[rank]["bs"], full_bs.numpy())  # bit-exact: one non-zero term each
         for b in range(3):  # exact sums: the same bits as one process summing every partial
             assert res[rank]["r2"][b] == O.fixed_sum(partials[b])
-        spans, recv = res[rank]["cols"]
-        w0, w1 = spans[rank]
+        wq, recv = res[rank]["cols"]
         b0, b1 = lines[rank]
-        a = env.pattern.act[b0:b1].numpy()
-        assert w0 == a[a >= 0].min() >> 5 and w1 == (a[a >= 0].max() >> 5) + 1
-        assert np.array_equal(recv[:, :w1 - w0], bits[:, w0:w1].numpy())  # every candidate, global order
-        assert np.array_equal(recv[:, w1 - w0], counts.numpy())
+        m = int((env.pattern.act[b0:b1] >= 0).sum())
+        assert wq[rank] == (m + 31) // 32 and recv.shape == (6, wq[rank] + 1)
+        # every candidate (global order): exactly the bits of this rank's actions, line-major
+        assert np.array_equal(_unpack(recv, m), _unpack_expected(env, bits, lines[rank]))
+        assert np.array_equal(recv[:, -1], counts.numpy())
         assert np.array_equal(res[rank]["slices"][0], acts.numpy())
         allr, best, mbest = res[rank]["samples"]
         np.testing.assert_array_equal(allr, [0.5, 2.5, 1.5, -1.0])
@@ -245,3 +262,55 @@ def test_fixed_point_sums_are_partition_invariant():
     assert O.fixed_value(O.fixed_limbs(2.0 ** -100)) == 0.0  # below 2^-96: truncated
     assert O.fixed_value(O.fixed_limbs(1.5) + O.fixed_limbs(float("inf"))) == float("inf")
     assert np.isnan(O.fixed_value(O.fixed_limbs(float("nan")) + O.fixed_limbs(float("inf"))))
+
+
+def _worker3(rank, world, port, q):
+    """Three ranks (a non-power-of-two world): the packed bitmap exchange on a PERMUTED numbering
+    (the windows of word_spans would be whole bitmaps there) and the pipelined M gather with the
+    256-line-aligned shards GFlowNet uses for both splits (unequal: 1000 lines = 4 blocks, 2+1+1)."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        out = {"cols": _columns_exchange(rank, world, bl=2, perm_seed=3)}
+        n = 1000
+        b0, b1 = shard_lines(n, rank, world, LINE_ALIGN)
+        lg = LineGather(n, align=LINE_ALIGN)
+        m = torch.arange(2 * (b1 - b0) * 5, dtype=torch.float32).view(2, b1 - b0, 5) + 1e4 * rank
+        lg.start(m)
+        lg.start(m + 1)
+        out["m"] = lg.result().numpy()
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_world3_packed_exchange_on_permuted_numbering_and_aligned_gather():
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker3, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    env, words, bits, counts = _columns_fixture(world, 2, perm_seed=3)
+    lines = [shard_lines(env.matrix_size, r, world, LINE_ALIGN) for r in range(world)]
+    spans = word_spans(env, world)
+    for rank in range(world):
+        wq, recv = res[rank]["cols"]
+        m = int((env.pattern.act[lines[rank][0]:lines[rank][1]] >= 0).sum())
+        assert np.array_equal(_unpack(recv, m), _unpack_expected(env, bits, lines[rank]))
+        assert np.array_equal(recv[:, -1], counts.numpy())
+        # ~1/P of each bitmap per rank (its own nnz), where the word windows are ~whole bitmaps
+        assert wq[rank] <= -(-env.E // 32) * (lines[rank][1] - lines[rank][0]) // env.matrix_size + 2
+        assert spans[rank][1] - spans[rank][0] > 0.9 * words
+    blocks = []
+    for r in range(world):
+        b0, b1 = shard_lines(1000, r, world, LINE_ALIGN)
+        blocks.append(torch.arange(2 * (b1 - b0) * 5, dtype=torch.float32).view(2, b1 - b0, 5) + 1e4 * r + 1)
+    for rank in range(world):
+        assert np.array_equal(res[rank]["m"], torch.cat(blocks, 1).numpy())

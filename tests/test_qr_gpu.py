@@ -164,3 +164,103 @@ def test_qr_fill_c4_full_size_vs_oracle():
     envg = PreconditionerEnv(n, A, A, side="AM", fill="lsq")
     res_g = envg.fill_partial(log.removed).sqrt()
     np.testing.assert_allclose(env.last_residual[:1].cpu().numpy(), res_g.cpu().numpy(), rtol=1e-10)
+
+
+def _random_cols(n, k, seed, diag=None):
+    """Sparse n x n COO with exactly k nonzeros per column: the diagonal (value ``diag``, default
+    k + 1) and k - 1 distinct random rows (N(0, 1) values), so the row unions of k columns are
+    nearly disjoint: |I| ~ k * WA (the wide-block QR instances)."""
+    rng = np.random.default_rng(seed)
+    rows = np.empty((n, k), np.int64)
+    rows[:, 0] = np.arange(n)
+    for j in range(n):
+        o = rng.choice(n - 1, k - 1, replace=False)
+        rows[j, 1:] = o + (o >= j)
+    vals = rng.standard_normal((n, k))
+    vals[:, 0] = k + 1.0 if diag is None else diag
+    cols = np.repeat(np.arange(n), k)
+    ind = torch.from_numpy(np.stack([rows.reshape(-1), cols]))
+    # coalesced: the raw COO order (the env's action ids) is then the row-major order the oracle's
+    # lines (built from scipy's CSR) number the entries by
+    return torch.sparse_coo_tensor(ind, torch.from_numpy(vals.reshape(-1)), (n, n)).coalesce()
+
+
+@pytest.mark.parametrize("kp,ka,lo,hi", [(5, 5, 17, 32), (7, 7, 33, 64), (13, 7, 65, 96)])
+def test_qr_wide_row_unions_every_instance(kp, ka, lo, hi):
+    """Random sparse A and pattern with nearly disjoint column supports, so the row unions |I| fall
+    in the ranges of the larger group instances: <5,5,L8> (17-32 rows), <7,7,L16,NT128> (33-64) and
+    <13,7,L32,RPL3> (65-96, the only group sum with the shfl_xor(16) step).  M from the fused kernel
+    and (widths <= 7) from the R cache within 1e-10 of the oracle's QR; the residual vs scipy."""
+    from gflownet_spai_amd import PreconditionerEnv, kernels
+    n = 1500
+    A = _random_cols(n, ka, 11)
+    P = A if kp == ka else _random_cols(n, kp, 12)
+    env = PreconditionerEnv(n, P, A, side="AM", fill="qr", keep_m=True)
+    assert lo <= env.qr_rows <= hi, env.qr_rows
+    assert (env.rcache is not None) == (kp <= 7)
+    A_sp, P_sp = _sp(A), _sp(P)
+    idx, act, a_idx, a_val = _lines(A_sp, P_sp, n)
+    removed = np.random.default_rng(1).random((2, env.init_nnz)) < np.array([[0.0], [0.3]])
+    bits = _bits(removed)
+    outs = {"cached" if env.rcache is not None else "fused":
+            kernels.fill_residual_qr(env.pattern, env.a_lines, env.qr_rows, bits, store_m=True,
+                                     m_dtype=torch.float64, rcache=env.rcache)}
+    outs["fused"] = kernels.fill_residual_qr(env.pattern, env.a_lines, env.qr_rows, bits, store_m=True,
+                                             m_dtype=torch.float64)
+    for name, (res2, m) in outs.items():
+        m = m.cpu().numpy()
+        for b in range(2):
+            keep = (idx >= 0) & ~removed[b][np.clip(act, 0, None)]
+            m_ref = O.lsq_fill(idx, keep, a_idx, a_val)
+            rel = np.linalg.norm(m[b] - m_ref) / np.linalg.norm(m_ref)
+            assert rel < 1e-10, (name, b, rel)
+            ref = O.residual_fro_fp64(A_sp.tocsc(), O.m_to_csc(idx, m[b], n, np.float64)) ** 2
+            assert float(res2[b]) == pytest.approx(ref, rel=1e-10), name
+
+
+def test_qr_row_overflow_gives_nan():
+    """A max_rows below the true largest |I| selects an instance too small for some lines: those
+    lines' residual is NaN (the row-overflow path, rowl == -2), for the fused kernel and for an R
+    cache built with the same wrong max_rows; never a silent wrong value."""
+    from gflownet_spai_amd import PreconditionerEnv, kernels
+    n = 600
+    A = _random_cols(n, 5, 21)
+    env = PreconditionerEnv(n, A, A, side="AM", fill="qr", keep_m=False)
+    assert env.qr_rows > 16
+    bits = _bits(np.zeros((1, env.init_nnz), bool))
+    res2, _ = kernels.fill_residual_qr(env.pattern, env.a_lines, 16, bits)
+    assert torch.isnan(res2).all()
+    rc = kernels.qr_cache(env.pattern, env.a_lines, 16)
+    res2c, _ = kernels.fill_residual_qr(env.pattern, env.a_lines, 16, bits, rcache=rc)
+    assert torch.isnan(res2c).all()
+    ok, _ = kernels.fill_residual_qr(env.pattern, env.a_lines, env.qr_rows, bits, rcache=env.rcache)
+    assert torch.isfinite(ok).all()
+
+
+@pytest.mark.parametrize("kind", ["2d", "3d7", "c5s"])
+def test_qr_cached_equals_fused(kind):
+    """The R-cache path (phase 1 once per env, spai_fill_lines_qr_cached) against the fused kernel
+    (phase 1 every call): the same reflections on the same numbers, only the rank floor's column
+    norms are recomputed from R, so M and the residuals agree to rounding (1e-13) — and the cached
+    path's exact per-block sums make 256-line-aligned shards bit-identical to one launch."""
+    from gflownet_spai_amd import PreconditionerEnv, kernels, poisson_2d, poisson_3d, thermal_like
+    from gflownet_spai_amd.distributed import LINE_ALIGN, shard_lines
+    A = {"2d": lambda: poisson_2d(80, torch.float32), "3d7": lambda: poisson_3d(14),
+         "c5s": lambda: thermal_like(40, 0, torch.float64)}[kind]()
+    n = A.shape[0]
+    envc = PreconditionerEnv(n, A, A, side="AM", fill="qr", keep_m=True)
+    envf = PreconditionerEnv(n, A, A, side="AM", fill="qr", keep_m=True, rcache=False)
+    assert envc.rcache is not None and envf.rcache is None and envc.gram is None
+    removed = np.random.default_rng(4).random((9, envc.init_nnz)) < 0.25  # 9: a chunk of 8 + 1
+    bits = _bits(removed)
+    rc = envc.fill_partial(bits)
+    rf = envf.fill_partial(bits)
+    np.testing.assert_allclose(rc.cpu().numpy(), rf.cpu().numpy(), rtol=1e-13)
+    np.testing.assert_allclose(envc.last_m.cpu().numpy(), envf.last_m.cpu().numpy(), rtol=1e-12, atol=1e-14)
+    for P in (2, 3):
+        lb = sum(envc.fill_partial(bits, *shard_lines(n, q, P, LINE_ALIGN), limbs=True) for q in range(P))
+        assert torch.equal(kernels.res2_from_limbs(lb), rc)
+    counts = torch.from_numpy(removed.sum(1).astype(np.int32)).to(DEV)
+    rw = envc.fill_rewards(bits, counts, torch.tensor(0.5))
+    assert torch.equal(envc.last_residual.double(), rc.sqrt())
+    assert torch.equal(rw, envc.rewards_from_res2(rc, counts, torch.tensor(0.5)))

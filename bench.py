@@ -298,12 +298,16 @@ def main():
     ap.add_argument("--fill", default="lsq", choices=["lsq", "qr"],
                     help="least-squares fill: normal equations from the Gram cache (lsq) or Householder QR (qr)")
     ap.add_argument("--no-graph", action="store_true", help="time eager steps (host launches) instead of graph replays")
-    ap.add_argument("--no-overlap", action="store_true",
-                    help="one GPU: run the fill + rewards after the trajectory sort on one stream instead of beside it")
+    ap.add_argument("--overlap", default="sort", choices=["sort", "fill", "none"],
+                    help="one GPU: the fill + rewards on a second stream beside the trajectory sort, the sort "
+                         "launched first (sort) or the fill first (fill); none: one stream")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="process-group backend (nccl = RCCL over xGMI; gloo only to rehearse the flow)")
     ap.add_argument("--share-gpu", action="store_true",
                     help="every rank on GPU 0 (rehearsal of the multi-rank flow on a one-GPU box, with --backend gloo)")
+    ap.add_argument("--sort-blocks", type=int, default=0,
+                    help="persistent blocks of the trajectory sort (0: one per CU); fewer leave CUs to the fill "
+                         "running beside it (--overlap)")
     ap.add_argument("--dist", action="store_true",
                     help="initialise the process group and run the --shard split's multi-GPU step even at one rank "
                          "(--gpus 1 --backend nccl: the columns split's graph segments, all_to_all and pipelined M "
@@ -335,6 +339,8 @@ def main():
 
     from gflownet_spai_amd import GFlowNet, PreconditionerEnv, kernels
     from gflownet_spai_amd.distributed import LINE_ALIGN
+    if args.sort_blocks:
+        kernels.set_sort_blocks(args.sort_blocks)
 
     dims, grid, dtype, text = CONFIGS[args.config]
     A, P = config_matrices(args.config)
@@ -352,7 +358,7 @@ def main():
     split = {"columns": "columns", "slices": "slices"}.get(shard) if dist_on else None
     model = GFlowNet(make_policy(env, P, dev), None, env, mode="throughput", seed=1234, sample_base=base,
                      shard=(rank, world, None) if split else None, split=split or "columns",
-                     overlap=not args.no_overlap)
+                     overlap=False if args.overlap == "none" else args.overlap)
     s0 = [P] * bl
     assembled = {}
     do_assemble = [args.assemble != "none" and dist_on and shard != "candidates"]

@@ -92,6 +92,7 @@ SIGNATURES = {
     "spai_qr_max_rows": (ctypes.c_int, [_c_i32, _c_i32, _c_p, _c_i32, _c_p, _c_p, _c_p]),
     "spai_fill_lines_qr": (ctypes.c_int, [_c_i32, _c_i32, _c_i32, _c_i32, _c_p, _c_p, _c_i32, _c_p, _c_p, _c_i32,
                                           _c_i32, _c_i32, _c_p, _c_i32, _c_i32, _c_p, _c_i32, _c_p, _c_sz, _c_p]),
+    "spai_set_sort_blocks": (ctypes.c_int, [_c_i32]),
     "spai_bitmap_pack": (ctypes.c_int, [_c_i32, _c_i32, _c_p, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_i64, _c_p, _c_p]),
     "spai_qr_cache_bytes": (_c_sz, [_c_i32, _c_i32, _c_i32]),
     "spai_qr_factor": (ctypes.c_int, [_c_i32, _c_i32, _c_p, _c_p, _c_i32, _c_p, _c_p, _c_i32, _c_i32, _c_p, _c_sz,

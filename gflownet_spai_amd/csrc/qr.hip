@@ -474,7 +474,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2))) void k_
 // stores, the line residuals summed per sample in a fixed order (the k_gram_fill partial layout:
 // 256-line blocks, so 256-line-aligned shards sum to one launch's bits).
 #ifndef QRS_WPE
-#define QRS_WPE 3
+#define QRS_WPE 4
 #endif
 template <int W, typename TM>
 __global__ __launch_bounds__(kQNT) __attribute__((amdgpu_waves_per_eu(W <= 5 ? QRS_WPE : 2))) void k_qr_solve(
@@ -501,7 +501,8 @@ __global__ __launch_bounds__(kQNT) __attribute__((amdgpu_waves_per_eu(W <= 5 ? Q
 #pragma unroll
     for (int p = 0; p < W; ++p) act[p] = (valid && p < wrt) ? av[p] : -1;
   }
-  double R0[T], c0[W], tail, cn[W];
+  double R0[T], c0[W], tail;
+  float cnf[W];  // ||D[:, p]||^2 in fp32: it only scales the rank floor (registers: 4 waves per SIMD at W = 5)
   const double* rp = rcache + (int64_t)(jj >> 6) * NQ * 64 + (jj & 63);
 #pragma unroll
   for (int q = 0; q < T; ++q) R0[q] = rp[q * 64];
@@ -516,14 +517,13 @@ __global__ __launch_bounds__(kQNT) __attribute__((amdgpu_waves_per_eu(W <= 5 ? Q
       const double x = R0[i * W - i * (i - 1) / 2 + (p - i)];
       s = fma(x, x, s);
     }
-    cn[p] = s;
+    cnf[p] = (float)s;
   }
-  int wofs[W];
-#pragma unroll
-  for (int p = 0; p < W; ++p) wofs[p] = act[p] >= 0 ? (act[p] >> 5) - word_base : 0;
+  // bitmap word offset of a slot (recomputed where used: no registers held across the samples)
+  auto wofs = [&](int p) { return act[p] >= 0 ? (act[p] >> 5) - word_base : 0; };
   uint32_t wd[W];  // the slots' bitmap words of the next sample are loaded while the current one is solved
 #pragma unroll
-  for (int p = 0; p < W; ++p) wd[p] = removed[wofs[p]];
+  for (int p = 0; p < W; ++p) wd[p] = removed[wofs(p)];
 #pragma unroll 1
   for (int b = 0; b < B; ++b) {
     bool keep[W];
@@ -532,7 +532,14 @@ __global__ __launch_bounds__(kQNT) __attribute__((amdgpu_waves_per_eu(W <= 5 ? Q
     if (b + 1 < B) {
       const uint32_t* rn = removed + (int64_t)(b + 1) * words;
 #pragma unroll
-      for (int p = 0; p < W; ++p) wd[p] = rn[wofs[p]];
+      for (int p = 0; p < W; ++p) wd[p] = rn[wofs(p)];
+    }
+    double cn[W];
+#pragma unroll
+    for (int p = 0; p < W; ++p) {
+      float f = cnf[p];
+      asm volatile("" : "+v"(f));  // widened per sample, not held as fp64 across the loop
+      cn[p] = (double)f;
     }
     double Rm[W][W], c[W], m[W];
 #pragma unroll

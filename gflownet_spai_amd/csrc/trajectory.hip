@@ -1593,8 +1593,20 @@ static int num_cus() {
 
 static int max_buckets(int32_t E) { return std::min(kMaxB, E / kTarget + 2); }
 
+// persistent grid of k_sort2 (0: one block per CU); spai_set_sort_blocks
+static int g_sort_blocks = 0;
+
 }  // namespace
 }  // namespace spai
+
+// k_sort2 takes a whole CU per block (153 KB of LDS, the register file at 4 waves per SIMD), so
+// nothing runs beside it on its CUs: fewer persistent blocks leave CUs to a concurrent kernel
+// (the fill on the second stream, GFlowNet overlap).  Process-wide; 0 = one block per CU.
+extern "C" int spai_set_sort_blocks(int32_t blocks) {
+  SPAI_CHECK_ARG(blocks >= 0, "spai_set_sort_blocks: blocks %d < 0", blocks);
+  spai::g_sort_blocks = blocks;
+  return SPAI_OK;
+}
 
 using namespace spai;
 
@@ -1733,7 +1745,8 @@ extern "C" int spai_rollout_sort(const float* logits, int64_t bstride, int32_t E
   const int nbm = max_buckets(E);
   const int nbt = (nbm + nparts - 1) / nparts * B;  // buckets of the part over the samples (upper bound)
   // persistent blocks, enough that none walks more than the 32 * kBigWords its oversized mask tracks
-  const int g2 = std::max(std::max(1, std::min(nbt, num_cus())), (nbt + 32 * kBigWords - 1) / (32 * kBigWords));
+  const int cus = g_sort_blocks > 0 ? std::min(g_sort_blocks, num_cus()) : num_cus();
+  const int g2 = std::max(std::max(1, std::min(nbt, cus)), (nbt + 32 * kBigWords - 1) / (32 * kBigWords));
   const int64_t wrs = bstride ? w.wstride : 0;
   k_sort2<<<g2, kSortNT, 0, s>>>(E, B, w.ntiles, w.nb, w.bstart, w.runs, w.staging, w.spl, t_cap, actions, fwd_probs,
                                  w.wrest, w.bwsuf, w.bigcnt, w.ww, wrs, w.scratch, part, nparts);

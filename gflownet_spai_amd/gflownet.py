@@ -27,7 +27,8 @@ from .preconditioner import Data
 
 class GFlowNet(nn.Module):
     def __init__(self, forward_policy, backward_policy, env, *, mode: str = "parity", seed: int | None = None,
-                 sample_base: int = 0, shard: tuple | None = None, split: str | None = None, overlap: bool = True):
+                 sample_base: int = 0, shard: tuple | None = None, split: str | None = None,
+                 overlap: bool | str = "sort"):
         super().__init__()
         if mode not in ("parity", "throughput"):
             raise ValueError("mode must be 'parity' or 'throughput'")
@@ -46,8 +47,11 @@ class GFlowNet(nn.Module):
         self._data_cache = {}
         self._bufs = {}      # persistent exchange buffers of the columns split (graph-replay safe)
         # one GPU, throughput mode: run the fill + rewards on a second stream beside the trajectory
-        # sort (the two chains share only the select phase's outputs)
-        self.overlap = overlap
+        # sort (the two chains share only the select phase's outputs); "sort" / True: the sort is
+        # launched first, "fill": the fill first, False: one stream, fill then sort
+        if overlap not in (False, True, "sort", "fill"):
+            raise ValueError("overlap must be False, True, 'sort' or 'fill'")
+        self.overlap = "sort" if overlap is True else overlap
         self._side = None
         # (rank, world, group): the multi-GPU split of DESIGN.md §6 (throughput mode)
         #   split="columns": rank r rolls out its own len(s0) candidates (global sample ids
@@ -244,6 +248,16 @@ class GFlowNet(nn.Module):
             return [(self._begin, False), (self.rollout_exchange, True), (self._end, False)]
         return [(self._begin, False), (self.rollout_exchange, False), (self._end, False)]
 
+    def _fork_fill(self, st: dict) -> None:
+        """fill + rewards of all lines on the side stream, after everything the current stream has
+        issued (the select phase, and with overlap="sort" the trajectory sort's launch)."""
+        dev = st["lg"].device
+        side = self._side_stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            st["rewards"] = self.env.fill_rewards(st["removed"], st["counts"], st["alpha"])
+        st["join"] = side
+
     def _side_stream(self, dev):
         if self._side is None or self._side.device != dev:
             self._side = torch.cuda.Stream(dev)
@@ -277,16 +291,13 @@ class GFlowNet(nn.Module):
         st.update(B=B, E=E, logits=logits, alpha=alpha, lg=lg, lmax=lmax, removed=removed, counts=counts, ws=ws,
                   part=(rank, world, group))
         if world == 1:  # all lines here: fill, exact sums and rewards (one launch after the fill)
-            if self.overlap:
+            if self.overlap == "fill":
                 # the fill needs only the removal bitmaps and the sort only the staged records: the
                 # fill + rewards run on a second stream beside rollout_sort / rollout_finish (under
                 # HIP-graph capture: two parallel branches), joined in _end
-                main = torch.cuda.current_stream(lg.device)
-                side = self._side_stream(lg.device)
-                side.wait_stream(main)
-                with torch.cuda.stream(side):
-                    st["rewards"] = env.fill_rewards(removed, counts, alpha)
-                st["join"] = side
+                self._fork_fill(st)
+            elif self.overlap:  # "sort": the same branches, the sort launched first (_end forks the fill)
+                st["fill_after_sort"] = True
             else:
                 st["rewards"] = env.fill_rewards(removed, counts, alpha)
         else:  # a split sums exact limbs of its lines
@@ -315,6 +326,8 @@ class GFlowNet(nn.Module):
         if world > 1:  # counts, T and the bucket positions need every part's buckets
             kernels.rollout_merge(lg, B, lmax, ws, rank, world, counts)
         actions, fwd = kernels.rollout_sort(lg, B, lmax, ws, rank, world)
+        if st.pop("fill_after_sort", False):
+            self._fork_fill(st)
         t_dev = kernels.rollout_finish(lg, B, lmax, counts, ws, actions, fwd, rank, world)
         if "join" in st:  # the fill's stream (rollout_begin) rejoins before anything reads its outputs
             torch.cuda.current_stream(lg.device).wait_stream(st.pop("join"))

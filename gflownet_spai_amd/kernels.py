@@ -185,6 +185,11 @@ def rollout_sort(lg, B, lmax, ws, part: int, nparts: int):
     return actions, fwd
 
 
+def set_sort_blocks(blocks: int) -> None:
+    """Persistent grid of the trajectory sort (spai_set_sort_blocks; 0 = one block per CU)."""
+    _lib.check(_l().spai_set_sort_blocks(int(blocks)), "spai_set_sort_blocks")
+
+
 def rollout_finish(lg, B, lmax, counts, ws, actions, fwd, part: int, nparts: int):
     """Terminal step and padding (last part) and T (int32 [1] device tensor)."""
     E = lg.shape[-1] - 1

@@ -117,6 +117,10 @@ int spai_parity_step(const float* logits, int64_t bstride, int32_t E1, int32_t B
  * fwd_probs of its slice) and spai_rollout_finish (the last part writes the terminal step and
  * the padding; t_out is written by every part). */
 size_t spai_rollout_workspace_bytes(int32_t E, int32_t B);
+/* Persistent grid of the sort phase (spai_rollout_sort's k_sort2, one whole CU per block): at most
+ * `blocks` blocks (0 = one per CU, the default), so a kernel launched on another stream beside the
+ * sort (the fill) keeps the remaining CUs.  Process-wide setting. */
+int spai_set_sort_blocks(int32_t blocks);
 int spai_rollout_select(const float* logits, int64_t bstride, int32_t E, int32_t B, const float* lmax,
                         uint64_t seed, uint64_t stream_id, uint64_t* stream_ctr, int32_t sample_base,
                         int32_t part, int32_t nparts, uint32_t* removed, int32_t words, int32_t* counts,

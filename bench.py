@@ -4,7 +4,9 @@ One step = one ``GFlowNet.sample_states`` call over a batch of B candidate preco
 of the 1024^2 5-point Poisson matrix (config C4, fp32): ForwardPolicy logits (GATv2 x2 +
 mean pool + fc on the state graph, random-init weights), throughput rollout (Gumbel-top-k,
 20 % expected removal, ordered trajectory log + forward probabilities), least-squares fill
-of M (column SPAI) and the ||A M - I||_F reward, all inputs resident in HBM.
+of M (column SPAI; Householder QR: every line's full block A[I, slots] factored once per env
+into an R cache, the masked re-triangularisation per step) and the ||A M - I||_F reward, all
+inputs resident in HBM.
 
 Multi-GPU (one process per GPU; `--gpus N` starts the N ranks itself, or run it under
 torch.distributed.run), DESIGN.md §6:
@@ -295,8 +297,10 @@ def main():
     ap.add_argument("--strong", action="store_true",
                     help="columns split: --batch is the GLOBAL batch (batch/P rollouts per GPU) instead of per GPU")
     ap.add_argument("--assemble", default="best", choices=["best", "all", "none"])
-    ap.add_argument("--fill", default="lsq", choices=["lsq", "qr"],
-                    help="least-squares fill: normal equations from the Gram cache (lsq) or Householder QR (qr)")
+    ap.add_argument("--fill", default="auto", choices=["auto", "lsq", "qr"],
+                    help="least-squares fill: Householder QR from the env's R cache (qr, the north star's algorithm) "
+                         "or the normal equations from the Gram cache (lsq); auto: qr where the cached QR solve is "
+                         "compiled (pattern lines <= 7 wide: c2, c4, c5s), lsq for c3's 13-wide lines")
     ap.add_argument("--no-graph", action="store_true", help="time eager steps (host launches) instead of graph replays")
     ap.add_argument("--overlap", default="sort", choices=["sort", "fill", "none"],
                     help="one GPU: the fill + rewards on a second stream beside the trajectory sort, the sort "
@@ -332,6 +336,13 @@ def main():
     dist_on = world > 1 or args.dist
     if dist_on:
         import torch.distributed as dist
+        if "RANK" not in os.environ:  # --dist on one GPU without a launcher: a one-rank group on 127.0.0.1
+            import socket
+            with socket.socket() as sk:
+                sk.bind(("127.0.0.1", 0))
+                port = sk.getsockname()[1]
+            os.environ.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+                              MASTER_PORT=str(port))
         if args.backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
@@ -343,6 +354,8 @@ def main():
         kernels.set_sort_blocks(args.sort_blocks)
 
     dims, grid, dtype, text = CONFIGS[args.config]
+    if args.fill == "auto":
+        args.fill = "lsq" if args.config == "c3" else "qr"
     A, P = config_matrices(args.config)
     n = A.shape[0]
     env = PreconditionerEnv(n, P, A, side="AM", fill=args.fill, keep_m=True, device=dev)

@@ -294,17 +294,22 @@ __device__ __forceinline__ double qr_rsq(double t) {
 // < p take no part: their entries of v are 0, so they are left exactly as they are).  Only which
 // rows are free depends on the mask — no data-dependent row index anywhere, so the back-
 // substitution is the plain triangular one.  Column p pivots when it is kept and its norm outside
-// the pivot rows exceeds 1e-12 ||D[:, p]|| (cn[p] = ||D[:, p]||^2: fp64 rank deficiency), else
+// the pivot rows exceeds 1e-12 ||D[:, p]|| (thr[p] = 1e-24 ||D[:, p]||^2: fp64 rank deficiency), else
 // m_p = 0 and row p becomes free (no reflection).  Rm (Rm[i][q], i <= q; the rest is never read)
 // and c are worked in place; m gets the solution; returns the line residual^2 = tail + sum of
 // (Q^T e)^2 over the free rows (sums of squares: no cancellation).
 template <int W>
 __device__ __forceinline__ double qr_masked_solve(double (&Rm)[W][W], double (&c)[W], double tail,
-                                                  const double (&cn)[W], const bool (&keep)[W], double (&m)[W]) {
+                                                  const double (&thr)[W], const bool (&keep)[W], double (&m)[W]) {
   bool piv[W];
   double rd[W];
+  {  // column 0 has no rows above it: its reflection would only flip row 0's sign (skipped)
+    const double x0 = Rm[0][0];
+    piv[0] = keep[0] && x0 * x0 > thr[0];
+    rd[0] = piv[0] ? qr_rcp(x0) : 0.0;
+  }
 #pragma unroll
-  for (int p = 0; p < W; ++p) {
+  for (int p = 1; p < W; ++p) {
     double v[W];  // the reflection vector over rows 0..p (0 on the pivot rows)
     const double xp = Rm[p][p];
     double sig = xp * xp;
@@ -313,7 +318,7 @@ __device__ __forceinline__ double qr_masked_solve(double (&Rm)[W][W], double (&c
       v[i] = piv[i] ? 0.0 : Rm[i][p];
       sig = fma(v[i], v[i], sig);
     }
-    piv[p] = keep[p] && sig > 1e-24 * cn[p];  // |R_pp| after the reflection > 1e-12 ||D[:, p]||
+    piv[p] = keep[p] && sig > thr[p];  // |R_pp| after the reflection > 1e-12 ||D[:, p]||
     const double rs = qr_rsq(piv[p] ? sig : 1.0);
     const double sq = sig * rs;                                 // sqrt(sig)
     const double alpha = __builtin_copysign(sq, -xp);           // the new R_pp (sign opposite to x_p)
@@ -385,12 +390,12 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(W <= 5 ? QR_
         const bool valid = li < nvl;
         const int l = blk0 + (valid ? li : 0);
         int act[W], wofs[W];
-        double cn[W];
+        double thr[W];
 #pragma unroll
         for (int p = 0; p < W; ++p) {
           act[p] = S.sAct[gl][p];
           wofs[p] = act[p] >= 0 ? (act[p] >> 5) - word_base : 0;
-          cn[p] = S.sCn[gl][p];
+          thr[p] = 1e-24 * S.sCn[gl][p];
         }
 #pragma unroll 1
         for (int s = t / NG; s < nb; s += NT / NG) {
@@ -406,7 +411,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(W <= 5 ? QR_
             for (int q = i; q < W; ++q) Rm[i][q] = S.sRf[gl][i * W - i * (i - 1) / 2 + (q - i)];
             c[i] = S.sC[gl][i];
           }
-          const double rs = qr_masked_solve<W>(Rm, c, S.sC[gl][W], cn, keep, m);
+          const double rs = qr_masked_solve<W>(Rm, c, S.sC[gl][W], thr, keep, m);
           if (valid) {
             if (m_out != nullptr) {
               TM* dst = m_out + ((int64_t)b * nloc + (l - line_begin)) * wrt;
@@ -485,6 +490,7 @@ __global__ __launch_bounds__(kQNT) __attribute__((amdgpu_waves_per_eu(W <= 5 ? Q
   static_assert(kQNT == kQLines, "one thread per line of a 256-line block");
   __shared__ double s_r2[kQChunk][kQNT];
   __shared__ __attribute__((aligned(16))) TM s_m[2][kQNT * W];
+  __shared__ double s_c0[W + 1][kQNT];  // the line's Q^T e and tail (LDS, not registers: 4 waves per SIMD)
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int lb = blockIdx.x;
   const int j = line_begin + lb * kQNT + t;
@@ -501,14 +507,13 @@ __global__ __launch_bounds__(kQNT) __attribute__((amdgpu_waves_per_eu(W <= 5 ? Q
 #pragma unroll
     for (int p = 0; p < W; ++p) act[p] = (valid && p < wrt) ? av[p] : -1;
   }
-  double R0[T], c0[W], tail;
-  float cnf[W];  // ||D[:, p]||^2 in fp32: it only scales the rank floor (registers: 4 waves per SIMD at W = 5)
+  double R0[T];
+  float thf[W];  // the rank floors 1e-24 ||D[:, p]||^2 in fp32 (registers: 4 waves per SIMD at W = 5)
   const double* rp = rcache + (int64_t)(jj >> 6) * NQ * 64 + (jj & 63);
 #pragma unroll
   for (int q = 0; q < T; ++q) R0[q] = rp[q * 64];
 #pragma unroll
-  for (int p = 0; p < W; ++p) c0[p] = rp[(T + p) * 64];
-  tail = rp[(T + W) * 64];
+  for (int p = 0; p <= W; ++p) s_c0[p][t] = rp[(T + p) * 64];  // read back by this thread only
 #pragma unroll
   for (int p = 0; p < W; ++p) {
     double s = 0.0;
@@ -517,7 +522,7 @@ __global__ __launch_bounds__(kQNT) __attribute__((amdgpu_waves_per_eu(W <= 5 ? Q
       const double x = R0[i * W - i * (i - 1) / 2 + (p - i)];
       s = fma(x, x, s);
     }
-    cnf[p] = (float)s;
+    thf[p] = (float)(1e-24 * s);  // (0 only below 1e-21: the floor then drops exact zeros only)
   }
   // bitmap word offset of a slot (recomputed where used: no registers held across the samples)
   auto wofs = [&](int p) { return act[p] >= 0 ? (act[p] >> 5) - word_base : 0; };
@@ -534,22 +539,30 @@ __global__ __launch_bounds__(kQNT) __attribute__((amdgpu_waves_per_eu(W <= 5 ? Q
 #pragma unroll
       for (int p = 0; p < W; ++p) wd[p] = rn[wofs(p)];
     }
-    double cn[W];
+    double thr[W];
 #pragma unroll
     for (int p = 0; p < W; ++p) {
-      float f = cnf[p];
+      float f = thf[p];
       asm volatile("" : "+v"(f));  // widened per sample, not held as fp64 across the loop
-      cn[p] = (double)f;
+      thr[p] = (double)f;
     }
     double Rm[W][W], c[W], m[W];
 #pragma unroll
     for (int i = 0; i < W; ++i) {
 #pragma unroll
       for (int q = i; q < W; ++q) Rm[i][q] = R0[i * W - i * (i - 1) / 2 + (q - i)];
-      c[i] = c0[i];
+      c[i] = s_c0[i][t];
     }
-    const double rs = qr_masked_solve<W>(Rm, c, tail, cn, keep, m);
+    const double rs = qr_masked_solve<W>(Rm, c, s_c0[W][t], thr, keep, m);
     s_r2[b % kQChunk][t] = valid ? rs : 0.0;
+#ifdef QRS_DIRECT  // A/B: M stored from the registers (no LDS staging, no barrier per sample)
+    if (m_out != nullptr && valid) {
+      TM* dst = m_out + ((int64_t)b * nloc + (j - line_begin)) * wrt;
+#pragma unroll
+      for (int p = 0; p < W; ++p)
+        if (p < wrt) nt_store(dst + p, (TM)m[p]);
+    }
+#else
     {  // M (no branch on m_out: store_m_block drops every store when it is null)
       TM* sm = s_m[b & 1];
       if (valid) {
@@ -561,6 +574,7 @@ __global__ __launch_bounds__(kQNT) __attribute__((amdgpu_waves_per_eu(W <= 5 ? Q
       store_m_block<kQNT, W, TM>(m_out ? m_out + ((int64_t)b * nloc + (int64_t)lb * kQNT) * wrt : nullptr, sm,
                                  nvl * wrt);
     }
+#endif
     if (b % kQChunk == kQChunk - 1 || b == B - 1) {  // the chunk's fixed-order block sums
       const int c0b = b - b % kQChunk, nb = b - c0b + 1;
       __syncthreads();

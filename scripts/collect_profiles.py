@@ -15,6 +15,7 @@ import shutil
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ROOF_KERNELS = {"c4": "k_gram_fill<5, ", "c2": "k_gram_fill<5, ", "c3": "k_gram_fill_wide<13, "}  # LSQ fill, any Gram type
+ROOF_KERNELS_QR = {"c4": "k_qr_solve<5, ", "c2": "k_qr_solve<5, ", "c5s": "k_qr_solve<7, ", "c3": "k_qr_fill<13, "}
 
 
 def short(name):
@@ -30,6 +31,7 @@ def main():
     ap.add_argument("--batch", type=int, default=8)
     ap.add_argument("--out", default=os.path.join(ROOT, "profiles"))
     ap.add_argument("--cmd", default="python bench.py --steps 10 --warmup 2 --no-cpu-baseline")
+    ap.add_argument("--fill", default="lsq", choices=["lsq", "qr"], help="the bench command's fill (its roofline kernel)")
     args = ap.parse_args()
     os.makedirs(args.out, exist_ok=True)
     stats = os.path.join(args.prof, "run_kernel_stats.csv")
@@ -55,8 +57,13 @@ def main():
         dst.update(e)
     with open(os.path.join(args.out, f"pmc_{args.tag}.json"), "w") as f:
         json.dump(summary, f, indent=1)
-    roof = [(k, v) for k, v in summary["kernels"].items()
-            if ROOF_KERNELS[args.config] in k and "true" in k and "hbm_bytes_per_launch" in v]
+    if args.fill == "qr":
+        roof = [(k, v) for k, v in summary["kernels"].items()
+                if ROOF_KERNELS_QR[args.config] in k and "hbm_bytes_per_launch" in v]
+    else:
+        roof = [(k, v) for k, v in summary["kernels"].items()
+                if ROOF_KERNELS[args.config] in k and "true" in k and "hbm_bytes_per_launch" in v]
+    key = args.config + ("_qr" if args.fill == "qr" else "")
     if roof:
         k, v = roof[0]
         rec = {"config": args.config, "batch": args.batch, "kernel": k, "avg_us": v.get("avg_us"),
@@ -70,7 +77,7 @@ def main():
             allrec = {}
         if "config" in allrec:  # older single-record form
             allrec = {allrec["config"]: allrec}
-        allrec[args.config] = rec
+        allrec[key] = rec
         # the generic residual leg's kernel (bench roofline_residual), when it ran in this command
         res = [(k, v) for k, v in summary["kernels"].items()
                if ("k_resid_shared<" in k or "k_resid_wide<" in k) and "hbm_bytes_per_launch" in v]

@@ -3,8 +3,8 @@
 # collectives), for each split; then the N=1 bench line.  Not a scaling measurement.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
-for sh in columns samples slices; do
-  timeout -k 10 300 python bench.py --gpus 2 --backend gloo --share-gpu --shard $sh --steps 5 --warmup 2 \
+for sh in ${SPLITS:-columns samples slices}; do
+  timeout -k 10 300 python bench.py --gpus ${RANKS:-2} --backend gloo --share-gpu --shard $sh --steps 5 --warmup 2 \
     --config ${CFG:-c2} --no-cpu-baseline > gpurun_out/rehearsal_$sh.log 2>&1 || { tail -30 gpurun_out/rehearsal_$sh.log; exit 1; }
   tail -1 gpurun_out/rehearsal_$sh.log | cut -c1-600
 done

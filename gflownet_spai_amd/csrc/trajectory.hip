@@ -745,30 +745,43 @@ void k_tile(const float* __restrict__ rr, const float* __restrict__ ww, int64_t 
       }
     __syncthreads();
     PROF(6)
+    // list rounds in use (block-uniform, usually 3-4 of kPerT): the unrolled per-entry loops
+    // branch over the empty rounds instead of evaluating them under a false predicate
+    const int nI = (totw + kGrpNT - 1) / kGrpNT;
 #pragma unroll
     for (int i = 0; i < kPerT; ++i) {
-      const int e = tid + i * kGrpNT;
-      const bool v = e < totw;
-      eo[i] = v ? l_ord[e] : 0u;
-      eid[i] = v ? (uint32_t)l_id[e] : 0u;
-      ew[i] = v ? l_w[e] : 0.0f;
+      eo[i] = 0u;
+      eid[i] = 0u;
+      ew[i] = 0.0f;
+      if (i < nI) {
+        const int e = tid + i * kGrpNT;
+        const bool v = e < totw;
+        eo[i] = v ? l_ord[e] : 0u;
+        eid[i] = v ? (uint32_t)l_id[e] : 0u;
+        ew[i] = v ? l_w[e] : 0.0f;
+      }
     }
     int ebc[kPerT];
 #pragma unroll
     for (int i = 0; i < kPerT; ++i) {
-      const uint32_t o = eo[i];
-      const uint32_t bin = o < lmn ? 0u : min((uint32_t)(kBins - 1), (o - lmn) >> lsh);
-      ebc[i] = s_lut[bin];
+      ebc[i] = 0;
+      if (i < nI) {
+        const uint32_t o = eo[i];
+        const uint32_t bin = o < lmn ? 0u : min((uint32_t)(kBins - 1), (o - lmn) >> lsh);
+        ebc[i] = s_lut[bin];
+      }
     }
     bool more;
     do {
       more = false;
 #pragma unroll
       for (int i = 0; i < kPerT; ++i) {
-        const uint32_t sv = s_spl[max(0, min(ebc[i], nbl - 1))];
-        const bool step = tid + i * kGrpNT < totw && ebc[i] < nbl && sv <= eo[i];
-        ebc[i] += step;
-        more |= step;
+        if (i < nI) {
+          const uint32_t sv = s_spl[max(0, min(ebc[i], nbl - 1))];
+          const bool step = tid + i * kGrpNT < totw && ebc[i] < nbl && sv <= eo[i];
+          ebc[i] += step;
+          more |= step;
+        }
       }
     } while (__any(more));
     PROF(7)

@@ -302,6 +302,8 @@ def main():
                          "or the normal equations from the Gram cache (lsq); auto: qr where the cached QR solve is "
                          "compiled (pattern lines <= 7 wide: c2, c4, c5s), lsq for c3's 13-wide lines")
     ap.add_argument("--no-graph", action="store_true", help="time eager steps (host launches) instead of graph replays")
+    ap.add_argument("--steps-per-graph", type=int, default=4,
+                    help="one GPU: consecutive steps captured in one HIP graph (1: one graph replay per step)")
     ap.add_argument("--overlap", default="sort", choices=["sort", "fill", "none"],
                     help="one GPU: the fill + rewards on a second stream beside the trajectory sort, the sort "
                          "launched first (sort) or the fill first (fill); none: one stream")
@@ -463,13 +465,39 @@ def main():
 
             for _ in range(max(1, args.warmup)):
                 log = step()
+            # a step without collectives (one GPU): spg consecutive steps in ONE graph, so the
+            # ~12 us between two graph launches is paid once per spg steps (every step is still a
+            # whole sample_states: its own select, sort, fill and Log, its own Philox stream id)
+            spg = max(1, args.steps_per_graph) if all(not c for _, c in phases) else 1
+            if spg > 1:
+                gm = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gm, pool=pool):
+                    for _ in range(spg):
+                        stm = {"s0": s0}
+                        for f, _c in phases:
+                            f(stm)
+                mlog = stm["log"]
+                gm.replay()
         else:
             step = eager_step
+            spg = 1
+
+        def steps(k):  # k timed steps: the remainder as single steps, then whole multi-step graphs
+            out = None
+            if spg > 1:
+                for _ in range(k % spg):
+                    out = step()
+                for _ in range(k // spg):
+                    gm.replay()  # the last capture: env.last_* and mlog name its last step's buffers
+                    out = mlog
+                return out
+            for _ in range(k):
+                out = step()
+            return out
 
         barrier()
         t0 = time.perf_counter()
-        for _ in range(args.steps):
-            log = step()
+        log = steps(args.steps)
         if gather is not None:
             gather.wait()
         barrier()
@@ -485,8 +513,7 @@ def main():
             do_assemble[0] = False
             barrier()
             t0 = time.perf_counter()
-            for _ in range(args.steps):
-                log = step()
+            log = steps(args.steps)
             barrier()
             dt_noasm = (time.perf_counter() - t0) / args.steps
             do_assemble[0] = True
@@ -538,6 +565,7 @@ def main():
             "value_without_assembly": B * n / dt_noasm,
             "ms_per_step_without_assembly": dt_noasm * 1e3,
             "graph": use_graph,
+            "steps_per_graph": spg,
             "ms_per_step_eager": dt_eager * 1e3,
             "final_residual_fro": float(res[0]),
             "final_residual_fro_mean": float(res.mean()),

@@ -264,3 +264,35 @@ def test_qr_cached_equals_fused(kind):
     rw = envc.fill_rewards(bits, counts, torch.tensor(0.5))
     assert torch.equal(envc.last_residual.double(), rc.sqrt())
     assert torch.equal(rw, envc.rewards_from_res2(rc, counts, torch.tensor(0.5)))
+
+
+@pytest.mark.parametrize("B", [1, 3])
+def test_qr_cached_narrow_lines_and_small_batches(B):
+    """A 1-D Laplacian (3-wide lines inside the 5-wide class: slots 3-4 are padding) with B = 1 and
+    3 (partial sample chunks), over a line range that starts and ends inside 256-line blocks: the
+    R-cache solve against the oracle's QR (1e-11) and the fused kernel (1e-13)."""
+    from gflownet_spai_amd import PreconditionerEnv, kernels
+    n = 1000
+    i = torch.arange(n)
+    rows = torch.cat([i, i[1:], i[:-1]])
+    cols = torch.cat([i, i[:-1], i[1:]])
+    vals = torch.cat([torch.full((n,), 2.0), torch.full((n - 1,), -1.0), torch.full((n - 1,), -1.0)]).double()
+    A = torch.sparse_coo_tensor(torch.stack([rows, cols]), vals, (n, n)).coalesce()
+    env = PreconditionerEnv(n, A, A, side="AM", fill="qr", keep_m=True)
+    assert env.pattern.width == 3 and env.rcache is not None
+    A_sp = _sp(A)
+    idx, act, a_idx, a_val = _lines(A_sp, A_sp, n)
+    removed = np.random.default_rng(9).random((B, env.init_nnz)) < 0.3
+    bits = _bits(removed)
+    lb, le = 256, 900  # a 256-aligned shard start, an end inside a block
+    res_c, m_c = kernels.fill_residual_qr(env.pattern, env.a_lines, env.qr_rows, bits, lb, le, store_m=True,
+                                          m_dtype=torch.float64, rcache=env.rcache)
+    res_f, m_f = kernels.fill_residual_qr(env.pattern, env.a_lines, env.qr_rows, bits, lb, le, store_m=True,
+                                          m_dtype=torch.float64)
+    np.testing.assert_allclose(res_c.cpu().numpy(), res_f.cpu().numpy(), rtol=1e-13)
+    np.testing.assert_allclose(m_c.cpu().numpy(), m_f.cpu().numpy(), rtol=1e-12, atol=1e-14)
+    for b in range(B):
+        keep = (idx >= 0) & ~removed[b][np.clip(act, 0, None)]
+        m_ref = O.lsq_fill(idx, keep, a_idx, a_val, np.arange(lb, le))
+        got = m_c[b].cpu().numpy()
+        assert np.linalg.norm(got - m_ref) / np.linalg.norm(m_ref) < 1e-11

@@ -302,8 +302,9 @@ def main():
                          "or the normal equations from the Gram cache (lsq); auto: qr where the cached QR solve is "
                          "compiled (pattern lines <= 7 wide: c2, c4, c5s), lsq for c3's 13-wide lines")
     ap.add_argument("--no-graph", action="store_true", help="time eager steps (host launches) instead of graph replays")
-    ap.add_argument("--steps-per-graph", type=int, default=4,
-                    help="one GPU: consecutive steps captured in one HIP graph (1: one graph replay per step)")
+    ap.add_argument("--steps-per-graph", type=int, default=8,
+                    help="one GPU: at most this many consecutive steps captured in one HIP graph (the largest count "
+                         "that divides --steps; 1: one graph replay per step)")
     ap.add_argument("--overlap", default="sort", choices=["sort", "fill", "none"],
                     help="one GPU: the fill + rewards on a second stream beside the trajectory sort, the sort "
                          "launched first (sort) or the fill first (fill); none: one stream")
@@ -469,6 +470,8 @@ def main():
             # ~12 us between two graph launches is paid once per spg steps (every step is still a
             # whole sample_states: its own select, sort, fill and Log, its own Philox stream id)
             spg = max(1, args.steps_per_graph) if all(not c for _, c in phases) else 1
+            while args.steps % spg:  # the largest count <= --steps-per-graph that divides the timed steps
+                spg -= 1
             if spg > 1:
                 gm = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(gm, pool=pool):

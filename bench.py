@@ -447,7 +447,10 @@ def main():
                     continue
                 if run:
                     g = torch.cuda.CUDAGraph()
-                    with torch.cuda.graph(g, pool=pool):
+                    if dist_on:  # no collective of the previous eager phase still in flight on RCCL's stream
+                        torch.cuda.synchronize()
+                    # thread_local: a HIP call from an RCCL helper thread cannot invalidate this capture
+                    with torch.cuda.graph(g, pool=pool, capture_error_mode="thread_local" if dist_on else "global"):
                         for f in run:
                             f(st)
                     pool = g.pool()

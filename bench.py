@@ -108,13 +108,14 @@ def fill_bytes(env, B, store_m: bool = True) -> float:
     Gram-cached path (the env's default for widths <= 7): per line the action ids and the
     Gram values (T + Wc, fp32 when the cache round-trips exactly, else fp64), per sample the
     removal bitmap and the stored values of M."""
+    from gflownet_spai_amd import kernels
     n, W = env.pattern.n, env.pattern.width
     s = env.a_lines.val.element_size() if env._lsq else 4
     per_sample = math.ceil(env.init_nnz / 32) * 4 + (n * W * s if store_m else 0) + 8
     if getattr(env, "rcache", None) is not None:  # QR fill: the action ids + the env-constant R cache
-        line = n * W * 4 + env.rcache.numel() * env.rcache.element_size()
+        line = n * W * 4 + kernels.rcache_nbytes(env.rcache)
     elif getattr(env, "gram", None) is not None:
-        line = n * W * 4 + env.gram.numel() * env.gram.element_size() + (n * W * 4 if env.fill == "copy" else 0)
+        line = n * W * 4 + kernels.cache_nbytes(env.gram) + (n * W * 4 if env.fill == "copy" else 0)
     else:
         sa = env.a_lines.val.element_size()
         line = n * W * (4 + 4 + 4) + n * env.a_lines.width * (4 + sa)
@@ -588,8 +589,10 @@ def main():
             if env.rcache is not None:  # phase 2 from the R cache: its bytes are the cache + the per-sample stream
                 out["roofline"] = roofline_obj(
                     f"k_qr_solve<{env.pattern.width}> (LSQ fill of M by Householder QR: masked re-triangularisation of "
-                    f"each line's cached R (the full block A[I, slots] factored once per env, rows {env.qr_rows}) + "
-                    f"||AM-I||^2)", fb, fill_ms, measured_traffic(args.config + "_qr", bl))
+                    f"each line's cached R (the full block A[I, slots] factored once per env, rows {env.qr_rows}"
+                    + (f"; the cache as its dictionary: {env.rcache.entries} distinct line entries"
+                       if isinstance(env.rcache, kernels.QrDict) else "") +
+                    ") + ||AM-I||^2)", fb, fill_ms, measured_traffic(args.config + "_qr", bl))
             else:
                 out["roofline"] = roofline_obj(f"k_qr_fill<{env.pattern.width},rows {env.qr_rows}> (LSQ fill of M by "
                                                f"Householder QR of each line's block A[I, J] + ||AM-I||^2)", sbq,

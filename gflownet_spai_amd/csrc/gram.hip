@@ -99,11 +99,14 @@ __global__ __launch_bounds__(kNT) void k_gram_build(int32_t n, int32_t wrt, int3
 // consecutive lines are consecutive doubles), then the thread solves every sample; the
 // squared line residuals of a chunk of kChunk samples go to LDS and are summed per sample
 // by one wave each in a fixed order (two barriers per chunk, none per sample).
-template <int W, typename TM, bool LSQ, typename GT>
+// kDict: gram is the cache's dictionary (spai_line_cache_dict: distinct entries of T + W values,
+// contiguous) and line_entry[j] names line j's entry; else the full cache, 64 lines interleaved.
+template <int W, typename TM, bool LSQ, typename GT, bool kDict>
 __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(W <= 5 ? FILL_WPE5 : 2))) void k_gram_fill(int32_t n, int32_t line_begin, int32_t line_end, int32_t wrt,
                                                    const int32_t* __restrict__ pat_act,
                                                    const float* __restrict__ pat_val,
-                                                   const GT* __restrict__ gram, int32_t B,
+                                                   const GT* __restrict__ gram,
+                                                   const int32_t* __restrict__ line_entry, int32_t B,
                                                    const uint32_t* __restrict__ removed, int32_t words,
                                                    int32_t word_base, TM* __restrict__ m_out,
                                                    double* __restrict__ partials) {
@@ -126,11 +129,12 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(W <= 5 ? FI
     val[p] = (!LSQ && valid && p < wrt) ? pat_val[(int64_t)jj * wrt + p] : 0.0f;
   }
   double G[T], c[W];
-  const GT* gp = gram + (int64_t)(jj >> 6) * (T + W) * 64 + (jj & 63);  // blocked: one 64-line block contiguous
+  constexpr int kStride = kDict ? 1 : 64;  // blocked: one 64-line block contiguous
+  const GT* gp = kDict ? gram + (int64_t)line_entry[jj] * (T + W) : gram + (int64_t)(jj >> 6) * (T + W) * 64 + (jj & 63);
 #pragma unroll
-  for (int q = 0; q < T; ++q) G[q] = (double)gp[q * 64];  // fp32 storage only when exact (spai_gram_compact)
+  for (int q = 0; q < T; ++q) G[q] = (double)gp[q * kStride];  // fp32 storage only when exact (spai_gram_compact)
 #pragma unroll
-  for (int p = 0; p < W; ++p) c[p] = (double)gp[(T + p) * 64];
+  for (int p = 0; p < W; ++p) c[p] = (double)gp[(T + p) * kStride];
   int wofs[W];  // bitmap word offsets / bit positions of the slots
 #pragma unroll
   for (int p = 0; p < W; ++p) wofs[p] = act[p] >= 0 ? (act[p] >> 5) - word_base : 0;  // row-relative
@@ -310,11 +314,15 @@ __device__ __forceinline__ double wide_lsq_solve(double (&a)[tri(W)], double (&y
 // per sample (left-looking LDL^T, T = W(W+1)/2 doubles in registers), one wave per SIMD.
 // Masking and the per-pivot floor are those of k_gram_fill: a removed slot k only gets
 // 1/D_k := 0, so L[.][k] = 0 and m_k = 0.
-template <int W, typename TM, bool LSQ, typename GT>
-__global__ __launch_bounds__(kNT) void k_gram_fill_wide(int32_t n, int32_t line_begin, int32_t line_end, int32_t wrt,
+// kDict: the dictionary form of the cache (as k_gram_fill).  Its few entries stay in the caches,
+// so the line's Gram values are re-read for every sample instead of held in registers: one
+// packed working copy (~250 VGPRs), two waves per SIMD.
+template <int W, typename TM, bool LSQ, typename GT, bool kDict>
+__global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(kDict ? 2 : 1))) void k_gram_fill_wide(int32_t n, int32_t line_begin, int32_t line_end, int32_t wrt,
                                                         const int32_t* __restrict__ pat_act,
                                                         const float* __restrict__ pat_val,
-                                                        const GT* __restrict__ gram, int32_t B,
+                                                        const GT* __restrict__ gram,
+                                                        const int32_t* __restrict__ line_entry, int32_t B,
                                                         const uint32_t* __restrict__ removed, int32_t words,
                                                         int32_t word_base, TM* __restrict__ m_out,
                                                         double* __restrict__ partials) {
@@ -323,8 +331,9 @@ __global__ __launch_bounds__(kNT) void k_gram_fill_wide(int32_t n, int32_t line_
   // per-sample line residuals of a chunk of kChunk samples (summed after the chunk: one barrier
   // pair per chunk, not per sample) and M staged through two LDS buffers (sample b writes buffer
   // b & 1 while sample b - 1's stores may still read the other)
+  // (kDict: ONE M buffer, a barrier before it is rewritten: <= 80 KB of LDS, two blocks per CU)
   __shared__ double s_r2[kChunk][kNT];
-  __shared__ __attribute__((aligned(16))) TM s_m[2][kNT * W];
+  __shared__ __attribute__((aligned(16))) TM s_m[kDict ? 1 : 2][kNT * W];
   __shared__ int32_t s_act[W][kNT];  // action ids of the slots (LDS, not registers: G needs them)
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int lb = blockIdx.x;
@@ -339,29 +348,49 @@ __global__ __launch_bounds__(kNT) void k_gram_fill_wide(int32_t n, int32_t line_
 #pragma unroll
     for (int p = 0; p < W; ++p) s_act[p][t] = (valid && p < wrt) ? av[p] : -1;
   }
-  const GT* gp = gram + (int64_t)(jj >> 6) * (T + W) * 64 + (jj & 63);
+  constexpr int kStride = kDict ? 1 : 64;
+  const GT* gp = kDict ? gram + (int64_t)line_entry[jj] * (T + W) : gram + (int64_t)(jj >> 6) * (T + W) * 64 + (jj & 63);
   const int nvl = min(kNT, line_end - (line_begin + lb * kNT));
-  // the slots' bitmap words of the next sample are loaded while the current one is solved
-  uint32_t wd[W];
+  // the slots' bitmap words of the next sample are loaded while the current one is solved (kDict:
+  // loaded per sample, no registers held across the samples; the other wave of the SIMD hides them)
+  constexpr int kWd = kDict ? 1 : W;
+  uint32_t wd[kWd];
+  if constexpr (!kDict) {
 #pragma unroll
-  for (int p = 0; p < W; ++p) {
-    const int ap = s_act[p][t];
-    wd[p] = removed[ap >= 0 ? (ap >> 5) - word_base : 0];  // unconditional (masked at use): no branch per slot
+    for (int p = 0; p < W; ++p) {
+      const int ap = s_act[p][t];
+      wd[p] = removed[ap >= 0 ? (ap >> 5) - word_base : 0];  // unconditional (masked at use): no branch per slot
+    }
   }
 #pragma unroll 1
   for (int b = 0; b < B; ++b) {
     uint32_t keep = 0;
-#pragma unroll
-    for (int p = 0; p < W; ++p) {
-      const int ap = s_act[p][t];
-      keep |= (uint32_t)((ap >= 0) & !((wd[p] >> (ap & 31)) & 1u)) << p;
-    }
-    if (b + 1 < B) {
-      const uint32_t* rn = removed + (int64_t)(b + 1) * words;
+    if constexpr (kDict) {
+      const uint32_t* rb = removed + (int64_t)b * words;
+      uint32_t wv[W];
 #pragma unroll
       for (int p = 0; p < W; ++p) {
         const int ap = s_act[p][t];
-        wd[p] = rn[ap >= 0 ? (ap >> 5) - word_base : 0];
+        wv[p] = rb[ap >= 0 ? (ap >> 5) - word_base : 0];
+      }
+#pragma unroll
+      for (int p = 0; p < W; ++p) {
+        const int ap = s_act[p][t];
+        keep |= (uint32_t)((ap >= 0) & !((wv[p] >> (ap & 31)) & 1u)) << p;
+      }
+    } else {
+#pragma unroll
+      for (int p = 0; p < W; ++p) {
+        const int ap = s_act[p][t];
+        keep |= (uint32_t)((ap >= 0) & !((wd[p] >> (ap & 31)) & 1u)) << p;
+      }
+      if (b + 1 < B) {
+        const uint32_t* rn = removed + (int64_t)(b + 1) * words;
+#pragma unroll
+        for (int p = 0; p < W; ++p) {
+          const int ap = s_act[p][t];
+          wd[kDict ? 0 : p] = rn[ap >= 0 ? (ap >> 5) - word_base : 0];
+        }
       }
     }
     double a[T], y[W];
@@ -370,12 +399,13 @@ __global__ __launch_bounds__(kNT) void k_gram_fill_wide(int32_t n, int32_t line_
     // no spills).  Re-reading them per sample instead (an opaque address, 254 VGPRs, two waves
     // per SIMD) measured 286 vs 183 us at C3: the L2 re-reads cost more than the occupancy buys.
     const GT* gps = gp;  // fp32 storage only when exact (spai_gram_compact): the same values
+    if constexpr (kDict) asm volatile("" : "+v"(gps));  // re-read per sample (cache hits), not held
 #pragma unroll
-    for (int q = 0; q < T; ++q) a[q] = (double)gps[q * 64];
+    for (int q = 0; q < T; ++q) a[q] = (double)gps[q * kStride];
     double r2 = 1.0;
     if constexpr (LSQ) {
 #pragma unroll
-      for (int k = 0; k < W; ++k) y[k] = (double)gps[(T + k) * 64];  // c, solved in place below
+      for (int k = 0; k < W; ++k) y[k] = (double)gps[(T + k) * kStride];  // c, solved in place below
       r2 = wide_lsq_solve<W>(a, y, keep);
     } else {
 #pragma unroll
@@ -383,7 +413,7 @@ __global__ __launch_bounds__(kNT) void k_gram_fill_wide(int32_t n, int32_t line_
         y[p] = ((keep >> p) & 1u) ? (double)pat_val[(int64_t)jj * wrt + (p < wrt ? p : 0)] : 0.0;
 #pragma unroll
       for (int p = 0; p < W; ++p) {
-        double acc = y[p] * a[gidx<W>(p, p)] - 2.0 * (double)gps[(T + p) * 64];
+        double acc = y[p] * a[gidx<W>(p, p)] - 2.0 * (double)gps[(T + p) * kStride];
 #pragma unroll
         for (int q = p + 1; q < W; ++q) acc += 2.0 * y[q] * a[gidx<W>(p, q)];
         r2 += y[p] * acc;
@@ -391,7 +421,8 @@ __global__ __launch_bounds__(kNT) void k_gram_fill_wide(int32_t n, int32_t line_
     }
     s_r2[b % kChunk][t] = valid ? r2 : 0.0;
     {  // M (no branch on m_out: store_m_block drops every store when it is null)
-      TM* sm = s_m[b & 1];
+      TM* sm = s_m[kDict ? 0 : (b & 1)];
+      if constexpr (kDict) __syncthreads();  // the previous sample's stores have read the buffer
       if (valid) {
 #pragma unroll
         for (int p = 0; p < W; ++p)
@@ -417,23 +448,32 @@ __global__ __launch_bounds__(kNT) void k_gram_fill_wide(int32_t n, int32_t line_
 
 static int gram_width(int32_t W) { return W <= 5 ? 5 : (W <= 7 ? 7 : (W <= 13 ? 13 : 0)); }
 
+template <int W, typename TM, bool LSQ, typename GT, bool kDict>
+void launch_fill_t(int32_t n, int32_t lb, int32_t le, int32_t wrt, const int32_t* pa, const float* pv, const void* g,
+                   const int32_t* ent, int32_t B, const uint32_t* rm, int32_t words, int32_t wb, void* mo,
+                   double* partials, int32_t nparts, hipStream_t s) {
+  if constexpr (W > 7)
+    k_gram_fill_wide<W, TM, LSQ, GT, kDict><<<nparts, kNT, 0, s>>>(n, lb, le, wrt, pa, pv, static_cast<const GT*>(g),
+                                                                    ent, B, rm, words, wb, static_cast<TM*>(mo),
+                                                                    partials);
+  else
+    k_gram_fill<W, TM, LSQ, GT, kDict><<<nparts, kNT, 0, s>>>(n, lb, le, wrt, pa, pv, static_cast<const GT*>(g), ent,
+                                                               B, rm, words, wb, static_cast<TM*>(mo), partials);
+}
 template <int W, typename TM, bool LSQ>
 hipError_t launch_fill(int32_t n, int32_t lb, int32_t le, int32_t wrt, const int32_t* pa, const float* pv,
-                       const void* g, bool g32, int32_t B, const uint32_t* rm, int32_t words, int32_t wb,
-                       void* mo, double* partials, int32_t nparts, hipStream_t s) {
-  if constexpr (W > 7) {
-    if (g32)
-      k_gram_fill_wide<W, TM, LSQ, float><<<nparts, kNT, 0, s>>>(n, lb, le, wrt, pa, pv, static_cast<const float*>(g),
-                                                                  B, rm, words, wb, static_cast<TM*>(mo), partials);
+                       const void* g, bool g32, const int32_t* ent, int32_t B, const uint32_t* rm, int32_t words,
+                       int32_t wb, void* mo, double* partials, int32_t nparts, hipStream_t s) {
+  if (g32) {
+    if (ent)
+      launch_fill_t<W, TM, LSQ, float, true>(n, lb, le, wrt, pa, pv, g, ent, B, rm, words, wb, mo, partials, nparts, s);
     else
-      k_gram_fill_wide<W, TM, LSQ, double><<<nparts, kNT, 0, s>>>(n, lb, le, wrt, pa, pv, static_cast<const double*>(g),
-                                                                   B, rm, words, wb, static_cast<TM*>(mo), partials);
-  } else if (g32)
-    k_gram_fill<W, TM, LSQ, float><<<nparts, kNT, 0, s>>>(n, lb, le, wrt, pa, pv, static_cast<const float*>(g), B, rm,
-                                                           words, wb, static_cast<TM*>(mo), partials);
-  else
-    k_gram_fill<W, TM, LSQ, double><<<nparts, kNT, 0, s>>>(n, lb, le, wrt, pa, pv, static_cast<const double*>(g), B,
-                                                            rm, words, wb, static_cast<TM*>(mo), partials);
+      launch_fill_t<W, TM, LSQ, float, false>(n, lb, le, wrt, pa, pv, g, ent, B, rm, words, wb, mo, partials, nparts, s);
+  } else if (ent) {
+    launch_fill_t<W, TM, LSQ, double, true>(n, lb, le, wrt, pa, pv, g, ent, B, rm, words, wb, mo, partials, nparts, s);
+  } else {
+    launch_fill_t<W, TM, LSQ, double, false>(n, lb, le, wrt, pa, pv, g, ent, B, rm, words, wb, mo, partials, nparts, s);
+  }
   return hipGetLastError();
 }
 
@@ -506,41 +546,41 @@ extern "C" int spai_gram_compact(int32_t n, int32_t W, const double* gram, float
 }
 
 // Fill + per-block partial sums only (res2 partials stay in the workspace for spai_fill_reduce).
-extern "C" int spai_fill_lines_gram(int32_t fill_mode, int32_t n, int32_t line_begin, int32_t line_end, int32_t W,
-                                    const int32_t* pat_act, const float* pat_val, const void* gram,
-                                    int32_t gram_dtype, int32_t B, const uint32_t* removed, int32_t words,
-                                    int32_t word_base, void* m_out, int32_t m_dtype, void* workspace,
-                                    size_t workspace_bytes, void* stream) {
+static int fill_lines_gram(int32_t fill_mode, int32_t n, int32_t line_begin, int32_t line_end, int32_t W,
+                           const int32_t* pat_act, const float* pat_val, const void* gram, int32_t gram_dtype,
+                           const int32_t* line_entry, int32_t B, const uint32_t* removed, int32_t words,
+                           int32_t word_base, void* m_out, int32_t m_dtype, void* workspace, size_t workspace_bytes,
+                           void* stream) {
   SPAI_CHECK_ARG(fill_mode == SPAI_FILL_COPY || fill_mode == SPAI_FILL_LSQ,
-                 "spai_fill_lines_gram: bad fill_mode %d", fill_mode);
-  SPAI_CHECK_ARG(m_dtype == SPAI_DTYPE_F32 || m_dtype == SPAI_DTYPE_F64, "spai_fill_lines_gram: bad m_dtype");
+                 "spai_fill_lines_gram(_dict): bad fill_mode %d", fill_mode);
+  SPAI_CHECK_ARG(m_dtype == SPAI_DTYPE_F32 || m_dtype == SPAI_DTYPE_F64, "spai_fill_lines_gram(_dict): bad m_dtype");
   SPAI_CHECK_ARG(n >= 1 && line_begin >= 0 && line_end >= line_begin && line_end <= n && W >= 1 && B >= 1 &&
                      words >= 1 && word_base >= 0,
-                 "spai_fill_lines_gram: bad shape");
-  SPAI_CHECK_ARG(workspace != nullptr, "spai_fill_lines_gram: null workspace");
+                 "spai_fill_lines_gram(_dict): bad shape");
+  SPAI_CHECK_ARG(workspace != nullptr, "spai_fill_lines_gram(_dict): null workspace");
   SPAI_CHECK_ARG(fill_mode != SPAI_FILL_COPY || m_dtype == SPAI_DTYPE_F32,
-                 "spai_fill_lines_gram: copy fill stores fp32 values (utils.py:350)");
+                 "spai_fill_lines_gram(_dict): copy fill stores fp32 values (utils.py:350)");
   hipStream_t s = (hipStream_t)stream;
   const int32_t nl = line_end - line_begin;
   if (nl == 0) return SPAI_OK;
   SPAI_CHECK_ARG(pat_act && gram && removed && (fill_mode == SPAI_FILL_LSQ || pat_val),
-                 "spai_fill_lines_gram: null input");
+                 "spai_fill_lines_gram(_dict): null input");
   const int wc = gram_width(W);
   if (wc == 0) {
-    set_error("spai_fill_lines_gram: width W=%d above the compiled 13", W);
+    set_error("spai_fill_lines_gram(_dict): width W=%d above the compiled 13", W);
     return SPAI_ERR_UNSUPPORTED;
   }
-  SPAI_CHECK_ARG(gram_dtype == SPAI_DTYPE_F64 || gram_dtype == SPAI_DTYPE_F32, "spai_fill_lines_gram: gram dtype %d",
+  SPAI_CHECK_ARG(gram_dtype == SPAI_DTYPE_F64 || gram_dtype == SPAI_DTYPE_F32, "spai_fill_lines_gram(_dict): gram dtype %d",
                  gram_dtype);
   const bool g32 = gram_dtype == SPAI_DTYPE_F32;
   const int32_t nparts = (nl + kNT - 1) / kNT;
-  SPAI_CHECK_ARG(workspace_bytes >= sizeof(double) * (size_t)nparts * B, "spai_fill_lines_gram: workspace too small");
+  SPAI_CHECK_ARG(workspace_bytes >= sizeof(double) * (size_t)nparts * B, "spai_fill_lines_gram(_dict): workspace too small");
   double* partials = static_cast<double*>(workspace);
   const uint32_t* rm = removed;
   const int32_t wb = word_base;
   hipError_t e;
   const bool lsq = fill_mode == SPAI_FILL_LSQ, f64 = m_dtype == SPAI_DTYPE_F64;
-#define SPAI_FILL_ARGS n, line_begin, line_end, W, pat_act, pat_val, gram, g32, B, rm, words, wb, m_out, partials, nparts, s
+#define SPAI_FILL_ARGS n, line_begin, line_end, W, pat_act, pat_val, gram, g32, line_entry, B, rm, words, wb, m_out, partials, nparts, s
   if (wc == 5) {
     e = !lsq ? launch_fill<5, float, false>(SPAI_FILL_ARGS)
         : f64 ? launch_fill<5, double, true>(SPAI_FILL_ARGS)
@@ -557,6 +597,23 @@ extern "C" int spai_fill_lines_gram(int32_t fill_mode, int32_t n, int32_t line_b
 #undef SPAI_FILL_ARGS
   SPAI_CHECK_HIP(e);
   return SPAI_OK;
+}
+extern "C" int spai_fill_lines_gram(int32_t fill_mode, int32_t n, int32_t line_begin, int32_t line_end, int32_t W,
+                                    const int32_t* pat_act, const float* pat_val, const void* gram,
+                                    int32_t gram_dtype, int32_t B, const uint32_t* removed, int32_t words,
+                                    int32_t word_base, void* m_out, int32_t m_dtype, void* workspace,
+                                    size_t workspace_bytes, void* stream) {
+  return fill_lines_gram(fill_mode, n, line_begin, line_end, W, pat_act, pat_val, gram, gram_dtype, nullptr, B,
+                         removed, words, word_base, m_out, m_dtype, workspace, workspace_bytes, stream);
+}
+extern "C" int spai_fill_lines_gram_dict(int32_t fill_mode, int32_t n, int32_t line_begin, int32_t line_end,
+                                         int32_t W, const int32_t* pat_act, const float* pat_val, const void* dict,
+                                         int32_t gram_dtype, const int32_t* line_entry, int32_t B,
+                                         const uint32_t* removed, int32_t words, int32_t word_base, void* m_out,
+                                         int32_t m_dtype, void* workspace, size_t workspace_bytes, void* stream) {
+  SPAI_CHECK_ARG(line_entry != nullptr, "spai_fill_lines_gram_dict: null line_entry");
+  return fill_lines_gram(fill_mode, n, line_begin, line_end, W, pat_act, pat_val, dict, gram_dtype, line_entry, B,
+                         removed, words, word_base, m_out, m_dtype, workspace, workspace_bytes, stream);
 }
 
 extern "C" int spai_fill_reduce(int32_t n_lines, int32_t B, const void* workspace, double* res2_out,

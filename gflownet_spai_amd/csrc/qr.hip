@@ -24,6 +24,10 @@
 //      normal equations of gram.hip already drop a column whose remaining norm is below ~3e-7 of
 //      its norm: 1e-13 of the squared norm); back-substitution gives m, and the line residual^2
 //      is the tail + (Q^T e) below the pivots (sums of squares: no cancellation).
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
 #include "spai_device.h"
 #include "spai_status.h"
 
@@ -481,11 +485,15 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2))) void k_
 #ifndef QRS_WPE
 #define QRS_WPE 4
 #endif
-template <int W, typename TM>
+// kDict: rcache is the cache's dictionary (spai_qr_cache_dict: its distinct entries, NQ doubles
+// each, contiguous) and line_entry[j] names line j's entry; else the full cache, 64 lines
+// interleaved per entry value (coalesced).
+template <int W, typename TM, bool kDict>
 __global__ __launch_bounds__(kQNT) __attribute__((amdgpu_waves_per_eu(W <= 5 ? QRS_WPE : 2))) void k_qr_solve(
     int32_t line_begin, int32_t line_end, int32_t wrt, const int32_t* __restrict__ pat_act,
-    const double* __restrict__ rcache, int32_t B, const uint32_t* __restrict__ removed, int32_t words,
-    int32_t word_base, TM* __restrict__ m_out, double* __restrict__ partials) {
+    const double* __restrict__ rcache, const int32_t* __restrict__ line_entry, int32_t B,
+    const uint32_t* __restrict__ removed, int32_t words, int32_t word_base, TM* __restrict__ m_out,
+    double* __restrict__ partials) {
   constexpr int T = W * (W + 1) / 2, NQ = qr_cache_q(W);
   static_assert(kQNT == kQLines, "one thread per line of a 256-line block");
   __shared__ double s_r2[kQChunk][kQNT];
@@ -509,11 +517,13 @@ __global__ __launch_bounds__(kQNT) __attribute__((amdgpu_waves_per_eu(W <= 5 ? Q
   }
   double R0[T];
   float thf[W];  // the rank floors 1e-24 ||D[:, p]||^2 in fp32 (registers: 4 waves per SIMD at W = 5)
-  const double* rp = rcache + (int64_t)(jj >> 6) * NQ * 64 + (jj & 63);
+  // a dictionary entry is shared by most lanes of a wave (stencil lines): broadcast loads from L2
+  constexpr int kStride = kDict ? 1 : 64;
+  const double* rp = kDict ? rcache + (int64_t)line_entry[jj] * NQ : rcache + (int64_t)(jj >> 6) * NQ * 64 + (jj & 63);
 #pragma unroll
-  for (int q = 0; q < T; ++q) R0[q] = rp[q * 64];
+  for (int q = 0; q < T; ++q) R0[q] = rp[q * kStride];
 #pragma unroll
-  for (int p = 0; p <= W; ++p) s_c0[p][t] = rp[(T + p) * 64];  // read back by this thread only
+  for (int p = 0; p <= W; ++p) s_c0[p][t] = rp[(T + p) * kStride];  // read back by this thread only
 #pragma unroll
   for (int p = 0; p < W; ++p) {
     double s = 0.0;
@@ -654,16 +664,25 @@ hipError_t dispatch_factor(int wc, int rows, bool a32, int32_t n, int32_t wrt, c
 #undef SPAI_QF_ARGS
 }
 
-template <int W>
-hipError_t launch_solve(bool f64, int32_t lb, int32_t le, int32_t wrt, const int32_t* pa, const double* rc, int32_t B,
-                        const uint32_t* rm, int32_t words, int32_t wb, void* mo, double* partials, int32_t nparts,
-                        hipStream_t s) {
-  if (f64)
-    k_qr_solve<W, double><<<nparts, kQNT, 0, s>>>(lb, le, wrt, pa, rc, B, rm, words, wb, static_cast<double*>(mo),
-                                                  partials);
+template <int W, typename TM>
+void launch_solve_t(const int32_t* ent, int32_t lb, int32_t le, int32_t wrt, const int32_t* pa, const double* rc,
+                    int32_t B, const uint32_t* rm, int32_t words, int32_t wb, void* mo, double* partials,
+                    int32_t nparts, hipStream_t s) {
+  if (ent)
+    k_qr_solve<W, TM, true><<<nparts, kQNT, 0, s>>>(lb, le, wrt, pa, rc, ent, B, rm, words, wb, static_cast<TM*>(mo),
+                                                    partials);
   else
-    k_qr_solve<W, float><<<nparts, kQNT, 0, s>>>(lb, le, wrt, pa, rc, B, rm, words, wb, static_cast<float*>(mo),
-                                                 partials);
+    k_qr_solve<W, TM, false><<<nparts, kQNT, 0, s>>>(lb, le, wrt, pa, rc, nullptr, B, rm, words, wb,
+                                                     static_cast<TM*>(mo), partials);
+}
+template <int W>
+hipError_t launch_solve(bool f64, const int32_t* ent, int32_t lb, int32_t le, int32_t wrt, const int32_t* pa,
+                        const double* rc, int32_t B, const uint32_t* rm, int32_t words, int32_t wb, void* mo,
+                        double* partials, int32_t nparts, hipStream_t s) {
+  if (f64)
+    launch_solve_t<W, double>(ent, lb, le, wrt, pa, rc, B, rm, words, wb, mo, partials, nparts, s);
+  else
+    launch_solve_t<W, float>(ent, lb, le, wrt, pa, rc, B, rm, words, wb, mo, partials, nparts, s);
   return hipGetLastError();
 }
 
@@ -765,9 +784,10 @@ extern "C" int spai_qr_factor(int32_t n, int32_t W, const int32_t* pat_idx, cons
 }
 
 extern "C" int spai_fill_lines_qr_cached(int32_t n, int32_t line_begin, int32_t line_end, int32_t W, int32_t WA,
-                                         const int32_t* pat_act, const double* rcache, int32_t B,
-                                         const uint32_t* removed, int32_t words, int32_t word_base, void* m_out,
-                                         int32_t m_dtype, void* workspace, size_t workspace_bytes, void* stream) {
+                                         const int32_t* pat_act, const double* rcache, const int32_t* line_entry,
+                                         int32_t B, const uint32_t* removed, int32_t words, int32_t word_base,
+                                         void* m_out, int32_t m_dtype, void* workspace, size_t workspace_bytes,
+                                         void* stream) {
   SPAI_CHECK_ARG(m_dtype == SPAI_DTYPE_F32 || m_dtype == SPAI_DTYPE_F64, "spai_fill_lines_qr_cached: bad m_dtype");
   SPAI_CHECK_ARG(n >= 1 && line_begin >= 0 && line_end >= line_begin && line_end <= n && W >= 1 && WA >= 1 &&
                      B >= 1 && words >= 1 && word_base >= 0,
@@ -789,10 +809,60 @@ extern "C" int spai_fill_lines_qr_cached(int32_t n, int32_t line_begin, int32_t 
   hipStream_t s = (hipStream_t)stream;
   const bool f64 = m_dtype == SPAI_DTYPE_F64;
   const hipError_t e =
-      wc == 5 ? launch_solve<5>(f64, line_begin, line_end, W, pat_act, rcache, B, removed, words, word_base, m_out,
-                                partials, nparts, s)
-              : launch_solve<7>(f64, line_begin, line_end, W, pat_act, rcache, B, removed, words, word_base, m_out,
-                                partials, nparts, s);
+      wc == 5 ? launch_solve<5>(f64, line_entry, line_begin, line_end, W, pat_act, rcache, B, removed, words,
+                                word_base, m_out, partials, nparts, s)
+              : launch_solve<7>(f64, line_entry, line_begin, line_end, W, pat_act, rcache, B, removed, words,
+                                word_base, m_out, partials, nparts, s);
   SPAI_CHECK_HIP(e);
+  return SPAI_OK;
+}
+
+// ---- the dictionary of a per-line cache (the R cache, the Gram cache): its distinct line
+// entries, bitwise, once per env on the host
+extern "C" int spai_line_cache_dict(int32_t n, int32_t nq, int32_t elem_bytes, const void* cache, size_t cache_bytes,
+                                    int32_t max_entries, void* dict, size_t dict_bytes, int32_t* line_entry,
+                                    int32_t* entries_out, void* stream) {
+  SPAI_CHECK_ARG(n >= 1 && nq >= 1 && (elem_bytes == 4 || elem_bytes == 8) && max_entries >= 1 && cache && dict &&
+                     line_entry && entries_out,
+                 "spai_line_cache_dict: bad arguments");
+  const size_t groups = (size_t)(n + 63) / 64, eb = (size_t)nq * elem_bytes;
+  SPAI_CHECK_ARG(cache_bytes >= groups * 64 * eb, "spai_line_cache_dict: cache too small");
+  SPAI_CHECK_ARG(dict_bytes >= (size_t)max_entries * eb, "spai_line_cache_dict: dict too small");
+  std::vector<unsigned char> h(groups * 64 * eb);
+  hipStream_t s = (hipStream_t)stream;
+  SPAI_CHECK_HIP(hipMemcpyAsync(h.data(), cache, h.size(), hipMemcpyDeviceToHost, s));
+  SPAI_CHECK_HIP(hipStreamSynchronize(s));
+  // open addressing over FNV-1a hashes of the entries' bytes; equal entries compared bitwise
+  size_t cap = 1;
+  while (cap < 2 * (size_t)std::min<int64_t>(n, (int64_t)max_entries + 1)) cap <<= 1;
+  std::vector<int32_t> slot(cap, -1);
+  std::vector<unsigned char> uniq, e(eb);
+  std::vector<int32_t> ent(n);
+  int32_t count = 0;
+  for (int32_t j = 0; j < n; ++j) {
+    // value q of line j sits at ((j / 64) * nq + q) * 64 + j % 64 (blocks of 64 lines)
+    const unsigned char* g = h.data() + ((size_t)(j >> 6) * nq * 64 + (j & 63)) * elem_bytes;
+    for (int q = 0; q < nq; ++q) std::memcpy(e.data() + (size_t)q * elem_bytes, g + (size_t)q * 64 * elem_bytes, elem_bytes);
+    uint64_t hv = 1469598103934665603ull;
+    for (size_t k = 0; k < eb; ++k) hv = (hv ^ e[k]) * 1099511628211ull;
+    size_t i = hv & (cap - 1);
+    for (;;) {
+      const int32_t u = slot[i];
+      if (u < 0 || std::memcmp(uniq.data() + (size_t)u * eb, e.data(), eb) == 0) break;
+      i = (i + 1) & (cap - 1);
+    }
+    if (slot[i] < 0) {
+      if (count == max_entries) {  // too many distinct entries: the caller keeps the full cache
+        *entries_out = max_entries + 1;
+        return SPAI_OK;
+      }
+      slot[i] = count++;
+      uniq.insert(uniq.end(), e.begin(), e.end());
+    }
+    ent[j] = slot[i];
+  }
+  SPAI_CHECK_HIP(hipMemcpy(dict, uniq.data(), uniq.size(), hipMemcpyHostToDevice));
+  SPAI_CHECK_HIP(hipMemcpy(line_entry, ent.data(), (size_t)n * sizeof(int32_t), hipMemcpyHostToDevice));
+  *entries_out = count;
   return SPAI_OK;
 }

@@ -6,6 +6,7 @@ allocator on the current stream, and launches through ctypes.  No CPU fallback.
 from __future__ import annotations
 
 import contextlib
+import ctypes
 
 import torch
 
@@ -328,7 +329,25 @@ def gram_compact(gram: torch.Tensor, pattern: Lines):
     return g32 if int(exact.item()) == 1 else None
 
 
-def fill_residual_gram(pattern: Lines, gram: torch.Tensor, removed: torch.Tensor, lsq: bool, line_begin: int = 0,
+def _fill_lines_gram(mode, pattern: Lines, gram, line_begin: int, line_end: int, removed, word_base: int, m, m_dtype,
+                     ws):
+    """spai_fill_lines_gram from the full Gram cache, spai_fill_lines_gram_dict from its CacheDict."""
+    B, words = removed.shape
+    if isinstance(gram, CacheDict):
+        st = _l().spai_fill_lines_gram_dict(mode, pattern.n, line_begin, line_end, pattern.width,
+                                            _lib.ptr(pattern.act), _lib.ptr(pattern.val), _lib.ptr(gram.table),
+                                            _DT[gram.dtype], _lib.ptr(gram.entry), B, _lib.ptr(removed), words,
+                                            word_base, _lib.ptr(m), _DT[m_dtype], _lib.ptr(ws), ws.numel(),
+                                            _lib.stream_ptr(removed.device))
+    else:
+        st = _l().spai_fill_lines_gram(mode, pattern.n, line_begin, line_end, pattern.width, _lib.ptr(pattern.act),
+                                       _lib.ptr(pattern.val), _lib.ptr(gram), _DT[gram.dtype], B, _lib.ptr(removed),
+                                       words, word_base, _lib.ptr(m), _DT[m_dtype], _lib.ptr(ws), ws.numel(),
+                                       _lib.stream_ptr(removed.device))
+    _lib.check(st, "spai_fill_lines_gram")
+
+
+def fill_residual_gram(pattern: Lines, gram, removed: torch.Tensor, lsq: bool, line_begin: int = 0,
                        line_end: int | None = None, store_m: bool = False, m_dtype=torch.float32, word_base: int = 0,
                        limbs: bool = False):
     """fill_residual from the env's Gram cache (same outputs)."""
@@ -346,11 +365,7 @@ def fill_residual_gram(pattern: Lines, gram: torch.Tensor, removed: torch.Tensor
     nb = _l().spai_fill_workspace_bytes(max(n_loc, 1), B)
     ws = _lib.workspace(nb, removed.device, "fill")
     with _timed("fill_residual"):  # the fill kernel alone (the bench's roofline kernel)
-        st = _l().spai_fill_lines_gram(mode, pattern.n, line_begin, line_end, pattern.width, _lib.ptr(pattern.act),
-                                       _lib.ptr(pattern.val), _lib.ptr(gram), _DT[gram.dtype], B, _lib.ptr(removed),
-                                       words, word_base, _lib.ptr(m), _DT[m_dtype], _lib.ptr(ws), ws.numel(),
-                                       _lib.stream_ptr(removed.device))
-    _lib.check(st, "spai_fill_lines_gram")
+        _fill_lines_gram(mode, pattern, gram, line_begin, line_end, removed, word_base, m, m_dtype, ws)
     _lib.check(_l().spai_fill_reduce(n_loc, B, _lib.ptr(ws), _lib.ptr(res2), _lib.ptr(lb),
                                      _lib.stream_ptr(removed.device)), "spai_fill_reduce")
     return (lb if limbs else res2), m
@@ -384,15 +399,69 @@ def qr_cache(pattern: Lines, a_lines: Lines, max_rows: int):
     return rc
 
 
+class CacheDict:
+    """A per-line cache (the R cache, the Gram cache) held as its dictionary (spai_line_cache_dict):
+    the distinct line entries ``table`` [entries * nq] and each line's entry ``entry`` [n] int32.
+    Accepted wherever the full cache is."""
+
+    def __init__(self, table: torch.Tensor, entry: torch.Tensor, entries: int):
+        self.table, self.entry, self.entries = table, entry, entries
+
+    @property
+    def dtype(self):
+        return self.table.dtype
+
+    @property
+    def nbytes(self) -> int:
+        return self.table.numel() * self.table.element_size() + self.entry.numel() * self.entry.element_size()
+
+
+QrDict = CacheDict  # (the R cache's dictionary)
+
+
+def cache_nbytes(cache) -> int:
+    """Bytes one rollout's fill reads of a per-line cache (full tensor or CacheDict)."""
+    return cache.nbytes if isinstance(cache, CacheDict) else cache.numel() * cache.element_size()
+
+
+rcache_nbytes = cache_nbytes
+
+
+def cache_dict(cache: torch.Tensor, n: int, max_frac: float = 0.25):
+    """A per-line cache in the blocked layout ([ceil(n/64)][nq][64]) as a CacheDict when its lines
+    have at most max_frac * n distinct entries (a stencil's interior lines share one: the same A
+    values in the same relative positions give the same cached values bit for bit), else None
+    (keep the full cache).  Env setup: one host round trip."""
+    lib = _l()
+    es = cache.element_size()
+    nq = cache.numel() // ((n + 63) // 64 * 64)
+    cap = max(1, int(n * max_frac))
+    table = torch.empty(cap * nq, dtype=cache.dtype, device=cache.device)
+    entry = torch.empty(n, dtype=torch.int32, device=cache.device)
+    cnt = ctypes.c_int32(0)
+    _lib.check(lib.spai_line_cache_dict(n, nq, es, _lib.ptr(cache), cache.numel() * es, cap, _lib.ptr(table),
+                                        table.numel() * es, _lib.ptr(entry), ctypes.byref(cnt),
+                                        _lib.stream_ptr(cache.device)), "spai_line_cache_dict")
+    if cnt.value > cap:
+        return None
+    return CacheDict(table[:cnt.value * nq].clone(), entry, cnt.value)
+
+
+def qr_dict(rcache: torch.Tensor, pattern: Lines, a_lines: Lines | None = None, max_frac: float = 0.25):
+    """The R cache as a CacheDict, or None (cache_dict)."""
+    return cache_dict(rcache, pattern.n, max_frac)
+
+
 def _fill_lines_qr(pattern: Lines, a_lines: Lines, max_rows: int, removed: torch.Tensor, line_begin: int,
-                   line_end: int, m, m_dtype, word_base: int, ws, rcache: torch.Tensor | None = None):
+                   line_end: int, m, m_dtype, word_base: int, ws, rcache=None):
     B, words = removed.shape
-    if rcache is not None:  # phase 2 only, from the env's R cache
+    if rcache is not None:  # phase 2 only, from the env's R cache (full, or its dictionary)
+        tab, ent = (rcache.table, rcache.entry) if isinstance(rcache, QrDict) else (rcache, None)
         with _timed("fill_residual"):  # the fill kernel alone
             st = _l().spai_fill_lines_qr_cached(pattern.n, line_begin, line_end, pattern.width, a_lines.width,
-                                                _lib.ptr(pattern.act), _lib.ptr(rcache), B, _lib.ptr(removed), words,
-                                                word_base, _lib.ptr(m), _DT[m_dtype], _lib.ptr(ws), ws.numel(),
-                                                _lib.stream_ptr(removed.device))
+                                                _lib.ptr(pattern.act), _lib.ptr(tab), _lib.ptr(ent), B,
+                                                _lib.ptr(removed), words, word_base, _lib.ptr(m), _DT[m_dtype],
+                                                _lib.ptr(ws), ws.numel(), _lib.stream_ptr(removed.device))
         _lib.check(st, "spai_fill_lines_qr_cached")
         return
     av = narrow_values(a_lines)  # fp32-exact A values are staged as fp32 (the same numbers)
@@ -406,7 +475,7 @@ def _fill_lines_qr(pattern: Lines, a_lines: Lines, max_rows: int, removed: torch
 
 def fill_residual_qr(pattern: Lines, a_lines: Lines, max_rows: int, removed: torch.Tensor, line_begin: int = 0,
                      line_end: int | None = None, store_m: bool = False, m_dtype=torch.float64, word_base: int = 0,
-                     limbs: bool = False, rcache: torch.Tensor | None = None):
+                     limbs: bool = False, rcache=None):
     """The least-squares fill by Householder QR (spai_fill_lines_qr, or spai_fill_lines_qr_cached from
     an R cache, + spai_fill_reduce): same outputs as fill_residual with lsq=True (res2 [B] or exact
     limbs, M or None)."""
@@ -477,7 +546,7 @@ def rewards(res2: torch.Tensor, counts: torch.Tensor, nnz0: int, n: int, r0: flo
     return residual, reward, reward32
 
 
-def fill_rewards_gram(pattern: Lines, gram: torch.Tensor, removed: torch.Tensor, lsq: bool, counts: torch.Tensor,
+def fill_rewards_gram(pattern: Lines, gram, removed: torch.Tensor, lsq: bool, counts: torch.Tensor,
                       nnz0: int, r0: float, f0: int, alpha: torch.Tensor, store_m: bool = False,
                       m_dtype=torch.float32):
     """One GPU, all lines: the Gram-cached fill, then the exact residual sums and the rewards in
@@ -493,10 +562,7 @@ def fill_rewards_gram(pattern: Lines, gram: torch.Tensor, removed: torch.Tensor,
     m = torch.empty(B, n, pattern.width, dtype=m_dtype, device=removed.device) if store_m else None
     ws = _lib.workspace(_l().spai_fill_workspace_bytes(n, B), removed.device, "fill")
     with _timed("fill_residual"):  # the fill kernel alone (the bench's roofline kernel)
-        st = _l().spai_fill_lines_gram(mode, n, 0, n, pattern.width, _lib.ptr(pattern.act), _lib.ptr(pattern.val),
-                                       _lib.ptr(gram), _DT[gram.dtype], B, _lib.ptr(removed), words, 0, _lib.ptr(m),
-                                       _DT[m_dtype], _lib.ptr(ws), ws.numel(), _lib.stream_ptr(removed.device))
-    _lib.check(st, "spai_fill_lines_gram")
+        _fill_lines_gram(mode, pattern, gram, 0, n, removed, 0, m, m_dtype, ws)
     return _reduce_rewards(ws, n, B, counts, nnz0, r0, f0, alpha, removed.device) + (m,)
 
 
@@ -514,7 +580,7 @@ def _reduce_rewards(ws, n, B, counts, nnz0, r0, f0, alpha, device):
 
 def fill_rewards_qr(pattern: Lines, a_lines: Lines, max_rows: int, removed: torch.Tensor, counts: torch.Tensor,
                     nnz0: int, r0: float, f0: int, alpha: torch.Tensor, store_m: bool = False,
-                    m_dtype=torch.float64, rcache: torch.Tensor | None = None):
+                    m_dtype=torch.float64, rcache=None):
     """fill_rewards_gram with the Householder-QR fill (spai_fill_lines_qr[_cached] + spai_fill_reduce_rewards)."""
     _lib.require_device(removed)
     removed = removed.contiguous()

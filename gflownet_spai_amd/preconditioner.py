@@ -21,6 +21,10 @@ Extensions (keyword-only, defaults = reference behaviour):
   rcache=True         fill="qr": factor every line's full block once per env (spai_qr_factor) and
                       solve each rollout's masked problems from that R cache; False: the fused
                       kernel refactors every call
+  cache_dict=True     keep the Gram / R cache as its dictionary (kernels.CacheDict,
+                      spai_line_cache_dict) when at most a quarter of the lines have distinct
+                      entries — a stencil's interior lines share one: the same bits from fewer
+                      HBM bytes (and two waves per SIMD for the 8-13-wide Gram fill)
 Documented deviations: alpha is taken from the ``alpha`` argument (the reference reads
 the never-set ``self.alpha``, preconditioner.py:163); fp64 original matrices are
 accepted (the reference raises in torch.mm, utils.py:350); a raw COO pattern with
@@ -57,7 +61,7 @@ def _default_device():
 class PreconditionerEnv(Env):
     def __init__(self, matrix_size: int, initial_matrix: Tensor, original_matrix: Tensor, *, side: str = "MA",
                  fill: str = "copy", keep_m: bool = False, device=None, compact_gram: bool = True,
-                 rcache: bool = True):
+                 rcache: bool = True, cache_dict: bool = True):
         if side not in ("MA", "AM"):
             raise ValueError("side must be 'MA' or 'AM'")
         if fill not in ("copy", "lsq", "qr"):
@@ -105,6 +109,12 @@ class PreconditionerEnv(Env):
             g32 = kernels.gram_compact(self.gram, self.pattern)
             if g32 is not None:
                 self.gram = g32
+        if cache_dict:  # the caches' distinct line entries only (stencils: a handful)
+            for name in ("gram", "rcache"):
+                full = getattr(self, name)
+                d = kernels.cache_dict(full, matrix_size) if full is not None else None
+                if d is not None:
+                    setattr(self, name, d)
 
         self.orig_residual = self.calculate_residual(self.original_matrix, self.original_matrix)
         self._r0 = float(self.orig_residual)  # host copy: no device sync inside the reward formula

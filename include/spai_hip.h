@@ -290,9 +290,32 @@ size_t spai_qr_cache_bytes(int32_t n, int32_t W, int32_t WA);
 int spai_qr_factor(int32_t n, int32_t W, const int32_t* pat_idx, const int32_t* pat_act, int32_t WA,
                    const int32_t* a_idx, const void* a_val, int32_t a_dtype, int32_t max_rows, double* rcache,
                    size_t rcache_bytes, void* stream);
+/* line_entry: NULL, or rcache is the cache's dictionary (spai_line_cache_dict) and line_entry [n]
+ * names each line's entry. */
 int spai_fill_lines_qr_cached(int32_t n, int32_t line_begin, int32_t line_end, int32_t W, int32_t WA,
-                              const int32_t* pat_act, const double* rcache, int32_t B, const uint32_t* removed,
-                              int32_t words, int32_t word_base, void* m_out, int32_t m_dtype, void* workspace,
+                              const int32_t* pat_act, const double* rcache, const int32_t* line_entry, int32_t B,
+                              const uint32_t* removed, int32_t words, int32_t word_base, void* m_out,
+                              int32_t m_dtype, void* workspace, size_t workspace_bytes, void* stream);
+
+/* ---------------------------------------------------------------- cache dictionaries
+ * The dictionary of a per-line cache in the blocked layout of spai_qr_factor / spai_gram_build
+ * (value q of line j at ((j / 64) * nq + q) * 64 + j % 64, elem_bytes 8 or 4): its distinct line
+ * entries, compared bitwise, into dict ([entries][nq] contiguous) and per line the index of its
+ * entry into line_entry [n].  *entries_out = the number of distinct entries, or max_entries + 1
+ * (nothing written) when there are more.  Env setup: synchronises `stream` and reads the cache
+ * back to the host.  A stencil's interior lines share one entry (the same A values in the same
+ * relative positions give the same R / Gram values bit for bit), so the per-rollout fills
+ * (spai_fill_lines_qr_cached with line_entry, spai_fill_lines_gram_dict) read 4 bytes per line
+ * instead of nq values and run the same arithmetic on the same values: the same bits.  The wide
+ * (8-13) Gram fill re-reads its dictionary entry per sample instead of holding it in registers
+ * (two waves per SIMD instead of one).  No reference counterpart (env-constant layout). */
+int spai_line_cache_dict(int32_t n, int32_t nq, int32_t elem_bytes, const void* cache, size_t cache_bytes,
+                         int32_t max_entries, void* dict, size_t dict_bytes, int32_t* line_entry,
+                         int32_t* entries_out, void* stream);
+int spai_fill_lines_gram_dict(int32_t fill_mode, int32_t n, int32_t line_begin, int32_t line_end, int32_t W,
+                              const int32_t* pat_act, const float* pat_val, const void* dict, int32_t gram_dtype,
+                              const int32_t* line_entry, int32_t B, const uint32_t* removed, int32_t words,
+                              int32_t word_base, void* m_out, int32_t m_dtype, void* workspace,
                               size_t workspace_bytes, void* stream);
 
 /* ---------------------------------------------------------------- multi-GPU bitmap exchange

@@ -434,8 +434,8 @@ def test_fp32_gram_cache_is_bit_identical(side, fill, dims):
     from gflownet_spai_amd import PreconditionerEnv, kernels, poisson_2d, poisson_3d
     A = poisson_2d(40) if dims == 2 else poisson_3d(9)
     n = A.shape[0]
-    env32 = PreconditionerEnv(n, A, A, side=side, fill=fill)
-    env64 = PreconditionerEnv(n, A, A, side=side, fill=fill, compact_gram=False)
+    env32 = PreconditionerEnv(n, A, A, side=side, fill=fill, cache_dict=False)
+    env64 = PreconditionerEnv(n, A, A, side=side, fill=fill, compact_gram=False, cache_dict=False)
     assert env32.gram.dtype == torch.float32 and env64.gram.dtype == torch.float64
     assert torch.equal(env32.gram.double(), env64.gram)
     E = env32.init_nnz
@@ -807,3 +807,38 @@ def test_residual_lines_shared_pattern_and_conflicting_lanes(dims, exact):
         alone = kernels.residual_lines(torch.from_numpy(idx[b:b + 1]).to(DEV), torch.from_numpy(val[b:b + 1]).to(DEV),
                                        a_lines).cpu().numpy()
         assert alone[0] == got[b]
+
+
+@pytest.mark.parametrize("kind", ["2d_lsq", "2d_copy", "3d_axial", "3d_axial_f64"])
+def test_gram_dict_is_bit_identical(kind):
+    """The Gram cache held as its dictionary (spai_line_cache_dict + spai_fill_lines_gram_dict; the
+    13-wide fill re-reads its entry per sample at two waves per SIMD) against the full cache: M,
+    the residual sums (one launch, 256-line-aligned shards) and the rewards bit for bit, for the
+    5-wide and the 13-wide (C3 geometry) fills, fp32 and fp64 caches."""
+    from gflownet_spai_amd import PreconditionerEnv, axial_pattern_3d, kernels, poisson_2d, poisson_3d
+    from gflownet_spai_amd.distributed import LINE_ALIGN, shard_lines
+    fill, side = ("copy", "MA") if kind == "2d_copy" else ("lsq", "AM")
+    if kind.startswith("2d"):
+        A = P = poisson_2d(70)
+    else:
+        A, P = poisson_3d(16), axial_pattern_3d(16)
+        if kind.endswith("f64"):  # non-fp32-exact values: the fp64 cache
+            c = A.coalesce()
+            A = torch.sparse_coo_tensor(c.indices(), c.values() * (1.0 + 1e-9), c.shape).coalesce()
+    n = A.shape[0]
+    envd = PreconditionerEnv(n, P, A, side=side, fill=fill, keep_m=True)
+    envf = PreconditionerEnv(n, P, A, side=side, fill=fill, keep_m=True, cache_dict=False)
+    assert isinstance(envd.gram, kernels.CacheDict) and torch.is_tensor(envf.gram)
+    assert envd.gram.dtype == envf.gram.dtype == (torch.float64 if kind.endswith("f64") else torch.float32)
+    assert kernels.cache_nbytes(envd.gram) < kernels.cache_nbytes(envf.gram) / 4
+    E = envd.init_nnz
+    rng = np.random.default_rng(12)
+    acts = torch.from_numpy(np.where(rng.random((9, E)) < 0.25, np.arange(E), -1))
+    removed, counts = kernels.actions_to_removed(acts.to(DEV), E)
+    rd, rf = envd.fill_partial(removed), envf.fill_partial(removed)
+    assert torch.equal(rd, rf) and torch.equal(envd.last_m, envf.last_m)
+    for q in range(3):
+        lb, le = shard_lines(n, q, 3, LINE_ALIGN)
+        assert torch.equal(envd.fill_partial(removed, lb, le, limbs=True), envf.fill_partial(removed, lb, le, limbs=True))
+    assert torch.equal(envd.fill_rewards(removed, counts, torch.tensor(0.5)),
+                       envf.fill_rewards(removed, counts, torch.tensor(0.5)))

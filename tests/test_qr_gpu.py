@@ -296,3 +296,47 @@ def test_qr_cached_narrow_lines_and_small_batches(B):
         m_ref = O.lsq_fill(idx, keep, a_idx, a_val, np.arange(lb, le))
         got = m_c[b].cpu().numpy()
         assert np.linalg.norm(got - m_ref) / np.linalg.norm(m_ref) < 1e-11
+
+
+@pytest.mark.parametrize("kind", ["2d", "3d7", "1d", "random"])
+def test_qr_dict_equals_full_cache(kind):
+    """The R cache held as its dictionary (spai_line_cache_dict: the distinct line entries + each
+    line's entry) against the full cache: the same values reach the same arithmetic, so M, the
+    residual sums and the rewards are bit-identical, on one launch and on 256-line-aligned shards.
+    Stencils have a handful of distinct entries (the interior lines share one); a random matrix
+    has one per line and keeps the full cache."""
+    from gflownet_spai_amd import PreconditionerEnv, kernels, poisson_2d, poisson_3d
+    from gflownet_spai_amd.distributed import LINE_ALIGN, shard_lines
+    if kind == "1d":
+        n = 1000
+        i = torch.arange(n)
+        A = torch.sparse_coo_tensor(torch.stack([torch.cat([i, i[1:], i[:-1]]), torch.cat([i, i[:-1], i[1:]])]),
+                                    torch.cat([torch.full((n,), 2.0), torch.full((2 * n - 2,), -1.0)]).double(),
+                                    (n, n)).coalesce()
+    elif kind == "random":
+        A = _random_cols(1500, 5, 31)
+    else:
+        A = {"2d": lambda: poisson_2d(80, torch.float32), "3d7": lambda: poisson_3d(14)}[kind]()
+    n = A.shape[0]
+    envd = PreconditionerEnv(n, A, A, side="AM", fill="qr", keep_m=True)
+    envf = PreconditionerEnv(n, A, A, side="AM", fill="qr", keep_m=True, cache_dict=False)
+    assert torch.is_tensor(envf.rcache)
+    if kind == "random":
+        assert torch.is_tensor(envd.rcache)  # one entry per line: no dictionary
+        return
+    assert isinstance(envd.rcache, kernels.QrDict)
+    assert envd.rcache.entries <= {"2d": 40, "3d7": 150, "1d": 6}[kind], envd.rcache.entries
+    assert kernels.rcache_nbytes(envd.rcache) < kernels.rcache_nbytes(envf.rcache) / 4
+    removed = np.random.default_rng(6).random((9, envd.init_nnz)) < 0.25
+    bits = _bits(removed)
+    rd, rf = envd.fill_partial(bits), envf.fill_partial(bits)
+    assert torch.equal(rd, rf)
+    assert torch.equal(envd.last_m, envf.last_m)
+    for P in (2, 3):
+        for q in range(P):
+            lb, le = shard_lines(n, q, P, LINE_ALIGN)
+            assert torch.equal(envd.fill_partial(bits, lb, le, limbs=True), envf.fill_partial(bits, lb, le, limbs=True))
+    counts = torch.from_numpy(removed.sum(1).astype(np.int32)).to(DEV)
+    assert torch.equal(envd.fill_rewards(bits, counts, torch.tensor(0.5)),
+                       envf.fill_rewards(bits, counts, torch.tensor(0.5)))
+    assert torch.equal(envd.last_m, envf.last_m)

@@ -24,7 +24,8 @@ Extensions (keyword-only, defaults = reference behaviour):
   cache_dict=True     keep the Gram / R cache as its dictionary (kernels.CacheDict,
                       spai_line_cache_dict) when at most a quarter of the lines have distinct
                       entries — a stencil's interior lines share one: the same bits from fewer
-                      HBM bytes (and two waves per SIMD for the 8-13-wide Gram fill)
+                      HBM bytes (and two waves per SIMD for the 8-13-wide Gram fill; the
+                      5/7-wide Gram fill keeps its full cache: no gain measured)
 Documented deviations: alpha is taken from the ``alpha`` argument (the reference reads
 the never-set ``self.alpha``, preconditioner.py:163); fp64 original matrices are
 accepted (the reference raises in torch.mm, utils.py:350); a raw COO pattern with
@@ -109,10 +110,13 @@ class PreconditionerEnv(Env):
             g32 = kernels.gram_compact(self.gram, self.pattern)
             if g32 is not None:
                 self.gram = g32
-        if cache_dict:  # the caches' distinct line entries only (stencils: a handful)
+        if cache_dict:  # the caches' distinct line entries only (stencils: a handful); the 5/7-wide
+            # Gram fill streams its full cache as fast (coalesced, 4 waves per SIMD either way)
             for name in ("gram", "rcache"):
                 full = getattr(self, name)
-                d = kernels.cache_dict(full, matrix_size) if full is not None else None
+                if full is None or (name == "gram" and self.pattern.width <= 7):
+                    continue
+                d = kernels.cache_dict(full, matrix_size)
                 if d is not None:
                     setattr(self, name, d)
 

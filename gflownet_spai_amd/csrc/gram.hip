@@ -112,7 +112,11 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(W <= 5 ? FI
                                                    double* __restrict__ partials) {
   constexpr int T = tri(W);
   __shared__ double s_r2[kChunk][kNT];
+#ifdef FILL_BLOCK_M
   __shared__ __attribute__((aligned(16))) TM s_m[2][kNT * W];
+#else
+  __shared__ __attribute__((aligned(16))) TM s_m[1][kNT * W];  // per-wave regions
+#endif
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int lb = blockIdx.x;
   const int j = line_begin + lb * kNT + t;
@@ -211,6 +215,7 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(W <= 5 ? FI
           mr[k] = v;
         }
       }
+#ifdef FILL_BLOCK_M  // A/B: M staged per block (a block barrier per sample)
       if (m_out != nullptr) {
         // M through LDS (double-buffered per sample): the block's lines of one sample are one
         // contiguous run of nvl * wrt values, written with 16-byte stores
@@ -232,6 +237,21 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(W <= 5 ? FI
         }
         for (int e = e0 + t; e < ne; e += kNT) nt_store(dst + e, sm[e]);
       }
+#else
+      {  // M staged per WAVE (its 64 lines are one contiguous run of M): no block barrier per sample
+        TM* sm = s_m[0] + wave * 64 * W;
+        if (valid) {
+#pragma unroll
+          for (int p = 0; p < W; ++p)
+            if (p < wrt) sm[lane * wrt + p] = (TM)mr[p];
+        }
+        __builtin_amdgcn_wave_barrier();
+        const int nw = min(max(nvl - wave * 64, 0), 64);
+        store_m_block<64, W, TM>(m_out ? m_out + ((int64_t)b * nloc + (int64_t)lb * kNT + wave * 64) * wrt : nullptr,
+                                 sm, nw * wrt, lane);
+        __builtin_amdgcn_wave_barrier();
+      }
+#endif
       double r2 = 0.0;
       if (valid) {
         if constexpr (LSQ) {
@@ -333,7 +353,11 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(kDict ? 2 :
   // b & 1 while sample b - 1's stores may still read the other)
   // (kDict: ONE M buffer, a barrier before it is rewritten: <= 80 KB of LDS, two blocks per CU)
   __shared__ double s_r2[kChunk][kNT];
+#ifdef FILL_BLOCK_M
   __shared__ __attribute__((aligned(16))) TM s_m[kDict ? 1 : 2][kNT * W];
+#else
+  __shared__ __attribute__((aligned(16))) TM s_m[1][kNT * W];  // per-wave regions
+#endif
   __shared__ int32_t s_act[W][kNT];  // action ids of the slots (LDS, not registers: G needs them)
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int lb = blockIdx.x;
@@ -420,6 +444,7 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(kDict ? 2 :
       }
     }
     s_r2[b % kChunk][t] = valid ? r2 : 0.0;
+#ifdef FILL_BLOCK_M
     {  // M (no branch on m_out: store_m_block drops every store when it is null)
       TM* sm = s_m[kDict ? 0 : (b & 1)];
       if constexpr (kDict) __syncthreads();  // the previous sample's stores have read the buffer
@@ -431,6 +456,21 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(kDict ? 2 :
       __syncthreads();
       store_m_block<kNT, W, TM>(m_out ? m_out + ((int64_t)b * nloc + (int64_t)lb * kNT) * wrt : nullptr, sm, nvl * wrt);
     }
+#else
+    {  // M staged per WAVE (its 64 lines are one contiguous run of M): no block barrier per sample
+      TM* sm = s_m[0] + wave * 64 * W;
+      if (valid) {
+#pragma unroll
+        for (int p = 0; p < W; ++p)
+          if (p < wrt) sm[lane * wrt + p] = (TM)y[p];
+      }
+      __builtin_amdgcn_wave_barrier();
+      const int nw = min(max(nvl - wave * 64, 0), 64);
+      store_m_block<64, W, TM>(m_out ? m_out + ((int64_t)b * nloc + (int64_t)lb * kNT + wave * 64) * wrt : nullptr,
+                               sm, nw * wrt, lane);
+      __builtin_amdgcn_wave_barrier();
+    }
+#endif
     if (b % kChunk == kChunk - 1 || b == B - 1) {  // the chunk's fixed-order block sums
       const int c0 = b - b % kChunk, nb = b - c0 + 1;
       __syncthreads();

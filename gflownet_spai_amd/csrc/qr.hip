@@ -497,7 +497,11 @@ __global__ __launch_bounds__(kQNT) __attribute__((amdgpu_waves_per_eu(W <= 5 ? Q
   constexpr int T = W * (W + 1) / 2, NQ = qr_cache_q(W);
   static_assert(kQNT == kQLines, "one thread per line of a 256-line block");
   __shared__ double s_r2[kQChunk][kQNT];
+#ifndef QRS_WAVE_M
   __shared__ __attribute__((aligned(16))) TM s_m[2][kQNT * W];
+#else
+  __shared__ __attribute__((aligned(16))) TM s_m[1][kQNT * W];  // per-wave regions
+#endif
   __shared__ double s_c0[W + 1][kQNT];  // the line's Q^T e and tail (LDS, not registers: 4 waves per SIMD)
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int lb = blockIdx.x;
@@ -573,6 +577,8 @@ __global__ __launch_bounds__(kQNT) __attribute__((amdgpu_waves_per_eu(W <= 5 ? Q
         if (p < wrt) nt_store(dst + p, (TM)m[p]);
     }
 #else
+#ifndef QRS_WAVE_M  // M staged per block; QRS_WAVE_M (A/B): per wave, no block barrier per sample —
+                    // 6 VGPRs spilled at 128, 0.127 vs 0.106 ms at C4 (the Gram fills gain from it)
     {  // M (no branch on m_out: store_m_block drops every store when it is null)
       TM* sm = s_m[b & 1];
       if (valid) {
@@ -584,6 +590,21 @@ __global__ __launch_bounds__(kQNT) __attribute__((amdgpu_waves_per_eu(W <= 5 ? Q
       store_m_block<kQNT, W, TM>(m_out ? m_out + ((int64_t)b * nloc + (int64_t)lb * kQNT) * wrt : nullptr, sm,
                                  nvl * wrt);
     }
+#else
+    {  // M staged per WAVE (its 64 lines are one contiguous run of M): no block barrier per sample
+      TM* sm = s_m[0] + wave * 64 * W;
+      if (valid) {
+#pragma unroll
+        for (int p = 0; p < W; ++p)
+          if (p < wrt) sm[lane * wrt + p] = (TM)m[p];
+      }
+      __builtin_amdgcn_wave_barrier();
+      const int nw = min(max(nvl - wave * 64, 0), 64);
+      store_m_block<64, W, TM>(m_out ? m_out + ((int64_t)b * nloc + (int64_t)lb * kQNT + wave * 64) * wrt : nullptr,
+                               sm, nw * wrt, lane);
+      __builtin_amdgcn_wave_barrier();
+    }
+#endif
 #endif
     if (b % kQChunk == kQChunk - 1 || b == B - 1) {  // the chunk's fixed-order block sums
       const int c0b = b - b % kQChunk, nb = b - c0b + 1;

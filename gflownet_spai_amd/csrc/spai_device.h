@@ -30,12 +30,14 @@ typedef unsigned int u4v __attribute__((ext_vector_type(4)));
 // dropped.  No branch skips a store, so the compiler's wait for the next sample's bitmap words
 // (loaded before these stores; vmcnt counts in order) is vmcnt(stores), not vmcnt(0): a drain of
 // the M stores per sample is an HBM write latency per sample.
+// NT = 64 with t = the lane: one wave stores its own 64 lines (no block barrier before it: a
+// wave's LDS operations complete in order).
 template <int NT, int W, typename TM>
-__device__ __forceinline__ void store_m_block(TM* dst, const TM* sm, int ne) {
+__device__ __forceinline__ void store_m_block(TM* dst, const TM* sm, int ne, int t = (int)threadIdx.x) {
   constexpr int kV = 16 / (int)sizeof(TM), kChunks = NT * W / kV;
   constexpr int kSt = (kChunks + NT - 1) / NT;
   static_assert(NT * W % kV == 0, "whole 16-byte chunks in the staging buffer");
-  const int t = threadIdx.x, nfull = ne / kV;
+  const int nfull = ne / kV;
   const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(dst, 0, dst ? nfull * 16 : 0, kBufWord3);
   const __amdgpu_buffer_rsrc_t re =
       __builtin_amdgcn_make_buffer_rsrc(dst, 0, dst ? ne * (int)sizeof(TM) : 0, kBufWord3);

@@ -592,15 +592,16 @@ __global__ __launch_bounds__(kQNT) __attribute__((amdgpu_waves_per_eu(W <= 5 ? Q
     }
 #else
     {  // M staged per WAVE (its 64 lines are one contiguous run of M): no block barrier per sample
-      TM* sm = s_m[0] + wave * 64 * W;
+      const int wv = __builtin_amdgcn_readfirstlane(wave);  // wave-uniform: scalar offsets
+      TM* sm = s_m[0] + wv * 64 * W;
       if (valid) {
 #pragma unroll
         for (int p = 0; p < W; ++p)
           if (p < wrt) sm[lane * wrt + p] = (TM)m[p];
       }
       __builtin_amdgcn_wave_barrier();
-      const int nw = min(max(nvl - wave * 64, 0), 64);
-      store_m_block<64, W, TM>(m_out ? m_out + ((int64_t)b * nloc + (int64_t)lb * kQNT + wave * 64) * wrt : nullptr,
+      const int nw = min(max(nvl - wv * 64, 0), 64);
+      store_m_block<64, W, TM>(m_out ? m_out + ((int64_t)b * nloc + (int64_t)lb * kQNT + wv * 64) * wrt : nullptr,
                                sm, nw * wrt, lane);
       __builtin_amdgcn_wave_barrier();
     }

@@ -38,6 +38,9 @@ SIGNATURES = {
     "spai_rollout_workspace_bytes": (_c_sz, [_c_i32, _c_i32]),
     "spai_rollout_select": (ctypes.c_int, [_c_p, _c_i64, _c_i32, _c_i32, _c_p, _c_u64, _c_u64, _c_p, _c_i32, _c_i32,
                                            _c_i32, _c_p, _c_i32, _c_p, _c_p, _c_sz, _c_p]),
+    "spai_rollout_select_pm": (ctypes.c_int, [_c_p, _c_i64, _c_i32, _c_i32, _c_p, _c_p, _c_i32, _c_u64, _c_u64, _c_p,
+                                              _c_i32, _c_i32, _c_i32, _c_p, _c_i32, _c_p, _c_p, _c_sz, _c_p]),
+    "spai_policy_lmax_parts": (ctypes.c_int32, [_c_i32]),
     "spai_rollout_merge": (ctypes.c_int, [_c_p, _c_i64, _c_i32, _c_i32, _c_p, _c_i32, _c_i32, _c_p, _c_p, _c_sz,
                                           _c_p]),
     "spai_rollout_sort": (ctypes.c_int, [_c_p, _c_i64, _c_i32, _c_i32, _c_p, _c_i32, _c_i32, _c_i64, _c_p, _c_p,

@@ -505,7 +505,7 @@ void launch_policy(int32_t n, const float* x, const int32_t* rp, const int32_t* 
     k_pool<C><<<1, kRedNT, 0, s>>>(n, g2, w.part, w.hpool);
     k_fc<F, C, false><<<gf, kNT, 0, s>>>(na, fw, fb, w.hpool, x, p1, p2, logits, w.pmax);
   }
-  k_max<<<1, kRedNT, 0, s>>>(gf, w.pmax, lmax, B);
+  if (B > 0) k_max<<<1, kRedNT, 0, s>>>(gf, w.pmax, lmax, B);  // B == 0: the caller reduces w.pmax (= lmax)
 }
 
 template <int F>
@@ -553,6 +553,8 @@ extern "C" int spai_policy_rows_constant(int32_t n_nodes, int32_t fin, const flo
   return SPAI_OK;
 }
 
+extern "C" int32_t spai_policy_lmax_parts(int32_t num_actions) { return num_actions > 0 ? fc_blocks(num_actions) : 0; }
+
 extern "C" int spai_policy_logits(int32_t n_nodes, int32_t fin, int32_t hid, const float* x, const int32_t* rowptr,
                                   const int32_t* src, const float* eattr, const float* gat1, const float* gat2,
                                   const float* fc_w, const float* fc_b, int32_t num_actions, float* logits,
@@ -560,12 +562,13 @@ extern "C" int spai_policy_logits(int32_t n_nodes, int32_t fin, int32_t hid, con
                                   void* stream) {
   SPAI_CHECK_ARG(x && gat1 && gat2 && fc_w && fc_b && logits && lmax && (const_rows || (rowptr && src && eattr)),
                  "spai_policy_logits: null pointer");
-  SPAI_CHECK_ARG(n_nodes > 0 && num_actions > 0 && B > 0, "spai_policy_logits: bad shape");
+  SPAI_CHECK_ARG(n_nodes > 0 && num_actions > 0 && B >= 0, "spai_policy_logits: bad shape");
   SPAI_CHECK_ARG(((uintptr_t)fc_w & 15) == 0, "spai_policy_logits: fc weight must be 16-byte aligned");
   SPAI_CHECK_ARG(workspace && workspace_bytes >= spai_policy_workspace_bytes(n_nodes, hid, num_actions),
                  "spai_policy_logits: workspace too small");
   PolicyWs w;
   policy_ws(n_nodes, hid, num_actions, workspace, &w);
+  if (B == 0) w.pmax = lmax;  // deferred maximum: the fc block maxima go to the caller's buffer
   hipStream_t s = (hipStream_t)stream;
   bool ok = false;
   switch (fin) {

@@ -359,8 +359,37 @@ __global__ __launch_bounds__(kSampNT) void k_presample(const float* __restrict__
                                                        uint32_t st0, uint32_t st1, const uint64_t* __restrict__ sctr,
                                                        int32_t sample_base,
                                                        uint32_t* __restrict__ samp, int32_t* __restrict__ samp_cnt,
-                                                       int32_t* __restrict__ ctl, int32_t nctl, float* __restrict__ tE_out) {
+                                                       int32_t* __restrict__ ctl, int32_t nctl, float* __restrict__ tE_out,
+                                                       const float* __restrict__ lmax_parts, int32_t n_lmax_parts,
+                                                       float* __restrict__ lmax_out, int32_t B) {
   const int tid = threadIdx.x;
+  if (lmax_parts != nullptr && blockIdx.x == gridDim.x - 1) {
+    // the deferred logits maximum (spai_policy_logits with B = 0 left its fc block maxima): one block
+    // reduces them here, so the policy needs no reduction launch; its first reader is k_splitters
+    constexpr int kRound = 8;
+    float v = -INFINITY;
+#pragma unroll 1
+    for (int k0 = 0; k0 < n_lmax_parts; k0 += kRound * kSampNT) {
+      float x[kRound];
+#pragma unroll
+      for (int j = 0; j < kRound; ++j) {
+        const int k = k0 + j * kSampNT + tid;
+        x[j] = k < n_lmax_parts ? lmax_parts[k] : -INFINITY;
+      }
+#pragma unroll
+      for (int j = 0; j < kRound; ++j) v = fmaxf(v, x[j]);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, kWave));
+    __shared__ float s_mx[kSampNT / 64];
+    if ((tid & 63) == 0) s_mx[tid >> 6] = v;
+    __syncthreads();
+    float r = s_mx[0];
+#pragma unroll
+    for (int k = 1; k < kSampNT / 64; ++k) r = fmaxf(r, s_mx[k]);
+    for (int bb = tid; bb < B; bb += kSampNT) lmax_out[bb] = r;
+    return;
+  }
   stream_words(sctr, st0, st1);
   {  // the rollout's control block (bucket totals, oversized-bucket list count, tdev) starts at 0;
      // its first users (k_tile, k_sort2, k_bscan) run after this launch on the same stream
@@ -1683,14 +1712,16 @@ static void launch_merge(const TrajWs& w, int32_t E, int32_t B, int64_t bstride,
                              counts, w.wrest, w.tdev, w.bwsuf);
 }
 
-extern "C" int spai_rollout_select(const float* logits, int64_t bstride, int32_t E, int32_t B, const float* lmax,
-                                   uint64_t seed, uint64_t stream_id, uint64_t* stream_ctr, int32_t sample_base,
-                                   int32_t part, int32_t nparts, uint32_t* removed, int32_t words, int32_t* counts,
-                                   void* workspace, size_t workspace_bytes, void* stream) {
+static int rollout_select(const float* logits, int64_t bstride, int32_t E, int32_t B, const float* lmax,
+                          const float* lmax_parts, int32_t n_lmax_parts, uint64_t seed, uint64_t stream_id,
+                          uint64_t* stream_ctr, int32_t sample_base, int32_t part, int32_t nparts, uint32_t* removed,
+                          int32_t words, int32_t* counts, void* workspace, size_t workspace_bytes, void* stream) {
   TrajWs w;
   const int st = select_args(logits, lmax, E, B, bstride, sample_base, part, nparts, workspace, workspace_bytes, &w,
                              "spai_rollout_select");
   if (st != SPAI_OK) return st;
+  SPAI_CHECK_ARG(!lmax_parts || (n_lmax_parts > 0 && bstride == 0),
+                 "spai_rollout_select_pm: block maxima need n > 0 and one shared logits row");
   SPAI_CHECK_ARG(removed && counts, "spai_rollout_select: null pointer");
   SPAI_CHECK_ARG(words == (E + 31) / 32, "spai_rollout_select: words must be ceil(E/32)");
   hipStream_t s = (hipStream_t)stream;
@@ -1699,8 +1730,11 @@ extern "C" int spai_rollout_select(const float* logits, int64_t bstride, int32_t
   const int nsb = (w.M + kSampNT - 1) / kSampNT;
   const int nwb = (int)((w.wstride + kRwChunk - 1) / kRwChunk);  // rate/weight blocks per logits row
   const int64_t rowsel = bstride ? 1 : 0;
-  k_presample<<<nsb * B, kSampNT, 0, s>>>(logits, bstride, E, w.M, nsb, s0, s1, t0, t1, stream_ctr, sample_base,
-                                          w.samp, w.samp_cnt, w.ctl, 4, w.tE);
+  // (+1 block: the deferred logits maximum, when given)
+  k_presample<<<nsb * B + (lmax_parts ? 1 : 0), kSampNT, 0, s>>>(logits, bstride, E, w.M, nsb, s0, s1, t0, t1,
+                                                                 stream_ctr, sample_base, w.samp, w.samp_cnt, w.ctl, 4,
+                                                                 w.tE, lmax_parts, n_lmax_parts,
+                                                                 const_cast<float*>(lmax), B);
   SPAI_CHECK_LAUNCH();
   k_splitters<<<B + nwb * (bstride ? B : 1), kSortNT, 0, s>>>(E, w.M, nsb, w.samp, w.samp_cnt, w.nb, w.spl, w.lut,
                                                              w.lut_base, B, logits, bstride, lmax, w.rr, w.ww,
@@ -1718,6 +1752,24 @@ extern "C" int spai_rollout_select(const float* logits, int64_t bstride, int32_t
     SPAI_CHECK_LAUNCH();
   }
   return SPAI_OK;
+}
+
+extern "C" int spai_rollout_select(const float* logits, int64_t bstride, int32_t E, int32_t B, const float* lmax,
+                                   uint64_t seed, uint64_t stream_id, uint64_t* stream_ctr, int32_t sample_base,
+                                   int32_t part, int32_t nparts, uint32_t* removed, int32_t words, int32_t* counts,
+                                   void* workspace, size_t workspace_bytes, void* stream) {
+  return rollout_select(logits, bstride, E, B, lmax, nullptr, 0, seed, stream_id, stream_ctr, sample_base, part,
+                        nparts, removed, words, counts, workspace, workspace_bytes, stream);
+}
+
+extern "C" int spai_rollout_select_pm(const float* logits, int64_t bstride, int32_t E, int32_t B, float* lmax,
+                                      const float* lmax_parts, int32_t n_lmax_parts, uint64_t seed,
+                                      uint64_t stream_id, uint64_t* stream_ctr, int32_t sample_base, int32_t part,
+                                      int32_t nparts, uint32_t* removed, int32_t words, int32_t* counts,
+                                      void* workspace, size_t workspace_bytes, void* stream) {
+  SPAI_CHECK_ARG(lmax_parts != nullptr, "spai_rollout_select_pm: null lmax_parts");
+  return rollout_select(logits, bstride, E, B, lmax, lmax_parts, n_lmax_parts, seed, stream_id, stream_ctr,
+                        sample_base, part, nparts, removed, words, counts, workspace, workspace_bytes, stream);
 }
 
 extern "C" int spai_rollout_merge(const float* logits, int64_t bstride, int32_t E, int32_t B, const float* lmax,

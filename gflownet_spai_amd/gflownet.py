@@ -91,7 +91,7 @@ class GFlowNet(nn.Module):
             self._ctr.fill_(int(value))  # replays from here draw stream ids value, value + 1, ...
 
     # ------------------------------------------------------------------ policy
-    def policy_logits(self, data, batch_size: int):
+    def policy_logits(self, data, batch_size: int, defer_max: bool = False):
         """(logits [E+1] fp32, alpha 0-d, lmax [B] or None) for this rollout.
 
         Uses ``forward_policy.logits_and_max(data, B)`` (ForwardPolicy here: the gfx950
@@ -101,7 +101,10 @@ class GFlowNet(nn.Module):
         sigmoid(alpha) values, as gflownet.py:89."""
         lmax = None
         if hasattr(self.forward_policy, "logits_and_max"):
-            logits, a, lmax = self.forward_policy.logits_and_max(data, batch_size)
+            if defer_max:  # (the throughput rollout's select forms the maximum: kernels.PendingMax)
+                logits, a, lmax = self.forward_policy.logits_and_max(data, batch_size, defer_max=True)
+            else:
+                logits, a, lmax = self.forward_policy.logits_and_max(data, batch_size)
         elif hasattr(self.forward_policy, "logits"):
             logits, a = self.forward_policy.logits(data)
         else:
@@ -207,14 +210,18 @@ class GFlowNet(nn.Module):
         log.rewards = env.last_reward32
         return log if return_log else None
 
-    def _logits(self, s0, need_z: bool = False):
-        """(logits, alpha, sampler logits fp32 on the device, lmax [B], z [B] or None)."""
+    def _logits(self, s0, need_z: bool = False, defer_max: bool = False):
+        """(logits, alpha, sampler logits fp32 on the device, lmax [B], z [B] or None).  defer_max:
+        lmax may come back as a kernels.PendingMax (the ForwardPolicy's fc block maxima, no reduction
+        launch), which kernels.rollout_select completes."""
         env = self.env
         B = len(s0)
         E = env.num_actions - 1
         if self._same_states(s0):
             data_list = self.state_to_data(s0[:1])
-            logits, alpha, lmax = self.policy_logits(data_list[0], B)
+            defer = (defer_max and not need_z and not torch.is_grad_enabled()
+                     and getattr(self.forward_policy, "supports_defer_max", False))
+            logits, alpha, lmax = self.policy_logits(data_list[0], B, defer_max=defer)
             if logits.numel() != E + 1:
                 raise ValueError(f"policy produced {logits.numel()} logits for {E + 1} actions")
         else:
@@ -284,10 +291,12 @@ class GFlowNet(nn.Module):
         env, s0 = self.env, st["s0"]
         B = len(s0)
         E = env.num_actions - 1
-        logits, alpha, lg, lmax, _ = self._logits(s0)
+        logits, alpha, lg, lmax, _ = self._logits(s0, defer_max=True)
         rank, world, group = self.shard if self.shard is not None else (0, 1, None)
         removed, counts, ws = kernels.rollout_select(lg, B, lmax, self.seed, 0, self.sample_base, self._counter(lg.device),
                                                      rank, world)
+        if isinstance(lmax, kernels.PendingMax):
+            lmax = lmax.out  # written by the select
         st.update(B=B, E=E, logits=logits, alpha=alpha, lg=lg, lmax=lmax, removed=removed, counts=counts, ws=ws,
                   part=(rank, world, group))
         if world == 1:  # all lines here: fill, exact sums and rewards (one launch after the fill)
@@ -348,11 +357,13 @@ class GFlowNet(nn.Module):
         bl = len(s0)
         E = env.num_actions - 1
         words = (E + 31) // 32
-        logits, alpha, lg, lmax, _ = self._logits(s0)
+        logits, alpha, lg, lmax, _ = self._logits(s0, defer_max=True)
         dev = lg.device
         sel = self._buf("select", (bl * words + bl,), torch.int32, dev)
         removed, counts, ws = kernels.rollout_select(lg, bl, lmax, self.seed, 0, self.sample_base + rank * bl,
                                                      self._counter(dev), out=sel)
+        if isinstance(lmax, kernels.PendingMax):
+            lmax = lmax.out  # written by the select
         plan = env.pack_plan(world)
         send = self._buf("send", (plan.send_words(bl),), torch.int32, dev)
         kernels.bitmap_pack(removed, counts, plan, out=send)  # line-major packed bits per destination

@@ -103,12 +103,30 @@ def rollout_select(lg: torch.Tensor, B: int, lmax: torch.Tensor, seed: int, stre
                                    stream_ctr.device != lg.device):
         raise ValueError("stream_ctr must be a 1-element int64 tensor on the logits' device")
     with _timed("rollout_select"):
-        st = _l().spai_rollout_select(_lib.ptr(lg), 0 if lg.dim() == 1 else E + 1, E, B, _lib.ptr(lmax),
-                                      seed & (2**64 - 1), stream_id & (2**64 - 1), _lib.ptr(stream_ctr),
-                                      sample_base, part, nparts, _lib.ptr(removed), words, _lib.ptr(counts),
-                                      _lib.ptr(ws), ws.numel(), _lib.stream_ptr(lg.device))
+        if isinstance(lmax, PendingMax):  # the policy's block maxima: reduced inside the select
+            if lg.dim() != 1:
+                raise ValueError("a deferred maximum needs one shared logits row")
+            st = _l().spai_rollout_select_pm(_lib.ptr(lg), 0, E, B, _lib.ptr(lmax.out), _lib.ptr(lmax.parts),
+                                             lmax.parts.numel(), seed & (2**64 - 1), stream_id & (2**64 - 1),
+                                             _lib.ptr(stream_ctr), sample_base, part, nparts, _lib.ptr(removed),
+                                             words, _lib.ptr(counts), _lib.ptr(ws), ws.numel(),
+                                             _lib.stream_ptr(lg.device))
+        else:
+            st = _l().spai_rollout_select(_lib.ptr(lg), 0 if lg.dim() == 1 else E + 1, E, B, _lib.ptr(lmax),
+                                          seed & (2**64 - 1), stream_id & (2**64 - 1), _lib.ptr(stream_ctr),
+                                          sample_base, part, nparts, _lib.ptr(removed), words, _lib.ptr(counts),
+                                          _lib.ptr(ws), ws.numel(), _lib.stream_ptr(lg.device))
     _lib.check(st, "spai_rollout_select")
     return removed, counts, ws
+
+
+class PendingMax:
+    """The logits' maximum not yet formed: ``parts`` holds the policy's fc block maxima
+    (spai_policy_logits with B = 0) and rollout_select writes the maximum into ``out`` [B] inside its
+    first launch (spai_rollout_select_pm) — one reduction launch fewer per step."""
+
+    def __init__(self, out: torch.Tensor, parts: torch.Tensor):
+        self.out, self.parts = out, parts
 
 
 def rollout_order(lg, B, lmax, counts, ws):

@@ -192,6 +192,8 @@ class ForwardPolicy(BasePolicy):
     attention weights, and spai_policy_logits evaluates that closed form instead of the
     graph kernels (detected on the device once per x)."""
 
+    supports_defer_max = True  # logits_and_max(..., defer_max=True): kernels.PendingMax
+
     def __init__(self, node_features: int, hidden_dim: int, max_num_actions: int):
         super().__init__(node_features, hidden_dim)
         self.gat2 = GATv2Layer(self.hid * self.in_head, self.hid, heads=self.out_head)
@@ -241,7 +243,7 @@ class ForwardPolicy(BasePolicy):
         self._const = (key, const, x)  # x pins the storage the key names
         return const
 
-    def _hip_logits(self, data, B: int):
+    def _hip_logits(self, data, B: int, defer_max: bool = False):
         x = data.x
         _lib.require_device(x)
         n, fin = x.shape
@@ -261,15 +263,17 @@ class ForwardPolicy(BasePolicy):
             raise ValueError("policy parameter shapes do not match node_features/hidden_dim")
         logits = torch.empty(1, num_actions, dtype=torch.float32, device=x.device)
         lmax = torch.empty(B, dtype=torch.float32, device=x.device)
+        # defer_max: the fc block maxima only (B = 0); the rollout's select reduces them (PendingMax)
+        buf = torch.empty(lib.spai_policy_lmax_parts(num_actions), dtype=torch.float32, device=x.device) \
+            if defer_max else lmax
         ws = _lib.workspace(lib.spai_policy_workspace_bytes(n, self.hid, num_actions), x.device, "policy")
         with kernels._timed("policy"):
             st = lib.spai_policy_logits(n, fin, self.hid, _lib.ptr(xf), _lib.ptr(rowptr), _lib.ptr(src),
                                           _lib.ptr(ea), _lib.ptr(p1), _lib.ptr(p2), _lib.ptr(w), _lib.ptr(fb),
-                                          num_actions, _lib.ptr(logits), _lib.ptr(lmax), B, int(const), _lib.ptr(ws),
-                                          ws.numel(),
-                                        _lib.stream_ptr(x.device))
+                                          num_actions, _lib.ptr(logits), _lib.ptr(buf), 0 if defer_max else B,
+                                          int(const), _lib.ptr(ws), ws.numel(), _lib.stream_ptr(x.device))
         _lib.check(st, "spai_policy_logits")
-        return logits, lmax
+        return logits, (kernels.PendingMax(lmax, buf) if defer_max else lmax)
 
     def _hip_backward_ok(self, data) -> bool:
         return self.hid in (4, 8) and data.x.shape[1] in (1, 2, 4)
@@ -319,14 +323,15 @@ class ForwardPolicy(BasePolicy):
         grads[id(self.fc.weight)], grads[id(self.fc.bias)] = fw, fb
         return grads
 
-    def logits_and_max(self, data, B: int = 1) -> Tuple[Tensor, Tensor, Tensor]:
+    def logits_and_max(self, data, B: int = 1, defer_max: bool = False) -> Tuple[Tensor, Tensor, Tensor]:
         """(logits [1, E+1], sigmoid(alpha), lmax [B]) — everything of forward() but the mask,
-        plus the logits' maximum for the sampler (no separate statistics pass)."""
+        plus the logits' maximum for the sampler (no separate statistics pass).  defer_max (no
+        autograd): lmax is a kernels.PendingMax the throughput rollout's select completes."""
         params = tuple(self.parameters())
         if torch.is_grad_enabled() and any(p.requires_grad for p in params):
             logits, lmax = _HipLogits.apply(self, data, B, *params)
             return logits, torch.sigmoid(self.alpha), lmax
-        logits, lmax = self._hip_logits(data, B)
+        logits, lmax = self._hip_logits(data, B, defer_max)
         return logits, self._sigmoid_alpha(), lmax
 
     def _sigmoid_alpha(self) -> Tensor:

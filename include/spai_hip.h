@@ -125,6 +125,16 @@ int spai_rollout_select(const float* logits, int64_t bstride, int32_t E, int32_t
                         uint64_t seed, uint64_t stream_id, uint64_t* stream_ctr, int32_t sample_base,
                         int32_t part, int32_t nparts, uint32_t* removed, int32_t words, int32_t* counts,
                         void* workspace, size_t workspace_bytes, void* stream);
+/* spai_rollout_select with the logits maximum still to be formed (the small launches):
+ * lmax_parts [n_lmax_parts] = the block maxima spai_policy_logits left with B = 0; one extra block
+ * of the select's first launch reduces them and writes lmax[0..B-1] (an output here) before its
+ * first reader.  One shared logits row only (bstride 0).  Otherwise identical to
+ * spai_rollout_select (same outputs, bits and workspace). */
+int spai_rollout_select_pm(const float* logits, int64_t bstride, int32_t E, int32_t B, float* lmax,
+                           const float* lmax_parts, int32_t n_lmax_parts, uint64_t seed, uint64_t stream_id,
+                           uint64_t* stream_ctr, int32_t sample_base, int32_t part, int32_t nparts,
+                           uint32_t* removed, int32_t words, int32_t* counts, void* workspace,
+                           size_t workspace_bytes, void* stream);
 int spai_rollout_merge(const float* logits, int64_t bstride, int32_t E, int32_t B, const float* lmax,
                        int32_t part, int32_t nparts, int32_t* counts, void* workspace, size_t workspace_bytes,
                        void* stream);
@@ -354,6 +364,10 @@ int spai_bitmap_pack(int32_t P, int32_t bl, const uint32_t* removed, int32_t wor
  * Compiled for fin in {1, 2, 4} and hid in {4, 8, 16, 32} (else SPAI_ERR_UNSUPPORTED).
  * Workspace: spai_policy_workspace_bytes(n_nodes, hid, num_actions). */
 size_t spai_policy_params(int32_t layer, int32_t fin, int32_t hid);
+/* B = 0 in spai_policy_logits defers the maximum: lmax then receives the fc kernel's per-block
+ * maxima (spai_policy_lmax_parts(num_actions) floats) and no reduction launch runs; the rollout's
+ * spai_rollout_select_pm reduces them (one launch fewer per step). */
+int32_t spai_policy_lmax_parts(int32_t num_actions);
 size_t spai_policy_workspace_bytes(int32_t n_nodes, int32_t hid, int32_t num_actions);
 /* *flag = 1 if every row of x [n_nodes][fin] equals row 0, else 0 (asynchronous, on stream). */
 int spai_policy_rows_constant(int32_t n_nodes, int32_t fin, const float* x, int32_t* flag, void* stream);

@@ -176,3 +176,33 @@ def test_policy_const_rows_closed_form_matches_general(fin, hid):
                                    lp(pol.gat2), pol.fc.weight.detach().cpu().numpy(),
                                    pol.fc.bias.detach().cpu().numpy(), 1501)
     close(got.cpu(), orc2)
+
+
+@pytest.mark.parametrize("grid", [16, 256])
+def test_deferred_max_in_select(grid):
+    """The logits maximum deferred to the rollout (spai_policy_logits with B = 0 leaves the fc block
+    maxima; spai_rollout_select_pm reduces them in an extra block of its first launch): the same
+    lmax as the policy's own reduction and bit-identical select outputs; a no-grad sample_states
+    (which defers) matches the oracle."""
+    from gflownet_spai_amd import kernels
+    A = poisson_2d(grid)
+    env = PreconditionerEnv(grid * grid, A, A, side="AM", fill="lsq")
+    E = env.num_actions - 1
+    pol = randomise(ForwardPolicy(-1, 4, E + 1), grid).to(DEV)
+    with torch.no_grad():
+        pol.fc.bias[E] += 2.0
+    g = GFlowNet(pol, None, env, mode="throughput", seed=5)
+    data = g.state_to_data([A])[0]
+    with torch.no_grad():
+        lg, _, lmax = pol.logits_and_max(data, 3)
+        lg2, _, pend = pol.logits_and_max(data, 3, defer_max=True)
+        assert isinstance(pend, kernels.PendingMax) and torch.equal(lg, lg2)
+        r1, c1, _ = kernels.rollout_select(lg.reshape(-1), 3, lmax, 5, 7)
+        r1, c1 = r1.clone(), c1.clone()
+        r2, c2, _ = kernels.rollout_select(lg2.reshape(-1), 3, pend, 5, 7)
+        assert torch.equal(pend.out, lmax) and float(lmax[0]) == float(lg.max())
+        assert torch.equal(r1, r2) and torch.equal(c1, c2)
+        log = g.sample_states([A] * 3, return_log=True)
+    r_o, a_o, f_o, c_o = O.throughput_rollout(lg.cpu().numpy().reshape(-1), 3, 5, 0)
+    assert np.array_equal(log.actions.cpu().numpy(), a_o) and np.array_equal(log.counts.cpu().numpy(), c_o)
+    np.testing.assert_allclose(log.fwd_probs.detach().cpu().numpy(), f_o, rtol=1e-6)

@@ -603,6 +603,12 @@ def main():
             sb *= (model.lines[1] - model.lines[0]) / n
         out["roofline"]["bytes_survey_8d"] = sb
         out["roofline"]["frac_survey_8d"] = sb / (fill_ms * 1e-3) / 1e9 / HBM_PEAK_GBS
+        # achieved / frac at SURVEY §8(d)'s algorithmic bytes (the contract's figure); the bytes the
+        # kernel streams instead (the env-constant Gram / R cache, or its dictionary, for A) beside them
+        rf = out["roofline"]
+        rf["bytes_cache_counted"], rf["frac_cache_counted"] = rf["bytes_per_launch"], rf["frac"]
+        rf["bytes_per_launch"], rf["achieved"] = sb, sb / (fill_ms * 1e-3) / 1e9
+        rf["frac"] = rf["achieved"] / HBM_PEAK_GBS
         if not dist_on:
             sel = roofline_obj("rollout_select phase: k_presample + k_splitters + k_tile + k_bsum (k_tile ~80 % of "
                                "it; latency-bound, not bandwidth-bound: see the PMC profile in DESIGN.md §5)",

@@ -17,7 +17,7 @@ for b in "${BL[@]}"; do
   i=$((i+1))
   echo "== bench $b"
   timeout -k 10 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline $b > $O/bench$i.log 2>&1 || { tail -20 $O/bench$i.log; exit 1; }
-  python -c "import json,sys; d=json.loads(open('$O/bench$i.log').read().strip().splitlines()[-1]); print(round(d['ms_per_step'],4), 'ms', {k: round(v,4) for k,v in d['phases_ms'].items()}, 'roof', d['roofline']['kernel'][:24], round(d['roofline']['avg_launch_ms'],4), round(d['roofline']['frac'],3), round(d['roofline']['frac_survey_8d'],3))"
+  python -c "import json,sys; d=json.loads(open('$O/bench$i.log').read().strip().splitlines()[-1]); print(round(d['ms_per_step'],4), 'ms', {k: round(v,4) for k,v in d['phases_ms'].items()}, 'roof', d['roofline']['kernel'][:24], round(d['roofline']['avg_launch_ms'],4), round(d['roofline']['frac'],3), round(d['roofline']['frac_cache_counted'],3))"
 done
 if [ -n "$PROF" ]; then
   echo "== rocprof $PROF"

@@ -306,7 +306,7 @@ def main():
     ap.add_argument("--steps-per-graph", type=int, default=8,
                     help="one GPU: at most this many consecutive steps captured in one HIP graph (the largest count "
                          "that divides --steps; 1: one graph replay per step)")
-    ap.add_argument("--overlap", default="sort", choices=["sort", "fill", "none"],
+    ap.add_argument("--overlap", default="sort", choices=["sort", "fill", "select", "none"],
                     help="one GPU: the fill + rewards on a second stream beside the trajectory sort, the sort "
                          "launched first (sort) or the fill first (fill); none: one stream")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],

@@ -49,8 +49,8 @@ class GFlowNet(nn.Module):
         # one GPU, throughput mode: run the fill + rewards on a second stream beside the trajectory
         # sort (the two chains share only the select phase's outputs); "sort" / True: the sort is
         # launched first, "fill": the fill first, False: one stream, fill then sort
-        if overlap not in (False, True, "sort", "fill"):
-            raise ValueError("overlap must be False, True, 'sort' or 'fill'")
+        if overlap not in (False, True, "sort", "fill", "select"):
+            raise ValueError("overlap must be False, True, 'sort', 'fill' or 'select'")
         self.overlap = "sort" if overlap is True else overlap
         self._side = None
         # (rank, world, group): the multi-GPU split of DESIGN.md §6 (throughput mode)
@@ -257,10 +257,15 @@ class GFlowNet(nn.Module):
 
     def _fork_fill(self, st: dict) -> None:
         """fill + rewards of all lines on the side stream, after everything the current stream has
-        issued (the select phase, and with overlap="sort" the trajectory sort's launch)."""
+        issued (the select phase, and with overlap="sort" the trajectory sort's launch) — or, with
+        overlap="select", after the select phase only (its event), though issued after the sort."""
         dev = st["lg"].device
         side = self._side_stream(dev)
-        side.wait_stream(torch.cuda.current_stream(dev))
+        ev = st.pop("select_done", None)
+        if ev is not None:
+            side.wait_event(ev)
+        else:
+            side.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(side):
             st["rewards"] = self.env.fill_rewards(st["removed"], st["counts"], st["alpha"])
         st["join"] = side
@@ -307,6 +312,10 @@ class GFlowNet(nn.Module):
                 self._fork_fill(st)
             elif self.overlap:  # "sort": the same branches, the sort launched first (_end forks the fill)
                 st["fill_after_sort"] = True
+                if self.overlap == "select":  # the fill depends on the select only, issued after the sort
+                    ev = torch.cuda.Event()
+                    ev.record(torch.cuda.current_stream(lg.device))
+                    st["select_done"] = ev
             else:
                 st["rewards"] = env.fill_rewards(removed, counts, alpha)
         else:  # a split sums exact limbs of its lines

@@ -845,3 +845,43 @@ def test_gram_dict_is_bit_identical(kind):
         assert torch.equal(envd.fill_partial(removed, lb, le, limbs=True), envf.fill_partial(removed, lb, le, limbs=True))
     assert torch.equal(envd.fill_rewards(removed, counts, torch.tensor(0.5)),
                        envf.fill_rewards(removed, counts, torch.tensor(0.5)))
+
+
+@pytest.mark.parametrize("overlap", ["sort", "fill", "select"])
+def test_overlap_modes_graph_replay_bit_identical(overlap):
+    """The fill + rewards on a second captured stream beside the trajectory sort (overlap="sort":
+    forked after the sort's launch; "fill": after the select; "select": issued after the sort but
+    depending on the select only): graph replays give the same actions, fwd_probs, M and rewards
+    bit for bit as the one-stream step (overlap=False) on the same Philox streams, QR fill."""
+    from gflownet_spai_amd import GFlowNet, PreconditionerEnv, poisson_2d
+    A = poisson_2d(32)
+    n = 32 * 32
+    env = PreconditionerEnv(n, A, A, side="AM", fill="qr", keep_m=True)
+    El = env.num_actions - 1
+    lgt = torch.randn(El + 1, generator=torch.Generator().manual_seed(8))
+    lgt[El] = 4.0
+    s0 = [A] * 4
+    res = {}
+    for ov in (False, overlap):
+        g = GFlowNet(FixedLogits(lgt).to(DEV), None, env, mode="throughput", seed=13, overlap=ov)
+        with torch.no_grad():
+            g.sample_states(s0, return_log=True)  # stream 0, eager (warms every cache)
+            torch.cuda.synchronize()
+            graph = torch.cuda.CUDAGraph()
+            side = torch.cuda.Stream()
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                g.sample_states(s0, return_log=True)  # stream 1
+            torch.cuda.current_stream().wait_stream(side)
+            with torch.cuda.graph(graph):
+                logc = g.sample_states(s0, return_log=True)
+            outs = []
+            for _ in range(2):  # streams 2, 3
+                graph.replay()
+                torch.cuda.synchronize()
+                T = int(logc._full[2])
+                outs.append((logc._full[0][:, :T].clone(), logc._full[1][:, :T].clone(), env.last_m.clone(),
+                             logc.rewards.clone()))
+        res[ov] = outs
+    for (a0, f0, m0, r0), (a1, f1, m1, r1) in zip(res[False], res[overlap]):
+        assert torch.equal(a0, a1) and torch.equal(f0, f1) and torch.equal(m0, m1) and torch.equal(r0, r1)

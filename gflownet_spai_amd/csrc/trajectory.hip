@@ -87,6 +87,7 @@ struct TrajWs {
   double* xch;            // exchange array: [B][2][kMaxB] bucket weight sums | winner counts, then
                           // [B][8] caller slots (the residual limbs); a part fills its own buckets
   int32_t* samp_cnt;      // [B][M / kSampNT] winners per presample block
+  uint32_t* samp_mm;      // [B][M / kSampNT][2] min / max winner key per presample block
   uint32_t* samp;         // [B][M] winner keys (orderable), block-compacted
   int32_t* nb;            // [B] buckets
   uint32_t* spl;          // [B][kMaxB] ascending orderable splitters
@@ -122,6 +123,7 @@ static void traj_ws(void* base, int32_t E, int32_t B, TrajWs* w) {
   w->lastbig = w->ctl + 2;
   w->xch = c.take<double>(xch_doubles(B));
   w->samp_cnt = c.take<int32_t>((size_t)B * nsb);
+  w->samp_mm = c.take<uint32_t>((size_t)B * nsb * 2);
   w->samp = c.take<uint32_t>((size_t)B * M);
   w->nb = c.take<int32_t>(B);
   w->spl = c.take<uint32_t>((size_t)B * kMaxB);
@@ -359,6 +361,7 @@ __global__ __launch_bounds__(kSampNT) void k_presample(const float* __restrict__
                                                        uint32_t st0, uint32_t st1, const uint64_t* __restrict__ sctr,
                                                        int32_t sample_base,
                                                        uint32_t* __restrict__ samp, int32_t* __restrict__ samp_cnt,
+                                                       uint32_t* __restrict__ samp_mm,
                                                        int32_t* __restrict__ ctl, int32_t nctl, float* __restrict__ tE_out,
                                                        const float* __restrict__ lmax_parts, int32_t n_lmax_parts,
                                                        float* __restrict__ lmax_out, int32_t B) {
@@ -418,10 +421,29 @@ __global__ __launch_bounds__(kSampNT) void k_presample(const float* __restrict__
       o = arrival_ord(t);
     }
   }
+  // the block's winner key range (for k_splitters' histogram range: no staging pass there)
+  __shared__ uint32_t s_kmn[kSampNT / 64], s_kmx[kSampNT / 64];
+  {
+    const uint32_t wmn = wave_min_u32(win ? o : 0xFFFFFFFFu), wmx = wave_max_u32(win ? o : 0u);
+    if ((tid & 63) == 0) {
+      s_kmn[tid >> 6] = wmn;
+      s_kmx[tid >> 6] = wmx;
+    }
+  }
   int tot;
-  const int pos = block_excl_scan<kSampNT>(win, s_wc, &tot);
+  const int pos = block_excl_scan<kSampNT>(win, s_wc, &tot);  // (its barriers publish s_kmn / s_kmx)
   if (win) samp[(int64_t)b * M + blk * kSampNT + pos] = o;
-  if (tid == 0) samp_cnt[b * nsb + blk] = tot;
+  if (tid == 0) {
+    samp_cnt[b * nsb + blk] = tot;
+    uint32_t mn = 0xFFFFFFFFu, mx = 0u;
+#pragma unroll
+    for (int w = 0; w < kSampNT / 64; ++w) {
+      mn = min(mn, s_kmn[w]);
+      mx = max(mx, s_kmx[w]);
+    }
+    samp_mm[(b * nsb + blk) * 2] = mn;
+    samp_mm[(b * nsb + blk) * 2 + 1] = mx;
+  }
 }
 
 // ------------------------------------------------------------------ k_splitters
@@ -431,6 +453,7 @@ __global__ __launch_bounds__(kSampNT) void k_presample(const float* __restrict__
 __global__ __launch_bounds__(kSortNT) void k_splitters(int32_t E, int32_t M, int32_t nsb,
                                                        const uint32_t* __restrict__ samp,
                                                        const int32_t* __restrict__ samp_cnt,
+                                                       const uint32_t* __restrict__ samp_mm,
                                                        int32_t* __restrict__ nb_out, uint32_t* __restrict__ spl,
                                                        uint16_t* __restrict__ lut, uint32_t* __restrict__ lut_base,
                                                        int32_t B, const float* __restrict__ logits, int64_t bstride,
@@ -442,12 +465,21 @@ __global__ __launch_bounds__(kSortNT) void k_splitters(int32_t E, int32_t M, int
   }
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   PROF_INIT
-  __shared__ uint32_t s_smp[kSampCap];  // the sampled winner keys, compacted
+  // (no key staging in LDS: the histogram is built from the keys' registers; ~21 KB of LDS)
   __shared__ int hist[kBins + 1];
   __shared__ int sblk[kMaxNsb + 1];
   __shared__ int s_wc[kSortNT / 64];
   __shared__ uint32_t s_mn[kSortNT / 64], s_mx[kSortNT / 64];
   const int c = tid < nsb ? samp_cnt[b * nsb + tid] : 0;
+  // the winner key range from k_presample's per-block ranges (one load round with the counts)
+  uint32_t mn = tid < nsb ? samp_mm[(b * nsb + tid) * 2] : 0xFFFFFFFFu;
+  uint32_t mx = tid < nsb ? samp_mm[(b * nsb + tid) * 2 + 1] : 0u;
+  mn = wave_min_u32(mn);
+  mx = wave_max_u32(mx);
+  if (lane == 0) {
+    s_mn[wave] = mn;
+    s_mx[wave] = mx;
+  }
   int total;
   const int ex = block_excl_scan<kSortNT>(c, s_wc, &total);
   if (tid < nsb) sblk[tid] = ex;
@@ -456,24 +488,30 @@ __global__ __launch_bounds__(kSortNT) void k_splitters(int32_t E, int32_t M, int
   __syncthreads();
   PROF(0)
   const int ns = min(total, kSampCap);
+  mn = 0xFFFFFFFFu;
+  mx = 0u;
+#pragma unroll
+  for (int w = 0; w < kSortNT / 64; ++w) {
+    mn = min(mn, s_mn[w]);
+    mx = max(mx, s_mx[w]);
+  }
+  const uint32_t range = ns > 0 ? mx - mn : 0u;
+  const int shift = range >= (uint32_t)kBins ? 32 - __clz((int)(range >> 12)) : 0;  // (range >> shift) < kBins
   const uint32_t* sb = samp + (int64_t)b * M;
-  // the first ns sampled winners, compacted into LDS in two halves with every load of a half in
+  // histogram of the first ns sampled winners, read in two halves with every load of a half in
   // flight at once: wave w reads presample blocks w*kBPW .. w*kBPW + kBPW - 1 (kSampNT keys
-  // each, kLPB per lane); the key range comes from the registers
+  // each, kLPB per lane)
   constexpr int kBPW = kMaxNsb / (kSortNT / 64), kLPB = kSampNT / 64, kHalf = kBPW / 2;
   static_assert(kMaxNsb % (kSortNT / 64) == 0 && kSampNT % 64 == 0 && kBPW % 2 == 0 && kHalf * kLPB <= 32,
-                "k_splitters staging (the 32-bit validity mask of a half)");
-  uint32_t mn = 0xFFFFFFFFu, mx = 0u;
+                "k_splitters key rounds (the 32-bit validity mask of a half)");
 #pragma unroll 1
   for (int h = 0; h < 2; ++h) {
     uint32_t v[kHalf * kLPB];
-    int pos[kHalf];
     uint32_t ok = 0;
 #pragma unroll
     for (int j = 0; j < kHalf; ++j) {
       const int k = wave * kBPW + h * kHalf + j;
       const int beg = k < nsb ? sblk[k] : ns, cnt = k < nsb ? min(sblk[k + 1], ns) - beg : 0;
-      pos[j] = beg;
 #pragma unroll
       for (int q = 0; q < kLPB; ++q) {
         const int i = lane + 64 * q;
@@ -486,35 +524,8 @@ __global__ __launch_bounds__(kSortNT) void k_splitters(int32_t E, int32_t M, int
     for (int j = 0; j < kHalf; ++j)
 #pragma unroll
       for (int q = 0; q < kLPB; ++q)
-        if ((ok >> (j * kLPB + q)) & 1u) {
-          const uint32_t x = v[j * kLPB + q];
-          mn = min(mn, x);
-          mx = max(mx, x);
-          s_smp[pos[j] + lane + 64 * q] = x;
-        }
+        if ((ok >> (j * kLPB + q)) & 1u) atomicAdd(&hist[(v[j * kLPB + q] - mn) >> shift], 1);
   }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    mn = min(mn, (uint32_t)__shfl_xor((int)mn, o, kWave));
-    mx = max(mx, (uint32_t)__shfl_xor((int)mx, o, kWave));
-  }
-  if (lane == 0) {
-    s_mn[wave] = mn;
-    s_mx[wave] = mx;
-  }
-  __syncthreads();
-  PROF(1)
-  mn = 0xFFFFFFFFu;
-  mx = 0u;
-#pragma unroll
-  for (int w = 0; w < kSortNT / 64; ++w) {
-    mn = min(mn, s_mn[w]);
-    mx = max(mx, s_mx[w]);
-  }
-  const uint32_t range = ns > 0 ? mx - mn : 0u;
-  const int shift = range >= (uint32_t)kBins ? 32 - __clz((int)(range >> 12)) : 0;  // (range >> shift) < kBins
-  // histogram of the staged keys
-  for (int p = tid; p < ns; p += kSortNT) atomicAdd(&hist[(s_smp[p] - mn) >> shift], 1);
   __syncthreads();
   PROF(2)
   // exclusive scan of the bins (4 per thread), in place
@@ -1732,11 +1743,13 @@ static int rollout_select(const float* logits, int64_t bstride, int32_t E, int32
   const int64_t rowsel = bstride ? 1 : 0;
   // (+1 block: the deferred logits maximum, when given)
   k_presample<<<nsb * B + (lmax_parts ? 1 : 0), kSampNT, 0, s>>>(logits, bstride, E, w.M, nsb, s0, s1, t0, t1,
-                                                                 stream_ctr, sample_base, w.samp, w.samp_cnt, w.ctl, 4,
+                                                                 stream_ctr, sample_base, w.samp, w.samp_cnt, w.samp_mm,
+                                                                 w.ctl, 4,
                                                                  w.tE, lmax_parts, n_lmax_parts,
                                                                  const_cast<float*>(lmax), B);
   SPAI_CHECK_LAUNCH();
-  k_splitters<<<B + nwb * (bstride ? B : 1), kSortNT, 0, s>>>(E, w.M, nsb, w.samp, w.samp_cnt, w.nb, w.spl, w.lut,
+  k_splitters<<<B + nwb * (bstride ? B : 1), kSortNT, 0, s>>>(E, w.M, nsb, w.samp, w.samp_cnt, w.samp_mm, w.nb, w.spl,
+                                                             w.lut,
                                                              w.lut_base, B, logits, bstride, lmax, w.rr, w.ww,
                                                              w.wstride);
   SPAI_CHECK_LAUNCH();

@@ -10,6 +10,7 @@
 #   ovl     overlap="sort" vs "select" (no variant)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+RUN_TESTS="$TESTS"; unset TESTS  # (gpu_ab.sh reads TESTS as a -k expression)
 mkdir -p gpurun_out
 tests() {
   [ -z "$1" ] && return 0
@@ -26,7 +27,7 @@ case "$1" in
     for a in "--fill qr" "--fill lsq"; do ROUNDS=2 BENCH_ARGS="$a" bash scripts/gpu_ab.sh blockm.so || exit 1; done
     ROUNDS=2 CFG=c3 bash scripts/gpu_ab.sh blockm.so || exit 1 ;;
   base)
-    tests "${TESTS:-tests/test_qr_gpu.py tests/test_hip_parity.py}" ""
+    tests "${RUN_TESTS:-tests/test_qr_gpu.py tests/test_hip_parity.py}" ""
     ROUNDS=${ROUNDS:-3} BENCH_ARGS="--fill qr" bash scripts/gpu_ab.sh base.so || exit 1
     for c in ${CFGS:-}; do ROUNDS=2 CFG=$c bash scripts/gpu_ab.sh base.so || exit 1; done ;;
   ovl)

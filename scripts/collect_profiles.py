@@ -5,7 +5,7 @@ fill_traffic.json (HBM bytes per launch of the roofline kernel, read back by ben
 HBM traffic per launch = (2 * FETCH_SIZE + WRITE_SIZE) * 1024: MI355X_MICROARCH.md §HBM
 (FETCH_SIZE reports half of the bytes of coalesced reads on gfx950; calibrated here against
 the fill kernel's known read bytes).
-usage: python scripts/collect_profiles.py <tag> <prof_dir> <pmc_dir> [--config c4 --batch 8 --out profiles]
+usage: python scripts/collect_profiles.py <tag> <prof_dir> <pmc_dir|-> [--config c4 --batch 8 --out profiles]
 """
 import argparse
 import csv
@@ -49,6 +49,8 @@ def main():
         f.write(f"# rocprofv3 --kernel-trace --stats ({args.tag})\n\nCommand on one MI355X: "
                 f"`rocprofv3 --kernel-trace --stats --output-format csv -- {args.cmd}`\n\n" + "\n".join(lines) + "\n")
     shutil.copy(stats, os.path.join(args.out, f"kernel_stats_{args.tag}.csv"))
+    if args.pmc == "-":  # kernel stats only (no PMC passes in this run)
+        return
     pmc = json.load(open(os.path.join(args.pmc, "summary.json")))
     for k, e in pmc.items():
         kk = k.replace("spai::", "")

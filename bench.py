@@ -135,10 +135,11 @@ def survey_fill_bytes(env, B, store_m: bool = True) -> float:
     return nnz_a * (s_a + 4) + 4 * (n + 1) + 4 * nnz_p + 4 * (n + 1) + B * per_sample
 
 
-def measured_traffic(cfg: str, B: int):
+def measured_traffic(cfg: str, B: int, kernel: str | None = None):
     """HBM bytes per launch of the roofline kernel from the committed PMC profile of this
     exact workload (profiles/fill_traffic.json, written by scripts/collect_profiles.py from
-    separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of `bench.py`), else None."""
+    separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of `bench.py`; ``kernel``: only a
+    record of that kernel), else None."""
     path = os.path.join(ROOT, "profiles", "fill_traffic.json")
     try:
         rec = json.load(open(path))
@@ -147,7 +148,7 @@ def measured_traffic(cfg: str, B: int):
     if "config" in rec:  # single-record form
         rec = {rec["config"]: rec}
     rec = rec.get(cfg, {})
-    if rec.get("batch") == B:
+    if rec.get("batch") == B and (kernel is None or kernel + "<" in rec.get("kernel", "")):
         return float(rec["hbm_bytes_per_launch"]), rec.get("source", "profiles/fill_traffic.json")
     return None
 
@@ -228,10 +229,14 @@ def generic_residual_leg(env, log, cfg: str, reps: int = 10):
     idx = torch.where(rem | (pat.idx < 0), torch.full_like(pat.idx, -1), pat.idx).contiguous()
     m = env.last_m.contiguous()
     B, n, W = m.shape
-    res2 = kernels.residual_lines(idx, m, a)  # warm-up
+    # 13-wide patterns: G, c from the env's Gram cache dictionary (the index matching is done once
+    # per env; spai_residual_lines_gram, bit-identical to the matching kernel)
+    gram = env.gram if isinstance(env.gram, kernels.CacheDict) and m.shape[2] == 13 else None
+    kw = dict(gram=gram, pattern=pat) if gram is not None else {}
+    res2 = kernels.residual_lines(idx, m, a, **kw)  # warm-up
     kernels.TIMERS = {}
     for _ in range(reps):
-        res2 = kernels.residual_lines(idx, m, a)
+        res2 = kernels.residual_lines(idx, m, a, **kw)
     torch.cuda.synchronize()
     ms = float(np.mean(kernels.timer_ms("residual_lines")))
     kernels.TIMERS = None
@@ -240,11 +245,13 @@ def generic_residual_leg(env, log, cfg: str, reps: int = 10):
     av = kernels.narrow_values(a)  # fp64 A with fp32-exact values is read as fp32 (same numbers)
     bytes_a = a.idx.numel() * 4 + av.numel() * av.element_size()
     bytes_m = n * W * (4 + m.element_size())
-    name = "k_resid_shared" if W <= 7 else "k_resid_wide"
+    name = "k_resid_shared" if W <= 7 else ("k_resid_gram" if gram is not None else "k_resid_wide")
+    extra = (f"; G, c from the pattern's Gram cache dictionary ({gram.entries} entries, "
+             f"{kernels.cache_nbytes(gram)} B)" if gram is not None else "")
     out = roofline_obj(f"{name}<{W},{a.width},{str(av.dtype)[6:]},{str(m.dtype)[6:]}> (||A M_b - I||_F^2 of "
                        f"B={B} arbitrary sparse M_b: the step's LSQ fills with their own kept index sets; "
-                       f"bytes = bytes(A) + B x bytes(M_b))", bytes_a + B * bytes_m, ms,
-                       traffic=measured_traffic(cfg + "_residual", B))
+                       f"bytes = bytes(A) + B x bytes(M_b){extra})", bytes_a + B * bytes_m, ms,
+                       traffic=measured_traffic(cfg + "_residual", B, name))
     out["max_rel_diff_vs_fused_fill"] = rel
     return out
 

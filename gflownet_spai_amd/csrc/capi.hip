@@ -16,6 +16,6 @@ void set_error(const char* fmt, ...) {
 }
 }  // namespace spai
 
-extern "C" int spai_abi_version(void) { return 16; }
+extern "C" int spai_abi_version(void) { return 17; }
 
 extern "C" const char* spai_last_error(void) { return spai::g_last_error.c_str(); }

@@ -489,6 +489,191 @@ __global__ __launch_bounds__(kNT) void k_resid_wide(int32_t line_begin, int32_t 
                                              val_bstride, a_idx, a_val, partials, sred);
 }
 
+// W > 7 with the pattern's Gram cache (spai_residual_lines_gram): the index matching of
+// k_resid_wide depends on A and the index sets only, and when a sample's index set is a
+// slot-aligned sub-pattern of a pattern whose Gram cache exists (PreconditionerEnv's candidate
+// pattern: every slot either the pattern's index or empty) the matching is already done — its
+// G_pq, G_pp and c_p are the cache's values (k_gram_build: the same products in the same order
+// as line_gram).  The line residual is then line_res2 on the cached values, per sample: one
+// thread per line, the cache as its dictionary (spai_line_cache_dict: a handful of distinct
+// entries, read from L1/L2 per sample, so no Gram is held in registers), the samples' index sets
+// and values streamed with the next sample's loads in flight.  A lane whose sample is not aligned
+// evaluates it from A (line_res2_lean).  Same per-sample block sums as k_resid_wide: the same bits.
+// line_res2_any with two A lines in registers at a time instead of all W: line q is re-read
+// (L1/L2) for every p < q, its address made opaque per use so the compiler cannot keep the W lines
+// live; the same operations in the same order (line_gram, then line_res2), so the same bits.
+// The unaligned lanes' path of k_resid_gram, which keeps that kernel's registers low.
+template <int WA, bool FULL, typename TA>
+__device__ __forceinline__ void a_line_opaque(int k, int wart, const int32_t* __restrict__ a_idx,
+                                              const TA* __restrict__ a_val, int (&ai)[WA], TA (&av)[WA]) {
+  int kk = k;
+  asm volatile("" : "+v"(kk));
+  const int64_t base = (int64_t)max(kk, 0) * wart;
+  int ii[WA];
+  TA xx[WA];
+  load_slots<WA, FULL, int>(a_idx + base, wart, ii);
+  load_slots<WA, FULL, TA>(a_val + base, wart, xx);
+#pragma unroll
+  for (int s = 0; s < WA; ++s) {
+    const bool on = kk >= 0 && s < wart;
+    ai[s] = on ? ii[s] : -1;
+    av[s] = on ? xx[s] : (TA)0;
+  }
+}
+template <int W>
+__device__ __forceinline__ void slot_of(const int (&k)[W], const double (&v)[W], int p, int& kp, double& vp) {
+  kp = -1;
+  vp = 0.0;
+#pragma unroll
+  for (int u = 0; u < W; ++u) {  // select chains: no dynamically indexed register arrays (scratch)
+    kp = u == p ? k[u] : kp;
+    vp = u == p ? v[u] : vp;
+  }
+}
+template <int W, int WA, bool FULL, typename TA>
+__device__ __forceinline__ double line_res2_lean(const int (&k)[W], const double (&v)[W], int j, int wart,
+                                                 const int32_t* __restrict__ a_idx, const TA* __restrict__ a_val) {
+  double r2 = 1.0;
+#pragma unroll 1
+  for (int p = 0; p < W; ++p) {
+    int kp, ip[WA];
+    double vp;
+    TA xp[WA];
+    slot_of<W>(k, v, p, kp, vp);
+    a_line_opaque<WA, FULL, TA>(kp, wart, a_idx, a_val, ip, xp);
+    double cp = 0.0, gpp = 0.0;
+#pragma unroll
+    for (int s = 0; s < WA; ++s) {
+      const double x = (double)xp[s];
+      gpp = fma(x, x, gpp);
+      cp += (ip[s] == j) ? x : 0.0;
+    }
+    double acc = fma(vp, gpp, -2.0 * cp);
+#pragma unroll 1
+    for (int q = p + 1; q < W; ++q) {
+      int kq, iq[WA];
+      double vq;
+      TA xq[WA];
+      slot_of<W>(k, v, q, kq, vq);
+      a_line_opaque<WA, FULL, TA>(kq, wart, a_idx, a_val, iq, xq);
+      acc = fma(vq, 2.0 * pair_dot<WA, TA>(ip, xp, iq, xq), acc);
+    }
+    r2 = fma(vp, acc, r2);
+  }
+  return r2;
+}
+
+template <int W, int WA, bool FULL, typename TA, typename TV, typename GT>
+__device__ __forceinline__ void resid_gram_body(int32_t line_begin, int32_t line_end, int32_t wrt, int32_t wart,
+                                                int32_t B, int32_t nblk, const int32_t* __restrict__ m_idx,
+                                                int64_t idx_bstride, const TV* __restrict__ m_val,
+                                                int64_t val_bstride, const int32_t* __restrict__ a_idx,
+                                                const TA* __restrict__ a_val, const int32_t* __restrict__ pat_idx,
+                                                const GT* __restrict__ gram, const int32_t* __restrict__ line_entry,
+                                                double* __restrict__ partials, double (&sred)[kChunk][kNT / 64]) {
+  constexpr int T = W * (W + 1) / 2;
+  const int blk = xcd_remap(blockIdx.x, gridDim.x);
+  const int j = line_begin + blk * kNT + threadIdx.x;
+  const bool valid = j < line_end;
+  const int jj = valid ? j : line_begin;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int pk[W];  // the cached pattern's indices of the line
+  {
+    int k[W];
+    load_slots<W, FULL, int>(pat_idx + (int64_t)jj * wrt, wrt, k);
+#pragma unroll
+    for (int p = 0; p < W; ++p) pk[p] = p < wrt ? k[p] : -1;
+  }
+  const GT* gp = gram + (int64_t)line_entry[jj] * (T + W);
+  int kn[W];
+  TV xn[W];
+  auto load_sample = [&](int b) {
+    load_slots<W, FULL, int>(m_idx + (int64_t)b * idx_bstride + (int64_t)jj * wrt, wrt, kn);
+    load_slots<W, FULL, TV>(m_val + (int64_t)b * val_bstride + (int64_t)jj * wrt, wrt, xn);
+  };
+  load_sample(0);
+#pragma unroll 1
+  for (int b0 = 0; b0 < B; b0 += kChunk) {
+    const int nb = min(kChunk, B - b0);
+    double r2s[kChunk];
+#pragma unroll
+    for (int i = 0; i < kChunk; ++i) r2s[i] = 0.0;
+#pragma unroll 1
+    for (int i = 0; i < nb; ++i) {
+      int k[W];
+      double v[W];
+      bool aligned = true;
+#pragma unroll
+      for (int p = 0; p < W; ++p) {
+        const int kp = (valid && p < wrt) ? kn[p] : -1;
+        k[p] = kp >= 0 ? kp : -1;
+        v[p] = kp >= 0 ? (double)xn[p] : 0.0;
+        aligned = aligned && (kp < 0 || kp == pk[p]);
+      }
+      if (b0 + i + 1 < B) load_sample(b0 + i + 1);  // in flight while this sample is evaluated
+      double r2 = 0.0;
+      if (valid && aligned) {  // line_res2 on the cached Gram
+        // the entry read as 16-byte pieces (entries are 16-byte aligned: T + W is a multiple of
+        // 16 / sizeof(GT); each piece loaded once per sample, a quarter / half of the load
+        // instructions of element loads)
+        typedef GT gvec_t __attribute__((ext_vector_type(16 / sizeof(GT))));
+        constexpr int kPer = 16 / sizeof(GT);
+        const gvec_t* gv = reinterpret_cast<const gvec_t*>(gp);  // (the compiler keeps the entry in
+        // registers across the samples: re-reading it per sample from L1 measured 103 vs 83 us at C3)
+        auto G = [&](int q) { return (double)gv[q / kPer][q % kPer]; };
+        r2 = 1.0;
+#pragma unroll
+        for (int p = 0; p < W; ++p) {
+          const int g0 = p * W - p * (p - 1) / 2;  // G_pp; G_pq at g0 + q - p
+          double acc = fma(v[p], G(g0), -2.0 * G(T + p));
+#pragma unroll
+          for (int q = p + 1; q < W; ++q) acc = fma(v[q], 2.0 * G(g0 + q - p), acc);
+          r2 = fma(v[p], acc, r2);
+        }
+      } else if (valid) {
+        r2 = line_res2_lean<W, WA, FULL, TA>(k, v, j, wart, a_idx, a_val);
+      }
+#pragma unroll
+      for (int u = 0; u < kChunk; ++u) r2s[u] = u == i ? r2 : r2s[u];
+    }
+#pragma unroll
+    for (int i = 0; i < kChunk; ++i) {
+      if (i < nb) {
+        const double r2 = wave_sum_dpp(r2s[i]);
+        if (lane == 0) sred[i][w] = r2;
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x < nb) {
+      double s = 0.0;
+#pragma unroll
+      for (int u = 0; u < kNT / 64; ++u) s += sred[threadIdx.x][u];
+      partials[(int64_t)(b0 + threadIdx.x) * nblk + blk] = s;
+    }
+    __syncthreads();
+  }
+}
+
+// (164 registers, 3 waves per SIMD; asking for 4 spills: 137 vs 103 us at C3)
+template <int W, int WA, typename TA, typename TV, typename GT>
+__global__ __launch_bounds__(kNT) void k_resid_gram(int32_t line_begin, int32_t line_end, int32_t wrt, int32_t wart,
+                                                    int32_t B, int32_t nblk, const int32_t* __restrict__ m_idx,
+                                                    int64_t idx_bstride, const TV* __restrict__ m_val,
+                                                    int64_t val_bstride, const int32_t* __restrict__ a_idx,
+                                                    const TA* __restrict__ a_val, const int32_t* __restrict__ pat_idx,
+                                                    const GT* __restrict__ gram, const int32_t* __restrict__ line_entry,
+                                                    double* __restrict__ partials) {
+  static_assert(sizeof(TA) == 4, "fp32(-exact) A values (the unaligned lanes' fallback)");
+  static_assert((W * (W + 1) / 2 + W) % (16 / sizeof(GT)) == 0, "16-byte aligned dictionary entries");
+  __shared__ double sred[kChunk][kNT / 64];
+  if (wrt == W && wart == WA)
+    resid_gram_body<W, WA, true, TA, TV, GT>(line_begin, line_end, wrt, wart, B, nblk, m_idx, idx_bstride, m_val,
+                                             val_bstride, a_idx, a_val, pat_idx, gram, line_entry, partials, sred);
+  else
+    resid_gram_body<W, WA, false, TA, TV, GT>(line_begin, line_end, wrt, wart, B, nblk, m_idx, idx_bstride, m_val,
+                                              val_bstride, a_idx, a_val, pat_idx, gram, line_entry, partials, sred);
+}
+
 // Wide lines (8 <= W <= 16, C3's 13-wide lines), SIXTEEN lanes per line: lane p of a 16-lane row
 // holds slot p only — the index and values of A line k_p (2 WA registers) and the chunk's 8
 // values v_ip — so a line's 78 entry-pair matchings are spread over its lanes at ~100 registers
@@ -787,10 +972,61 @@ static const ResidVariant kResid[] = {
     {13, 7, SPAI_DTYPE_F32, SPAI_DTYPE_F64, launch_resid<13, 7, float, double>},
 };
 
+template <typename TV, typename GT>
+void launch_resid_gram(int32_t lb, int32_t le, int32_t wrt, int32_t wart, int32_t B, int32_t nblk, const int32_t* mi,
+                       int64_t ib, const void* mv, int64_t vb, const int32_t* ai, const void* av, const int32_t* pat_idx,
+                       const void* gram, const int32_t* line_entry, double* partials, hipStream_t s) {
+  k_resid_gram<13, 7, float, TV, GT><<<nblk, kNT, 0, s>>>(lb, le, wrt, wart, B, nblk, mi, ib, static_cast<const TV*>(mv),
+                                                          vb, ai, static_cast<const float*>(av), pat_idx,
+                                                          static_cast<const GT*>(gram), line_entry, partials);
+}
+
 }  // namespace
 }  // namespace spai
 
 using namespace spai;
+
+extern "C" int spai_residual_lines_gram(int32_t n, int32_t line_begin, int32_t line_end, int32_t W,
+                                        const int32_t* m_idx, int64_t idx_bstride, const void* m_val, int32_t m_dtype,
+                                        int64_t val_bstride, int32_t WA, const int32_t* a_idx, const void* a_val,
+                                        int32_t a_dtype, const int32_t* pat_idx, const void* gram_dict,
+                                        int32_t gram_dtype, const int32_t* line_entry, int32_t B, double* res2_out,
+                                        void* workspace, size_t workspace_bytes, void* stream) {
+  SPAI_CHECK_ARG(n >= 1 && line_begin >= 0 && line_end >= line_begin && line_end <= n && W >= 1 && WA >= 1 &&
+                     B >= 1 && idx_bstride >= 0 && val_bstride >= 0,
+                 "spai_residual_lines_gram: bad shape");
+  SPAI_CHECK_ARG(m_idx && m_val && a_idx && a_val && pat_idx && gram_dict && line_entry && res2_out && workspace,
+                 "spai_residual_lines_gram: null pointer");
+  SPAI_CHECK_ARG(m_dtype == SPAI_DTYPE_F32 || m_dtype == SPAI_DTYPE_F64, "spai_residual_lines_gram: bad m_dtype");
+  SPAI_CHECK_ARG(gram_dtype == SPAI_DTYPE_F32 || gram_dtype == SPAI_DTYPE_F64,
+                 "spai_residual_lines_gram: bad gram_dtype");
+  SPAI_CHECK_ARG(((uintptr_t)gram_dict & 15) == 0, "spai_residual_lines_gram: gram_dict not 16-byte aligned");
+  if (W != 13 || WA > 7 || a_dtype != SPAI_DTYPE_F32) {
+    set_error("spai_residual_lines_gram: 13-wide lines of M over A lines <= 7 wide with fp32(-exact) A values only "
+              "(W=%d WA=%d a_dtype %d): use spai_residual_lines",
+              W, WA, a_dtype);
+    return SPAI_ERR_UNSUPPORTED;
+  }
+  const int32_t nl = line_end - line_begin;
+  hipStream_t s = (hipStream_t)stream;
+  if (nl == 0) {
+    SPAI_CHECK_HIP(hipMemsetAsync(res2_out, 0, sizeof(double) * B, s));
+    return SPAI_OK;
+  }
+  SPAI_CHECK_ARG(workspace_bytes >= spai_residual_workspace_bytes(nl, B),
+                 "spai_residual_lines_gram: workspace too small");
+  const int32_t nblk = (nl + kNT - 1) / kNT;
+  double* partials = static_cast<double*>(workspace);
+  const bool m32 = m_dtype == SPAI_DTYPE_F32, g32 = gram_dtype == SPAI_DTYPE_F32;
+  auto fn = m32 ? (g32 ? launch_resid_gram<float, float> : launch_resid_gram<float, double>)
+                : (g32 ? launch_resid_gram<double, float> : launch_resid_gram<double, double>);
+  fn(line_begin, line_end, W, WA, B, nblk, m_idx, idx_bstride, m_val, val_bstride, a_idx, a_val, pat_idx, gram_dict,
+     line_entry, partials, s);
+  SPAI_CHECK_LAUNCH();
+  k_resid_reduce<<<B, kNT, 0, s>>>(partials, nblk, res2_out);
+  SPAI_CHECK_LAUNCH();
+  return SPAI_OK;
+}
 
 extern "C" size_t spai_residual_workspace_bytes(int32_t n_lines, int32_t B) {
   if (n_lines < 0 || B < 1) return 0;

@@ -239,11 +239,16 @@ def narrow_values(a_lines: Lines) -> torch.Tensor:
 
 
 def residual_lines(m_idx: torch.Tensor, m_val: torch.Tensor, a_lines: Lines, line_begin: int = 0,
-                   line_end: int | None = None) -> torch.Tensor:
+                   line_end: int | None = None, gram=None, pattern: Lines | None = None) -> torch.Tensor:
     """res2 [B] fp64 = sum over lines [begin, end) of ||sum_p M_b[l,p] A_line(idx_b[l,p]) - e_l||^2
     for B ARBITRARY sparse M_b in ELL lines: m_idx [B, n, W] or [n, W] (one index set for every
     sample) int32 with -1 = empty slot, m_val [B, n, W] fp32/fp64 (the generic SpMM residual of
-    preconditioner.py:79-93; spai_residual_lines)."""
+    preconditioner.py:79-93; spai_residual_lines).
+
+    ``gram`` (a CacheDict of ``pattern``'s Gram cache over these A lines, as PreconditionerEnv
+    keeps for 13-wide patterns): lines whose index sets are slot-aligned sub-patterns of
+    ``pattern`` take G, c from it instead of matching A (spai_residual_lines_gram; the same bits).
+    Other widths and dtypes run the matching kernel."""
     _lib.require_device(m_val)
     if m_val.dim() == 2:
         m_val = m_val.unsqueeze(0)
@@ -260,12 +265,22 @@ def residual_lines(m_idx: torch.Tensor, m_val: torch.Tensor, a_lines: Lines, lin
     res2 = torch.empty(B, dtype=torch.float64, device=m_val.device)
     nb = _l().spai_residual_workspace_bytes(max(line_end - line_begin, 0), B)
     ws = _lib.workspace(nb, m_val.device, "residual")
+    use_gram = (isinstance(gram, CacheDict) and pattern is not None and W == 13 and pattern.width == W
+                and pattern.n == n and a_lines.width <= 7 and a_val.dtype == torch.float32)
     with _timed("residual_lines"):
-        st = _l().spai_residual_lines(n, line_begin, line_end, W, _lib.ptr(m_idx), n * W if m_idx.dim() == 3 else 0,
-                                      _lib.ptr(m_val), _DT[m_val.dtype], n * W, a_lines.width, _lib.ptr(a_lines.idx),
-                                      _lib.ptr(a_val), _DT[a_val.dtype], B, _lib.ptr(res2),
-                                      _lib.ptr(ws), ws.numel(), _lib.stream_ptr(m_val.device))
-    _lib.check(st, "spai_residual_lines")
+        if use_gram:
+            st = _l().spai_residual_lines_gram(n, line_begin, line_end, W, _lib.ptr(m_idx),
+                                               n * W if m_idx.dim() == 3 else 0, _lib.ptr(m_val), _DT[m_val.dtype],
+                                               n * W, a_lines.width, _lib.ptr(a_lines.idx), _lib.ptr(a_val),
+                                               _DT[a_val.dtype], _lib.ptr(pattern.idx), _lib.ptr(gram.table),
+                                               _DT[gram.dtype], _lib.ptr(gram.entry), B, _lib.ptr(res2),
+                                               _lib.ptr(ws), ws.numel(), _lib.stream_ptr(m_val.device))
+        else:
+            st = _l().spai_residual_lines(n, line_begin, line_end, W, _lib.ptr(m_idx),
+                                          n * W if m_idx.dim() == 3 else 0, _lib.ptr(m_val), _DT[m_val.dtype], n * W,
+                                          a_lines.width, _lib.ptr(a_lines.idx), _lib.ptr(a_val), _DT[a_val.dtype], B,
+                                          _lib.ptr(res2), _lib.ptr(ws), ws.numel(), _lib.stream_ptr(m_val.device))
+    _lib.check(st, "spai_residual_lines_gram" if use_gram else "spai_residual_lines")
     return res2
 
 

@@ -82,7 +82,7 @@ def main():
         allrec[key] = rec
         # the generic residual leg's kernel (bench roofline_residual), when it ran in this command
         res = [(k, v) for k, v in summary["kernels"].items()
-               if ("k_resid_shared<" in k or "k_resid_wide<" in k) and "hbm_bytes_per_launch" in v]
+               if ("k_resid_shared<" in k or "k_resid_wide<" in k or "k_resid_gram<" in k) and "hbm_bytes_per_launch" in v]
         if res:
             k, v = res[0]
             allrec[args.config + "_residual"] = {

@@ -70,7 +70,7 @@ def test_binding_signatures_match_header_parameter_lists():
 
 def test_integration_stub_matches_header():
     """The reference-side binding published in INTEGRATION.md binds every function it calls with
-    the header's parameter list (ABI 16), and calls each with that many arguments."""
+    the header's parameter list (ABI 17), and calls each with that many arguments."""
     import ast
     from .abi_header import integration_stub, parse_header
     hdr = parse_header()

@@ -809,6 +809,53 @@ def test_residual_lines_shared_pattern_and_conflicting_lanes(dims, exact):
         assert alone[0] == got[b]
 
 
+@pytest.mark.parametrize("mdt", [torch.float64, torch.float32])
+def test_residual_lines_gram_cache_bit_identical(mdt):
+    """spai_residual_lines_gram (13-wide C3 geometry, the env's Gram cache dictionary) against the
+    index-matching kernel (spai_residual_lines) bit for bit, B = 9 samples: every sample a
+    slot-aligned sub-pattern of the env's pattern (random removals -> -1), except sample 3, which
+    puts a foreign index into one slot of ~10 % of the lines (those lines are matched from A by the
+    lean fallback).  Also a fully aligned batch, and both against scipy's ||A M_b - I||_F^2."""
+    from gflownet_spai_amd import PreconditionerEnv, axial_pattern_3d, kernels, poisson_3d
+    A, P = poisson_3d(16), axial_pattern_3d(16)
+    n = A.shape[0]
+    env = PreconditionerEnv(n, P, A, side="AM", fill="lsq")
+    assert isinstance(env.gram, kernels.CacheDict) and env.pattern.width == 13
+    pat = env.pattern.idx.cpu().numpy()
+    rng = np.random.default_rng(21)
+    B, W = 9, 13
+    idx = np.repeat(pat[None], B, 0).copy()
+    idx[rng.random(idx.shape) < 0.25] = -1
+    aligned = idx.copy()
+    for l in np.nonzero(rng.random(n) < 0.1)[0]:
+        p = int(np.argmax(pat[l] >= 0))
+        new = int(rng.integers(0, n))
+        while new in set(pat[l].tolist()):
+            new = int(rng.integers(0, n))
+        idx[3, l, p] = new
+    val = torch.from_numpy(rng.standard_normal((B, n, W))).to(mdt)
+    c = A.coalesce()
+    Asp = sp.csr_matrix((c.values().double().numpy(), (c.indices()[0].numpy(), c.indices()[1].numpy())), shape=(n, n))
+    I = sp.identity(n, format="csr")
+    for ix in (aligned, idx):
+        ti = torch.from_numpy(ix).to(DEV)
+        ref = kernels.residual_lines(ti, val.to(DEV), env.a_lines)
+        got = kernels.residual_lines(ti, val.to(DEV), env.a_lines, gram=env.gram, pattern=env.pattern)
+        assert torch.equal(got, ref)
+        g = got.cpu().numpy()
+        for b in (0, 3):
+            ok = ix[b] >= 0
+            lines, _ = np.nonzero(ok)
+            M = sp.csr_matrix((val[b].double().numpy()[ok], (ix[b][ok], lines)), shape=(n, n))
+            assert g[b] == pytest.approx(sp.linalg.norm(Asp @ M - I) ** 2, rel=1e-12)
+    # line shards sum to the whole (256-line blocks: the same partial sums)
+    ti = torch.from_numpy(idx).to(DEV)
+    h = 256 * (n // 512)
+    parts = (kernels.residual_lines(ti, val.to(DEV), env.a_lines, 0, h, gram=env.gram, pattern=env.pattern) +
+             kernels.residual_lines(ti, val.to(DEV), env.a_lines, h, n, gram=env.gram, pattern=env.pattern))
+    np.testing.assert_allclose(parts.cpu().numpy(), got.cpu().numpy(), rtol=1e-13)
+
+
 @pytest.mark.parametrize("kind", ["2d_lsq", "2d_copy", "3d_axial", "3d_axial_f64"])
 def test_gram_dict_is_bit_identical(kind):
     # (the env holds 5/7-wide Gram caches in full; the dictionary is built here explicitly)

@@ -229,9 +229,17 @@ def generic_residual_leg(env, log, cfg: str, reps: int = 10):
     idx = torch.where(rem | (pat.idx < 0), torch.full_like(pat.idx, -1), pat.idx).contiguous()
     m = env.last_m.contiguous()
     B, n, W = m.shape
-    # 13-wide patterns: G, c from the env's Gram cache dictionary (the index matching is done once
-    # per env; spai_residual_lines_gram, bit-identical to the matching kernel)
-    gram = env.gram if isinstance(env.gram, kernels.CacheDict) and m.shape[2] == 13 else None
+    # 13-wide lines: G, c from the pattern's Gram cache dictionary (the index matching done once per
+    # env, untimed: the env's own cache, or one built here when the env keeps none — the QR fill
+    # reads its R cache; spai_residual_lines_gram, bit-identical to the matching kernel).  5/7-wide
+    # lines keep the matching kernel: their matching is cheap (C4: 80 us from the dictionary vs 70)
+    gram = env.gram if W > 7 else None
+    if gram is None and W > 7:
+        gram = kernels.gram_build(pat, a)
+        g32 = kernels.gram_compact(gram, pat)
+        gram = g32 if g32 is not None else gram
+    if torch.is_tensor(gram):
+        gram = kernels.cache_dict(gram, pat.n)
     kw = dict(gram=gram, pattern=pat) if gram is not None else {}
     res2 = kernels.residual_lines(idx, m, a, **kw)  # warm-up
     kernels.TIMERS = {}
@@ -245,7 +253,7 @@ def generic_residual_leg(env, log, cfg: str, reps: int = 10):
     av = kernels.narrow_values(a)  # fp64 A with fp32-exact values is read as fp32 (same numbers)
     bytes_a = a.idx.numel() * 4 + av.numel() * av.element_size()
     bytes_m = n * W * (4 + m.element_size())
-    name = "k_resid_shared" if W <= 7 else ("k_resid_gram" if gram is not None else "k_resid_wide")
+    name = "k_resid_gram" if gram is not None else ("k_resid_shared" if W <= 7 else "k_resid_wide")
     extra = (f"; G, c from the pattern's Gram cache dictionary ({gram.entries} entries, "
              f"{kernels.cache_nbytes(gram)} B)" if gram is not None else "")
     out = roofline_obj(f"{name}<{W},{a.width},{str(av.dtype)[6:]},{str(m.dtype)[6:]}> (||A M_b - I||_F^2 of "

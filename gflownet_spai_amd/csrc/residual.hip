@@ -618,9 +618,10 @@ __device__ __forceinline__ void resid_gram_body(int32_t line_begin, int32_t line
         // instructions of element loads)
         typedef GT gvec_t __attribute__((ext_vector_type(16 / sizeof(GT))));
         constexpr int kPer = 16 / sizeof(GT);
+        constexpr bool kVec = (T + W) % kPer == 0;  // 16-byte aligned entries (W = 5, 13; not 7)
         const gvec_t* gv = reinterpret_cast<const gvec_t*>(gp);  // (the compiler keeps the entry in
         // registers across the samples: re-reading it per sample from L1 measured 103 vs 83 us at C3)
-        auto G = [&](int q) { return (double)gv[q / kPer][q % kPer]; };
+        auto G = [&](int q) { return kVec ? (double)gv[q / kPer][q % kPer] : (double)gp[q]; };
         r2 = 1.0;
 #pragma unroll
         for (int p = 0; p < W; ++p) {
@@ -664,7 +665,6 @@ __global__ __launch_bounds__(kNT) void k_resid_gram(int32_t line_begin, int32_t 
                                                     const GT* __restrict__ gram, const int32_t* __restrict__ line_entry,
                                                     double* __restrict__ partials) {
   static_assert(sizeof(TA) == 4, "fp32(-exact) A values (the unaligned lanes' fallback)");
-  static_assert((W * (W + 1) / 2 + W) % (16 / sizeof(GT)) == 0, "16-byte aligned dictionary entries");
   __shared__ double sred[kChunk][kNT / 64];
   if (wrt == W && wart == WA)
     resid_gram_body<W, WA, true, TA, TV, GT>(line_begin, line_end, wrt, wart, B, nblk, m_idx, idx_bstride, m_val,
@@ -972,13 +972,19 @@ static const ResidVariant kResid[] = {
     {13, 7, SPAI_DTYPE_F32, SPAI_DTYPE_F64, launch_resid<13, 7, float, double>},
 };
 
-template <typename TV, typename GT>
+template <int W, int WA, typename TV, typename GT>
 void launch_resid_gram(int32_t lb, int32_t le, int32_t wrt, int32_t wart, int32_t B, int32_t nblk, const int32_t* mi,
                        int64_t ib, const void* mv, int64_t vb, const int32_t* ai, const void* av, const int32_t* pat_idx,
                        const void* gram, const int32_t* line_entry, double* partials, hipStream_t s) {
-  k_resid_gram<13, 7, float, TV, GT><<<nblk, kNT, 0, s>>>(lb, le, wrt, wart, B, nblk, mi, ib, static_cast<const TV*>(mv),
+  k_resid_gram<W, WA, float, TV, GT><<<nblk, kNT, 0, s>>>(lb, le, wrt, wart, B, nblk, mi, ib, static_cast<const TV*>(mv),
                                                           vb, ai, static_cast<const float*>(av), pat_idx,
                                                           static_cast<const GT*>(gram), line_entry, partials);
+}
+using ResidGramFn = decltype(&launch_resid_gram<5, 5, float, float>);
+template <int W, int WA>
+ResidGramFn pick_resid_gram(bool m32, bool g32) {
+  return m32 ? (g32 ? launch_resid_gram<W, WA, float, float> : launch_resid_gram<W, WA, float, double>)
+             : (g32 ? launch_resid_gram<W, WA, double, float> : launch_resid_gram<W, WA, double, double>);
 }
 
 }  // namespace
@@ -1001,9 +1007,11 @@ extern "C" int spai_residual_lines_gram(int32_t n, int32_t line_begin, int32_t l
   SPAI_CHECK_ARG(gram_dtype == SPAI_DTYPE_F32 || gram_dtype == SPAI_DTYPE_F64,
                  "spai_residual_lines_gram: bad gram_dtype");
   SPAI_CHECK_ARG(((uintptr_t)gram_dict & 15) == 0, "spai_residual_lines_gram: gram_dict not 16-byte aligned");
-  if (W != 13 || WA > 7 || a_dtype != SPAI_DTYPE_F32) {
-    set_error("spai_residual_lines_gram: 13-wide lines of M over A lines <= 7 wide with fp32(-exact) A values only "
-              "(W=%d WA=%d a_dtype %d): use spai_residual_lines",
+  // the cache's width is the pattern's: W exactly 5 (A <= 5 wide), 7 or 13 (A <= 7 wide)
+  const bool shape_ok = (W == 5 && WA <= 5) || ((W == 7 || W == 13) && WA <= 7);
+  if (!shape_ok || a_dtype != SPAI_DTYPE_F32) {
+    set_error("spai_residual_lines_gram: lines of M 5 / 7 / 13 wide over A lines <= 5 / 7 / 7 wide with fp32(-exact) "
+              "A values only (W=%d WA=%d a_dtype %d): use spai_residual_lines",
               W, WA, a_dtype);
     return SPAI_ERR_UNSUPPORTED;
   }
@@ -1018,8 +1026,8 @@ extern "C" int spai_residual_lines_gram(int32_t n, int32_t line_begin, int32_t l
   const int32_t nblk = (nl + kNT - 1) / kNT;
   double* partials = static_cast<double*>(workspace);
   const bool m32 = m_dtype == SPAI_DTYPE_F32, g32 = gram_dtype == SPAI_DTYPE_F32;
-  auto fn = m32 ? (g32 ? launch_resid_gram<float, float> : launch_resid_gram<float, double>)
-                : (g32 ? launch_resid_gram<double, float> : launch_resid_gram<double, double>);
+  const ResidGramFn fn = W == 5 ? pick_resid_gram<5, 5>(m32, g32)
+                                : (W == 7 ? pick_resid_gram<7, 7>(m32, g32) : pick_resid_gram<13, 7>(m32, g32));
   fn(line_begin, line_end, W, WA, B, nblk, m_idx, idx_bstride, m_val, val_bstride, a_idx, a_val, pat_idx, gram_dict,
      line_entry, partials, s);
   SPAI_CHECK_LAUNCH();

@@ -245,10 +245,11 @@ def residual_lines(m_idx: torch.Tensor, m_val: torch.Tensor, a_lines: Lines, lin
     sample) int32 with -1 = empty slot, m_val [B, n, W] fp32/fp64 (the generic SpMM residual of
     preconditioner.py:79-93; spai_residual_lines).
 
-    ``gram`` (a CacheDict of ``pattern``'s Gram cache over these A lines, as PreconditionerEnv
-    keeps for 13-wide patterns): lines whose index sets are slot-aligned sub-patterns of
-    ``pattern`` take G, c from it instead of matching A (spai_residual_lines_gram; the same bits).
-    Other widths and dtypes run the matching kernel."""
+    ``gram`` (a CacheDict of ``pattern``'s Gram cache over these A lines: PreconditionerEnv keeps
+    one for 13-wide patterns, kernels.cache_dict(env.gram, n) makes one of a 5/7-wide cache): lines
+    whose index sets are slot-aligned sub-patterns of ``pattern`` take G, c from it instead of
+    matching A (spai_residual_lines_gram; the same bits). Other widths and dtypes run the matching
+    kernel."""
     _lib.require_device(m_val)
     if m_val.dim() == 2:
         m_val = m_val.unsqueeze(0)
@@ -265,8 +266,9 @@ def residual_lines(m_idx: torch.Tensor, m_val: torch.Tensor, a_lines: Lines, lin
     res2 = torch.empty(B, dtype=torch.float64, device=m_val.device)
     nb = _l().spai_residual_workspace_bytes(max(line_end - line_begin, 0), B)
     ws = _lib.workspace(nb, m_val.device, "residual")
-    use_gram = (isinstance(gram, CacheDict) and pattern is not None and W == 13 and pattern.width == W
-                and pattern.n == n and a_lines.width <= 7 and a_val.dtype == torch.float32)
+    use_gram = (isinstance(gram, CacheDict) and pattern is not None and pattern.width == W and pattern.n == n
+                and (W, a_lines.width) in ((5, 5), (5, 4), (5, 3), (7, 7), (7, 6), (7, 5), (13, 7), (13, 6), (13, 5))
+                and a_val.dtype == torch.float32)
     with _timed("residual_lines"):
         if use_gram:
             st = _l().spai_residual_lines_gram(n, line_begin, line_end, W, _lib.ptr(m_idx),

@@ -170,8 +170,8 @@ int spai_residual_lines(int32_t n, int32_t line_begin, int32_t line_end, int32_t
                         int64_t idx_bstride, const void* m_val, int32_t m_dtype, int64_t val_bstride, int32_t WA,
                         const int32_t* a_idx, const void* a_val, int32_t a_dtype, int32_t B, double* res2_out,
                         void* workspace, size_t workspace_bytes, void* stream);
-/* The same sums with the index matching taken from a pattern's Gram cache (13-wide lines of M
- * over A lines <= 7 wide, A values fp32 or fp32-exact narrowed): pat_idx [n][W] the pattern's
+/* The same sums with the index matching taken from a pattern's Gram cache (lines of M 5 / 7 / 13
+ * wide over A lines <= 5 / 7 / 7 wide, A values fp32 or fp32-exact narrowed): pat_idx [n][W] the pattern's
  * indices, gram_dict / line_entry its Gram cache as a dictionary (spai_gram_build's blocked
  * cache -> spai_line_cache_dict: distinct entries of W(W+1)/2 + W values, gram_dtype fp32/fp64;
  * 16-byte aligned).

@@ -809,21 +809,30 @@ def test_residual_lines_shared_pattern_and_conflicting_lanes(dims, exact):
         assert alone[0] == got[b]
 
 
-@pytest.mark.parametrize("mdt", [torch.float64, torch.float32])
-def test_residual_lines_gram_cache_bit_identical(mdt):
-    """spai_residual_lines_gram (13-wide C3 geometry, the env's Gram cache dictionary) against the
-    index-matching kernel (spai_residual_lines) bit for bit, B = 9 samples: every sample a
-    slot-aligned sub-pattern of the env's pattern (random removals -> -1), except sample 3, which
-    puts a foreign index into one slot of ~10 % of the lines (those lines are matched from A by the
-    lean fallback).  Also a fully aligned batch, and both against scipy's ||A M_b - I||_F^2."""
-    from gflownet_spai_amd import PreconditionerEnv, axial_pattern_3d, kernels, poisson_3d
-    A, P = poisson_3d(16), axial_pattern_3d(16)
+@pytest.mark.parametrize("geom,mdt", [("3d13", torch.float64), ("3d13", torch.float32), ("2d5", torch.float32),
+                                      ("3d7", torch.float64)])
+def test_residual_lines_gram_cache_bit_identical(geom, mdt):
+    """spai_residual_lines_gram (the 13-wide C3 geometry with the env's Gram cache dictionary; the
+    5-wide 2-D and 7-wide 3-D stencil patterns with a dictionary made from the env's full cache)
+    against the index-matching kernel (spai_residual_lines) bit for bit, B = 9 samples: every
+    sample a slot-aligned sub-pattern of the env's pattern (random removals -> -1), except sample
+    3, which puts a foreign index into one slot of ~10 % of the lines (those lines are matched from
+    A by the lean fallback).  Also a fully aligned batch, and both against scipy's
+    ||A M_b - I||_F^2."""
+    from gflownet_spai_amd import PreconditionerEnv, axial_pattern_3d, kernels, poisson_2d, poisson_3d
+    if geom == "3d13":
+        A, P = poisson_3d(16), axial_pattern_3d(16)
+    else:
+        A = P = poisson_2d(40) if geom == "2d5" else poisson_3d(12)
     n = A.shape[0]
     env = PreconditionerEnv(n, P, A, side="AM", fill="lsq")
-    assert isinstance(env.gram, kernels.CacheDict) and env.pattern.width == 13
+    W = env.pattern.width
+    assert W == int(geom[2:])
+    gram = env.gram if W == 13 else kernels.cache_dict(env.gram, n)
+    assert isinstance(gram, kernels.CacheDict)
     pat = env.pattern.idx.cpu().numpy()
     rng = np.random.default_rng(21)
-    B, W = 9, 13
+    B = 9
     idx = np.repeat(pat[None], B, 0).copy()
     idx[rng.random(idx.shape) < 0.25] = -1
     aligned = idx.copy()
@@ -840,7 +849,7 @@ def test_residual_lines_gram_cache_bit_identical(mdt):
     for ix in (aligned, idx):
         ti = torch.from_numpy(ix).to(DEV)
         ref = kernels.residual_lines(ti, val.to(DEV), env.a_lines)
-        got = kernels.residual_lines(ti, val.to(DEV), env.a_lines, gram=env.gram, pattern=env.pattern)
+        got = kernels.residual_lines(ti, val.to(DEV), env.a_lines, gram=gram, pattern=env.pattern)
         assert torch.equal(got, ref)
         g = got.cpu().numpy()
         for b in (0, 3):
@@ -851,8 +860,8 @@ def test_residual_lines_gram_cache_bit_identical(mdt):
     # line shards sum to the whole (256-line blocks: the same partial sums)
     ti = torch.from_numpy(idx).to(DEV)
     h = 256 * (n // 512)
-    parts = (kernels.residual_lines(ti, val.to(DEV), env.a_lines, 0, h, gram=env.gram, pattern=env.pattern) +
-             kernels.residual_lines(ti, val.to(DEV), env.a_lines, h, n, gram=env.gram, pattern=env.pattern))
+    parts = (kernels.residual_lines(ti, val.to(DEV), env.a_lines, 0, h, gram=gram, pattern=env.pattern) +
+             kernels.residual_lines(ti, val.to(DEV), env.a_lines, h, n, gram=gram, pattern=env.pattern))
     np.testing.assert_allclose(parts.cpu().numpy(), got.cpu().numpy(), rtol=1e-13)
 
 

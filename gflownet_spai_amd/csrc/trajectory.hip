@@ -9,11 +9,13 @@
 // Ordering ~1e6 winners per sample is a SAMPLE SORT whose only global data movement is
 // one coalesced staging write and one gather of contiguous runs:
 //   k_presample  arrival times of a pseudo-random stratified subset of <= 65536 actions per
-//                sample (1.2 % of the Philox work at C4); winners kept in subset order.  Its
+//                sample (1.2 % of the Philox work at C4); winners kept in subset order, each
+//                block's key range, the terminal's arrival time; with the policy's fc block
+//                maxima (spai_rollout_select_pm) one extra block reduces them to lmax.
+//   k_splitters  per sample: value-linear histogram quantiles of the sampled winner keys
+//                -> nb ~ est/4096 bucket splitters and a 4096-bin bucket lookup table.  Its
 //                extra blocks precompute the per-action inverse rates r and weights
 //                w = e^(l - lmax) once per logits row (shared by every sample of the row).
-//   k_splitters  per sample: value-linear histogram quantiles of the sampled winner keys
-//                -> nb ~ est/4096 bucket splitters and a 4096-bin bucket lookup table.
 //   k_tile       one kTile (8192)-action tile of one sample per 512-thread block, two blocks
 //                per CU (the samples of a tile share an XCD and its L2): Philox4x32-10 +
 //                deterministic fp32 arrival times (in registers), removal bitmap words, the

@@ -489,7 +489,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2))) void k_
 // each, contiguous) and line_entry[j] names line j's entry; else the full cache, 64 lines
 // interleaved per entry value (coalesced).
 template <int W, typename TM, bool kDict>
-__global__ __launch_bounds__(kQNT) __attribute__((amdgpu_waves_per_eu(W <= 5 ? QRS_WPE : 2))) void k_qr_solve(
+__global__ __launch_bounds__(kQNT) __attribute__((amdgpu_waves_per_eu(W <= 5 ? QRS_WPE : (W <= 7 ? 2 : 1)))) void k_qr_solve(
     int32_t line_begin, int32_t line_end, int32_t wrt, const int32_t* __restrict__ pat_act,
     const double* __restrict__ rcache, const int32_t* __restrict__ line_entry, int32_t B,
     const uint32_t* __restrict__ removed, int32_t words, int32_t word_base, TM* __restrict__ m_out,
@@ -502,7 +502,10 @@ __global__ __launch_bounds__(kQNT) __attribute__((amdgpu_waves_per_eu(W <= 5 ? Q
 #else
   __shared__ __attribute__((aligned(16))) TM s_m[1][kQNT * W];  // per-wave regions
 #endif
-  __shared__ double s_c0[W + 1][kQNT];  // the line's Q^T e and tail (LDS, not registers: 4 waves per SIMD)
+  // W > 7 (13-wide lines): the line's 91-value R is not held across the samples (with the working
+  // copy it would take ~370 registers) but re-read per sample from the cache (its dictionary: L1/L2)
+  constexpr bool kHold = W <= 7;
+  __shared__ double s_c0[kHold ? W + 1 : 1][kQNT];  // the line's Q^T e and tail (LDS, not registers: 4 waves per SIMD)
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int lb = blockIdx.x;
   const int j = line_begin + lb * kQNT + t;
@@ -519,21 +522,24 @@ __global__ __launch_bounds__(kQNT) __attribute__((amdgpu_waves_per_eu(W <= 5 ? Q
 #pragma unroll
     for (int p = 0; p < W; ++p) act[p] = (valid && p < wrt) ? av[p] : -1;
   }
-  double R0[T];
+  double R0[kHold ? T : 1];
   float thf[W];  // the rank floors 1e-24 ||D[:, p]||^2 in fp32 (registers: 4 waves per SIMD at W = 5)
   // a dictionary entry is shared by most lanes of a wave (stencil lines): broadcast loads from L2
   constexpr int kStride = kDict ? 1 : 64;
   const double* rp = kDict ? rcache + (int64_t)line_entry[jj] * NQ : rcache + (int64_t)(jj >> 6) * NQ * 64 + (jj & 63);
+  auto rval = [&](int q) { return kHold ? R0[q] : rp[q * kStride]; };
+  if constexpr (kHold) {
 #pragma unroll
-  for (int q = 0; q < T; ++q) R0[q] = rp[q * kStride];
+    for (int q = 0; q < T; ++q) R0[q] = rp[q * kStride];
 #pragma unroll
-  for (int p = 0; p <= W; ++p) s_c0[p][t] = rp[(T + p) * kStride];  // read back by this thread only
+    for (int p = 0; p <= W; ++p) s_c0[p][t] = rp[(T + p) * kStride];  // read back by this thread only
+  }
 #pragma unroll
   for (int p = 0; p < W; ++p) {
     double s = 0.0;
 #pragma unroll
     for (int i = 0; i <= p; ++i) {
-      const double x = R0[i * W - i * (i - 1) / 2 + (p - i)];
+      const double x = rval(i * W - i * (i - 1) / 2 + (p - i));
       s = fma(x, x, s);
     }
     thf[p] = (float)(1e-24 * s);  // (0 only below 1e-21: the floor then drops exact zeros only)
@@ -560,14 +566,27 @@ __global__ __launch_bounds__(kQNT) __attribute__((amdgpu_waves_per_eu(W <= 5 ? Q
       asm volatile("" : "+v"(f));  // widened per sample, not held as fp64 across the loop
       thr[p] = (double)f;
     }
-    double Rm[W][W], c[W], m[W];
+    double Rm[W][W], c[W], m[W], tail;
+    if constexpr (kHold) {
 #pragma unroll
-    for (int i = 0; i < W; ++i) {
+      for (int i = 0; i < W; ++i) {
 #pragma unroll
-      for (int q = i; q < W; ++q) Rm[i][q] = R0[i * W - i * (i - 1) / 2 + (q - i)];
-      c[i] = s_c0[i][t];
+        for (int q = i; q < W; ++q) Rm[i][q] = R0[i * W - i * (i - 1) / 2 + (q - i)];
+        c[i] = s_c0[i][t];
+      }
+      tail = s_c0[W][t];
+    } else {
+      const double* rps = rp;
+      asm volatile("" : "+v"(rps));  // opaque per sample: re-read, not held across the samples
+#pragma unroll
+      for (int i = 0; i < W; ++i) {
+#pragma unroll
+        for (int q = i; q < W; ++q) Rm[i][q] = rps[(i * W - i * (i - 1) / 2 + (q - i)) * kStride];
+        c[i] = rps[(T + i) * kStride];
+      }
+      tail = rps[(T + W) * kStride];
     }
-    const double rs = qr_masked_solve<W>(Rm, c, s_c0[W][t], thr, keep, m);
+    const double rs = qr_masked_solve<W>(Rm, c, tail, thr, keep, m);
     s_r2[b % kQChunk][t] = valid ? rs : 0.0;
 #ifdef QRS_DIRECT  // A/B: M stored from the registers (no LDS staging, no barrier per sample)
     if (m_out != nullptr && valid) {
@@ -819,9 +838,9 @@ extern "C" int spai_fill_lines_qr_cached(int32_t n, int32_t line_begin, int32_t 
   if (nl == 0) return SPAI_OK;
   SPAI_CHECK_ARG(pat_act && rcache && removed, "spai_fill_lines_qr_cached: null input");
   const int wc = qr_cache_class(W, WA);
-  if (wc != 5 && wc != 7) {
-    set_error("spai_fill_lines_qr_cached: width class %d (W=%d WA=%d): the cached solve is compiled for 5 and 7", wc,
-              W, WA);
+  if (wc != 5 && wc != 7 && wc != 13) {
+    set_error("spai_fill_lines_qr_cached: width class %d (W=%d WA=%d): the cached solve is compiled for 5, 7 and 13",
+              wc, W, WA);
     return SPAI_ERR_UNSUPPORTED;
   }
   const int32_t nparts = (nl + kQNT - 1) / kQNT;
@@ -831,10 +850,12 @@ extern "C" int spai_fill_lines_qr_cached(int32_t n, int32_t line_begin, int32_t 
   hipStream_t s = (hipStream_t)stream;
   const bool f64 = m_dtype == SPAI_DTYPE_F64;
   const hipError_t e =
-      wc == 5 ? launch_solve<5>(f64, line_entry, line_begin, line_end, W, pat_act, rcache, B, removed, words,
-                                word_base, m_out, partials, nparts, s)
-              : launch_solve<7>(f64, line_entry, line_begin, line_end, W, pat_act, rcache, B, removed, words,
-                                word_base, m_out, partials, nparts, s);
+      wc == 5   ? launch_solve<5>(f64, line_entry, line_begin, line_end, W, pat_act, rcache, B, removed, words,
+                                  word_base, m_out, partials, nparts, s)
+      : wc == 7 ? launch_solve<7>(f64, line_entry, line_begin, line_end, W, pat_act, rcache, B, removed, words,
+                                  word_base, m_out, partials, nparts, s)
+                : launch_solve<13>(f64, line_entry, line_begin, line_end, W, pat_act, rcache, B, removed, words,
+                                   word_base, m_out, partials, nparts, s);
   SPAI_CHECK_HIP(e);
   return SPAI_OK;
 }

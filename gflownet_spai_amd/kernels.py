@@ -419,12 +419,13 @@ def qr_max_rows(pattern: Lines, a_lines: Lines) -> int:
 
 def qr_cache(pattern: Lines, a_lines: Lines, max_rows: int):
     """The R cache of the QR fill (spai_qr_factor): per line the Householder R of its full block
-    A[I, slots], Q^T e_l and the tail, fp64, built once per env.  None for width classes the
-    cached solve is not compiled for (13-wide lines: the fused spai_fill_lines_qr runs instead)."""
+    A[I, slots], Q^T e_l and the tail, fp64, built once per env (pattern widths <= 13 over A
+    widths <= 7; the 13-wide solve re-reads its line's R per sample at one wave per SIMD).  None
+    for wider lines (the fused spai_fill_lines_qr runs instead)."""
     _lib.require_device(pattern.idx)
     lib = _l()
     nb = lib.spai_qr_cache_bytes(pattern.n, pattern.width, a_lines.width)
-    if nb == 0 or not (pattern.width <= 7 and a_lines.width <= 7):
+    if nb == 0 or not (pattern.width <= 13 and a_lines.width <= 7):
         return None
     rc = torch.zeros(nb // 8, dtype=torch.float64, device=pattern.idx.device)
     av = narrow_values(a_lines)

@@ -15,7 +15,7 @@ import shutil
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ROOF_KERNELS = {"c4": "k_gram_fill<5, ", "c2": "k_gram_fill<5, ", "c3": "k_gram_fill_wide<13, "}  # LSQ fill, any Gram type
-ROOF_KERNELS_QR = {"c4": "k_qr_solve<5, ", "c2": "k_qr_solve<5, ", "c5s": "k_qr_solve<7, ", "c3": "k_qr_fill<13, "}
+ROOF_KERNELS_QR = {"c4": "k_qr_solve<5, ", "c2": "k_qr_solve<5, ", "c5s": "k_qr_solve<7, ", "c3": "k_qr_solve<13, "}
 
 
 def short(name):

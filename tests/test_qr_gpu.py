@@ -190,14 +190,14 @@ def test_qr_wide_row_unions_every_instance(kp, ka, lo, hi):
     """Random sparse A and pattern with nearly disjoint column supports, so the row unions |I| fall
     in the ranges of the larger group instances: <5,5,L8> (17-32 rows), <7,7,L16,NT128> (33-64) and
     <13,7,L32,RPL3> (65-96, the only group sum with the shfl_xor(16) step).  M from the fused kernel
-    and (widths <= 7) from the R cache within 1e-10 of the oracle's QR; the residual vs scipy."""
+    and from the R cache within 1e-10 of the oracle's QR; the residual vs scipy."""
     from gflownet_spai_amd import PreconditionerEnv, kernels
     n = 1500
     A = _random_cols(n, ka, 11)
     P = A if kp == ka else _random_cols(n, kp, 12)
     env = PreconditionerEnv(n, P, A, side="AM", fill="qr", keep_m=True)
     assert lo <= env.qr_rows <= hi, env.qr_rows
-    assert (env.rcache is not None) == (kp <= 7)
+    assert env.rcache is not None  # (13-wide lines too: the cached solve re-reads R per sample)
     A_sp, P_sp = _sp(A), _sp(P)
     idx, act, a_idx, a_val = _lines(A_sp, P_sp, n)
     removed = np.random.default_rng(1).random((2, env.init_nnz)) < np.array([[0.0], [0.3]])
@@ -237,19 +237,21 @@ def test_qr_row_overflow_gives_nan():
     assert torch.isfinite(ok).all()
 
 
-@pytest.mark.parametrize("kind", ["2d", "3d7", "c5s"])
+@pytest.mark.parametrize("kind", ["2d", "3d7", "c5s", "3d13"])
 def test_qr_cached_equals_fused(kind):
     """The R-cache path (phase 1 once per env, spai_fill_lines_qr_cached) against the fused kernel
     (phase 1 every call): the same reflections on the same numbers, only the rank floor's column
     norms are recomputed from R, so M and the residuals agree to rounding (1e-13) — and the cached
     path's exact per-block sums make 256-line-aligned shards bit-identical to one launch."""
-    from gflownet_spai_amd import PreconditionerEnv, kernels, poisson_2d, poisson_3d, thermal_like
+    from gflownet_spai_amd import PreconditionerEnv, axial_pattern_3d, kernels, poisson_2d, poisson_3d, thermal_like
     from gflownet_spai_amd.distributed import LINE_ALIGN, shard_lines
-    A = {"2d": lambda: poisson_2d(80, torch.float32), "3d7": lambda: poisson_3d(14),
+    A = {"2d": lambda: poisson_2d(80, torch.float32), "3d7": lambda: poisson_3d(14), "3d13": lambda: poisson_3d(12),
          "c5s": lambda: thermal_like(40, 0, torch.float64)}[kind]()
+    P = axial_pattern_3d(12) if kind == "3d13" else A  # 3d13: the C3 geometry (13-wide lines, cached solve)
     n = A.shape[0]
-    envc = PreconditionerEnv(n, A, A, side="AM", fill="qr", keep_m=True)
-    envf = PreconditionerEnv(n, A, A, side="AM", fill="qr", keep_m=True, rcache=False)
+    envc = PreconditionerEnv(n, P, A, side="AM", fill="qr", keep_m=True)
+    envf = PreconditionerEnv(n, P, A, side="AM", fill="qr", keep_m=True, rcache=False)
+    assert envc.pattern.width == (13 if kind == "3d13" else envc.pattern.width)
     assert envc.rcache is not None and envf.rcache is None and envc.gram is None
     removed = np.random.default_rng(4).random((9, envc.init_nnz)) < 0.25  # 9: a chunk of 8 + 1
     bits = _bits(removed)

@@ -308,8 +308,8 @@ int spai_fill_lines_qr(int32_t n, int32_t line_begin, int32_t line_end, int32_t 
  * pattern's action ids, one thread per line: the kept columns R_J re-triangularised by Householder
  * reflections of at most W rows (R_J has the singular values of A[I, J]: no normal equations),
  * back-substitution, the same rank floor (the column norms are recomputed as sum_i R_ip^2) and the
- * same outputs / workspace / partial layout as spai_fill_lines_qr (width classes 5 and 7; 13 ->
- * SPAI_ERR_UNSUPPORTED, use spai_fill_lines_qr).  No reference counterpart (utils.py:331-353 copies). */
+ * same outputs / workspace / partial layout as spai_fill_lines_qr (width classes 5, 7 and 13; the
+ * 13-wide class re-reads its line's R per sample).  No reference counterpart (utils.py:331-353 copies). */
 size_t spai_qr_cache_bytes(int32_t n, int32_t W, int32_t WA);
 int spai_qr_factor(int32_t n, int32_t W, const int32_t* pat_idx, const int32_t* pat_act, int32_t WA,
                    const int32_t* a_idx, const void* a_val, int32_t a_dtype, int32_t max_rows, double* rcache,

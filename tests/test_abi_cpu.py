@@ -52,6 +52,18 @@ def test_argument_validation_without_gpu():
         _lib.check(rc, "spai_rollout_select")
     assert lib.spai_fill_workspace_bytes(1000, 4) >= 1000 * 4 * 8
     assert lib.spai_logits_stats_workspace_bytes(10, 2) > 0
+    # the Gram-cached residual: null cache, misaligned cache, and widths outside 5 / 7 / 13 (rejected
+    # before any device access: the pointers below are never dereferenced)
+    p = 4096
+    args = lambda W, WA, gram, a_dt: (100, 0, 100, W, p, 0, p, _lib.DTYPE_F32, 0, WA, p, p, a_dt, p, gram,
+                                      _lib.DTYPE_F32, p, 1, p, p, 1 << 20, None)
+    rc = lib.spai_residual_lines_gram(*args(13, 7, None, _lib.DTYPE_F32))
+    assert rc == _lib.SPAI_ERR_INVALID and b"null pointer" in lib.spai_last_error()
+    rc = lib.spai_residual_lines_gram(*args(13, 7, p + 4, _lib.DTYPE_F32))
+    assert rc == _lib.SPAI_ERR_INVALID and b"16-byte aligned" in lib.spai_last_error()
+    for W, WA, a_dt in ((9, 7, _lib.DTYPE_F32), (5, 7, _lib.DTYPE_F32), (13, 7, _lib.DTYPE_F64)):
+        rc = lib.spai_residual_lines_gram(*args(W, WA, p, a_dt))
+        assert rc == _lib.SPAI_ERR_UNSUPPORTED and b"spai_residual_lines" in lib.spai_last_error()
 
 
 def test_binding_signatures_match_header_parameter_lists():

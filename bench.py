@@ -49,6 +49,9 @@ CONFIGS = {
     "c2": (2, 256, torch.float32, "C2: 256^2 5-pt Poisson (65,536 x 65,536 CSR, fp32), pattern = A"),
     "c3": (3, 64, torch.float64, "C3: 64^3 7-pt 3-D Laplacian (262,144 x 262,144, fp64), 13-wide axial pattern "
                                  "(nnz/col <= 13)"),
+    "c2lu": ("lu", 256, torch.float32, "C2 L@U: the reference driver's own candidate (GFlowNet100.py:126-153,173): "
+                                       "spilu L@U of the 256^2 5-pt Poisson matrix (65,536 unknowns, 2,162,871 nnz, "
+                                       "lines up to 744 wide, fp32) as initial_matrix = original_matrix"),
     "c5s": ("thermal", 1108, torch.float64, "C5 stand-in: synthetic thermal2-like heat-conduction matrix "
                                             "(1,227,664 x 1,227,664, 8,584,786 nnz, 7 per row, lognormal "
                                             "conductivities, randomly permuted numbering, fp64), pattern = A"),
@@ -59,6 +62,12 @@ def config_matrices(cfg: str):
     """(A, candidate pattern) of a bench config."""
     from gflownet_spai_amd import axial_pattern_3d, poisson_2d, poisson_3d, thermal_like
     dims, grid, dtype, _ = CONFIGS[cfg]
+    if dims == "lu":  # GFlowNet100.py:126-153: the driver samples from spilu's L@U, original = initial
+        import scipy.sparse as sp
+        from gflownet_spai_amd.utils import lu_candidate_matrix
+        A = poisson_2d(grid, torch.float64).coalesce()
+        C = lu_candidate_matrix(sp.csr_matrix((A.values().numpy(), tuple(A.indices().numpy())), shape=A.shape))
+        return C, C
     if dims == "thermal":
         A = thermal_like(grid, 0, dtype)
         return A, A
@@ -273,6 +282,31 @@ def select_bytes(env, B: int, winners: float) -> float:
     return 4 * E1 + 2 * 8 * E1 + B * 4 * math.ceil((E1 - 1) / 32) + 12 * winners
 
 
+def rollout_bytes(env, B: int) -> float:
+    """SURVEY.md §8(d)'s algorithmic bytes of the throughput rollout: the logits once per batch,
+    4 (E + 1), and the B removal bitmaps, B ceil(E / 8).  One k_tile launch covers all of it (every
+    action of every sample), so these are also k_tile's algorithmic bytes per launch."""
+    E1 = env.num_actions
+    return 4 * E1 + B * math.ceil((E1 - 1) / 8)
+
+
+def pmc_record(cfg: str, B: int, kernel: str):
+    """The committed PMC summary of ``kernel`` for this workload (profiles/fill_traffic.json key
+    ``<cfg>_<kernel>``): (HBM bytes per launch, VALU wave-instructions per launch, source) or None."""
+    path = os.path.join(ROOT, "profiles", "fill_traffic.json")
+    try:
+        rec = json.load(open(path)).get(f"{cfg}_{kernel}", {})
+    except (OSError, ValueError):
+        return None
+    if rec.get("batch") != B:
+        return None
+    return float(rec["hbm_bytes_per_launch"]), rec.get("valu_insts_per_launch"), rec.get("source")
+
+
+VALU_CLOCK_GHZ = 2.4  # MI355X_MICROARCH.md: peak engine clock
+N_SIMDS = 256 * 4
+
+
 def roofline_obj(kernel, nbytes, ms, traffic=None):
     """traffic: (HBM bytes per launch, source) from a committed PMC pass of the same workload
     (measured_traffic: NOT measured in this run; `traffic_source` names the file), or None."""
@@ -313,7 +347,10 @@ def main():
     ap.add_argument("--strong", action="store_true",
                     help="columns split: --batch is the GLOBAL batch (batch/P rollouts per GPU) instead of per GPU")
     ap.add_argument("--assemble", default="best", choices=["best", "all", "none"])
-    ap.add_argument("--fill", default="auto", choices=["auto", "lsq", "qr"],
+    ap.add_argument("--side", default="auto", choices=["auto", "AM", "MA"],
+                    help="reward side: ||AM - I|| (the north star's column SPAI) or ||MA - I|| (the reference's "
+                         "calculate_residual); auto: MA for c2lu (the driver's configuration), else AM")
+    ap.add_argument("--fill", default="auto", choices=["auto", "lsq", "qr", "copy"],
                     help="least-squares fill: Householder QR from the env's R cache (qr, the north star's algorithm) "
                          "or the normal equations from the Gram cache (lsq); auto: qr where the cached QR solve is "
                          "compiled (pattern lines <= 7 wide: c2, c4, c5s), lsq for c3's 13-wide lines")
@@ -374,10 +411,12 @@ def main():
 
     dims, grid, dtype, text = CONFIGS[args.config]
     if args.fill == "auto":
-        args.fill = "lsq" if args.config == "c3" else "qr"
+        args.fill = {"c3": "lsq", "c2lu": "copy"}.get(args.config, "qr")
+    if args.side == "auto":
+        args.side = "MA" if args.config == "c2lu" else "AM"
     A, P = config_matrices(args.config)
     n = A.shape[0]
-    env = PreconditionerEnv(n, P, A, side="AM", fill=args.fill, keep_m=True, device=dev)
+    env = PreconditionerEnv(n, P, A, side=args.side, fill=args.fill, keep_m=True, device=dev)
     E = env.num_actions - 1
     shard = args.shard if dist_on else "columns"  # one GPU: every split is the same one-GPU step
     if shard in ("samples", "slices") or (shard == "columns" and args.strong):
@@ -442,6 +481,22 @@ def main():
         dt_eager = (time.perf_counter() - t0) / k_eager
         phase_ms = {k: float(np.mean(kernels.timer_ms(k))) for k in kernels.TIMERS}
         kernels.TIMERS = None
+        if dist_on:  # every rank's phase times, max over ranks (the collectives wait on the slowest rank)
+            names = sorted(phase_ms)
+            t = torch.tensor([phase_ms[k] for k in names], device=dev, dtype=torch.float64)
+            torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+            phase_ms_max = dict(zip(names, t.tolist()))
+        kernel_ms = {}
+        if kernels.kernel_timers_available():
+            # single kernels inside the multi-kernel entry points (k_tile, k_sort2, the fill): HIP events
+            # around each launch on its stream, in a second eager pass (their records would add to the
+            # phase times above)
+            kernels.kernel_timer_arm(True)
+            for _ in range(k_eager):
+                log = eager_step()
+            barrier()
+            kernels.kernel_timer_arm(False)
+            kernel_ms = {k: ms for k, (cnt, ms) in kernels.kernel_timer_read().items() if cnt > 0}
 
         use_graph = not args.no_graph
         if use_graph:
@@ -547,7 +602,9 @@ def main():
     counts = log.counts.cpu().numpy()
 
     if rank == 0:
-        fill_ms = phase_ms.get("fill_residual", float("nan"))
+        # the fill kernel's own launch time (kernel timers), else its phase
+        fill_ms = kernel_ms.get("k_qr_solve" if args.fill == "qr" else "k_gram_fill",
+                                phase_ms.get("fill_residual", float("nan")))
         fb = fill_bytes(env, B if shard == "columns" else bl)
         if split:  # the rank's fill covers its own lines only (rank 0: the first shard)
             fb *= (model.lines[1] - model.lines[0]) / n
@@ -565,7 +622,9 @@ def main():
         metric = {"c4": "SPAI columns/sec + final ||AM-I||_F, 2D Poisson 1024^2, at 1/2/4/8 GPU",
                   "c2": "SPAI columns/sec + final ||AM-I||_F, 2D Poisson 256^2 (C2)",
                   "c3": "SPAI columns/sec + final ||AM-I||_F, 3D Laplacian 64^3 fp64 (C3)",
-                  "c5s": "SPAI columns/sec + final ||AM-I||_F, thermal2-like stand-in fp64 (C5 stand-in)"}[args.config]
+                  "c5s": "SPAI columns/sec + final ||AM-I||_F, thermal2-like stand-in fp64 (C5 stand-in)",
+                  "c2lu": "SPAI columns/sec + final ||MA-I||_F, the driver's L@U candidate of 256^2 Poisson (copy fill)"
+                  }[args.config]
         out = {
             "metric": metric,
             "value": B * n / dt,
@@ -580,8 +639,10 @@ def main():
             "dtype": "f32 storage, f64 solve/accumulate" if dtype == torch.float32 else "f64",
             "data": "synthetic (random-init seeded ForwardPolicy GATv2x2+fc, hid=4, evaluated on the state graph in "
                     "every step; terminal fc bias set for 20% expected removal; matrix from its stencil)",
-            "config": {"workload": workload + ": ForwardPolicy logits + throughput rollout + LSQ fill" +
-                                   (" (Householder QR)" if args.fill == "qr" else "") + " + ||AM-I||_F",
+            "config": {"workload": workload + ": ForwardPolicy logits + throughput rollout + " +
+                                   ("copy fill (the reference's)" if args.fill == "copy" else "LSQ fill") +
+                                   (" (Householder QR)" if args.fill == "qr" else "") + f" + ||{args.side[0]}"
+                                   f"{args.side[1]}-I||_F",
                        "N": n, "E": E, "global_batch": B, "rollouts_per_gpu": bl,
                        "parallelism": f"{shard} sharded x{world}"},
             "value_without_assembly": B * n / dt_noasm,
@@ -624,14 +685,55 @@ def main():
         rf["bytes_cache_counted"], rf["frac_cache_counted"] = rf["bytes_per_launch"], rf["frac"]
         rf["bytes_per_launch"], rf["achieved"] = sb, sb / (fill_ms * 1e-3) / 1e9
         rf["frac"] = rf["achieved"] / HBM_PEAK_GBS
+        # the fill (the reward kernel the north star's >= 40 % names) is reported as roofline_fill;
+        # the headline roofline is the step's DOMINANT kernel, k_tile (the rollout's select)
+        out["roofline_fill"] = out.pop("roofline")
+        out["kernel_ms"] = kernel_ms
+        tile_ms = kernel_ms.get("k_tile")
+        if tile_ms:
+            rb = rollout_bytes(env, bl)
+            pm = pmc_record(args.config, bl, "tile")
+            rt = roofline_obj("k_tile (throughput rollout select: Philox4x32-10 + fp32 arrival time per (action, "
+                              "sample), removal bitmaps, bucket grouping of the winners; bytes = SURVEY 8(d) rollout: "
+                              "4 (E+1) logits + B ceil(E/8) bitmaps)", rb, tile_ms,
+                              (pm[0], pm[2]) if pm else None)
+            if pm:
+                rt["traffic_over_bytes"] = pm[0] / rb
+                if pm[1]:  # issue-time bound: a wave64 VALU instruction holds a SIMD for 4 cycles
+                    issue_ms = pm[1] * 4 / N_SIMDS / (VALU_CLOCK_GHZ * 1e9) * 1e3
+                    rt["valu"] = {"wave_insts_per_launch": pm[1],
+                                  "lane_insts_per_action_sample": pm[1] * 64 / ((env.num_actions - 1) * bl),
+                                  "issue_ms_at_peak_clock": issue_ms, "issue_frac_of_launch": issue_ms / tile_ms,
+                                  "source": pm[2]}
+            out["roofline"] = rt
+        else:  # (a library without the kernel timers: the fill stays the headline)
+            out["roofline"] = out["roofline_fill"]
         if not dist_on:
             sel = roofline_obj("rollout_select phase: k_presample + k_splitters + k_tile + k_bsum (k_tile ~80 % of "
-                               "it; latency-bound, not bandwidth-bound: see the PMC profile in DESIGN.md §5)",
+                               "it; VALU/latency-bound, not bandwidth-bound: DESIGN.md §3); bytes = the implementation's "
+                               "own streams (logits, rates/weights, bitmaps, 12-byte staged winners)",
                                select_bytes(env, bl, float(counts.sum())),
                                phase_ms.get("rollout_select", float("nan")))
+            sel["bytes_survey_8d"] = rollout_bytes(env, bl)
+            sel["frac_survey_8d"] = sel["bytes_survey_8d"] / (sel["avg_launch_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS
             out["roofline_select"] = sel
-            with torch.no_grad():
-                out["roofline_residual"] = generic_residual_leg(env, log, args.config)
+            if env.pattern.width <= 13 and env.a_lines.width <= 7:  # (the generic residual's widths)
+                with torch.no_grad():
+                    out["roofline_residual"] = generic_residual_leg(env, log, args.config)
+        if dist_on:  # the multi-GPU step explains itself: collective phases, max over ranks (HIP events on the
+            # compute stream: the time it waits for each collective), the group and the library
+            out["phases_ms_max_over_ranks"] = phase_ms_max
+            col = {"bitmap_all_to_all_issue": "_c_send", "bitmap_all_to_all_wait": "_c_recv",
+                   "limb_all_reduce": "_c_reduce", "slices_all_reduce": "rollout_exchange"}
+            out["collectives_ms"] = {name: v for name, key in col.items()
+                                     for k, v in phase_ms_max.items() if k.endswith(key)}
+            if "line_gather_wait" in phase_ms_max:
+                out["collectives_ms"]["line_gather_wait"] = phase_ms_max["line_gather_wait"]
+            out["world_size"] = torch.distributed.get_world_size()
+            out["backend"] = torch.distributed.get_backend()
+            if args.backend == "nccl":
+                v = torch.cuda.nccl.version()
+                out["rccl_version"] = ".".join(str(x) for x in v) if isinstance(v, tuple) else str(v)
         if not args.no_cpu_baseline and not dist_on:
             with torch.no_grad():
                 lg_host = model.forward_policy.logits(model.state_to_data(s0[:1])[0])[0].reshape(-1).cpu().numpy()

@@ -21,7 +21,7 @@ if os.environ.get("SPAI_LIB_VARIANT"):  # A/B timing of kernel variants built un
 SPAI_OK, SPAI_ERR_INVALID, SPAI_ERR_HIP, SPAI_ERR_UNSUPPORTED = 0, 1, 2, 3
 FILL_COPY, FILL_LSQ = 0, 1  # (the Householder-QR fill has its own entry point)
 DTYPE_F32, DTYPE_F64 = 0, 1
-ABI_VERSION = 17
+ABI_VERSION = 18
 RES2_LIMBS = 8  # SPAI_RES2_LIMBS
 
 _c_i32, _c_i64, _c_u64, _c_sz, _c_p = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_size_t, ctypes.c_void_p
@@ -30,6 +30,8 @@ _c_i32, _c_i64, _c_u64, _c_sz, _c_p = ctypes.c_int32, ctypes.c_int64, ctypes.c_u
 SIGNATURES = {
     "spai_abi_version": (ctypes.c_int, []),
     "spai_last_error": (ctypes.c_char_p, []),
+    "spai_kernel_timer_arm": (ctypes.c_int, [_c_i32, _c_i32]),
+    "spai_kernel_timer_read": (ctypes.c_int, [_c_i32, _c_p, _c_p]),
     "spai_logits_stats_workspace_bytes": (_c_sz, [_c_i32, _c_i32]),
     "spai_logits_stats": (ctypes.c_int, [_c_p, _c_i64, _c_i32, _c_i32, _c_p, _c_p, _c_p, _c_sz, _c_p]),
     "spai_parity_step_workspace_bytes": (_c_sz, [_c_i32, _c_i32]),

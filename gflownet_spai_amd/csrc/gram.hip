@@ -18,6 +18,7 @@
 // the stored (rounded) values up to d^T G d, d = rounding of m (<= 1e-14 relative for fp32 M).
 #include "spai_device.h"
 #include "spai_status.h"
+#include "spai_timer.h"
 
 namespace spai {
 namespace {
@@ -494,6 +495,7 @@ template <int W, typename TM, bool LSQ, typename GT, bool kDict>
 void launch_fill_t(int32_t n, int32_t lb, int32_t le, int32_t wrt, const int32_t* pa, const float* pv, const void* g,
                    const int32_t* ent, int32_t B, const uint32_t* rm, int32_t words, int32_t wb, void* mo,
                    double* partials, int32_t nparts, hipStream_t s) {
+  KernelTimer kt(SPAI_TIMER_GRAM, s);
   if constexpr (W > 7)
     k_gram_fill_wide<W, TM, LSQ, GT, kDict><<<nparts, kNT, 0, s>>>(n, lb, le, wrt, pa, pv, static_cast<const GT*>(g),
                                                                     ent, B, rm, words, wb, static_cast<TM*>(mo),

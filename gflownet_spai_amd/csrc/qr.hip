@@ -26,10 +26,12 @@
 //      is the tail + (Q^T e) below the pivots (sums of squares: no cancellation).
 #include <algorithm>
 #include <cstring>
+#include <type_traits>
 #include <vector>
 
 #include "spai_device.h"
 #include "spai_status.h"
+#include "spai_timer.h"
 
 namespace spai {
 namespace {
@@ -522,11 +524,101 @@ __global__ __launch_bounds__(kQNT) __attribute__((amdgpu_waves_per_eu(W <= 5 ? Q
 #pragma unroll
     for (int p = 0; p < W; ++p) act[p] = (valid && p < wrt) ? av[p] : -1;
   }
-  double R0[kHold ? T : 1];
-  float thf[W];  // the rank floors 1e-24 ||D[:, p]||^2 in fp32 (registers: 4 waves per SIMD at W = 5)
   // a dictionary entry is shared by most lanes of a wave (stencil lines): broadcast loads from L2
   constexpr int kStride = kDict ? 1 : 64;
-  const double* rp = kDict ? rcache + (int64_t)line_entry[jj] * NQ : rcache + (int64_t)(jj >> 6) * NQ * 64 + (jj & 63);
+  const int ent = kDict ? line_entry[jj] : 0;
+  // Block-shared (entry, mask) table (dictionary form, 2^W * 8 <= 256 lanes): a (line, sample)'s
+  // masked solve depends on the sample only through the W keep bits of its slots, and on the line
+  // only through its dictionary entry.  When the block's 256 lines use at most 8 distinct entries (a
+  // stencil's lines: 1-5 per block), the block solves every (entry, mask) pair ONCE — lane t solves
+  // mask t % 2^W of entry t / 2^W with the same qr_masked_solve on the same values — into an LDS
+  // table, and every (line, sample) takes its M values and residual from it: bit-identical to solving
+  // it on its own lane, one solve per lane instead of one per lane and sample.  Other blocks (more
+  // entries, the full cache) solve per line.
+#ifdef QRS_NO_TABLE  // (A/B variant: every block solves per line)
+  constexpr bool kTab = false;
+#else
+  constexpr bool kTab = kDict && kHold && (1 << W) * 8 <= kQNT;
+#endif
+  constexpr int kMasks = 1 << W, kTabE = kQNT / kMasks;
+  __shared__ int s_te[kTab ? 4 * (kTabE + 1) + kTabE + 1 : 1];  // per wave: distinct entries (+ count), then the block's
+  int myslot = 0;
+  bool table = false;
+  if constexpr (kTab) {
+    int* s_wte = s_te;                       // [4][kTabE + 1]: a wave's distinct entries, its count last
+    int* s_bte = s_te + 4 * (kTabE + 1);     // [kTabE] the block's distinct entries, then their count
+    {  // the wave's distinct entries (in lane order of first appearance; kTabE + 1 = overflow)
+      uint64_t rem = __ballot(valid);
+      int cnt = 0;
+      while (rem != 0ull && cnt <= kTabE) {
+        const int l0 = __builtin_ctzll(rem);
+        const int e = __builtin_amdgcn_readlane(ent, l0);
+        rem &= ~__ballot(ent == e);
+        if (lane == 0 && cnt < kTabE) s_wte[wave * (kTabE + 1) + cnt] = e;
+        ++cnt;
+      }
+      if (lane == 0) s_wte[wave * (kTabE + 1) + kTabE] = cnt;
+    }
+    __syncthreads();
+    if (wave == 0) {  // merge: lane i < 4 kTabE holds wave i / kTabE's candidate i % kTabE
+      const int w = lane / kTabE, i = lane % kTabE;
+      const int wc = lane < 4 * kTabE ? s_wte[w * (kTabE + 1) + kTabE] : 0;
+      const bool cand = lane < 4 * kTabE && i < wc;
+      const int e = cand ? s_wte[w * (kTabE + 1) + i] : -1;
+      bool first = cand;
+      for (int k = 0; k < lane && k < 4 * kTabE; ++k) {  // an earlier candidate with the same entry
+        const int wk = k / kTabE, ik = k % kTabE;
+        if (ik < s_wte[wk * (kTabE + 1) + kTabE] && s_wte[wk * (kTabE + 1) + ik] == e) first = false;
+      }
+      const uint64_t fm = __ballot(first);
+      const int pos = __builtin_popcountll(fm & ((1ull << lane) - 1ull));
+      const int tot = __builtin_popcountll(fm);
+      const bool over = __ballot(lane < 4 && s_wte[lane * (kTabE + 1) + kTabE] > kTabE) != 0ull;
+      if (first && pos < kTabE) s_bte[pos] = e;
+      if (lane == 0) s_bte[kTabE] = over ? kTabE + 1 : tot;
+    }
+    __syncthreads();
+    const int K = s_bte[kTabE];
+    table = K <= kTabE;  // block-uniform
+    if (table) {
+#pragma unroll
+      for (int k = 0; k < kTabE; ++k)
+        if (k < K && s_bte[k] == ent) myslot = k;
+    }
+  }
+  double R0[kHold ? T : 1];
+  float thf[W];  // the rank floors 1e-24 ||D[:, p]||^2 in fp32 (registers: 4 waves per SIMD at W = 5)
+  const double* rp = kDict ? rcache + (int64_t)ent * NQ : rcache + (int64_t)(jj >> 6) * NQ * 64 + (jj & 63);
+  if (kTab && table) {
+    // lane t: mask t % kMasks of the block's entry t / kMasks, from the dictionary entry itself
+    const int k = t / kMasks, mk = t % kMasks;
+    const int K = s_te[4 * (kTabE + 1) + kTabE];
+    if (k < K) {
+      const double* re = rcache + (int64_t)s_te[4 * (kTabE + 1) + k] * NQ;
+      double Rm[W][W], c[W], m[W], thr[W];
+      bool keep[W];
+#pragma unroll
+      for (int i = 0; i < W; ++i) {
+#pragma unroll
+        for (int q = i; q < W; ++q) Rm[i][q] = re[i * W - i * (i - 1) / 2 + (q - i)];
+        c[i] = re[T + i];
+      }
+      const double tail = re[T + W];
+#pragma unroll
+      for (int p = 0; p < W; ++p) {  // the same floors, from the same R values, as the per-line path
+        double sq = 0.0;
+#pragma unroll
+        for (int i = 0; i <= p; ++i) sq = fma(Rm[i][p], Rm[i][p], sq);
+        thr[p] = (double)(float)(1e-24 * sq);
+        keep[p] = (mk >> p) & 1;
+      }
+      const double rs = qr_masked_solve<W>(Rm, c, tail, thr, keep, m);
+#pragma unroll
+      for (int p = 0; p < W; ++p) s_c0[kHold ? p : 0][t] = m[p];
+      s_c0[kHold ? W : 0][t] = rs;
+    }
+    __syncthreads();  // the table is complete
+  } else {
   auto rval = [&](int q) { return kHold ? R0[q] : rp[q * kStride]; };
   if constexpr (kHold) {
 #pragma unroll
@@ -544,11 +636,16 @@ __global__ __launch_bounds__(kQNT) __attribute__((amdgpu_waves_per_eu(W <= 5 ? Q
     }
     thf[p] = (float)(1e-24 * s);  // (0 only below 1e-21: the floor then drops exact zeros only)
   }
+  }
   // bitmap word offset of a slot (recomputed where used: no registers held across the samples)
   auto wofs = [&](int p) { return act[p] >= 0 ? (act[p] >> 5) - word_base : 0; };
   uint32_t wd[W];  // the slots' bitmap words of the next sample are loaded while the current one is solved
 #pragma unroll
   for (int p = 0; p < W; ++p) wd[p] = removed[wofs(p)];
+  // the sample loop, instantiated twice: from the wave's table (R0 and the floors dead inside) or
+  // solving per line; the branch between them is wave-uniform
+  auto sample_loop = [&](auto tab_tag) {
+  constexpr bool kTabLoop = decltype(tab_tag)::value;
 #pragma unroll 1
   for (int b = 0; b < B; ++b) {
     bool keep[W];
@@ -559,6 +656,16 @@ __global__ __launch_bounds__(kQNT) __attribute__((amdgpu_waves_per_eu(W <= 5 ? Q
 #pragma unroll
       for (int p = 0; p < W; ++p) wd[p] = rn[wofs(p)];
     }
+    double m[W], rs;
+    if constexpr (kTabLoop) {  // the block's table
+      int mt = 0;
+#pragma unroll
+      for (int p = 0; p < W; ++p) mt |= (int)keep[p] << p;
+      const int slot = myslot * kMasks + mt;
+#pragma unroll
+      for (int p = 0; p < W; ++p) m[p] = s_c0[kHold ? p : 0][slot];
+      rs = s_c0[kHold ? W : 0][slot];
+    } else {
     double thr[W];
 #pragma unroll
     for (int p = 0; p < W; ++p) {
@@ -566,7 +673,7 @@ __global__ __launch_bounds__(kQNT) __attribute__((amdgpu_waves_per_eu(W <= 5 ? Q
       asm volatile("" : "+v"(f));  // widened per sample, not held as fp64 across the loop
       thr[p] = (double)f;
     }
-    double Rm[W][W], c[W], m[W], tail;
+    double Rm[W][W], c[W], tail;
     if constexpr (kHold) {
 #pragma unroll
       for (int i = 0; i < W; ++i) {
@@ -586,7 +693,8 @@ __global__ __launch_bounds__(kQNT) __attribute__((amdgpu_waves_per_eu(W <= 5 ? Q
       }
       tail = rps[(T + W) * kStride];
     }
-    const double rs = qr_masked_solve<W>(Rm, c, tail, thr, keep, m);
+    rs = qr_masked_solve<W>(Rm, c, tail, thr, keep, m);
+    }
     s_r2[b % kQChunk][t] = valid ? rs : 0.0;
 #ifdef QRS_DIRECT  // A/B: M stored from the registers (no LDS staging, no barrier per sample)
     if (m_out != nullptr && valid) {
@@ -639,6 +747,9 @@ __global__ __launch_bounds__(kQNT) __attribute__((amdgpu_waves_per_eu(W <= 5 ? Q
       __syncthreads();
     }
   }
+  };
+  if (kTab && table) sample_loop(std::true_type{});
+  else sample_loop(std::false_type{});
 }
 
 // (W class, A width class, rows) -> instance
@@ -709,6 +820,7 @@ template <int W, typename TM>
 void launch_solve_t(const int32_t* ent, int32_t lb, int32_t le, int32_t wrt, const int32_t* pa, const double* rc,
                     int32_t B, const uint32_t* rm, int32_t words, int32_t wb, void* mo, double* partials,
                     int32_t nparts, hipStream_t s) {
+  KernelTimer kt(SPAI_TIMER_QR, s);
   if (ent)
     k_qr_solve<W, TM, true><<<nparts, kQNT, 0, s>>>(lb, le, wrt, pa, rc, ent, B, rm, words, wb, static_cast<TM*>(mo),
                                                     partials);

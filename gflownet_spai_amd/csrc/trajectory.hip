@@ -40,6 +40,7 @@
 // in a fixed order: results are bit-reproducible run to run.
 #include "spai_device.h"
 #include "spai_status.h"
+#include "spai_timer.h"
 
 namespace spai {
 namespace {
@@ -66,11 +67,12 @@ constexpr int kMaxNsb = kSampM / kSampNT;  // presample blocks per sample (256)
 #define KTARGET 4096
 #endif
 constexpr int kTarget = KTARGET;            // winners per bucket (target)
-constexpr int kMaxB = 1024;                // buckets per sample (11 bits in the LDS record)
+constexpr int kMaxB = 2048;                // buckets per sample (11 bits in the LDS record)
 constexpr int kCap2 = 8192;               // LDS capacity of k_sort2 (records per bucket)
 constexpr int kMaxSub = 4096;              // value sub-buckets per bucket in k_sort2
 constexpr int kBigWords = 256;             // k_sort2: buckets per block tracked for the oversized pass (x32)
 constexpr int kSortNT = 1024;
+constexpr int kRwChunk = 4 * kSortNT;      // actions per rate/weight block of k_splitters
 constexpr int kMaxTiles = 2048;            // E <= kMaxTiles * kTile actions
 constexpr int kFinNT = 256;
 constexpr int kMaxSamples = 1024;          // B per rollout call
@@ -99,6 +101,7 @@ struct TrajWs {
   int64_t wstride;        // row stride of rr / ww: E + 1 rounded up to 4 (16-byte aligned rows)
   float* rr;              // [B][wstride] inverse rates r_a = e^(l_E - l_a) (row 0 only: shared logits)
   float* ww;              // [B][wstride] weights w_a = e^(l_a - lmax)
+  uint64_t* wfix;         // [B][nwb][2] fixed-point weight total of each kRwChunk-action chunk (row 0 only: shared)
   uint32_t* runs;         // [B][kMaxB][ntiles] run of bucket k in tile t: offset << 16 | count (k_tile)
   double* tbw;            // [B][kMaxB][ntiles] weight sum of that run
   double* tile_wrest;     // [B][ntiles]
@@ -135,6 +138,7 @@ static void traj_ws(void* base, int32_t E, int32_t B, TrajWs* w) {
   w->wstride = ((int64_t)E + 1 + 3) & ~(int64_t)3;
   w->rr = c.take<float>((size_t)B * w->wstride);
   w->ww = c.take<float>((size_t)B * w->wstride);
+  w->wfix = c.take<uint64_t>((size_t)B * 2 * ((w->wstride + kRwChunk - 1) / kRwChunk));
   w->runs = c.take<uint32_t>((size_t)B * kMaxB * w->ntiles);
   w->tbw = c.take<double>((size_t)B * kMaxB * w->ntiles);
   w->tile_wrest = c.take<double>((size_t)B * w->ntiles);
@@ -322,13 +326,29 @@ __device__ __forceinline__ void stream_words(const uint64_t* sctr, uint32_t& st0
   }
 }
 
+// w (fp32 in [0, 1]) as the fixed-point integer of k_tile's per-bucket sums: w * 2^47 for
+// w >= 2^-20, else w * 2^69, truncated — from the float's bits (mantissa shifted by its
+// exponent), identical to (uint64)(w * 2^s) in fp64 at a fraction of its instructions.
+__device__ __forceinline__ uint64_t weight_fixed(float w) {
+  const uint32_t bits = __float_as_uint(w);
+  const int ex = (int)(bits >> 23);  // w >= 0: no sign bit
+  if (ex == 0) return 0ull;          // zero or denormal (< 2^-126): below both units
+  const uint64_t man = (uint64_t)((bits & 0x7FFFFFu) | 0x800000u);  // w = man * 2^(ex - 150)
+  const int sh = ex - 150 + (ex >= 107 ? 47 : 69);                  // 2^-20 <=> ex >= 107
+  return sh >= 0 ? man << sh : man >> min(-sh, 63);
+}
+
 // Inverse rates r = e^(l_E - l) and weights w = e^(l - lmax) of one chunk (NT * 4 actions) of
-// one logits row, for k_tile; the row padding past E gets r = inf (never a winner), w = 0.
+// one logits row, for k_tile; the row padding past E gets r = inf (never a winner), w = 0.  Also
+// the chunk's total weight over its actions < E as exact fixed point (weight_fixed: hi units for
+// w >= 2^-20, lo units below), wfix[row][chunk][2]: k_tile forms a tile's untouched mass as that
+// total minus its winners' (integers, so the result is independent of any summation order).
 // Run by the extra blocks of k_splitters, so this HBM stream overlaps the B splitter blocks.
 template <int NT>
 __device__ __forceinline__ void rates_weights_chunk(int q, const float* __restrict__ logits, int64_t bstride,
                                                     int32_t E, const float* __restrict__ lmax,
-                                                    float* __restrict__ rr, float* __restrict__ ww, int64_t wstride) {
+                                                    float* __restrict__ rr, float* __restrict__ ww, int64_t wstride,
+                                                    uint64_t* __restrict__ wfix) {
   constexpr int kPer = 4, kChunkA = NT * kPer;
   const int tid = threadIdx.x;
   const int nwb = (int)((wstride + kChunkA - 1) / kChunkA);
@@ -344,20 +364,40 @@ __device__ __forceinline__ void rates_weights_chunk(int q, const float* __restri
     const int64_t i = beg + j * NT;
     l[j] = i <= E ? lg[i] : 0.0f;
   }
+  uint64_t fh = 0, fl = 0;
 #pragma unroll
   for (int j = 0; j < kPer; ++j) {
     const int64_t i = beg + j * NT;
     if (i <= E) {
       r[i] = det_expf(lE - l[j]);
-      w[i] = action_weight(l[j], lm);
+      const float wv = action_weight(l[j], lm);
+      w[i] = wv;
+      if (i < E) {
+        const uint64_t f = weight_fixed(wv);
+        if (wv >= 9.5367431640625e-07f) fh += f;
+        else fl += f;
+      }
     } else if (i < wstride) {
       r[i] = __uint_as_float(0x7f800000u);
       w[i] = 0.0f;
     }
   }
+  __shared__ uint64_t s_fx[NT / 64][2];
+  fh = (uint64_t)wave_sum_i64((int64_t)fh);
+  fl = (uint64_t)wave_sum_i64((int64_t)fl);
+  if ((tid & 63) == 0) {
+    s_fx[tid >> 6][0] = fh;
+    s_fx[tid >> 6][1] = fl;
+  }
+  __syncthreads();
+  if (tid < 2) {
+    uint64_t t = 0;
+#pragma unroll
+    for (int v = 0; v < NT / 64; ++v) t += s_fx[v][tid];
+    wfix[(int64_t)q * 2 + tid] = t;
+  }
 }
 
-constexpr int kRwChunk = 4 * kSortNT;  // actions per rate/weight block of k_splitters
 __global__ __launch_bounds__(kSampNT) void k_presample(const float* __restrict__ logits, int64_t bstride, int32_t E,
                                                        int32_t M, int32_t nsb, uint32_t seed0, uint32_t seed1,
                                                        uint32_t st0, uint32_t st1, const uint64_t* __restrict__ sctr,
@@ -460,9 +500,10 @@ __global__ __launch_bounds__(kSortNT) void k_splitters(int32_t E, int32_t M, int
                                                        uint16_t* __restrict__ lut, uint32_t* __restrict__ lut_base,
                                                        int32_t B, const float* __restrict__ logits, int64_t bstride,
                                                        const float* __restrict__ lmax, float* __restrict__ rr,
-                                                       float* __restrict__ ww, int64_t wstride) {
+                                                       float* __restrict__ ww, int64_t wstride,
+                                                       uint64_t* __restrict__ wfix) {
   if ((int)blockIdx.x >= B) {  // blocks [B, ...): rates and weights of the logits rows
-    rates_weights_chunk<kSortNT>(blockIdx.x - B, logits, bstride, E, lmax, rr, ww, wstride);
+    rates_weights_chunk<kSortNT>(blockIdx.x - B, logits, bstride, E, lmax, rr, ww, wstride, wfix);
     return;
   }
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -593,18 +634,6 @@ __global__ __launch_bounds__(kSortNT) void k_splitters(int32_t E, int32_t M, int
 }
 
 
-// w (fp32 in [0, 1]) as the fixed-point integer of k_tile's per-bucket sums: w * 2^47 for
-// w >= 2^-20, else w * 2^69, truncated — from the float's bits (mantissa shifted by its
-// exponent), identical to (uint64)(w * 2^s) in fp64 at a fraction of its instructions.
-__device__ __forceinline__ uint64_t weight_fixed(float w) {
-  const uint32_t bits = __float_as_uint(w);
-  const int ex = (int)(bits >> 23);  // w >= 0: no sign bit
-  if (ex == 0) return 0ull;          // zero or denormal (< 2^-126): below both units
-  const uint64_t man = (uint64_t)((bits & 0x7FFFFFu) | 0x800000u);  // w = man * 2^(ex - 150)
-  const int sh = ex - 150 + (ex >= 107 ? 47 : 69);                  // 2^-20 <=> ex >= 107
-  return sh >= 0 ? man << sh : man >> min(-sh, 63);
-}
-
 // ------------------------------------------------------------------ k_tile
 // Selection and grouping fused, one 8192-action tile of one sample per block: arrival times
 // of the tile (16 actions per thread; times and weights kept in registers), the removed
@@ -629,11 +658,11 @@ void k_tile(const float* __restrict__ rr, const float* __restrict__ ww, int64_t 
             const uint32_t* __restrict__ spl_, const uint16_t* __restrict__ lut_,
             const uint32_t* __restrict__ lut_base, uint32_t* __restrict__ staging,
             uint32_t* __restrict__ runs, double* __restrict__ tbw, double* __restrict__ tile_wrest,
-            const float* __restrict__ tE_in) {
+            const float* __restrict__ tE_in, const uint64_t* __restrict__ wfix, int32_t nwb) {
   // LDS regions (two blocks per CU: <= 80 KB per block):
-  //   s_r0: the fixed-point bucket sums during the histogram, then the slot path's record window
-  //   s_r1: the compacted winner list: keys, weights, tile-local ids (slot path: the window's
-  //         weights)
+  //   s_r0: the slot path's record window
+  //   s_r1: the compacted winner list: keys, weights, tile-local ids; once the list is read into
+  //         registers, the fixed-point bucket sums (slot path: those sums, then the window's weights)
   __shared__ __attribute__((aligned(16))) uint64_t s_r0[kWin];
   __shared__ __attribute__((aligned(16))) uint32_t s_r1[2 * kList + kList / 2];
   static_assert(kWin <= 2 * kList + kList / 2 && kList % 2 == 0, "LDS region sizes");
@@ -646,7 +675,8 @@ void k_tile(const float* __restrict__ rr, const float* __restrict__ ww, int64_t 
   __shared__ int s_off[kMaxB + 1];  // histogram, then tile-local bucket offsets
   __shared__ __attribute__((aligned(16))) uint16_t s_lut[kBins];
   __shared__ int s_wc[kGrpNT / 64];
-  __shared__ double s_wr[kGrpNT / 64];
+  __shared__ uint64_t s_fxo[2];              // fixed-point weight of the winners of OTHER parts' buckets
+  __shared__ uint64_t s_fxw[kGrpNT / 64][2];  // per wave: the tile's winner weight (hi, lo units)
 #ifdef KTILE_NOREMAP
   const int wg = (blockIdx.x % (gridDim.x / B)) * B + blockIdx.x / (gridDim.x / B);  // sample-major order
 #else
@@ -679,10 +709,23 @@ void k_tile(const float* __restrict__ rr, const float* __restrict__ ww, int64_t 
   // per-bucket weight sums of the tile's winners as exact fixed point (integer LDS atomics: the
   // result is independent of their order): w >= 2^-20 in units of 2^-47, smaller w in units of
   // 2^-69 (a tile adds <= 2^14 terms, so neither overflows 64 bits; every w >= 2^-45 is exact).
-  // The two [kMaxB] u64 arrays live in the record window, unused until the placement.
-  static_assert(kWin * 8 >= 2 * kMaxB * 8, "fixed-point accumulators alias the record window");
-  uint64_t* s_fx = s_r0;
-  for (int k = tid; k < 2 * kMaxB; k += kGrpNT) s_fx[k] = 0ull;
+  // The two [kMaxB] u64 arrays live in the list region once the list has been read (zeroed then).
+  static_assert((2 * kList + kList / 2) * 4 >= 2 * kMaxB * 8, "fixed-point accumulators alias the list");
+  uint64_t* s_fx = reinterpret_cast<uint64_t*>(s_r1);
+  if (tid < 2) s_fxo[tid] = 0ull;
+  // the tile's total weight (k_splitters' chunk sums, fixed point): the untouched mass is that
+  // minus the winners' weight, exact in integers (no fp64 sum per slot)
+  static_assert(kTile % kRwChunk == 0, "whole rate/weight chunks per tile");
+  uint64_t tot_h = 0, tot_l = 0;
+  {
+    const uint64_t* wf = wfix + ((int64_t)(rowsel ? b : 0) * nwb + (int64_t)tile * (kTile / kRwChunk)) * 2;
+#pragma unroll
+    for (int c = 0; c < kTile / kRwChunk; ++c)
+      if (tile * (kTile / kRwChunk) + c < nwb) {
+        tot_h += wf[2 * c];
+        tot_l += wf[2 * c + 1];
+      }
+  }
   const uint32_t lmn = lut_base[2 * b];
   const int lsh = (int)lut_base[2 * b + 1];
   const int a_t = tile * kTile;  // first action of the tile
@@ -699,18 +742,20 @@ void k_tile(const float* __restrict__ rr, const float* __restrict__ ww, int64_t 
       const float4 w4 = *reinterpret_cast<const float4*>(wrow + a0);
       rvk[4 * g] = r4.x, rvk[4 * g + 1] = r4.y, rvk[4 * g + 2] = r4.z, rvk[4 * g + 3] = r4.w;
       lvk[4 * g] = w4.x, lvk[4 * g + 1] = w4.y, lvk[4 * g + 2] = w4.z, lvk[4 * g + 3] = w4.w;
-    } else {
+    } else {  // past the row: never a winner (r = inf, as the row's own padding)
 #pragma unroll
-      for (int s = 0; s < 4; ++s) rvk[4 * g + s] = lvk[4 * g + s] = 0.0f;
+      for (int s = 0; s < 4; ++s) {
+        rvk[4 * g + s] = __uint_as_float(0x7f800000u);
+        lvk[4 * g + s] = 0.0f;
+      }
     }
   }
   // the terminal's arrival time, computed once per sample by k_presample (a scalar load issued
   // with the block's other scalar loads, instead of a Philox call per thread on the critical path)
   const float tE = tE_in[b];
   PROF(0)
-  uint32_t ord[4 * kTileG];
+  uint32_t ord[4 * kTileG];  // trajectory-order keys (read for the winners only)
   uint32_t win = 0;  // bit 4g + s: action a_t + g * 4 * kGrpNT + 4 * tid + s is a winner
-  double wr = 0.0;
 #pragma unroll
   for (int g = 0; g < kTileG; ++g) {
     const int a0 = a_t + g * 4 * kGrpNT + 4 * tid;
@@ -720,11 +765,10 @@ void k_tile(const float* __restrict__ rr, const float* __restrict__ ww, int64_t 
     const float ts[4] = {t01.x, t01.y, t23.x, t23.y};
     uint32_t nib = 0;
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {  // branch-free (selects, no exec-mask branches per slot)
-      const bool real = a0 + s < E, w = real && ts[s] < tE;
-      nib |= (uint32_t)w << s;
-      ord[4 * g + s] = w ? arrival_ord(ts[s]) : 0u;
-      wr += (real && !w) ? (double)lvk[4 * g + s] : 0.0;
+    for (int s = 0; s < 4; ++s) {  // branch-free; a slot past E has r = inf (never a winner) and the
+                                   // terminal's own slot t = t_E (not below it)
+      nib |= (uint32_t)(ts[s] < tE) << s;
+      ord[4 * g + s] = arrival_ord(ts[s]);
     }
     win |= nib << (4 * g);
     // removed bitmap: 8 adjacent threads make one 32-bit word (OR over the 8 lanes by DPP:
@@ -736,31 +780,11 @@ void k_tile(const float* __restrict__ rr, const float* __restrict__ ww, int64_t 
     const int wi = a0 >> 5;
     if ((tid & 7) == 0 && a0 < E && wi < words) removed[(int64_t)b * words + wi] = x;
   }
-  wr = wave_incl_scan_d(wr);  // lane 63 holds the wave's total (DPP, fixed order)
-  if (lane == 63) s_wr[wave] = wr;
   __syncthreads();  // splitter tables, zeroed histogram
   PROF(1)
-  if (tid == 0) {
-    double t = 0.0;
-#pragma unroll
-    for (int w = 0; w < kGrpNT / 64; ++w) t += s_wr[w];
-    tile_wrest[(int64_t)b * ntiles + tile] = t;
-  }
   const int nbl = nb - 1;
-  // this part's winners: bucket k = nbl - #(splitters <= key) in [k0, k1) <=> spl[nbl - k1] <= key
-  // (when nbl - k1 >= 0) and key < spl[nbl - k0] (when nbl - k0 <= nb - 2); the other winners
-  // are only in the bitmap and the counts their own part stages
-  {
-    const int jlo = nbl - k1, jhi = nbl - k0;
-    const uint32_t slo = jlo >= 0 ? s_spl[jlo] : 0u, shi = jhi <= nb - 2 ? s_spl[jhi] : 0u;
-    const bool clo = jlo >= 0, chi = jhi <= nb - 2;
-    uint32_t mine = 0;
-#pragma unroll
-    for (int q = 0; q < 4 * kTileG; ++q)
-      mine |= (((win >> q) & 1u) && (!clo || slo <= ord[q]) && (!chi || ord[q] < shi)) ? 1u << q : 0u;
-    win = mine;
-  }
-  // bucket histogram of the part's winners; each winner keeps its bucket and its rank inside
+  // bucket histogram of the part's winners (buckets [k0, k1); the winners of other parts only add
+  // their weight to s_fxo, for the untouched mass); each winner keeps its bucket and its rank inside
   // the bucket (the histogram atomic's return; any order: the level-2 sort orders buckets fully)
   static_assert(kMaxB <= (1 << 11) && kTile <= (1 << 21), "bucket | rank << 11 packing");
   // Compacted path (the usual case: the part's winners fit the list, i.e. <= ~49 % of the tile):
@@ -803,6 +827,8 @@ void k_tile(const float* __restrict__ rr, const float* __restrict__ ww, int64_t 
         ew[i] = v ? l_w[e] : 0.0f;
       }
     }
+    lds_barrier();  // the list is in registers: its region takes the bucket sums
+    for (int k = tid; k < 2 * kMaxB; k += kGrpNT) s_fx[k] = 0ull;
     int ebc[kPerT];
 #pragma unroll
     for (int i = 0; i < kPerT; ++i) {
@@ -827,17 +853,24 @@ void k_tile(const float* __restrict__ rr, const float* __restrict__ ww, int64_t 
       }
     } while (__any(more));
     PROF(7)
+    lds_barrier();  // the sums are zero
 #pragma unroll
     for (int i = 0; i < kPerT; ++i) {
-      ebr[i] = 0u;
+      ebr[i] = 0xFFFFFFFFu;  // (not stored: beyond the list or another part's bucket)
       if (tid + i * kGrpNT < totw) {
         const int bk = nbl - ebc[i];
-        ebr[i] = (uint32_t)bk | ((uint32_t)atomicAdd(&s_off[bk], 1) << 11);
-        atomicAdd((unsigned long long*)&s_fx[bk + (ew[i] >= 9.5367431640625e-07f ? 0 : kMaxB)],
-                  (unsigned long long)weight_fixed(ew[i]));
+        const bool hi = ew[i] >= 9.5367431640625e-07f;
+        const unsigned long long f = (unsigned long long)weight_fixed(ew[i]);
+        if (bk >= k0 && bk < k1) {
+          ebr[i] = (uint32_t)bk | ((uint32_t)atomicAdd(&s_off[bk], 1) << 11);
+          atomicAdd((unsigned long long*)&s_fx[bk + (hi ? 0 : kMaxB)], f);
+        } else {
+          atomicAdd((unsigned long long*)&s_fxo[hi ? 0 : 1], f);
+        }
       }
     }
   } else {
+  for (int k = tid; k < 2 * kMaxB; k += kGrpNT) s_fx[k] = 0ull;
   // slot path (dense tiles): bucket of a winner's orderable key (buckets numbered in
   // trajectory order, descending key): value-linear lookup table, then the splitters, for all
   // the thread's slots at once: the table guesses of every slot are read together, then
@@ -860,16 +893,25 @@ void k_tile(const float* __restrict__ rr, const float* __restrict__ ww, int64_t 
       more |= step;
     }
   } while (__any(more));
+  lds_barrier();  // the sums are zero
+  uint32_t mine = 0;  // the winners of this part's buckets
 #pragma unroll
   for (int q = 0; q < 4 * kTileG; ++q) {
     br[q] = 0u;
     if ((win >> q) & 1u) {
       const int bk = nbl - bc[q];
-      br[q] = (uint32_t)bk | ((uint32_t)atomicAdd(&s_off[bk], 1) << 11);
-      atomicAdd((unsigned long long*)&s_fx[bk + (lvk[q] >= 9.5367431640625e-07f ? 0 : kMaxB)],
-                (unsigned long long)weight_fixed(lvk[q]));
+      const bool hi = lvk[q] >= 9.5367431640625e-07f;
+      const unsigned long long f = (unsigned long long)weight_fixed(lvk[q]);
+      if (bk >= k0 && bk < k1) {
+        mine |= 1u << q;
+        br[q] = (uint32_t)bk | ((uint32_t)atomicAdd(&s_off[bk], 1) << 11);
+        atomicAdd((unsigned long long*)&s_fx[bk + (hi ? 0 : kMaxB)], f);
+      } else {
+        atomicAdd((unsigned long long*)&s_fxo[hi ? 0 : 1], f);
+      }
     }
   }
+  win = mine;
   }
   __syncthreads();
   PROF(2)
@@ -877,14 +919,31 @@ void k_tile(const float* __restrict__ rr, const float* __restrict__ ww, int64_t 
   // of other parts count 0)
   constexpr int kQ = kMaxB / kGrpNT;
   int hv[kQ], loc = 0;
+  uint64_t wh = tid == 0 ? s_fxo[0] : 0ull, wl = tid == 0 ? s_fxo[1] : 0ull;  // the tile's winner weight
 #pragma unroll
   for (int q = 0; q < kQ; ++q) {
     const int k = tid * kQ + q;
     hv[q] = k < nb ? s_off[k] : 0;
     loc += hv[q];
+    wh += s_fx[k];  // (0 past nb and outside [k0, k1))
+    wl += s_fx[kMaxB + k];
+  }
+  wh = (uint64_t)wave_sum_i64((int64_t)wh);
+  wl = (uint64_t)wave_sum_i64((int64_t)wl);
+  if (lane == 0) {
+    s_fxw[wave][0] = wh;
+    s_fxw[wave][1] = wl;
   }
   int tot;
-  int run = block_excl_scan<kGrpNT>(loc, s_wc, &tot);
+  int run = block_excl_scan<kGrpNT>(loc, s_wc, &tot);  // (its barriers publish s_fxw)
+  if (tid == 0) {  // the untouched mass of the tile: its total weight minus its winners', exact
+#pragma unroll
+    for (int w = 0; w < kGrpNT / 64; ++w) {
+      tot_h -= s_fxw[w][0];
+      tot_l -= s_fxw[w][1];
+    }
+    tile_wrest[(int64_t)b * ntiles + tile] = (double)tot_h * 7.105427357601002e-15 + (double)tot_l * 1.6940658945086007e-21;
+  }
   // bucket-major run table [b][bucket][tile] written directly (k_sort2 reads one bucket's runs
   // as a contiguous row): neighbouring tiles fill neighbouring words of a row, so the scattered
   // 4-byte stores merge in L2; this replaced a separate transpose kernel (k_runs, 26 us at C4)
@@ -909,7 +968,7 @@ void k_tile(const float* __restrict__ rr, const float* __restrict__ ww, int64_t 
     // tile's region stays in L2)
 #pragma unroll
     for (int i = 0; i < kPerT; ++i) {
-      if (tid + i * kGrpNT < totw) {
+      if (ebr[i] != 0xFFFFFFFFu) {
         const int p = s_off[ebr[i] & 0x7FFu] + (int)(ebr[i] >> 11);
         st[p] = make_uint3((uint32_t)a_t + eid[i], ~eo[i], __float_as_uint(ew[i]));
       }
@@ -1753,11 +1812,14 @@ static int rollout_select(const float* logits, int64_t bstride, int32_t E, int32
   k_splitters<<<B + nwb * (bstride ? B : 1), kSortNT, 0, s>>>(E, w.M, nsb, w.samp, w.samp_cnt, w.samp_mm, w.nb, w.spl,
                                                              w.lut,
                                                              w.lut_base, B, logits, bstride, lmax, w.rr, w.ww,
-                                                             w.wstride);
+                                                             w.wstride, w.wfix);
   SPAI_CHECK_LAUNCH();
-  k_tile<<<w.ntiles * B, kGrpNT, 0, s>>>(w.rr, w.ww, w.wstride, rowsel, E, B, w.ntiles, s0, s1, t0, t1, stream_ctr,
-                                         sample_base, part, nparts, removed, words, w.nb, w.spl, w.lut, w.lut_base,
-                                         w.staging, w.runs, w.tbw, w.tile_wrest, w.tE);
+  {
+    KernelTimer kt(SPAI_TIMER_TILE, s);
+    k_tile<<<w.ntiles * B, kGrpNT, 0, s>>>(w.rr, w.ww, w.wstride, rowsel, E, B, w.ntiles, s0, s1, t0, t1, stream_ctr,
+                                           sample_base, part, nparts, removed, words, w.nb, w.spl, w.lut, w.lut_base,
+                                           w.staging, w.runs, w.tbw, w.tile_wrest, w.tE, w.wfix, nwb);
+  }
   SPAI_CHECK_LAUNCH();
   k_bsum<<<dim3(max_buckets(E) + 1, B), kBsumNT, 0, s>>>(w.ntiles, w.nb, w.runs, w.tbw, w.xch, stream_ctr, part,
                                                          nparts);
@@ -1828,8 +1890,11 @@ extern "C" int spai_rollout_sort(const float* logits, int64_t bstride, int32_t E
   const int cus = g_sort_blocks > 0 ? std::min(g_sort_blocks, num_cus()) : num_cus();
   const int g2 = std::max(std::max(1, std::min(nbt, cus)), (nbt + 32 * kBigWords - 1) / (32 * kBigWords));
   const int64_t wrs = bstride ? w.wstride : 0;
-  k_sort2<<<g2, kSortNT, 0, s>>>(E, B, w.ntiles, w.nb, w.bstart, w.runs, w.staging, w.spl, t_cap, actions, fwd_probs,
-                                 w.wrest, w.bwsuf, w.bigcnt, w.ww, wrs, w.scratch, part, nparts);
+  {
+    KernelTimer kt(SPAI_TIMER_SORT, s);
+    k_sort2<<<g2, kSortNT, 0, s>>>(E, B, w.ntiles, w.nb, w.bstart, w.runs, w.staging, w.spl, t_cap, actions,
+                                   fwd_probs, w.wrest, w.bwsuf, w.bigcnt, w.ww, wrs, w.scratch, part, nparts);
+  }
   SPAI_CHECK_LAUNCH();
   return SPAI_OK;
 }

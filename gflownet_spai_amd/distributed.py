@@ -140,7 +140,9 @@ class LineGather:
         B, n_loc, W = m_local.shape
         self.rng = [shard_lines(self.n, r, world, self.align) for r in range(world)]
         chunk = max(e - b for b, e in self.rng)
-        self.wait()  # the previous gather has read buf and written out
+        from .kernels import _timed
+        with _timed("line_gather_wait"):  # (bench.py: the stream's wait for the previous gather)
+            self.wait()  # the previous gather has read buf and written out
         if self.buf is None or self.buf.shape != (B, chunk, W) or self.buf.dtype != m_local.dtype:
             self.buf = torch.zeros(B, chunk, W, dtype=m_local.dtype, device=m_local.device)  # padding rows stay 0
             self.out = torch.empty(world, B, chunk, W, dtype=m_local.dtype, device=m_local.device)

@@ -41,6 +41,31 @@ def timer_ms(name: str) -> list:
     return [s.elapsed_time(e) for s, e in (TIMERS or {}).get(name, [])]
 
 
+# single kernels inside the multi-kernel entry points (spai_kernel_timer_*): HIP events recorded
+# by the library on the launch stream around each launch while armed (not under graph capture)
+KERNEL_TIMERS = {"k_tile": 0, "k_sort2": 1, "k_qr_solve": 2, "k_gram_fill": 3}
+
+
+def kernel_timers_available() -> bool:
+    return hasattr(_l(), "spai_kernel_timer_arm")  # (absent from older variant libraries in A/B runs)
+
+
+def kernel_timer_arm(on: bool, names=tuple(KERNEL_TIMERS)) -> None:
+    for k in names:
+        _lib.check(_l().spai_kernel_timer_arm(KERNEL_TIMERS[k], int(bool(on))), "spai_kernel_timer_arm")
+
+
+def kernel_timer_read(names=tuple(KERNEL_TIMERS)) -> dict:
+    """{kernel: (launches recorded, mean ms)} (waits for the recorded events)."""
+    out = {}
+    for k in names:
+        cnt, ms = ctypes.c_int32(0), ctypes.c_double(0.0)
+        _lib.check(_l().spai_kernel_timer_read(KERNEL_TIMERS[k], ctypes.byref(cnt), ctypes.byref(ms)),
+                   "spai_kernel_timer_read")
+        out[k] = (int(cnt.value), float(ms.value))
+    return out
+
+
 def logits_stats(logits: torch.Tensor, B: int):
     """lmax [B] fp32 and z [B] fp64 of logits [E+1] (shared) or [B, E+1]."""
     _lib.require_device(logits)

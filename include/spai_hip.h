@@ -51,6 +51,22 @@ extern "C" {
 int spai_abi_version(void);
 const char* spai_last_error(void);
 
+/* ---------------------------------------------------------------- per-launch kernel timing
+ * HIP-event durations of single kernels inside the multi-kernel entry points, measured on the
+ * launch stream (bench.py's roofline objects need the kernel's own average duration, not its
+ * phase's).  spai_kernel_timer_arm(kernel, 1) clears the kernel's records and arms it: every
+ * later launch of that kernel records a start / stop event pair on its stream (at most 256 pairs;
+ * none while the stream is being captured into a graph); arm(kernel, 0) stops recording.
+ * spai_kernel_timer_read waits for the recorded events and returns their count and mean duration
+ * in ms.  Process-wide, not re-entrant.  kernel: */
+#define SPAI_TIMER_TILE 0  /* k_tile of spai_rollout_select(_pm): the step's dominant kernel */
+#define SPAI_TIMER_SORT 1  /* k_sort2 of spai_rollout_sort */
+#define SPAI_TIMER_QR 2    /* k_qr_solve of spai_fill_lines_qr_cached (the bench's fill) */
+#define SPAI_TIMER_GRAM 3  /* k_gram_fill / k_gram_fill_wide of spai_fill_lines_gram(_dict) */
+#define SPAI_TIMER_COUNT 4
+int spai_kernel_timer_arm(int32_t kernel, int32_t on);
+int spai_kernel_timer_read(int32_t kernel, int32_t* count, double* avg_ms);
+
 /* ---------------------------------------------------------------- logits statistics
  * lmax[b] = max_a logits[b, a], z[b] = sum_a exp(logits[b, a] - lmax[b]) (fp64), over the
  * E1 = E + 1 actions of each of B rows spaced `bstride` floats apart (bstride 0 = one row

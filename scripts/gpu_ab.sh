@@ -13,6 +13,6 @@ for r in $(seq 1 ${ROUNDS:-2}); do
 for v in tree "$@"; do
   if [ "$v" = tree ]; then unset SPAI_LIB_VARIANT; else export SPAI_LIB_VARIANT=$v; fi
   timeout -k 10 300 python bench.py --config ${CFG:-c4} --steps ${STEPS:-30} --warmup 3 --no-cpu-baseline ${BENCH_ARGS} > gpurun_out/ab_$v.log 2>&1 || { tail -20 gpurun_out/ab_$v.log; exit 1; }
-  tail -1 gpurun_out/ab_$v.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('$v', round(d['ms_per_step'],4), {k: round(v,4) for k,v in d['phases_ms'].items() if k in ('rollout_select','rollout_sort','rollout_finish','fill_residual','policy')})"
+  tail -1 gpurun_out/ab_$v.log | python scripts/ab_line.py $v
 done
 done

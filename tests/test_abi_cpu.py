@@ -45,8 +45,8 @@ def test_argument_validation_without_gpu():
     assert rc == _lib.SPAI_ERR_INVALID and b"null pointer" in lib.spai_last_error()
     rc = lib.spai_rollout_merge(None, 0, 10, 1, None, 0, 2, None, None, 0, None)
     assert rc == _lib.SPAI_ERR_INVALID and b"null pointer" in lib.spai_last_error()
-    assert lib.spai_rollout_ws_offset(1000, 2, 6) == 2 * 2 * 1024 + 2 * 8
-    assert lib.spai_rollout_ws_offset(1000, 2, 3) == 1024 and lib.spai_rollout_ws_offset(1000, 2, 9) == -1
+    assert lib.spai_rollout_ws_offset(1000, 2, 6) == 2 * 2 * 2048 + 2 * 8
+    assert lib.spai_rollout_ws_offset(1000, 2, 3) == 2048 and lib.spai_rollout_ws_offset(1000, 2, 9) == -1
     assert 0 < lib.spai_rollout_ws_offset(1000, 2, 2) < lib.spai_rollout_workspace_bytes(1000, 2)
     with pytest.raises(ValueError):
         _lib.check(rc, "spai_rollout_select")
@@ -127,3 +127,20 @@ def test_sharded_gflownet_needs_an_explicit_split_and_aligned_lines():
         assert rngs[0][0] == 0 and rngs[-1][1] == env.matrix_size
         assert all(rngs[i][1] == rngs[i + 1][0] for i in range(2))
         assert all(b % LINE_ALIGN == 0 for b, _ in rngs)
+
+
+@pytest.mark.skipif(not os.path.exists(_lib.LIB_PATH), reason="libspai_hip.so not built (run build())")
+def test_kernel_timer_arguments_without_gpu():
+    """spai_kernel_timer_*: out-of-range kernels are rejected; an armed timer with no launch recorded
+    reads back zero launches (neither call touches the device then)."""
+    lib = _lib.load()
+    assert lib.spai_kernel_timer_arm(4, 1) == _lib.SPAI_ERR_INVALID and b"out of range" in lib.spai_last_error()
+    assert lib.spai_kernel_timer_arm(-1, 0) == _lib.SPAI_ERR_INVALID
+    cnt, ms = ctypes.c_int32(-1), ctypes.c_double(-1.0)
+    assert lib.spai_kernel_timer_read(9, ctypes.byref(cnt), ctypes.byref(ms)) == _lib.SPAI_ERR_INVALID
+    assert lib.spai_kernel_timer_read(0, None, None) == _lib.SPAI_ERR_INVALID
+    for k in range(4):
+        assert lib.spai_kernel_timer_arm(k, 1) == _lib.SPAI_OK
+        assert lib.spai_kernel_timer_read(k, ctypes.byref(cnt), ctypes.byref(ms)) == _lib.SPAI_OK
+        assert cnt.value == 0 and ms.value == 0.0
+        assert lib.spai_kernel_timer_arm(k, 0) == _lib.SPAI_OK

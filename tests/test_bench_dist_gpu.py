@@ -30,6 +30,14 @@ def test_bench_columns_step_under_rccl_matches_one_gpu(tmp_path, fill):
            "nccl", "--fill", fill, "--steps", "3", "--warmup", "1", "--no-cpu-baseline", "--dump", str(dump)]
     r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=400)
     assert r.returncode == 0, r.stderr[-3000:]
+    # the bench line explains the multi-GPU step: the collective phases (max over ranks), the group, RCCL
+    import json
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["world_size"] == 1 and line["backend"] == "nccl" and line["rccl_version"]
+    col = line["collectives_ms"]
+    for k in ("bitmap_all_to_all_issue", "bitmap_all_to_all_wait", "limb_all_reduce", "line_gather_wait"):
+        assert k in col and col[k] >= 0.0, (k, col)
+    assert set(line["phases_ms_max_over_ranks"]) == set(line["phases_ms"])
     d = torch.load(dump, weights_only=True)
     assert d["shard"] == "columns" and d["world"] == 1 and "m_assembled" in d
 

@@ -166,3 +166,68 @@ def test_env_from_mtx_file_copy_fill_vs_oracle(tmp_path):
         mr, mc, mv = O.copy_fill_coo(rows, cols, vals, removed[k], n)
         M = sp.csr_matrix((mv.astype(np.float64), (mr, mc)), shape=(n, n))
         assert res[k] == pytest.approx(O.residual_fro_fp64(M, Ccsr), rel=1e-12)
+
+
+@pytest.mark.gpu
+def test_lu_candidate_driver_config_64_vs_oracle():
+    """The reference driver's own configuration at 64^2: the candidate is
+    spilu's L@U of a 4,096-unknown Poisson matrix (GFlowNet100.py:126-153) with lines up to ~230
+    wide, and initial_matrix = original_matrix = that candidate (GFlowNet100.py:173), side MA, copy
+    fill (preconditioner.py:32-52).  env.update on 8 random removal sets (5-80 % removed) and on a
+    throughput rollout's removal sets: every ||M C - I||_F (the any-width copy residual, k_line_hash)
+    against the fp64 oracle, and every reward against the reference formula."""
+    from oracle import spai_oracle as O
+    from gflownet_spai_amd import GFlowNet, PreconditionerEnv
+    A = poisson_2d(64).coalesce()
+    Acsr = sp.csr_matrix((A.values().double().numpy(), tuple(A.indices().numpy())), shape=A.shape)
+    C = lu_candidate_matrix(Acsr)
+    n = C.shape[0]
+    rows, cols = C._indices().numpy()
+    vals = C._values().numpy()
+    assert np.bincount(rows, minlength=n).max() > 13 * 10  # lines far wider than the stencil kernels'
+    env = PreconditionerEnv(n, C, C)
+    E = env.num_actions - 1
+    assert E == C._nnz()
+    Ccsr = sp.csr_matrix((vals.astype(np.float64), (rows, cols)), shape=(n, n))
+    rng = np.random.default_rng(64)
+    fracs = np.array([0.05, 0.1, 0.2, 0.3, 0.4, 0.5, 0.65, 0.8])
+    K = fracs.size
+    removed = rng.random((K, E)) < fracs[:, None]
+    T = int(removed.sum(1).max())
+    acts = -np.ones((K, T + 1), np.int64)
+    for k in range(K):
+        ids = np.flatnonzero(removed[k])
+        acts[k, :ids.size] = rng.permutation(ids)
+        acts[k, ids.size] = E
+    alpha = 0.5
+    rw = torch.stack(env.update(None, torch.from_numpy(acts), torch.tensor(alpha))).cpu().numpy()
+    res = env.last_residual.cpu().numpy()
+    r0 = O.residual_fro_fp64(Ccsr, Ccsr)
+    for k in range(K):
+        mr, mc, mv = O.copy_fill_coo(rows, cols, vals, removed[k], n)
+        M = sp.csr_matrix((mv.astype(np.float64), (mr, mc)), shape=(n, n))
+        ref = O.residual_fro_fp64(M, Ccsr)
+        assert res[k] == pytest.approx(ref, rel=1e-12)
+        assert rw[k] == pytest.approx(O.reward(ref, E - int(removed[k].sum()), alpha, r0, 2 * E * n, n), rel=1e-9)
+
+    # a throughput rollout over this candidate: its removal sets are the oracle's, its residuals too
+    class Fixed(torch.nn.Module):
+        def __init__(self, l):
+            super().__init__()
+            self.l = l
+
+        def logits(self, data):
+            return self.l.to(env.device), torch.tensor(0.5, device=env.device)
+
+    lg = torch.randn(E + 1, generator=torch.Generator().manual_seed(3))
+    lg[E] = 2.0
+    with torch.no_grad():
+        log = GFlowNet(Fixed(lg), None, env, mode="throughput", seed=9).sample_states([C] * 4, return_log=True)
+    rem_o, a_o, _, c_o = O.throughput_rollout(lg.numpy(), 4, 9, 0)
+    assert np.array_equal(log.counts.cpu().numpy(), c_o)
+    assert np.array_equal(log.actions.cpu().numpy(), a_o)
+    res = env.last_residual.cpu().numpy()
+    for k in range(4):
+        mr, mc, mv = O.copy_fill_coo(rows, cols, vals, rem_o[k], n)
+        M = sp.csr_matrix((mv.astype(np.float64), (mr, mc)), shape=(n, n))
+        assert res[k] == pytest.approx(O.residual_fro_fp64(M, Ccsr), rel=1e-12)

@@ -169,17 +169,22 @@ __global__ __launch_bounds__(kNT) void k_line(int32_t line_begin, int32_t line_e
 // Generic COPY-fill residual for lines of any width (e.g. the reference drivers' spilu
 // L@U candidate patterns, GFlowNet100.py:137-153): one workgroup per line accumulates the
 // line of M*A (or A*M) of one sample in an LDS open-addressing table of fp64 sums keyed by
-// the other index (the diagonal is seeded with -1), then sums the squares.
-__device__ __forceinline__ void hash_add(int* keys, double* vals, int tb, int key, double v) {
+// the other index (the diagonal is seeded with -1), then sums the squares.  The table is sized
+// per line: 2 x (1 + the products the line can make), capped by the launch's allocation; the A
+// lines are walked up to their first -1 slot (left-packed ELL, as build_lines lays them out), so
+// the work is the line's real products, not its padded width squared.  A probe that finds the table
+// full (more distinct keys than the cap) flags the line: its partial is NaN, never a hang.
+__device__ __forceinline__ bool hash_add(int* keys, double* vals, int tb, int key, double v) {
   unsigned h = ((unsigned)key * 2654435761u) % (unsigned)tb;
-  while (true) {
+  for (int probe = 0; probe < tb; ++probe) {
     const int prev = atomicCAS(&keys[h], -1, key);
     if (prev == -1 || prev == key) {
       atomicAdd(&vals[h], v);
-      return;
+      return true;
     }
     h = (h + 1 == (unsigned)tb) ? 0u : h + 1;
   }
+  return false;  // full
 }
 
 template <typename TA>
@@ -195,18 +200,36 @@ __global__ __launch_bounds__(kNT) void k_line_hash(int32_t line_begin, int32_t l
   double* vals = reinterpret_cast<double*>(smem);
   int* keys = reinterpret_cast<int*>(smem + (size_t)tb * sizeof(double));
   __shared__ double sred[kNT / 64];
+  __shared__ int s_cnt[kNT / 64];
+  __shared__ int s_full;
   const int j = line_begin + blockIdx.x;
   const int64_t nloc = line_end - line_begin;
-  const int nprod = wrt * wart;
   const int64_t base = (int64_t)j * wrt;
+  // this line's table size: 2 x (1 + its products over every slot), a multiple of 64, capped by tb
+  int np = 0;
+  for (int p = threadIdx.x; p < wrt; p += kNT) {
+    const int k = pat_idx[base + p];
+    if (k < 0) continue;
+    int s = 0;
+    while (s < wart && a_idx[(int64_t)k * wart + s] >= 0) ++s;
+    np += s;
+  }
+  np = wave_sum(np);
+  if ((threadIdx.x & 63) == 0) s_cnt[threadIdx.x >> 6] = np;
+  if (threadIdx.x == 0) s_full = 0;
+  __syncthreads();
+  int tot = 0;
+#pragma unroll
+  for (int w = 0; w < kNT / 64; ++w) tot += s_cnt[w];
+  const int tbl = min(tb, max(64, (2 * (tot + 1) + 63) / 64 * 64));
   for (int b = 0; b < B; ++b) {
     const uint32_t* rb = removed + (int64_t)b * words;
-    for (int t = threadIdx.x; t < tb; t += kNT) {
+    for (int t = threadIdx.x; t < tbl; t += kNT) {
       keys[t] = -1;
       vals[t] = 0.0;
     }
     __syncthreads();
-    if (threadIdx.x == 0) hash_add(keys, vals, tb, j, -1.0);
+    if (threadIdx.x == 0 && !hash_add(keys, vals, tbl, j, -1.0)) s_full = 1;
     if (m_out != nullptr) {
       for (int p = threadIdx.x; p < wrt; p += kNT) {
         const int k = pat_idx[base + p], a = pat_act[base + p];
@@ -214,23 +237,25 @@ __global__ __launch_bounds__(kNT) void k_line_hash(int32_t line_begin, int32_t l
         m_out[((int64_t)b * nloc + (j - line_begin)) * wrt + p] = keep ? pat_val[base + p] : 0.0f;
       }
     }
-    for (int f = threadIdx.x; f < nprod; f += kNT) {
-      const int p = f / wart, s = f - p * wart;
+    for (int p = threadIdx.x; p < wrt; p += kNT) {
       const int k = pat_idx[base + p];
       if (k < 0) continue;
       const int a = pat_act[base + p];
       if ((rb[(a >> 5) - word_base] >> (a & 31)) & 1u) continue;
-      const int64_t o = (int64_t)k * wart + s;
-      const int l = a_idx[o];
-      if (l < 0) continue;
-      hash_add(keys, vals, tb, l, (double)pat_val[base + p] * (double)a_val[o]);
+      const double mv = (double)pat_val[base + p];
+      for (int s = 0; s < wart; ++s) {
+        const int64_t o = (int64_t)k * wart + s;
+        const int l = a_idx[o];
+        if (l < 0) break;
+        if (!hash_add(keys, vals, tbl, l, mv * (double)a_val[o])) s_full = 1;
+      }
     }
     __syncthreads();
     double s2 = 0.0;
-    for (int t = threadIdx.x; t < tb; t += kNT)
+    for (int t = threadIdx.x; t < tbl; t += kNT)
       if (keys[t] >= 0) s2 += vals[t] * vals[t];
     s2 = block_sum<kNT>(s2, sred);
-    if (threadIdx.x == 0) partials[(int64_t)b * gridDim.x + blockIdx.x] = s2;
+    if (threadIdx.x == 0) partials[(int64_t)b * gridDim.x + blockIdx.x] = s_full ? __builtin_nan("") : s2;
     __syncthreads();
   }
 }
@@ -330,8 +355,10 @@ extern "C" int spai_fill_residual(int32_t fill_mode, int32_t n, int32_t line_beg
     }
   }
   if (!v) {
+    // any width: the hash kernel (copy fill); its table holds up to kHashMaxEntries keys per line
+    // (a line with more distinct keys gets a NaN residual)
     const int64_t bound = std::min<int64_t>((int64_t)W * WA + 1, (int64_t)n);
-    if (fill_mode == SPAI_FILL_COPY && bound < kHashMaxEntries) {
+    if (fill_mode == SPAI_FILL_COPY) {
       const int32_t tb = (int32_t)std::min<int64_t>(kHashMaxEntries, std::max<int64_t>(64, 2 * bound));
       double* partials = static_cast<double*>(workspace);
       hipError_t e = a_dtype == SPAI_DTYPE_F32

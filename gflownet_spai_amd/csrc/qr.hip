@@ -39,6 +39,11 @@ namespace {
 constexpr int kQNT = 256;     // threads per block (k_qr_rows; the fill instances choose theirs)
 constexpr int kQLines = 256;  // lines per block (= distributed.LINE_ALIGN)
 constexpr int kQChunk = 8;    // samples per residual chunk
+constexpr int kQTabW = 5;     // widths whose (entry, mask) solutions are tabled per launch (2^W masks)
+// a table record: the W solution values in M's type, then the residual^2 (fp64) in the last 8 bytes;
+// whole 16-byte pieces (float M, W = 5: 32 bytes)
+template <int W, typename TM>
+__host__ __device__ constexpr int qr_rec_bytes() { return ((W * (int)sizeof(TM) + 7) / 8 * 8 + 8 + 15) / 16 * 16; }
 
 // Sum over the L lanes of a group (L = 4, 8, 16, 32 consecutive lanes), valid on every lane of
 // the group with identical bits (each step adds a commutative pair).
@@ -524,101 +529,11 @@ __global__ __launch_bounds__(kQNT) __attribute__((amdgpu_waves_per_eu(W <= 5 ? Q
 #pragma unroll
     for (int p = 0; p < W; ++p) act[p] = (valid && p < wrt) ? av[p] : -1;
   }
-  // a dictionary entry is shared by most lanes of a wave (stencil lines): broadcast loads from L2
-  constexpr int kStride = kDict ? 1 : 64;
-  const int ent = kDict ? line_entry[jj] : 0;
-  // Block-shared (entry, mask) table (dictionary form, 2^W * 8 <= 256 lanes): a (line, sample)'s
-  // masked solve depends on the sample only through the W keep bits of its slots, and on the line
-  // only through its dictionary entry.  When the block's 256 lines use at most 8 distinct entries (a
-  // stencil's lines: 1-5 per block), the block solves every (entry, mask) pair ONCE — lane t solves
-  // mask t % 2^W of entry t / 2^W with the same qr_masked_solve on the same values — into an LDS
-  // table, and every (line, sample) takes its M values and residual from it: bit-identical to solving
-  // it on its own lane, one solve per lane instead of one per lane and sample.  Other blocks (more
-  // entries, the full cache) solve per line.
-#ifdef QRS_NO_TABLE  // (A/B variant: every block solves per line)
-  constexpr bool kTab = false;
-#else
-  constexpr bool kTab = kDict && kHold && (1 << W) * 8 <= kQNT;
-#endif
-  constexpr int kMasks = 1 << W, kTabE = kQNT / kMasks;
-  __shared__ int s_te[kTab ? 4 * (kTabE + 1) + kTabE + 1 : 1];  // per wave: distinct entries (+ count), then the block's
-  int myslot = 0;
-  bool table = false;
-  if constexpr (kTab) {
-    int* s_wte = s_te;                       // [4][kTabE + 1]: a wave's distinct entries, its count last
-    int* s_bte = s_te + 4 * (kTabE + 1);     // [kTabE] the block's distinct entries, then their count
-    {  // the wave's distinct entries (in lane order of first appearance; kTabE + 1 = overflow)
-      uint64_t rem = __ballot(valid);
-      int cnt = 0;
-      while (rem != 0ull && cnt <= kTabE) {
-        const int l0 = __builtin_ctzll(rem);
-        const int e = __builtin_amdgcn_readlane(ent, l0);
-        rem &= ~__ballot(ent == e);
-        if (lane == 0 && cnt < kTabE) s_wte[wave * (kTabE + 1) + cnt] = e;
-        ++cnt;
-      }
-      if (lane == 0) s_wte[wave * (kTabE + 1) + kTabE] = cnt;
-    }
-    __syncthreads();
-    if (wave == 0) {  // merge: lane i < 4 kTabE holds wave i / kTabE's candidate i % kTabE
-      const int w = lane / kTabE, i = lane % kTabE;
-      const int wc = lane < 4 * kTabE ? s_wte[w * (kTabE + 1) + kTabE] : 0;
-      const bool cand = lane < 4 * kTabE && i < wc;
-      const int e = cand ? s_wte[w * (kTabE + 1) + i] : -1;
-      bool first = cand;
-      for (int k = 0; k < lane && k < 4 * kTabE; ++k) {  // an earlier candidate with the same entry
-        const int wk = k / kTabE, ik = k % kTabE;
-        if (ik < s_wte[wk * (kTabE + 1) + kTabE] && s_wte[wk * (kTabE + 1) + ik] == e) first = false;
-      }
-      const uint64_t fm = __ballot(first);
-      const int pos = __builtin_popcountll(fm & ((1ull << lane) - 1ull));
-      const int tot = __builtin_popcountll(fm);
-      const bool over = __ballot(lane < 4 && s_wte[lane * (kTabE + 1) + kTabE] > kTabE) != 0ull;
-      if (first && pos < kTabE) s_bte[pos] = e;
-      if (lane == 0) s_bte[kTabE] = over ? kTabE + 1 : tot;
-    }
-    __syncthreads();
-    const int K = s_bte[kTabE];
-    table = K <= kTabE;  // block-uniform
-    if (table) {
-#pragma unroll
-      for (int k = 0; k < kTabE; ++k)
-        if (k < K && s_bte[k] == ent) myslot = k;
-    }
-  }
   double R0[kHold ? T : 1];
   float thf[W];  // the rank floors 1e-24 ||D[:, p]||^2 in fp32 (registers: 4 waves per SIMD at W = 5)
-  const double* rp = kDict ? rcache + (int64_t)ent * NQ : rcache + (int64_t)(jj >> 6) * NQ * 64 + (jj & 63);
-  if (kTab && table) {
-    // lane t: mask t % kMasks of the block's entry t / kMasks, from the dictionary entry itself
-    const int k = t / kMasks, mk = t % kMasks;
-    const int K = s_te[4 * (kTabE + 1) + kTabE];
-    if (k < K) {
-      const double* re = rcache + (int64_t)s_te[4 * (kTabE + 1) + k] * NQ;
-      double Rm[W][W], c[W], m[W], thr[W];
-      bool keep[W];
-#pragma unroll
-      for (int i = 0; i < W; ++i) {
-#pragma unroll
-        for (int q = i; q < W; ++q) Rm[i][q] = re[i * W - i * (i - 1) / 2 + (q - i)];
-        c[i] = re[T + i];
-      }
-      const double tail = re[T + W];
-#pragma unroll
-      for (int p = 0; p < W; ++p) {  // the same floors, from the same R values, as the per-line path
-        double sq = 0.0;
-#pragma unroll
-        for (int i = 0; i <= p; ++i) sq = fma(Rm[i][p], Rm[i][p], sq);
-        thr[p] = (double)(float)(1e-24 * sq);
-        keep[p] = (mk >> p) & 1;
-      }
-      const double rs = qr_masked_solve<W>(Rm, c, tail, thr, keep, m);
-#pragma unroll
-      for (int p = 0; p < W; ++p) s_c0[kHold ? p : 0][t] = m[p];
-      s_c0[kHold ? W : 0][t] = rs;
-    }
-    __syncthreads();  // the table is complete
-  } else {
+  // a dictionary entry is shared by most lanes of a wave (stencil lines): broadcast loads from L2
+  constexpr int kStride = kDict ? 1 : 64;
+  const double* rp = kDict ? rcache + (int64_t)line_entry[jj] * NQ : rcache + (int64_t)(jj >> 6) * NQ * 64 + (jj & 63);
   auto rval = [&](int q) { return kHold ? R0[q] : rp[q * kStride]; };
   if constexpr (kHold) {
 #pragma unroll
@@ -636,16 +551,11 @@ __global__ __launch_bounds__(kQNT) __attribute__((amdgpu_waves_per_eu(W <= 5 ? Q
     }
     thf[p] = (float)(1e-24 * s);  // (0 only below 1e-21: the floor then drops exact zeros only)
   }
-  }
   // bitmap word offset of a slot (recomputed where used: no registers held across the samples)
   auto wofs = [&](int p) { return act[p] >= 0 ? (act[p] >> 5) - word_base : 0; };
   uint32_t wd[W];  // the slots' bitmap words of the next sample are loaded while the current one is solved
 #pragma unroll
   for (int p = 0; p < W; ++p) wd[p] = removed[wofs(p)];
-  // the sample loop, instantiated twice: from the wave's table (R0 and the floors dead inside) or
-  // solving per line; the branch between them is wave-uniform
-  auto sample_loop = [&](auto tab_tag) {
-  constexpr bool kTabLoop = decltype(tab_tag)::value;
 #pragma unroll 1
   for (int b = 0; b < B; ++b) {
     bool keep[W];
@@ -656,16 +566,6 @@ __global__ __launch_bounds__(kQNT) __attribute__((amdgpu_waves_per_eu(W <= 5 ? Q
 #pragma unroll
       for (int p = 0; p < W; ++p) wd[p] = rn[wofs(p)];
     }
-    double m[W], rs;
-    if constexpr (kTabLoop) {  // the block's table
-      int mt = 0;
-#pragma unroll
-      for (int p = 0; p < W; ++p) mt |= (int)keep[p] << p;
-      const int slot = myslot * kMasks + mt;
-#pragma unroll
-      for (int p = 0; p < W; ++p) m[p] = s_c0[kHold ? p : 0][slot];
-      rs = s_c0[kHold ? W : 0][slot];
-    } else {
     double thr[W];
 #pragma unroll
     for (int p = 0; p < W; ++p) {
@@ -673,7 +573,7 @@ __global__ __launch_bounds__(kQNT) __attribute__((amdgpu_waves_per_eu(W <= 5 ? Q
       asm volatile("" : "+v"(f));  // widened per sample, not held as fp64 across the loop
       thr[p] = (double)f;
     }
-    double Rm[W][W], c[W], tail;
+    double Rm[W][W], c[W], m[W], tail;
     if constexpr (kHold) {
 #pragma unroll
       for (int i = 0; i < W; ++i) {
@@ -693,8 +593,7 @@ __global__ __launch_bounds__(kQNT) __attribute__((amdgpu_waves_per_eu(W <= 5 ? Q
       }
       tail = rps[(T + W) * kStride];
     }
-    rs = qr_masked_solve<W>(Rm, c, tail, thr, keep, m);
-    }
+    const double rs = qr_masked_solve<W>(Rm, c, tail, thr, keep, m);
     s_r2[b % kQChunk][t] = valid ? rs : 0.0;
 #ifdef QRS_DIRECT  // A/B: M stored from the registers (no LDS staging, no barrier per sample)
     if (m_out != nullptr && valid) {
@@ -747,9 +646,136 @@ __global__ __launch_bounds__(kQNT) __attribute__((amdgpu_waves_per_eu(W <= 5 ? Q
       __syncthreads();
     }
   }
+}
+
+// Every (entry, keep mask) solution of the R cache's dictionary, once per launch of the cached
+// fill (k_qr_lookup's table): thread g solves mask g % 2^W of entry g / 2^W with the per-line path's
+// arithmetic on the same values (its R, Q^T e and tail from the entry, the rank floors recomputed as
+// sum_i R_ip^2 in the same order) and writes the record {m_0 .. m_{W-1}, residual^2} (fp64).
+constexpr int kQTabMaxEntries = 4096;  // (table <= 6.3 MB at W = 5; larger dictionaries solve per line)
+template <int W, typename TM>
+__global__ __launch_bounds__(kQNT) void k_qr_table(int32_t entries, const double* __restrict__ dict,
+                                                   char* __restrict__ mtab) {
+  constexpr int T = W * (W + 1) / 2, NQ = qr_cache_q(W), kMasks = 1 << W;
+  const int g = blockIdx.x * kQNT + threadIdx.x;
+  const int e = g / kMasks, mk = g % kMasks;
+  if (e >= entries) return;
+  const double* re = dict + (int64_t)e * NQ;
+  double Rm[W][W], c[W], m[W], thr[W];
+  bool keep[W];
+#pragma unroll
+  for (int i = 0; i < W; ++i) {
+#pragma unroll
+    for (int q = i; q < W; ++q) Rm[i][q] = re[i * W - i * (i - 1) / 2 + (q - i)];
+    c[i] = re[T + i];
+  }
+  const double tail = re[T + W];
+#pragma unroll
+  for (int p = 0; p < W; ++p) {
+    double sq = 0.0;
+#pragma unroll
+    for (int i = 0; i <= p; ++i) sq = fma(Rm[i][p], Rm[i][p], sq);
+    thr[p] = (double)(float)(1e-24 * sq);
+    keep[p] = (mk >> p) & 1;
+  }
+  const double rs = qr_masked_solve<W>(Rm, c, tail, thr, keep, m);
+  constexpr int kRec = qr_rec_bytes<W, TM>();
+  char* out = mtab + (int64_t)g * kRec;
+#pragma unroll
+  for (int p = 0; p < W; ++p) reinterpret_cast<TM*>(out)[p] = (TM)m[p];  // (the per-line path's conversion)
+  *reinterpret_cast<double*>(out + kRec - 8) = rs;
+}
+
+// The cached fill from that table: per line the W action ids and the entry index; per sample the
+// W keep bits pick the record {M values, residual^2} (the next sample's record loads while this one
+// is stored).  No solve and no per-line R or Q^T e held, so more blocks per CU than k_qr_solve; M
+// staged per block and stored, and the residual sums formed, exactly as k_qr_solve does (the same
+// bits as solving every (line, sample) on its own lane).
+template <int W, typename TM>
+__global__ __launch_bounds__(kQNT) __attribute__((amdgpu_waves_per_eu(6))) void k_qr_lookup(
+    int32_t line_begin, int32_t line_end, int32_t wrt, const int32_t* __restrict__ pat_act,
+    const int32_t* __restrict__ line_entry, int32_t B, const uint32_t* __restrict__ removed, int32_t words,
+    int32_t word_base, TM* __restrict__ m_out, double* __restrict__ partials, const char* __restrict__ mtab) {
+  constexpr int kMasks = 1 << W, kRec = qr_rec_bytes<W, TM>(), kRW = kRec / 16;
+  typedef unsigned int u4t __attribute__((ext_vector_type(4)));
+  __shared__ double s_r2[kQChunk][kQNT];
+  __shared__ __attribute__((aligned(16))) TM s_m[2][kQNT * W];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int lb = blockIdx.x;
+  const int j = line_begin + lb * kQNT + t;
+  const bool valid = j < line_end;
+  const int64_t nloc = line_end - line_begin;
+  const int jj = valid ? j : line_begin;  // clamped: loads stay in bounds
+  const int nvl = min(kQNT, line_end - (line_begin + lb * kQNT));
+  int act[W];
+  {
+    int av[W];
+#pragma unroll
+    for (int p = 0; p < W; ++p) av[p] = pat_act[(int64_t)jj * wrt + min(p, wrt - 1)];
+#pragma unroll
+    for (int p = 0; p < W; ++p) act[p] = (valid && p < wrt) ? av[p] : -1;
+  }
+  const u4t* tab = reinterpret_cast<const u4t*>(mtab) + (int64_t)line_entry[jj] * kMasks * kRW;
+  auto wofs = [&](int p) { return act[p] >= 0 ? (act[p] >> 5) - word_base : 0; };
+  auto mask_of = [&](const uint32_t (&w)[W]) {
+    int mt = 0;
+#pragma unroll
+    for (int p = 0; p < W; ++p) mt |= (int)(act[p] >= 0 && !((w[p] >> (act[p] & 31)) & 1u)) << p;
+    return mt;
   };
-  if (kTab && table) sample_loop(std::true_type{});
-  else sample_loop(std::false_type{});
+  uint32_t wd[W];
+#pragma unroll
+  for (int p = 0; p < W; ++p) wd[p] = removed[wofs(p)];
+  u4t rc[kRW], rn[kRW];
+  {
+    const int mt = mask_of(wd);
+#pragma unroll
+    for (int k = 0; k < kRW; ++k) rc[k] = tab[mt * kRW + k];
+  }
+  if (B > 1) {
+#pragma unroll
+    for (int p = 0; p < W; ++p) wd[p] = removed[(int64_t)words + wofs(p)];
+  }
+#pragma unroll 1
+  for (int b = 0; b < B; ++b) {
+    if (b + 1 < B) {  // the next sample's record (its words arrived during this sample's predecessor)
+      const int mt = mask_of(wd);
+#pragma unroll
+      for (int k = 0; k < kRW; ++k) rn[k] = tab[mt * kRW + k];
+      if (b + 2 < B) {
+#pragma unroll
+        for (int p = 0; p < W; ++p) wd[p] = removed[(int64_t)(b + 2) * words + wofs(p)];
+      }
+    }
+    const TM* mv = reinterpret_cast<const TM*>(&rc[0]);
+    const double rs = *reinterpret_cast<const double*>(reinterpret_cast<const char*>(&rc[0]) + kRec - 8);
+    s_r2[b % kQChunk][t] = valid ? rs : 0.0;
+    {
+      TM* sm = s_m[b & 1];
+      if (valid) {
+#pragma unroll
+        for (int p = 0; p < W; ++p)
+          if (p < wrt) sm[t * wrt + p] = mv[p];
+      }
+      __syncthreads();
+      store_m_block<kQNT, W, TM>(m_out ? m_out + ((int64_t)b * nloc + (int64_t)lb * kQNT) * wrt : nullptr, sm,
+                                 nvl * wrt);
+    }
+    if (b % kQChunk == kQChunk - 1 || b == B - 1) {  // the chunk's fixed-order block sums (k_qr_solve's)
+      const int c0b = b - b % kQChunk, nb = b - c0b + 1;
+      __syncthreads();
+      for (int u = wave; u < nb; u += kQNT / 64) {
+        double acc = 0.0;
+#pragma unroll
+        for (int q = 0; q < kQNT / 64; ++q) acc += s_r2[u][q * 64 + lane];
+        acc = wave_sum(acc);
+        if (lane == 0) partials[(int64_t)(c0b + u) * gridDim.x + lb] = acc;
+      }
+      __syncthreads();
+    }
+#pragma unroll
+    for (int k = 0; k < kRW; ++k) rc[k] = rn[k];
+  }
 }
 
 // (W class, A width class, rows) -> instance
@@ -817,10 +843,19 @@ hipError_t dispatch_factor(int wc, int rows, bool a32, int32_t n, int32_t wrt, c
 }
 
 template <int W, typename TM>
-void launch_solve_t(const int32_t* ent, int32_t lb, int32_t le, int32_t wrt, const int32_t* pa, const double* rc,
-                    int32_t B, const uint32_t* rm, int32_t words, int32_t wb, void* mo, double* partials,
-                    int32_t nparts, hipStream_t s) {
-  KernelTimer kt(SPAI_TIMER_QR, s);
+void launch_solve_t(const int32_t* ent, int32_t entries, int32_t lb, int32_t le, int32_t wrt, const int32_t* pa,
+                    const double* rc, int32_t B, const uint32_t* rm, int32_t words, int32_t wb, void* mo,
+                    double* partials, int32_t nparts, double* mtab, hipStream_t s) {
+  KernelTimer kt(SPAI_TIMER_QR, s);  // (the table and the solve: the fill's whole time)
+  if constexpr (W <= kQTabW) {
+    if (ent && mtab) {  // every (entry, mask) solution once, then the lines read theirs
+      const int nt = entries << W;
+      k_qr_table<W, TM><<<(nt + kQNT - 1) / kQNT, kQNT, 0, s>>>(entries, rc, reinterpret_cast<char*>(mtab));
+      k_qr_lookup<W, TM><<<nparts, kQNT, 0, s>>>(lb, le, wrt, pa, ent, B, rm, words, wb, static_cast<TM*>(mo),
+                                                 partials, reinterpret_cast<const char*>(mtab));
+      return;
+    }
+  }
   if (ent)
     k_qr_solve<W, TM, true><<<nparts, kQNT, 0, s>>>(lb, le, wrt, pa, rc, ent, B, rm, words, wb, static_cast<TM*>(mo),
                                                     partials);
@@ -829,13 +864,13 @@ void launch_solve_t(const int32_t* ent, int32_t lb, int32_t le, int32_t wrt, con
                                                      static_cast<TM*>(mo), partials);
 }
 template <int W>
-hipError_t launch_solve(bool f64, const int32_t* ent, int32_t lb, int32_t le, int32_t wrt, const int32_t* pa,
-                        const double* rc, int32_t B, const uint32_t* rm, int32_t words, int32_t wb, void* mo,
-                        double* partials, int32_t nparts, hipStream_t s) {
+hipError_t launch_solve(bool f64, const int32_t* ent, int32_t entries, int32_t lb, int32_t le, int32_t wrt,
+                        const int32_t* pa, const double* rc, int32_t B, const uint32_t* rm, int32_t words, int32_t wb,
+                        void* mo, double* partials, int32_t nparts, double* mtab, hipStream_t s) {
   if (f64)
-    launch_solve_t<W, double>(ent, lb, le, wrt, pa, rc, B, rm, words, wb, mo, partials, nparts, s);
+    launch_solve_t<W, double>(ent, entries, lb, le, wrt, pa, rc, B, rm, words, wb, mo, partials, nparts, mtab, s);
   else
-    launch_solve_t<W, float>(ent, lb, le, wrt, pa, rc, B, rm, words, wb, mo, partials, nparts, s);
+    launch_solve_t<W, float>(ent, entries, lb, le, wrt, pa, rc, B, rm, words, wb, mo, partials, nparts, mtab, s);
   return hipGetLastError();
 }
 
@@ -938,9 +973,9 @@ extern "C" int spai_qr_factor(int32_t n, int32_t W, const int32_t* pat_idx, cons
 
 extern "C" int spai_fill_lines_qr_cached(int32_t n, int32_t line_begin, int32_t line_end, int32_t W, int32_t WA,
                                          const int32_t* pat_act, const double* rcache, const int32_t* line_entry,
-                                         int32_t B, const uint32_t* removed, int32_t words, int32_t word_base,
-                                         void* m_out, int32_t m_dtype, void* workspace, size_t workspace_bytes,
-                                         void* stream) {
+                                         int32_t entries, int32_t B, const uint32_t* removed, int32_t words,
+                                         int32_t word_base, void* m_out, int32_t m_dtype, void* workspace,
+                                         size_t workspace_bytes, void* stream) {
   SPAI_CHECK_ARG(m_dtype == SPAI_DTYPE_F32 || m_dtype == SPAI_DTYPE_F64, "spai_fill_lines_qr_cached: bad m_dtype");
   SPAI_CHECK_ARG(n >= 1 && line_begin >= 0 && line_end >= line_begin && line_end <= n && W >= 1 && WA >= 1 &&
                      B >= 1 && words >= 1 && word_base >= 0,
@@ -955,19 +990,28 @@ extern "C" int spai_fill_lines_qr_cached(int32_t n, int32_t line_begin, int32_t 
               wc, W, WA);
     return SPAI_ERR_UNSUPPORTED;
   }
+  SPAI_CHECK_ARG(!line_entry || entries >= 1, "spai_fill_lines_qr_cached: a dictionary needs entries >= 1");
   const int32_t nparts = (nl + kQNT - 1) / kQNT;
   SPAI_CHECK_ARG(workspace_bytes >= sizeof(double) * (size_t)nparts * B,
                  "spai_fill_lines_qr_cached: workspace too small");
   double* partials = static_cast<double*>(workspace);
+  // the (entry, mask) table after the partials, when the dictionary is small and the workspace has room
+  double* mtab = nullptr;
+  {
+    const size_t off = align_up(sizeof(double) * (size_t)nparts * B);
+    const size_t tb = sizeof(double) * (size_t)entries * (1u << kQTabW) * (kQTabW + 1);
+    if (line_entry && wc <= kQTabW && entries <= kQTabMaxEntries && workspace_bytes >= off + tb)
+      mtab = reinterpret_cast<double*>(static_cast<char*>(workspace) + off);
+  }
   hipStream_t s = (hipStream_t)stream;
   const bool f64 = m_dtype == SPAI_DTYPE_F64;
   const hipError_t e =
-      wc == 5   ? launch_solve<5>(f64, line_entry, line_begin, line_end, W, pat_act, rcache, B, removed, words,
-                                  word_base, m_out, partials, nparts, s)
-      : wc == 7 ? launch_solve<7>(f64, line_entry, line_begin, line_end, W, pat_act, rcache, B, removed, words,
-                                  word_base, m_out, partials, nparts, s)
-                : launch_solve<13>(f64, line_entry, line_begin, line_end, W, pat_act, rcache, B, removed, words,
-                                   word_base, m_out, partials, nparts, s);
+      wc == 5   ? launch_solve<5>(f64, line_entry, entries, line_begin, line_end, W, pat_act, rcache, B, removed,
+                                  words, word_base, m_out, partials, nparts, mtab, s)
+      : wc == 7 ? launch_solve<7>(f64, line_entry, entries, line_begin, line_end, W, pat_act, rcache, B, removed,
+                                  words, word_base, m_out, partials, nparts, nullptr, s)
+                : launch_solve<13>(f64, line_entry, entries, line_begin, line_end, W, pat_act, rcache, B, removed,
+                                   words, word_base, m_out, partials, nparts, nullptr, s);
   SPAI_CHECK_HIP(e);
   return SPAI_OK;
 }

@@ -480,6 +480,25 @@ class CacheDict:
 QrDict = CacheDict  # (the R cache's dictionary)
 
 
+def qr_class(W: int, WA: int) -> int:
+    """Width class of the QR fill (qr.hip qr_class): 5, 7 or 13."""
+    if W <= 5 and WA <= 5:
+        return 5
+    if W <= 7 and WA <= 7:
+        return 7
+    return 13
+
+
+def qr_cache_q(wc: int) -> int:
+    """Values per line of the R cache of width class wc: packed R, Q^T e, tail (qr.hip qr_cache_q)."""
+    return wc * (wc + 1) // 2 + wc + 1
+
+
+def qr_table_offset(n_lines: int, B: int) -> int:
+    """Byte offset of spai_fill_lines_qr_cached's (entry, mask) table in its workspace."""
+    return ((n_lines + 255) // 256 * B * 8 + 255) // 256 * 256
+
+
 def cache_nbytes(cache) -> int:
     """Bytes one rollout's fill reads of a per-line cache (full tensor or CacheDict)."""
     return cache.nbytes if isinstance(cache, CacheDict) else cache.numel() * cache.element_size()
@@ -517,10 +536,17 @@ def _fill_lines_qr(pattern: Lines, a_lines: Lines, max_rows: int, removed: torch
                    line_end: int, m, m_dtype, word_base: int, ws, rcache=None):
     B, words = removed.shape
     if rcache is not None:  # phase 2 only, from the env's R cache (full, or its dictionary)
-        tab, ent = (rcache.table, rcache.entry) if isinstance(rcache, QrDict) else (rcache, None)
+        if isinstance(rcache, QrDict):
+            nq = qr_cache_q(qr_class(pattern.width, a_lines.width))
+            if rcache.table.dtype != torch.float64 or rcache.table.numel() != rcache.entries * nq:
+                raise ValueError(f"the R cache dictionary holds {rcache.table.numel()} fp64 values, not "
+                                 f"{rcache.entries} entries x {nq} (a Gram cache dictionary passed as an R cache?)")
+            tab, ent, n_ent = rcache.table, rcache.entry, rcache.entries
+        else:
+            tab, ent, n_ent = rcache, None, 0
         with _timed("fill_residual"):  # the fill kernel alone
             st = _l().spai_fill_lines_qr_cached(pattern.n, line_begin, line_end, pattern.width, a_lines.width,
-                                                _lib.ptr(pattern.act), _lib.ptr(tab), _lib.ptr(ent), B,
+                                                _lib.ptr(pattern.act), _lib.ptr(tab), _lib.ptr(ent), n_ent, B,
                                                 _lib.ptr(removed), words, word_base, _lib.ptr(m), _DT[m_dtype],
                                                 _lib.ptr(ws), ws.numel(), _lib.stream_ptr(removed.device))
         _lib.check(st, "spai_fill_lines_qr_cached")
@@ -548,7 +574,10 @@ def fill_residual_qr(pattern: Lines, a_lines: Lines, max_rows: int, removed: tor
     n_loc = line_end - line_begin
     res2, lb = _fill_out(B, removed.device, limbs)
     m = torch.empty(B, n_loc, pattern.width, dtype=m_dtype, device=removed.device) if store_m else None
-    ws = _lib.workspace(_l().spai_fill_workspace_bytes(max(n_loc, 1), B), removed.device, "fill")
+    nb = _l().spai_fill_workspace_bytes(max(n_loc, 1), B)
+    if isinstance(rcache, QrDict):  # room for the cached fill's (entry, mask) table after the partials
+        nb = max(nb, qr_table_offset(n_loc, B) + rcache.entries * 32 * 6 * 8)
+    ws = _lib.workspace(nb, removed.device, "fill")
     _fill_lines_qr(pattern, a_lines, max_rows, removed, line_begin, line_end, m, m_dtype, word_base, ws, rcache)
     _lib.check(_l().spai_fill_reduce(n_loc, B, _lib.ptr(ws), _lib.ptr(res2), _lib.ptr(lb),
                                      _lib.stream_ptr(removed.device)), "spai_fill_reduce")
@@ -648,7 +677,10 @@ def fill_rewards_qr(pattern: Lines, a_lines: Lines, max_rows: int, removed: torc
     B = removed.shape[0]
     n = pattern.n
     m = torch.empty(B, n, pattern.width, dtype=m_dtype, device=removed.device) if store_m else None
-    ws = _lib.workspace(_l().spai_fill_workspace_bytes(n, B), removed.device, "fill")
+    nb = _l().spai_fill_workspace_bytes(n, B)
+    if isinstance(rcache, QrDict):  # room for the cached fill's (entry, mask) table after the partials
+        nb = max(nb, qr_table_offset(n, B) + rcache.entries * 32 * 6 * 8)
+    ws = _lib.workspace(nb, removed.device, "fill")
     _fill_lines_qr(pattern, a_lines, max_rows, removed, 0, n, m, m_dtype, 0, ws, rcache)
     return _reduce_rewards(ws, n, B, counts, nnz0, r0, f0, alpha, removed.device) + (m,)
 

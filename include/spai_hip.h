@@ -240,9 +240,9 @@ int spai_res2_from_limbs(int32_t B, const int64_t* limbs, double* res2_out, void
  * the per-sample sums; either may be NULL, not both.
  * a_idx/a_val: [n][WA] lines of the original matrix A (n x n) in the same orientation.
  * Widths W, WA <= 7 run the register kernel (one thread per line, all samples); wider
- * COPY lines run the LDS hash kernel (one workgroup per line and sample, bounded by
- * min(W*WA + 1, n) < 13000 distinct entries per line); anything else returns
- * SPAI_ERR_UNSUPPORTED. */
+ * COPY lines run the LDS hash kernel (one workgroup per line, every sample; A lines read up to
+ * their first -1 slot, i.e. left-packed ELL; up to 13000 distinct entries in a line of the
+ * product, a line with more gets a NaN residual); anything else returns SPAI_ERR_UNSUPPORTED. */
 size_t spai_fill_workspace_bytes(int32_t n_lines, int32_t B);
 int spai_fill_residual(int32_t fill_mode, int32_t n, int32_t line_begin, int32_t line_end, int32_t W,
                        const int32_t* pat_idx, const int32_t* pat_act, const float* pat_val, int32_t WA,
@@ -330,12 +330,17 @@ size_t spai_qr_cache_bytes(int32_t n, int32_t W, int32_t WA);
 int spai_qr_factor(int32_t n, int32_t W, const int32_t* pat_idx, const int32_t* pat_act, int32_t WA,
                    const int32_t* a_idx, const void* a_val, int32_t a_dtype, int32_t max_rows, double* rcache,
                    size_t rcache_bytes, void* stream);
-/* line_entry: NULL, or rcache is the cache's dictionary (spai_line_cache_dict) and line_entry [n]
- * names each line's entry. */
+/* line_entry: NULL, or rcache is the cache's dictionary (spai_line_cache_dict) of `entries` entries
+ * and line_entry [n] names each line's entry.  With a dictionary of <= 4096 entries and the 5-wide
+ * class, every (entry, keep mask) solution is computed once per call into an (entry, mask) table
+ * placed in the workspace after the partials (at the first 256-byte boundary past
+ * ceil((line_end - line_begin) / 256) * B doubles; entries * 32 * 6 doubles; without that room the
+ * per-line solves run) and each (line, sample) reads its M values and residual from it: the same
+ * arithmetic on the same values, so the same bits as solving it on the line's own lane (ABI 19). */
 int spai_fill_lines_qr_cached(int32_t n, int32_t line_begin, int32_t line_end, int32_t W, int32_t WA,
-                              const int32_t* pat_act, const double* rcache, const int32_t* line_entry, int32_t B,
-                              const uint32_t* removed, int32_t words, int32_t word_base, void* m_out,
-                              int32_t m_dtype, void* workspace, size_t workspace_bytes, void* stream);
+                              const int32_t* pat_act, const double* rcache, const int32_t* line_entry,
+                              int32_t entries, int32_t B, const uint32_t* removed, int32_t words, int32_t word_base,
+                              void* m_out, int32_t m_dtype, void* workspace, size_t workspace_bytes, void* stream);
 
 /* ---------------------------------------------------------------- cache dictionaries
  * The dictionary of a per-line cache in the blocked layout of spai_qr_factor / spai_gram_build

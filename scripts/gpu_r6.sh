@@ -8,6 +8,7 @@
 #   bench   the C4 bench line (and BENCH_CFGS configs)
 #   prof    rocprofv3 kernel stats of the C4 bench (TAG names the profiles)
 #   pmc     PMC passes of the C4 bench (scripts/pmc_kernels.sh)
+#   qrbench scripts/qr_fill_bench.py (the cached QR fill alone: M stored or not, batch sizes)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 TAG=${TAG:-r6}
@@ -48,6 +49,9 @@ for st in ${STEPS:-tests bench}; do
         PMC_TIMEOUT=300 bash scripts/pmc_kernels.sh $O/pmc_$c python bench.py --config $c --steps 10 --warmup 2 \
           --no-cpu-baseline > $O/pmc_$c.log 2>&1 || { tail -20 $O/pmc_$c.log; exit 1; }
       done ;;
+    qrbench)
+      timeout -k 10 300 python scripts/qr_fill_bench.py --config ${QR_CFG:-c4} > $O/qr_fill_bench.log 2>&1 || { tail -20 $O/qr_fill_bench.log; exit 1; }
+      cat $O/qr_fill_bench.log | grep '^{' ;;
     *) echo "unknown step $st"; exit 2 ;;
   esac
 done

@@ -1214,7 +1214,8 @@ __device__ __forceinline__ void big_bucket(const int n, const int ntiles, const 
     const double exs = block_excl_scan_d<kSortNT>(w, s_wd, &t);
     if (i >= 0) {
       act_out[i] = (int64_t)a;
-      fwd_out[i] = (float)(w / (later + (carry + exs + w)));
+      const double den = later + (carry + exs + w);  // (as k_sort2)
+      fwd_out[i] = den >= 1e-30 ? (float)w * __builtin_amdgcn_rcpf((float)den) : (float)(w / den);
     }
     carry += t;
   }
@@ -1242,8 +1243,9 @@ __global__ __launch_bounds__(kSortNT) void k_sort2(int32_t E, int32_t B, int32_t
                                                    const double* __restrict__ bwsuf, int32_t* __restrict__ bigcnt,
                                                    const float* __restrict__ ww, int64_t wrow_stride,
                                                    uint64_t* __restrict__ scratch, int32_t part, int32_t nparts) {
-  __shared__ uint64_t A[kCap2];  // the bucket's records (ranked in place); high half: actions awaiting store
-  __shared__ __attribute__((aligned(16))) float L[kCap2];  // weights in trajectory order
+  // the bucket's records (ranked in place; once placed, {weight bits, action} in trajectory order);
+  // high half: actions awaiting store
+  __shared__ __attribute__((aligned(16))) uint64_t A[kCap2];
   __shared__ __attribute__((aligned(16))) float S[kCap2];  // step probabilities awaiting store
   __shared__ __attribute__((aligned(16))) int s_sub[kMaxSub + 4];
   __shared__ int s_nbp[kMaxSamples + 1];
@@ -1539,22 +1541,22 @@ __global__ __launch_bounds__(kSortNT) void k_sort2(int32_t E, int32_t B, int32_t
     issue(6);
 #pragma unroll
     for (int j = 0; j < kPer; ++j)
-      if (j * kSortNT + tid < n) {
-        A[sb[j]] = mine[j];
-        L[sb[j]] = lw[j];
-      }
+      if (j * kSortNT + tid < n)  // the key has done its work: the weight's bits take its place
+        A[sb[j]] = ((uint64_t)__float_as_uint(lw[j]) << 32) | (uint32_t)mine[j];
     lds_barrier();
     PROF(10)
     // fp64 in-bucket inclusive suffix sums: thread t owns the kPer-record chunk
     // c = kSortNT - 1 - t (chunks counted from the end of the bucket, so the exclusive scan over
     // lower threads is the mass of every later record), read and written as aligned 16-byte
     // vectors (conflict-free); fixed order -> deterministic
-    static_assert(kPer == 8 && kPer * kSortNT == kCap2, "two float4 per chunk");
+    static_assert(kPer == 8 && kPer * kSortNT == kCap2, "four 16-byte record pairs per chunk");
     const int cb = (kSortNT - 1 - tid) * kPer;  // first record of this thread's chunk
     float lv[kPer];
-    {
-      const float4 l0 = reinterpret_cast<const float4*>(L)[cb / 4], l1 = reinterpret_cast<const float4*>(L)[cb / 4 + 1];
-      lv[0] = l0.x, lv[1] = l0.y, lv[2] = l0.z, lv[3] = l0.w, lv[4] = l1.x, lv[5] = l1.y, lv[6] = l1.z, lv[7] = l1.w;
+#pragma unroll
+    for (int k = 0; k < kPer / 2; ++k) {  // 16-byte LDS reads of the chunk's placed records
+      const ulonglong2 r2 = reinterpret_cast<const ulonglong2*>(A)[cb / 2 + k];
+      lv[2 * k] = __uint_as_float((uint32_t)(r2.x >> 32));
+      lv[2 * k + 1] = __uint_as_float((uint32_t)(r2.y >> 32));
     }
     double loc = 0.0;
 #pragma unroll
@@ -1575,7 +1577,11 @@ __global__ __launch_bounds__(kSortNT) void k_sort2(int32_t E, int32_t B, int32_t
       fv[j] = 0.0f;
       if (cb + j < n) {
         run += (double)lv[j];
-        fv[j] = (float)((double)lv[j] / (later + run));
+        // w / (mass still available): the fp64 mass rounded to fp32, then the hardware reciprocal
+        // (1 ulp) and one product: <= ~2.5 ulp of the exact quotient (the log's fp32 tolerance);
+        // masses below 1e-30 (fp32 denormals for the reciprocal) divide in fp64
+        const double den = later + run;
+        fv[j] = den >= 1e-30 ? lv[j] * __builtin_amdgcn_rcpf((float)den) : (float)((double)lv[j] / den);
       }
     }
     reinterpret_cast<float4*>(S)[cb / 4] = make_float4(fv[0], fv[1], fv[2], fv[3]);
@@ -1611,7 +1617,7 @@ __global__ __launch_bounds__(kSortNT) void k_sort2(int32_t E, int32_t B, int32_t
       const int32_t* bs = bstart + (int64_t)bb * (kMaxB + 1);
       const int s0 = bs[kk], n = bs[kk + 1] - s0;
       const double later = wrest[bb] + bwsuf[(int64_t)bb * kMaxB + kk];
-      int* s_pre = reinterpret_cast<int*>(L);
+      int* s_pre = reinterpret_cast<int*>(S);  // (S is free after the loop's last flush)
       int* s_loc = s_pre + (kMaxTiles + 1);
       const uint32_t* rr = runs + ((int64_t)bb * kMaxB + kk) * ntiles;  // [b][bucket][tile]
       const uint32_t q0 = t0 < ntiles ? rr[t0] : 0u, q1 = t1 < ntiles ? rr[t1] : 0u;

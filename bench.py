@@ -655,17 +655,26 @@ def main():
             "removed_per_candidate_mean": float(counts.mean()),
             "phases_ms": phase_ms,
             "roofline": roofline_obj(f"k_gram_fill<{env.pattern.width},{gram_t},LSQ> (LSQ fill of M + ||AM-I||^2; A "
-                                     f"reaches it through the env-constant Gram cache)", fb, fill_ms,
-                                     measured_traffic(args.config, bl)),
+                                     f"reaches it through the env-constant Gram cache)" if args.fill != "copy" else
+                                     f"k_line{'_hash' if env.pattern.width > 7 else ''} (the reference's copy fill + "
+                                     f"||{args.side[0]}{args.side[1]}-I||^2 of lines up to {env.pattern.width} wide)",
+                                     fb, fill_ms, measured_traffic(args.config, bl)),
         }
         if args.fill == "qr":  # the Householder-QR fill reads A itself: SURVEY §8(d)'s bytes are its bytes
             sbq = survey_fill_bytes(env, B if shard == "columns" else bl)
             if split:
                 sbq *= (model.lines[1] - model.lines[0]) / n
             if env.rcache is not None:  # phase 2 from the R cache: its bytes are the cache + the per-sample stream
+                tabled = (isinstance(env.rcache, kernels.QrDict) and env.rcache.entries <= 4096 and
+                          kernels.qr_class(env.pattern.width, env.a_lines.width) == 5)
+                head = (f"k_qr_table<5> + k_qr_lookup<5> (LSQ fill of M by Householder QR: every (dictionary entry, "
+                        f"keep mask) masked re-triangularisation of the cached R solved once per call "
+                        f"({env.rcache.entries} entries x 32 masks), each (line, sample) reading its M and residual "
+                        f"from that table" if tabled else
+                        f"k_qr_solve<{env.pattern.width}> (LSQ fill of M by Householder QR: masked "
+                        f"re-triangularisation of each line's cached R")
                 out["roofline"] = roofline_obj(
-                    f"k_qr_solve<{env.pattern.width}> (LSQ fill of M by Householder QR: masked re-triangularisation of "
-                    f"each line's cached R (the full block A[I, slots] factored once per env, rows {env.qr_rows}"
+                    head + f" (the full block A[I, slots] factored once per env, rows {env.qr_rows}"
                     + (f"; the cache as its dictionary: {env.rcache.entries} distinct line entries"
                        if isinstance(env.rcache, kernels.QrDict) else "") +
                     ") + ||AM-I||^2)", fb, fill_ms, measured_traffic(args.config + "_qr", bl))

@@ -15,7 +15,7 @@ import shutil
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ROOF_KERNELS = {"c4": "k_gram_fill<5, ", "c2": "k_gram_fill<5, ", "c3": "k_gram_fill_wide<13, "}  # LSQ fill, any Gram type
-ROOF_KERNELS_QR = {"c4": "k_qr_solve<5, ", "c2": "k_qr_solve<5, ", "c5s": "k_qr_solve<7, ", "c3": "k_qr_solve<13, "}
+ROOF_KERNELS_QR = {"c4": "k_qr_lookup<5, ", "c2": "k_qr_lookup<5, ", "c5s": "k_qr_solve<7, ", "c3": "k_qr_solve<13, "}
 
 
 def short(name):
@@ -72,6 +72,12 @@ def main():
                "hbm_bytes_per_launch": v["hbm_bytes_per_launch"], "FETCH_SIZE_KB": v["pmc"].get("FETCH_SIZE"),
                "WRITE_SIZE_KB": v["pmc"].get("WRITE_SIZE"), "source": f"profiles/pmc_{args.tag}.json",
                "command": args.cmd}
+        # the cached QR fill's (entry, mask) table kernel runs before the lookup in the same call
+        tab = [(k2, v2) for k2, v2 in summary["kernels"].items() if "k_qr_table<" in k2 and "hbm_bytes_per_launch" in v2]
+        if "k_qr_lookup<" in k and tab:
+            rec["kernel"] = f"{tab[0][0]} + {k}"
+            rec["hbm_bytes_per_launch"] += tab[0][1]["hbm_bytes_per_launch"]
+            rec["avg_us"] = (rec["avg_us"] or 0.0) + (tab[0][1].get("avg_us") or 0.0)
         path = os.path.join(args.out, "fill_traffic.json")
         try:
             allrec = json.load(open(path))
@@ -90,6 +96,18 @@ def main():
                 "hbm_bytes_per_launch": v["hbm_bytes_per_launch"], "FETCH_SIZE_KB": v["pmc"].get("FETCH_SIZE"),
                 "WRITE_SIZE_KB": v["pmc"].get("WRITE_SIZE"), "source": f"profiles/pmc_{args.tag}.json",
                 "command": args.cmd}
+        # the rollout's dominant kernels (bench roofline: k_tile; k_sort2 for reference), with the
+        # VALU instruction count the bench's issue-time estimate uses
+        for short_name, key2 in (("k_tile", "_tile"), ("k_sort2", "_sort")):
+            kk = [(k, v) for k, v in summary["kernels"].items() if k.replace("spai::", "").startswith(short_name)
+                  and "hbm_bytes_per_launch" in v]
+            if kk:
+                k, v = kk[0]
+                allrec[args.config + key2] = {
+                    "config": args.config, "batch": args.batch, "kernel": k, "avg_us": v.get("avg_us"),
+                    "hbm_bytes_per_launch": v["hbm_bytes_per_launch"], "valu_insts_per_launch": v["pmc"].get("SQ_INSTS_VALU"),
+                    "FETCH_SIZE_KB": v["pmc"].get("FETCH_SIZE"), "WRITE_SIZE_KB": v["pmc"].get("WRITE_SIZE"),
+                    "source": f"profiles/pmc_{args.tag}.json", "command": args.cmd}
         json.dump(allrec, open(path, "w"), indent=1)
         print(json.dumps(rec))
 

@@ -8,6 +8,7 @@
 #   bench   the C4 bench line (and BENCH_CFGS configs)
 #   prof    rocprofv3 kernel stats of the C4 bench (TAG names the profiles)
 #   pmc     PMC passes of the C4 bench (scripts/pmc_kernels.sh)
+#   phases  scripts/kernel_phases.py on the SPAI_PROF variant (build/variants/libspai_prof.so)
 #   qrbench scripts/qr_fill_bench.py (the cached QR fill alone: M stored or not, batch sizes)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -52,6 +53,9 @@ for st in ${STEPS:-tests bench}; do
     qrbench)
       timeout -k 10 300 python scripts/qr_fill_bench.py --config ${QR_CFG:-c4} > $O/qr_fill_bench.log 2>&1 || { tail -20 $O/qr_fill_bench.log; exit 1; }
       cat $O/qr_fill_bench.log | grep '^{' ;;
+    phases)
+      SPAI_LIB_VARIANT=libspai_prof.so timeout -k 10 300 python scripts/kernel_phases.py > $O/phases.log 2>&1 || { tail -20 $O/phases.log; exit 1; }
+      cat $O/phases.log ;;
     *) echo "unknown step $st"; exit 2 ;;
   esac
 done

@@ -865,6 +865,47 @@ def test_residual_lines_gram_cache_bit_identical(geom, mdt):
     np.testing.assert_allclose(parts.cpu().numpy(), got.cpu().numpy(), rtol=1e-13)
 
 
+def test_residual_lines_gram_noninteger_stencil_bit_identical():
+    """the Gram-cached residual on a stencil with non-integer fp64 values (its Gram cache
+    stays fp64, compact_gram=False, and is not fp32-exact): spai_residual_lines_gram with the cache's
+    dictionary (25 distinct entries, the fp64 16-byte entry loads) against the index-matching kernel
+    bit for bit — the cache's products must be summed in line_gram's order — and against scipy."""
+    from gflownet_spai_amd import PreconditionerEnv, kernels, poisson_2d
+    g = 40
+    base = poisson_2d(g, torch.float64).coalesce()
+    r, c = base.indices()
+    n = g * g
+    # a translation-invariant 5-point stencil with unequal, non-integer coefficients
+    dr, dc = r // g - c // g, r % g - c % g
+    f64 = lambda x: torch.full(r.shape, x, dtype=torch.float64)  # (fp64 values, none exact in fp32)
+    v = torch.where(r == c, f64(4.37), torch.where(dr == 0, torch.where(dc > 0, f64(-1.13), f64(-0.91)),
+                                                   torch.where(dr > 0, f64(-1.27), f64(-0.79))))
+    assert not torch.equal(v.float().double(), v)
+    A = torch.sparse_coo_tensor(base.indices(), v, (n, n))
+    env = PreconditionerEnv(n, A, A, side="AM", fill="lsq", compact_gram=False)
+    assert env.gram.dtype == torch.float64
+    gram = kernels.cache_dict(env.gram, n)
+    assert isinstance(gram, kernels.CacheDict) and gram.entries == 25
+    W = env.pattern.width
+    pat = env.pattern.idx.cpu().numpy()
+    rng = np.random.default_rng(5)
+    B = 8
+    idx = np.repeat(pat[None], B, 0).copy()
+    idx[rng.random(idx.shape) < 0.3] = -1
+    val = torch.from_numpy(rng.standard_normal((B, n, W)))
+    ti = torch.from_numpy(idx).to(DEV)
+    ref = kernels.residual_lines(ti, val.to(DEV), env.a_lines)
+    got = kernels.residual_lines(ti, val.to(DEV), env.a_lines, gram=gram, pattern=env.pattern)
+    assert torch.equal(got, ref)
+    Asp = sp.csr_matrix((v.numpy(), (r.numpy(), c.numpy())), shape=(n, n))
+    I = sp.identity(n, format="csr")
+    for b in (0, 5):
+        ok = idx[b] >= 0
+        lines, _ = np.nonzero(ok)
+        M = sp.csr_matrix((val[b].numpy()[ok], (idx[b][ok], lines)), shape=(n, n))
+        assert float(got[b]) == pytest.approx(sp.linalg.norm(Asp @ M - I) ** 2, rel=1e-12)
+
+
 @pytest.mark.parametrize("kind", ["2d_lsq", "2d_copy", "3d_axial", "3d_axial_f64"])
 def test_gram_dict_is_bit_identical(kind):
     # (the env holds 5/7-wide Gram caches in full; the dictionary is built here explicitly)

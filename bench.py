@@ -448,16 +448,16 @@ def main():
             return
         m = env.last_m  # columns: [B, this shard's lines, W] of EVERY candidate; slices: the same B on every rank
         if args.assemble == "best":  # the candidate with the highest reward: the preconditioner kept
-            m = m.index_select(0, torch.argmax(log.rewards_all).view(1))
-        gather.start(m)
+            gather.start(m, rows=torch.argmax(log.rewards_all).view(1))
+        else:
+            gather.start(m)
 
     phases = model.rollout_phases()
 
     def eager_step():
         st = {"s0": s0}
-        for i, (fn, coll) in enumerate(phases):
-            with kernels._timed(f"phase{i}_{fn.__name__.strip('_')}"):
-                fn(st)
+        for i, (fn, kind) in enumerate(phases):
+            model.run_phase(fn, kind, st, timer=f"phase{i}_{fn.__name__.strip('_')}")
         with kernels._timed("assemble"):
             assemble(st["log"])
         return st["log"]
@@ -512,30 +512,77 @@ def main():
             barrier()
             st = {"s0": s0}
             program, pool, run = [], None, []
-            for fn, coll in phases + [(None, True)]:
-                if fn is not None and not coll:
-                    run.append(fn)
+            cur = torch.cuda.current_stream(dev)
+
+            def capture(run):
+                """One graph of consecutive device phases; its program entry keeps the first phase's
+                stream order (kind "side": replayed on the model's side stream, forked from the
+                current one; "join": after the side stream's work)."""
+                nonlocal pool
+                kind = run[0][1]
+                g = torch.cuda.CUDAGraph()
+                if dist_on:  # no collective of the previous eager phase still in flight on RCCL's stream
+                    torch.cuda.synchronize()
+                # a side segment runs beside later main segments: its own memory pool (graphs that
+                # share a pool may reuse each other's freed blocks, safe only when replayed in order)
+                gp = None if kind == "side" else pool
+                # thread_local: a HIP call from an RCCL helper thread cannot invalidate this capture
+                with torch.cuda.graph(g, pool=gp, capture_error_mode="thread_local" if dist_on else "global"):
+                    for f, _k in run:
+                        f(st)
+                if kind != "side":
+                    pool = g.pool()
+                if kind == "side":
+                    sstream = model._side_stream(dev)
+
+                    def rep():
+                        sstream.wait_stream(cur)
+                        with torch.cuda.stream(sstream):
+                            g.replay()
+                    return rep
+                if kind == "join":
+                    sstream = model._side_stream(dev)
+
+                    def rep():
+                        cur.wait_stream(sstream)
+                        g.replay()
+                    return rep
+                return g.replay
+
+            # segments: maximal runs of device phases, cut at every collective, around every "side"
+            # phase and before every "join" phase
+            for fn, kind in phases + [(None, True)]:
+                if fn is not None and kind is not True and kind != "side" and not (kind == "join" and run):
+                    run.append((fn, kind))
                     continue
                 if run:
-                    g = torch.cuda.CUDAGraph()
-                    if dist_on:  # no collective of the previous eager phase still in flight on RCCL's stream
-                        torch.cuda.synchronize()
-                    # thread_local: a HIP call from an RCCL helper thread cannot invalidate this capture
-                    with torch.cuda.graph(g, pool=pool, capture_error_mode="thread_local" if dist_on else "global"):
-                        for f in run:
-                            f(st)
-                    pool = g.pool()
-                    program.append(g.replay)
+                    program.append(("graph:" + "+".join(f.__name__.strip("_") for f, _k in run), capture(run)))
                     run = []
-                if fn is not None:
+                if fn is None:
+                    break
+                if kind is True:
                     fn(st)  # a collective, eagerly (allocates its persistent buffers before the next capture)
-                    program.append(lambda f=fn: f(st))
+                    program.append((fn.__name__.strip("_"), lambda f=fn: f(st)))
+                elif kind == "side":
+                    program.append(("graph(side):" + fn.__name__.strip("_"), capture([(fn, kind)])))
+                else:  # "join" opens the next segment
+                    run.append((fn, kind))
             glog = st["log"]
 
-            def step():
-                for p in program:
-                    p()
-                assemble(glog)
+            def step(host=None):
+                for name, p in program:
+                    if host is None:
+                        p()
+                    else:  # host issue time per program entry (diagnostic pass)
+                        t = time.perf_counter()
+                        p()
+                        host.setdefault(name, []).append(time.perf_counter() - t)
+                if host is None:
+                    assemble(glog)
+                else:
+                    t = time.perf_counter()
+                    assemble(glog)
+                    host.setdefault("assemble", []).append(time.perf_counter() - t)
                 return glog
 
             for _ in range(max(1, args.warmup)):
@@ -543,7 +590,7 @@ def main():
             # a step without collectives (one GPU): spg consecutive steps in ONE graph, so the
             # ~12 us between two graph launches is paid once per spg steps (every step is still a
             # whole sample_states: its own select, sort, fill and Log, its own Philox stream id)
-            spg = max(1, args.steps_per_graph) if all(not c for _, c in phases) else 1
+            spg = max(1, args.steps_per_graph) if all(not k for _, k in phases) else 1
             while args.steps % spg:  # the largest count <= --steps-per-graph that divides the timed steps
                 spg -= 1
             if spg > 1:
@@ -594,6 +641,15 @@ def main():
             barrier()
             dt_noasm = (time.perf_counter() - t0) / args.steps
             do_assemble[0] = True
+        host_us = None
+        if use_graph and dist_on:  # host issue time of each program entry (a pass after the timed steps)
+            host = {}
+            for _ in range(k_eager):
+                step(host)
+            if gather is not None:
+                gather.wait()
+            barrier()
+            host_us = {k: 1e6 * float(np.mean(v)) for k, v in host.items()}
     if dist_on:
         t = torch.tensor([dt, dt_eager, dt_noasm], device=dev, dtype=torch.float64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
@@ -738,6 +794,9 @@ def main():
                                      for k, v in phase_ms_max.items() if k.endswith(key)}
             if "line_gather_wait" in phase_ms_max:
                 out["collectives_ms"]["line_gather_wait"] = phase_ms_max["line_gather_wait"]
+            if host_us is not None:  # rank 0's host time to issue each graph replay / eager collective
+                out["host_issue_us"] = host_us
+                out["host_issue_us_total"] = sum(host_us.values())
             out["world_size"] = torch.distributed.get_world_size()
             out["backend"] = torch.distributed.get_backend()
             if args.backend == "nccl":

@@ -21,7 +21,7 @@ if os.environ.get("SPAI_LIB_VARIANT"):  # A/B timing of kernel variants built un
 SPAI_OK, SPAI_ERR_INVALID, SPAI_ERR_HIP, SPAI_ERR_UNSUPPORTED = 0, 1, 2, 3
 FILL_COPY, FILL_LSQ = 0, 1  # (the Householder-QR fill has its own entry point)
 DTYPE_F32, DTYPE_F64 = 0, 1
-ABI_VERSION = 19
+ABI_VERSION = 20
 RES2_LIMBS = 8  # SPAI_RES2_LIMBS
 
 _c_i32, _c_i64, _c_u64, _c_sz, _c_p = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_size_t, ctypes.c_void_p
@@ -102,6 +102,7 @@ SIGNATURES = {
                                           _c_i32, _c_i32, _c_p, _c_i32, _c_i32, _c_p, _c_i32, _c_p, _c_sz, _c_p]),
     "spai_set_sort_blocks": (ctypes.c_int, [_c_i32]),
     "spai_bitmap_pack": (ctypes.c_int, [_c_i32, _c_i32, _c_p, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_i64, _c_p, _c_p]),
+    "spai_window_pack": (ctypes.c_int, [_c_i32, _c_i32, _c_p, _c_i32, _c_p, _c_p, _c_p, _c_p, _c_i64, _c_p, _c_p]),
     "spai_qr_cache_bytes": (_c_sz, [_c_i32, _c_i32, _c_i32]),
     "spai_qr_factor": (ctypes.c_int, [_c_i32, _c_i32, _c_p, _c_p, _c_i32, _c_p, _c_p, _c_i32, _c_i32, _c_p, _c_sz,
                                       _c_p]),

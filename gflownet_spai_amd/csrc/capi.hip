@@ -82,6 +82,6 @@ extern "C" int spai_kernel_timer_read(int32_t kernel, int32_t* count, double* av
   return SPAI_OK;
 }
 
-extern "C" int spai_abi_version(void) { return 19; }
+extern "C" int spai_abi_version(void) { return 20; }
 
 extern "C" const char* spai_last_error(void) { return spai::g_last_error.c_str(); }

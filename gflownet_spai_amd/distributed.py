@@ -135,9 +135,13 @@ class LineGather:
             self.work.wait()
             self.work = None
 
-    def start(self, m_local: torch.Tensor) -> "LineGather":
+    def start(self, m_local: torch.Tensor, rows: torch.Tensor | None = None) -> "LineGather":
+        """rows: optional int64 index tensor on the device — gather only those candidates of
+        m_local (copied straight into the send buffer, no intermediate)."""
         world = dist.get_world_size(self.group)
         B, n_loc, W = m_local.shape
+        if rows is not None:
+            B = rows.numel()
         self.rng = [shard_lines(self.n, r, world, self.align) for r in range(world)]
         chunk = max(e - b for b, e in self.rng)
         from .kernels import _timed
@@ -146,7 +150,12 @@ class LineGather:
         if self.buf is None or self.buf.shape != (B, chunk, W) or self.buf.dtype != m_local.dtype:
             self.buf = torch.zeros(B, chunk, W, dtype=m_local.dtype, device=m_local.device)  # padding rows stay 0
             self.out = torch.empty(world, B, chunk, W, dtype=m_local.dtype, device=m_local.device)
-        self.buf[:, :n_loc].copy_(m_local)
+        if rows is None:
+            self.buf[:, :n_loc].copy_(m_local)
+        elif n_loc == chunk:
+            torch.index_select(m_local, 0, rows, out=self.buf)
+        else:
+            self.buf[:, :n_loc].copy_(m_local.index_select(0, rows))
         self.work = all_gather_into_(self.out.view(-1), self.buf.view(-1), self.group, async_op=True)
         return self
 
@@ -189,13 +198,22 @@ class PackPlan:
     spai_hip.h spai_bitmap_pack); rank r receives [P * bl, wq[r] + 1] and its fill reads the bits
     through ``local_pattern(env, r)``: the pattern with each of r's action ids replaced by its
     position in r's segment.  Every rank receives exactly nnz(shard) bits per candidate for any
-    numbering of the matrix (action ids are raw COO positions, preconditioner.py:23-25)."""
+    numbering of the matrix (action ids are raw COO positions, preconditioner.py:23-25).
 
-    def __init__(self, env, world: int):
+    ``mode="window"`` (spai_window_pack; "auto" picks it when the windows total <= 1.25x the
+    packed words, as for a stencil in row-major raw order, where rank q's ids span its rows +- the
+    stencil's reach): q receives the contiguous bitmap words [lo[q], lo[q] + wq[q]) of its ids,
+    copied without the gather, and reads them through ids shifted by 32 lo[q]."""
+
+    WINDOW_SLACK = 1.25
+
+    def __init__(self, env, world: int, mode: str = "auto"):
+        if mode not in ("auto", "window", "gather"):
+            raise ValueError(f"mode must be auto, window or gather, not {mode!r}")
         act = env.pattern.act
         dev = act.device
         self.world = world
-        ids, seg, self.wq, self.lines = [], [0], [], []
+        ids, seg, self.wq, self.lines, win = [], [0], [], [], []
         for q in range(world):
             b, e = shard_lines(env.matrix_size, q, world, LINE_ALIGN)
             a = act[b:e].reshape(-1)
@@ -204,9 +222,19 @@ class PackPlan:
             seg.append(seg[-1] + a.numel())
             self.wq.append((a.numel() + 31) // 32)
             self.lines.append((b, e))
+            win.append((int(a.min()) >> 5, (int(a.max()) >> 5) + 1) if a.numel() else (0, 0))
         self.ids = torch.cat(ids).to(torch.int32).contiguous()
         self.seg = torch.tensor(seg, dtype=torch.int64, device=dev)
         self.max_seg = max(seg[q + 1] - seg[q] for q in range(world))
+        if mode == "auto":
+            mode = "window" if sum(h - l for l, h in win) <= self.WINDOW_SLACK * sum(self.wq) else "gather"
+        self.mode = mode
+        if mode == "window":
+            self.lo_words = [l for l, _ in win]
+            self.wq = [h - l for l, h in win]
+            self.lo = torch.tensor(self.lo_words, dtype=torch.int64, device=dev)
+            self.span = torch.tensor(self.wq, dtype=torch.int64, device=dev)
+            self.max_span = max(self.wq)
         self._off = {}
         self._local = {}
 
@@ -231,16 +259,24 @@ class PackPlan:
             act = env.pattern.act.clone()
             blk = act[b:e]
             ok = blk >= 0
-            loc = torch.cumsum(ok.reshape(-1).to(torch.int64), 0).view_as(blk) - 1
+            if self.mode == "window":  # bit positions within the rank's word window
+                loc = blk.to(torch.int64) - 32 * self.lo_words[rank]
+            else:  # positions in the rank's line-major segment
+                loc = torch.cumsum(ok.reshape(-1).to(torch.int64), 0).view_as(blk) - 1
             act[b:e] = torch.where(ok, loc.to(torch.int32), blk)
             self._local[rank] = dataclasses.replace(env.pattern, act=act)
         return self._local[rank]
 
 
 def pack_bits_reference(removed: torch.Tensor, counts: torch.Tensor, plan: "PackPlan", bl: int) -> torch.Tensor:
-    """torch restatement of spai_bitmap_pack (test infrastructure: the CPU gloo tests build the
-    send buffer with it; the GPU tests check the kernel against it)."""
+    """torch restatement of spai_bitmap_pack / spai_window_pack (test infrastructure: the CPU gloo
+    tests build the send buffer with it; the GPU tests check the kernels against it)."""
     out = []
+    if plan.mode == "window":
+        for q in range(plan.world):
+            w = removed.view(torch.int32)[:, plan.lo_words[q]:plan.lo_words[q] + plan.wq[q]]
+            out.append(torch.cat([w, counts.view(bl, 1).to(torch.int32)], 1).reshape(-1))
+        return torch.cat(out)
     seg = plan.seg.tolist()
     for q in range(plan.world):
         a = plan.ids[seg[q]:seg[q + 1]].long().to(removed.device)

@@ -15,6 +15,7 @@ Then ``env.update`` semantics: removal bitmaps -> fill -> residual -> rewards.
 """
 from __future__ import annotations
 
+import contextlib
 from typing import List
 
 import torch
@@ -194,8 +195,8 @@ class GFlowNet(nn.Module):
         """gflownet.py:125-197: sample B trajectories from the initial states, score them, log."""
         if self.mode == "throughput":
             st = {"s0": s0}
-            for phase, _ in self.rollout_phases():
-                phase(st)
+            for phase, kind in self.rollout_phases():
+                self.run_phase(phase, kind, st)
             return st["log"] if return_log else None
         env = self.env
         B = len(s0)
@@ -246,14 +247,35 @@ class GFlowNet(nn.Module):
     # Philox stream id lives on the device and the select phase advances it, so a replayed graph
     # draws a fresh rollout.  Every phase takes the step's state dict (``{"s0": s0}`` to start;
     # the last phase leaves the Log in ``st["log"]``).
+    # Phase kinds: False = device work on the current stream; True = a collective (eager under
+    # bench.py's graphs); "side" = device work on the side stream, forked from the current stream at
+    # its position; "join" = device work on the current stream after the side stream's work.  A
+    # "side" phase is a graph segment of its own, replayed on the side stream, so it runs beside the
+    # collectives and device phases between it and the join.
     def rollout_phases(self) -> list:
-        """[(phase, is_collective)] in execution order."""
+        """[(phase, kind)] in execution order."""
         if self.split == "columns":
-            return [(self._c_begin, False), (self._c_send, True), (self._c_order, False), (self._c_recv, True),
-                    (self._c_fill, False), (self._c_reduce, True), (self._c_end, False)]
+            return [(self._c_select, False), (self._c_pack, False), (self._c_order, "side"), (self._c_send, True),
+                    (self._c_recv, True), (self._c_fill, False), (self._c_reduce, True), (self._c_end, "join")]
         if self.split == "slices":
             return [(self._begin, False), (self.rollout_exchange, True), (self._end, False)]
         return [(self._begin, False), (self.rollout_exchange, False), (self._end, False)]
+
+    def run_phase(self, fn, kind, st: dict, timer: str | None = None) -> None:
+        """Run one phase eagerly with its kind's stream order (timer: kernels._timed name, recorded
+        on the stream the phase runs on)."""
+        tm = kernels._timed(timer) if timer else contextlib.nullcontext()
+        if kind == "side":
+            dev = st["dev"]
+            side = self._side_stream(dev)
+            side.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(side), tm:
+                fn(st)
+            return
+        if kind == "join":
+            torch.cuda.current_stream(st["dev"]).wait_stream(self._side_stream(st["dev"]))
+        with tm:
+            fn(st)
 
     def _fork_fill(self, st: dict) -> None:
         """fill + rewards of all lines on the side stream, after everything the current stream has
@@ -272,7 +294,11 @@ class GFlowNet(nn.Module):
 
     def _side_stream(self, dev):
         if self._side is None or self._side.device != dev:
-            self._side = torch.cuda.Stream(dev)
+            # high priority: HIP multiplexes streams onto GPU_MAX_HW_QUEUES (4) hardware queues, and a
+            # default-priority stream can land on the current stream's queue, where its work runs
+            # strictly after everything queued before it (measured: the columns split's sort, no
+            # overlap); a high-priority stream gets a queue of its own
+            self._side = torch.cuda.Stream(dev, priority=-1)
         return self._side
 
     def _counter(self, dev):
@@ -360,7 +386,7 @@ class GFlowNet(nn.Module):
         st["log"] = log
 
     # the columns split: rollouts by candidates, fill + residual by column shards
-    def _c_begin(self, st: dict) -> None:
+    def _c_select(self, st: dict) -> None:
         env, s0 = self.env, st["s0"]
         rank, world, group = self.shard
         bl = len(s0)
@@ -373,12 +399,17 @@ class GFlowNet(nn.Module):
                                                      self._counter(dev), out=sel)
         if isinstance(lmax, kernels.PendingMax):
             lmax = lmax.out  # written by the select
-        plan = env.pack_plan(world)
-        send = self._buf("send", (plan.send_words(bl),), torch.int32, dev)
-        kernels.bitmap_pack(removed, counts, plan, out=send)  # line-major packed bits per destination
-        recv = self._buf("recv", (world * bl, plan.wq[rank] + 1), torch.int32, dev)
         st.update(B=bl, E=E, logits=logits, alpha=alpha, lg=lg, lmax=lmax, removed=removed, counts=counts, ws=ws,
-                  send=send, recv=recv, plan=plan, part=(rank, world, group))
+                  dev=dev, part=(rank, world, group))
+
+    def _c_pack(self, st: dict) -> None:
+        rank, world, _ = st["part"]
+        bl, dev = st["B"], st["dev"]
+        plan = self.env.pack_plan(world)
+        send = self._buf("send", (plan.send_words(bl),), torch.int32, dev)
+        kernels.bitmap_pack(st["removed"], st["counts"], plan, out=send)  # line-major packed bits per destination
+        recv = self._buf("recv", (world * bl, plan.wq[rank] + 1), torch.int32, dev)
+        st.update(send=send, recv=recv, plan=plan)
 
     def _c_send(self, st: dict) -> None:
         from .distributed import exchange_packed
@@ -386,7 +417,7 @@ class GFlowNet(nn.Module):
         st["a2a"] = exchange_packed(st["send"], st["recv"], st["plan"], st["B"], rank, group, async_op=True)
 
     def _c_order(self, st: dict) -> None:
-        # this rank's own trajectories, while the bitmaps are in flight
+        # this rank's own trajectories (side stream), beside the exchange and the fill
         B, lg, lmax, ws = st["B"], st["lg"], st["lmax"], st["ws"]
         actions, fwd = kernels.rollout_sort(lg, B, lmax, ws, 0, 1)
         st["traj"] = (actions, fwd, kernels.rollout_finish(lg, B, lmax, st["counts"], ws, actions, fwd, 0, 1))

@@ -587,7 +587,8 @@ def fill_residual_qr(pattern: Lines, a_lines: Lines, max_rows: int, removed: tor
 def bitmap_pack(removed: torch.Tensor, counts: torch.Tensor, plan, out: torch.Tensor | None = None) -> torch.Tensor:
     """The columns split's all_to_all send buffer (spai_bitmap_pack): per destination q of
     ``plan`` (distributed.PackPlan) and candidate b, b's removal bits of q's line-major action ids
-    packed 32 per word, then counts[b]; int32 [plan.send_words(bl)]."""
+    packed 32 per word (or, plan.mode "window", spai_window_pack: q's contiguous word window), then
+    counts[b]; int32 [plan.send_words(bl)]."""
     _lib.require_device(removed)
     bl, words = removed.shape
     off, total = plan.out_off(bl)
@@ -597,11 +598,18 @@ def bitmap_pack(removed: torch.Tensor, counts: torch.Tensor, plan, out: torch.Te
         raise ValueError(f"out must be a contiguous int32 buffer of {total} words")
     if removed.stride(1) != 1 or counts.dtype != torch.int32:
         raise ValueError("removed rows must be contiguous and counts int32")
+    if plan.mode == "window" and max(lo + w for lo, w in zip(plan.lo_words, plan.wq)) > words:
+        raise ValueError("the plan's word windows exceed the bitmap rows")
     with _timed("bitmap_pack"):
-        st = _l().spai_bitmap_pack(plan.world, bl, _lib.ptr(removed), removed.stride(0), _lib.ptr(counts),
-                                   _lib.ptr(plan.ids), _lib.ptr(plan.seg), _lib.ptr(off), plan.max_seg,
-                                   _lib.ptr(out), _lib.stream_ptr(removed.device))
-    _lib.check(st, "spai_bitmap_pack")
+        if plan.mode == "window":  # contiguous word windows (spai_window_pack)
+            st = _l().spai_window_pack(plan.world, bl, _lib.ptr(removed), removed.stride(0), _lib.ptr(counts),
+                                       _lib.ptr(plan.lo), _lib.ptr(plan.span), _lib.ptr(off), plan.max_span,
+                                       _lib.ptr(out), _lib.stream_ptr(removed.device))
+        else:
+            st = _l().spai_bitmap_pack(plan.world, bl, _lib.ptr(removed), removed.stride(0), _lib.ptr(counts),
+                                       _lib.ptr(plan.ids), _lib.ptr(plan.seg), _lib.ptr(off), plan.max_seg,
+                                       _lib.ptr(out), _lib.stream_ptr(removed.device))
+    _lib.check(st, "spai_bitmap_pack" if plan.mode != "window" else "spai_window_pack")
     return out
 
 

@@ -376,6 +376,16 @@ int spai_fill_lines_gram_dict(int32_t fill_mode, int32_t n, int32_t line_begin, 
 int spai_bitmap_pack(int32_t P, int32_t bl, const uint32_t* removed, int32_t words, const int32_t* counts,
                      const int32_t* ids, const int64_t* seg, const int64_t* out_off, int64_t max_seg, uint32_t* out,
                      void* stream);
+/* The same send buffer for a numbering whose shards' action ids lie in compact bitmap windows
+ * (a stencil in row-major raw order: rank q's ids span its rows +- the stencil's reach, about 1/P
+ * of the bitmap), without the gather (ABI 20): q's block at out + out_off[q] is [bl][span[q] + 1]
+ * words = removed[b][lo[q] .. lo[q] + span[q]) (row stride `words`), then counts[b].  The
+ * receiver reads bit (a - 32 lo[rank]) of its rows for action id a.  lo, span, out_off: [P] int64
+ * in device memory; max_span = max span[q] <= words.  distributed.PackPlan picks this layout when
+ * the windows total <= 1.25x the packed words. */
+int spai_window_pack(int32_t P, int32_t bl, const uint32_t* removed, int32_t words, const int32_t* counts,
+                     const int64_t* lo, const int64_t* span, const int64_t* out_off, int64_t max_span, uint32_t* out,
+                     void* stream);
 
 /* ---------------------------------------------------------------- forward policy
  * logits[a] = fc(mean_pool(relu(GATv2_2(relu(GATv2_1(x))))))[a] for a < num_actions and

@@ -61,18 +61,22 @@ def _env(kind):
     return PreconditionerEnv(A.shape[0], P, A, side="AM", fill="lsq", keep_m=True), P, A
 
 
-@pytest.mark.parametrize("kind,P,bl", [("2d", 2, 3), ("2d", 3, 2), ("2d", 8, 1), ("3d", 3, 2),
-                                       ("c4", 2, 1), ("c4", 4, 1), ("c4", 8, 1), ("c4", 3, 2),
-                                       ("thermal", 8, 1), ("thermal", 3, 2)])
-def test_columns_split_in_process_bit_identical(kind, P, bl):
+@pytest.mark.parametrize("kind,P,bl,mode", [("2d", 2, 3, "auto"), ("2d", 3, 2, "auto"), ("2d", 8, 1, "auto"),
+                                            ("3d", 3, 2, "auto"), ("c4", 2, 1, "auto"), ("c4", 4, 1, "auto"),
+                                            ("c4", 8, 1, "auto"), ("c4", 3, 2, "auto"), ("thermal", 8, 1, "auto"),
+                                            ("thermal", 3, 2, "auto"), ("2d", 3, 2, "gather"), ("c4", 8, 1, "gather"),
+                                            ("c4", 3, 2, "gather")])
+def test_columns_split_in_process_bit_identical(kind, P, bl, mode):
     """P ranks in one process (C4 geometry included: 1024^2, E = 5,238,784, P = 2/4/8 with one
     candidate per rank, and P = 3 whose shards are not equal; and the C5 stand-in's randomly
     PERMUTED numbering, whose action ids scatter every shard over the whole bitmap): the packed
     line-major exchange (spai_bitmap_pack == its torch restatement), 256-line shards and the
     shard-local action tables reproduce the one-process batch bit for bit, and every rank receives
-    exactly nnz(shard) bits per candidate (~1/P of a bitmap) whatever the numbering."""
+    exactly nnz(shard) bits per candidate (~1/P of a bitmap) whatever the numbering.  mode "auto"
+    picks the word windows (spai_window_pack, no gather) for the stencil numberings and the packed
+    gather for the permuted one; "gather" forces the packed exchange on a stencil."""
     from gflownet_spai_amd import kernels
-    from gflownet_spai_amd.distributed import LINE_ALIGN, pack_bits_reference, shard_lines, word_spans
+    from gflownet_spai_amd.distributed import LINE_ALIGN, PackPlan, pack_bits_reference, shard_lines, word_spans
     env, _, _ = _env(kind)
     n, E = env.matrix_size, env.num_actions - 1
     words = (E + 31) // 32
@@ -86,7 +90,13 @@ def test_columns_split_in_process_bit_identical(kind, P, bl):
     alpha = torch.tensor(0.4)
     rw1 = env.rewards_from_res2(res2_1, counts1, alpha)
     # P ranks: own candidates, then the all_to_all of packed rows + counts
-    plan = env.pack_plan(P)
+    plan = PackPlan(env, P, mode)
+    # auto: windows for the 2-D stencils (the 12^3 3-D pattern's halo is wide next to its shards:
+    # either layout), the gather for the permuted numbering
+    want = mode if mode != "auto" else {"thermal": "gather", "3d": plan.mode}.get(kind, "window")
+    assert plan.mode == want
+    if mode == "auto":
+        assert env.pack_plan(P).mode == plan.mode  # the plan the GFlowNet step uses
     sends = []
     for r in range(P):
         sel = torch.empty(bl * words + bl, dtype=torch.int32, device=DEV)
@@ -97,9 +107,13 @@ def test_columns_split_in_process_bit_identical(kind, P, bl):
         sends.append(send)
     nnz = [int(plan.seg[q + 1] - plan.seg[q]) for q in range(P)]
     assert sum(nnz) == E
-    for q in range(P):  # exactly the shard's bits: ~1/P of a bitmap per candidate
+    for q in range(P):  # exactly the shard's bits (windows: within 1.25x of them): ~1/P of a bitmap per candidate
         b, e = shard_lines(n, q, P, LINE_ALIGN)
-        assert plan.wq[q] == -(-nnz[q] // 32) and nnz[q] == int((env.pattern.act[b:e] >= 0).sum())
+        assert nnz[q] == int((env.pattern.act[b:e] >= 0).sum())
+        if plan.mode == "gather":
+            assert plan.wq[q] == -(-nnz[q] // 32)
+    if plan.mode == "window":
+        assert sum(plan.wq) <= 1.25 * sum(-(-x // 32) for x in nnz)
     if kind == "thermal":  # the word windows of this numbering would be whole bitmaps
         spans = word_spans(env, P)
         assert all(w1 - w0 > 0.95 * words for w0, w1 in spans)

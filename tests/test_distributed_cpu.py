@@ -67,6 +67,8 @@ def _worker(rank, world, port, q):
         lgth.start(ma)
         lgth.start(ma + 1)
         out["m_pipe"] = lgth.result().numpy()
+        lgth.start(ma + 1, rows=torch.tensor([1]))  # one candidate, selected into the send buffer
+        out["m_row"] = lgth.result().numpy()
         out["rewards"] = gather_rewards(torch.arange(B, dtype=torch.float64) + 10 * rank).numpy()
         # the slices split's exchange: each part fills the bucket weight sums and winner counts
         # of its own bucket range (zero elsewhere, the exchange array's [B][2][kMaxB] layout)
@@ -84,6 +86,7 @@ def _worker(rank, world, port, q):
         out["r2"] = [O.fixed_value(row) for row in summed.numpy()]
         out["bs"] = bs.numpy()
         out["cols"] = _columns_exchange(rank, world)
+        out["cols_win"] = _columns_exchange(rank, world, mode="auto")
         # the samples split: 2 local candidates per rank, global best's M reduced to rank 0
         rw = torch.tensor([[0.5, 2.5], [1.5, -1.0]], dtype=torch.float64)[rank]
         ml = torch.arange(2 * 3 * 4, dtype=torch.float64).view(2, 3, 4) + 100 * rank
@@ -137,18 +140,19 @@ def _columns_fixture(world, bl, perm_seed=None):
     return env, words, torch.from_numpy(bits), torch.from_numpy(counts)
 
 
-def _columns_exchange(rank, world, bl=3, perm_seed=None):
+def _columns_exchange(rank, world, bl=3, perm_seed=None, mode="gather"):
     """The columns split's all_to_all: rank r holds candidates r*bl .. and sends every rank q the
     bits of q's line-major action ids packed 32 per word, plus the counts (spai_bitmap_pack,
-    restated in torch); it receives every candidate's packed row of its own shard."""
+    restated in torch); it receives every candidate's packed row of its own shard.  mode="auto"
+    on a stencil numbering: the word windows instead (spai_window_pack)."""
     env, words, bits, counts = _columns_fixture(world, bl, perm_seed)
-    plan = PackPlan(env, world)
+    plan = PackPlan(env, world, mode)
     mine = slice(rank * bl, (rank + 1) * bl)
     send = pack_bits_reference(bits[mine], counts[mine], plan, bl)
     assert send.numel() == plan.send_words(bl)
     recv = torch.full((world * bl, plan.wq[rank] + 1), -7, dtype=torch.int32)
     exchange_packed(send, recv, plan, bl, rank).wait()
-    return plan.wq, recv.numpy()
+    return plan.wq, recv.numpy(), plan.mode, getattr(plan, "lo_words", None)
 
 
 def _unpack_expected(env, bits, lines):
@@ -214,6 +218,7 @@ def test_world2_column_sharded_reward_and_assembly():
         blocks.append(torch.arange(2 * (b1a - b0a) * 5, dtype=torch.float32).view(2, b1a - b0a, 5) + 1000 * q_ + 1)
     for rank in (0, 1):  # the second of two pipelined gathers, on every rank
         assert np.array_equal(res[rank]["m_pipe"], torch.cat(blocks, 1).numpy())
+        assert np.array_equal(res[rank]["m_row"], torch.cat(blocks, 1).numpy()[1:2])
     full_bs, partials = _split_fixture()
     acts, fwd, _, _ = _slices_fixture()
     env, words, bits, counts = _columns_fixture(2, 3)
@@ -223,13 +228,24 @@ def test_world2_column_sharded_reward_and_assembly():
         assert np.array_equal(res[rank]["bs"], full_bs.numpy())  # bit-exact: one non-zero term each
         for b in range(3):  # exact sums: the same bits as one process summing every partial
             assert res[rank]["r2"][b] == O.fixed_sum(partials[b])
-        wq, recv = res[rank]["cols"]
+        wq, recv, mode, _ = res[rank]["cols"]
         b0, b1 = lines[rank]
         m = int((env.pattern.act[b0:b1] >= 0).sum())
-        assert wq[rank] == (m + 31) // 32 and recv.shape == (6, wq[rank] + 1)
+        assert mode == "gather" and wq[rank] == (m + 31) // 32 and recv.shape == (6, wq[rank] + 1)
         # every candidate (global order): exactly the bits of this rank's actions, line-major
         assert np.array_equal(_unpack(recv, m), _unpack_expected(env, bits, lines[rank]))
         assert np.array_equal(recv[:, -1], counts.numpy())
+        # the stencil numbering's word windows (auto -> window): the rank's contiguous bitmap words,
+        # every one of its action ids a read as bit a - 32 lo of the received rows
+        wq, recv, mode, lo = res[rank]["cols_win"]
+        assert mode == "window" and recv.shape == (6, wq[rank] + 1)
+        assert np.array_equal(recv[:, :-1], bits.numpy()[:, lo[rank]:lo[rank] + wq[rank]])
+        a = env.pattern.act[b0:b1].reshape(-1)
+        a = (a[a >= 0].long() - 32 * lo[rank]).numpy()
+        assert a.min() >= 0 and a.max() < 32 * wq[rank]
+        assert np.array_equal(_unpack(recv, 32 * wq[rank])[:, a], _unpack_expected(env, bits, lines[rank]))
+        assert np.array_equal(recv[:, -1], counts.numpy())
+        assert wq[rank] <= 1.25 * ((m + 31) // 32) + 2
         assert np.array_equal(res[rank]["slices"][0], acts.numpy())
         allr, best, mbest = res[rank]["samples"]
         np.testing.assert_array_equal(allr, [0.5, 2.5, 1.5, -1.0])
@@ -272,7 +288,7 @@ def _worker3(rank, world, port, q):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        out = {"cols": _columns_exchange(rank, world, bl=2, perm_seed=3)}
+        out = {"cols": _columns_exchange(rank, world, bl=2, perm_seed=3, mode="auto")}  # auto -> gather here
         n = 1000
         b0, b1 = shard_lines(n, rank, world, LINE_ALIGN)
         lg = LineGather(n, align=LINE_ALIGN)
@@ -301,7 +317,8 @@ def test_world3_packed_exchange_on_permuted_numbering_and_aligned_gather():
     lines = [shard_lines(env.matrix_size, r, world, LINE_ALIGN) for r in range(world)]
     spans = word_spans(env, world)
     for rank in range(world):
-        wq, recv = res[rank]["cols"]
+        wq, recv, mode, _ = res[rank]["cols"]
+        assert mode == "gather"
         m = int((env.pattern.act[lines[rank][0]:lines[rank][1]] >= 0).sum())
         assert np.array_equal(_unpack(recv, m), _unpack_expected(env, bits, lines[rank]))
         assert np.array_equal(recv[:, -1], counts.numpy())

@@ -691,8 +691,11 @@ __global__ __launch_bounds__(kQNT) void k_qr_table(int32_t entries, const double
 // is stored).  No solve and no per-line R or Q^T e held, so more blocks per CU than k_qr_solve; M
 // staged per block and stored, and the residual sums formed, exactly as k_qr_solve does (the same
 // bits as solving every (line, sample) on its own lane).
+#ifndef QR_LOOKUP_WPE
+#define QR_LOOKUP_WPE 6
+#endif
 template <int W, typename TM>
-__global__ __launch_bounds__(kQNT) __attribute__((amdgpu_waves_per_eu(6))) void k_qr_lookup(
+__global__ __launch_bounds__(kQNT) __attribute__((amdgpu_waves_per_eu(QR_LOOKUP_WPE))) void k_qr_lookup(
     int32_t line_begin, int32_t line_end, int32_t wrt, const int32_t* __restrict__ pat_act,
     const int32_t* __restrict__ line_entry, int32_t B, const uint32_t* __restrict__ removed, int32_t words,
     int32_t word_base, TM* __restrict__ m_out, double* __restrict__ partials, const char* __restrict__ mtab) {
@@ -723,58 +726,64 @@ __global__ __launch_bounds__(kQNT) __attribute__((amdgpu_waves_per_eu(6))) void 
     for (int p = 0; p < W; ++p) mt |= (int)(act[p] >= 0 && !((w[p] >> (act[p] & 31)) & 1u)) << p;
     return mt;
   };
-  uint32_t wd[W];
+  // per group of kG samples: their W * kG bitmap words in flight together, then their kG records
+  // in flight together with the next group's bitmap words, so a block waits on ~1 memory round
+  // trip per group instead of one per sample
+  constexpr int kG = 4;
+  static_assert(kQChunk % kG == 0, "whole sample groups per residual chunk");
+  uint32_t wv[kG][W];
 #pragma unroll
-  for (int p = 0; p < W; ++p) wd[p] = removed[wofs(p)];
-  u4t rc[kRW], rn[kRW];
-  {
-    const int mt = mask_of(wd);
+  for (int i = 0; i < kG; ++i)
 #pragma unroll
-    for (int k = 0; k < kRW; ++k) rc[k] = tab[mt * kRW + k];
-  }
-  if (B > 1) {
-#pragma unroll
-    for (int p = 0; p < W; ++p) wd[p] = removed[(int64_t)words + wofs(p)];
-  }
+    for (int p = 0; p < W; ++p) wv[i][p] = i < B ? removed[(int64_t)i * words + wofs(p)] : 0u;
 #pragma unroll 1
-  for (int b = 0; b < B; ++b) {
-    if (b + 1 < B) {  // the next sample's record (its words arrived during this sample's predecessor)
-      const int mt = mask_of(wd);
+  for (int b0 = 0; b0 < B; b0 += kQChunk) {
+    const int nb = min(kQChunk, B - b0);
 #pragma unroll
-      for (int k = 0; k < kRW; ++k) rn[k] = tab[mt * kRW + k];
-      if (b + 2 < B) {
+    for (int g0 = 0; g0 < kQChunk; g0 += kG) {
+      if (g0 < nb) {
+        u4t rc[kG][kRW];
 #pragma unroll
-        for (int p = 0; p < W; ++p) wd[p] = removed[(int64_t)(b + 2) * words + wofs(p)];
+        for (int i = 0; i < kG; ++i) {
+          const int mt = mask_of(wv[i]);
+#pragma unroll
+          for (int k = 0; k < kRW; ++k) rc[i][k] = g0 + i < nb ? tab[mt * kRW + k] : (u4t){0u, 0u, 0u, 0u};
+        }
+        const int bn = b0 + g0 + kG;  // the next group's first sample
+#pragma unroll
+        for (int i = 0; i < kG; ++i)
+#pragma unroll
+          for (int p = 0; p < W; ++p) wv[i][p] = bn + i < B ? removed[(int64_t)(bn + i) * words + wofs(p)] : 0u;
+#pragma unroll
+        for (int i = 0; i < kG; ++i) {
+          if (g0 + i < nb) {
+            const int b = b0 + g0 + i;
+            const TM* mv = reinterpret_cast<const TM*>(&rc[i][0]);
+            const double rs = *reinterpret_cast<const double*>(reinterpret_cast<const char*>(&rc[i][0]) + kRec - 8);
+            s_r2[g0 + i][t] = valid ? rs : 0.0;
+            TM* sm = s_m[b & 1];
+            if (valid) {
+#pragma unroll
+              for (int p = 0; p < W; ++p)
+                if (p < wrt) sm[t * wrt + p] = mv[p];
+            }
+            __syncthreads();
+            store_m_block<kQNT, W, TM>(m_out ? m_out + ((int64_t)b * nloc + (int64_t)lb * kQNT) * wrt : nullptr, sm,
+                                       nvl * wrt);
+          }
+        }
       }
     }
-    const TM* mv = reinterpret_cast<const TM*>(&rc[0]);
-    const double rs = *reinterpret_cast<const double*>(reinterpret_cast<const char*>(&rc[0]) + kRec - 8);
-    s_r2[b % kQChunk][t] = valid ? rs : 0.0;
-    {
-      TM* sm = s_m[b & 1];
-      if (valid) {
+    // the chunk's fixed-order block sums (k_qr_solve's)
+    __syncthreads();
+    for (int u = wave; u < nb; u += kQNT / 64) {
+      double acc = 0.0;
 #pragma unroll
-        for (int p = 0; p < W; ++p)
-          if (p < wrt) sm[t * wrt + p] = mv[p];
-      }
-      __syncthreads();
-      store_m_block<kQNT, W, TM>(m_out ? m_out + ((int64_t)b * nloc + (int64_t)lb * kQNT) * wrt : nullptr, sm,
-                                 nvl * wrt);
+      for (int q = 0; q < kQNT / 64; ++q) acc += s_r2[u][q * 64 + lane];
+      acc = wave_sum(acc);
+      if (lane == 0) partials[(int64_t)(b0 + u) * gridDim.x + lb] = acc;
     }
-    if (b % kQChunk == kQChunk - 1 || b == B - 1) {  // the chunk's fixed-order block sums (k_qr_solve's)
-      const int c0b = b - b % kQChunk, nb = b - c0b + 1;
-      __syncthreads();
-      for (int u = wave; u < nb; u += kQNT / 64) {
-        double acc = 0.0;
-#pragma unroll
-        for (int q = 0; q < kQNT / 64; ++q) acc += s_r2[u][q * 64 + lane];
-        acc = wave_sum(acc);
-        if (lane == 0) partials[(int64_t)(c0b + u) * gridDim.x + lb] = acc;
-      }
-      __syncthreads();
-    }
-#pragma unroll
-    for (int k = 0; k < kRW; ++k) rc[k] = rn[k];
+    __syncthreads();
   }
 }
 

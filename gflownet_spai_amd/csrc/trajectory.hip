@@ -663,8 +663,11 @@ void k_tile(const float* __restrict__ rr, const float* __restrict__ ww, int64_t 
   //   s_r0: the slot path's record window
   //   s_r1: the compacted winner list: keys, weights, tile-local ids; once the list is read into
   //         registers, the fixed-point bucket sums (slot path: those sums, then the window's weights)
-  __shared__ __attribute__((aligned(16))) uint64_t s_r0[kWin];
-  __shared__ __attribute__((aligned(16))) uint32_t s_r1[2 * kList + kList / 2];
+  // one array: the compact path's output staging (3 words per winner) spans both regions
+  __shared__ __attribute__((aligned(16))) uint32_t s_r01[2 * kWin + 2 * kList + kList / 2];
+  static_assert(2 * kWin + 2 * kList + kList / 2 >= 3 * kList, "compact staging fits the two regions");
+  uint64_t* s_r0 = reinterpret_cast<uint64_t*>(s_r01);
+  uint32_t* s_r1 = s_r01 + 2 * kWin;
   static_assert(kWin <= 2 * kList + kList / 2 && kList % 2 == 0, "LDS region sizes");
   uint64_t* w_rec = s_r0;  // one window of the slot path's grouped output
   float* w_log = reinterpret_cast<float*>(s_r1);
@@ -964,14 +967,25 @@ void k_tile(const float* __restrict__ rr, const float* __restrict__ ww, int64_t 
   PROF(3)
   uint3* st = reinterpret_cast<uint3*>(staging) + ((int64_t)b * ntiles + tile) * kTile;
   if (compact) {
-    // straight to the staging position from the registers (one 12-byte store per winner; the
-    // tile's region stays in L2)
+    // placed at their tile-local positions in LDS, then written out in order as 16-byte vectors
+    // (whole cache lines instead of one scattered 12-byte store per winner)
 #pragma unroll
     for (int i = 0; i < kPerT; ++i) {
       if (ebr[i] != 0xFFFFFFFFu) {
         const int p = s_off[ebr[i] & 0x7FFu] + (int)(ebr[i] >> 11);
-        st[p] = make_uint3((uint32_t)a_t + eid[i], ~eo[i], __float_as_uint(ew[i]));
+        s_r01[3 * p] = (uint32_t)a_t + eid[i];
+        s_r01[3 * p + 1] = ~eo[i];
+        s_r01[3 * p + 2] = __float_as_uint(ew[i]);
       }
+    }
+    __syncthreads();
+    {
+      const int nw = 3 * tot, nv = nw >> 2;
+      uint4* sv = reinterpret_cast<uint4*>(st);
+      const uint4* lv = reinterpret_cast<const uint4*>(s_r01);
+      for (int v = tid; v < nv; v += kGrpNT) sv[v] = lv[v];
+      uint32_t* sw = reinterpret_cast<uint32_t*>(st);
+      if (tid < nw - 4 * nv) sw[4 * nv + tid] = s_r01[4 * nv + tid];
     }
     PROF(4)
     PROF(5)

@@ -347,6 +347,10 @@ def main():
     ap.add_argument("--strong", action="store_true",
                     help="columns split: --batch is the GLOBAL batch (batch/P rollouts per GPU) instead of per GPU")
     ap.add_argument("--assemble", default="best", choices=["best", "all", "none"])
+    ap.add_argument("--pipeline", action=argparse.BooleanOptionalAction, default=True,
+                    help="one GPU: consecutive steps on two alternating stream lanes, step k+1's policy and "
+                         "select beside step k's sort, fill and padding (GFlowNet(pipeline=True); every step "
+                         "still does all of its work; --no-pipeline: one step after the other)")
     ap.add_argument("--side", default="auto", choices=["auto", "AM", "MA"],
                     help="reward side: ||AM - I|| (the north star's column SPAI) or ||MA - I|| (the reference's "
                          "calculate_residual); auto: MA for c2lu (the driver's configuration), else AM")
@@ -429,7 +433,8 @@ def main():
     split = {"columns": "columns", "slices": "slices"}.get(shard) if dist_on else None
     model = GFlowNet(make_policy(env, P, dev), None, env, mode="throughput", seed=1234, sample_base=base,
                      shard=(rank, world, None) if split else None, split=split or "columns",
-                     overlap=False if args.overlap == "none" else args.overlap)
+                     overlap=False if args.overlap == "none" else args.overlap,
+                     pipeline=args.pipeline and not dist_on)
     s0 = [P] * bl
     assembled = {}
     do_assemble = [args.assemble != "none" and dist_on and shard != "candidates"]
@@ -504,10 +509,12 @@ def main():
                 gather.wait()  # no RCCL gather in flight while a graph is captured
             # capture every maximal run of collective-free phases as one HIP graph (one GPU: the
             # whole step is one graph); the collectives run eagerly between the replays
+            model.pipeline_join()
             side = torch.cuda.Stream(dev)
             side.wait_stream(torch.cuda.current_stream(dev))
             with torch.cuda.stream(side):
                 eager_step()
+                model.pipeline_join()
             torch.cuda.current_stream(dev).wait_stream(side)
             barrier()
             st = {"s0": s0}
@@ -530,6 +537,7 @@ def main():
                 with torch.cuda.graph(g, pool=gp, capture_error_mode="thread_local" if dist_on else "global"):
                     for f, _k in run:
                         f(st)
+                    model.pipeline_join()  # (a pipelined step's lanes rejoin inside its capture)
                 if kind != "side":
                     pool = g.pool()
                 if kind == "side":
@@ -595,11 +603,13 @@ def main():
                 spg -= 1
             if spg > 1:
                 gm = torch.cuda.CUDAGraph()
+                model.pipeline_join()
                 with torch.cuda.graph(gm, pool=pool):
                     for _ in range(spg):
                         stm = {"s0": s0}
                         for f, _c in phases:
                             f(stm)
+                    model.pipeline_join()  # --pipeline: consecutive steps overlap inside the graph
                 mlog = stm["log"]
                 gm.replay()
         else:
@@ -705,6 +715,7 @@ def main():
             "ms_per_step_without_assembly": dt_noasm * 1e3,
             "graph": use_graph,
             "steps_per_graph": spg,
+            "pipeline": bool(args.pipeline and not dist_on),
             "ms_per_step_eager": dt_eager * 1e3,
             "final_residual_fro": float(res[0]),
             "final_residual_fro_mean": float(res.mean()),

@@ -29,7 +29,7 @@ from .preconditioner import Data
 class GFlowNet(nn.Module):
     def __init__(self, forward_policy, backward_policy, env, *, mode: str = "parity", seed: int | None = None,
                  sample_base: int = 0, shard: tuple | None = None, split: str | None = None,
-                 overlap: bool | str = "sort"):
+                 overlap: bool | str = "sort", pipeline: bool = False):
         super().__init__()
         if mode not in ("parity", "throughput"):
             raise ValueError("mode must be 'parity' or 'throughput'")
@@ -54,6 +54,14 @@ class GFlowNet(nn.Module):
             raise ValueError("overlap must be False, True, 'sort', 'fill' or 'select'")
         self.overlap = "sort" if overlap is True else overlap
         self._side = None
+        # pipeline=True (one GPU, throughput mode, a fixed policy): consecutive steps alternate
+        # between two stream lanes, and step k+1 waits only for step k's select phase (the Philox
+        # stream counter it advances), so its policy and select run beside step k's sort, fill and
+        # padding.  Every step still does all of its work, in the same order within the step, on
+        # buffers of its own lane.  The lanes are forked from the caller's stream once; results are
+        # complete after pipeline_join() (or a device synchronisation).
+        self.pipeline = bool(pipeline)
+        self._pl = None
         # (rank, world, group): the multi-GPU split of DESIGN.md §6 (throughput mode)
         #   split="columns": rank r rolls out its own len(s0) candidates (global sample ids
         #     sample_base + r*len(s0) ..), one all_to_all ships each rank the bitmap words of its
@@ -282,7 +290,7 @@ class GFlowNet(nn.Module):
         issued (the select phase, and with overlap="sort" the trajectory sort's launch) — or, with
         overlap="select", after the select phase only (its event), though issued after the sort."""
         dev = st["lg"].device
-        side = self._side_stream(dev)
+        side = st["lane"][1] if "lane" in st else self._side_stream(dev)
         ev = st.pop("select_done", None)
         if ev is not None:
             side.wait_event(ev)
@@ -318,7 +326,58 @@ class GFlowNet(nn.Module):
         self._begin(st)
         return st
 
+    def _lane(self, dev):
+        """The pipelined step's lane: (stream, side stream), alternating per step, forked from the
+        caller's stream (under graph capture only lanes that carry work are forked and joined)."""
+        pl = self._pl
+        if pl is None or pl["dev"] != dev:
+            mk = lambda: torch.cuda.Stream(dev, priority=-1)  # (own hardware queues: see _side_stream)
+            pl = self._pl = {"dev": dev, "lanes": [(mk(), mk()), (mk(), mk())], "i": 0, "sel": None, "used": []}
+        p = pl["i"]
+        pl["i"] ^= 1
+        lane = pl["lanes"][p]
+        # every dependency between lanes goes through the caller's stream: it waits for the previous
+        # step's select, and the lane forks from it (HIP's stream capture crashed on lanes waiting
+        # on each other's events directly, scripts/pipeline_capture_diag.py); the caller's stream
+        # carries no work of its own in between, so the lanes still overlap
+        cur = torch.cuda.current_stream(dev)
+        if pl["sel"] is not None:
+            cur.wait_event(pl["sel"])
+        lane[0].wait_stream(cur)
+        if p not in pl["used"]:
+            pl["used"].append(p)
+        return lane
+
+    def pipeline_join(self) -> None:
+        """The caller's stream waits for every pipelined step issued so far (required before a
+        graph capture ends and before the host reads a pipelined step's results)."""
+        pl = self._pl
+        if pl is None:
+            return
+        cur = torch.cuda.current_stream(pl["dev"])
+        for p in pl["used"]:  # (each step joins its fill's side stream into its lane)
+            cur.wait_stream(pl["lanes"][p][0])
+        pl["used"] = []
+        pl["sel"] = None
+
     def _begin(self, st: dict) -> None:
+        if self.pipeline and self.mode == "throughput" and self.shard is None:
+            ln, sd = self._lane(torch.device(self.env.device))  # (after the previous step's select: the
+            pl = self._pl                                         # stream counter it advances)
+            # (no second-level fork: HIP's stream capture fails on a stream forked from a forked stream
+            # — scripts/pipeline_capture_diag.py — so a lane runs its fill after its sort, in order,
+            # and the concurrency comes from the other lane's step)
+            st["lane"] = (ln, sd)
+            st["no_fork"] = True
+            with torch.cuda.stream(ln):
+                self._begin_body(st)
+                ev = torch.cuda.Event()
+                ev.record(ln)
+                pl["sel"] = ev
+            return
+        self._begin_body(st)
+
+    def _begin_body(self, st: dict) -> None:
         env, s0 = self.env, st["s0"]
         B = len(s0)
         E = env.num_actions - 1
@@ -331,7 +390,9 @@ class GFlowNet(nn.Module):
         st.update(B=B, E=E, logits=logits, alpha=alpha, lg=lg, lmax=lmax, removed=removed, counts=counts, ws=ws,
                   part=(rank, world, group))
         if world == 1:  # all lines here: fill, exact sums and rewards (one launch after the fill)
-            if self.overlap == "fill":
+            if st.get("no_fork"):
+                st["fill_after_sort"] = "inline"
+            elif self.overlap == "fill":
                 # the fill needs only the removal bitmaps and the sort only the staged records: the
                 # fill + rewards run on a second stream beside rollout_sort / rollout_finish (under
                 # HIP-graph capture: two parallel branches), joined in _end
@@ -364,13 +425,23 @@ class GFlowNet(nn.Module):
         return st["log"]
 
     def _end(self, st: dict) -> None:
+        if "lane" in st:
+            with torch.cuda.stream(st["lane"][0]):
+                self._end_body(st)
+            return
+        self._end_body(st)
+
+    def _end_body(self, st: dict) -> None:
         env = self.env
         rank, world, group = st["part"]
         B, E, lg, lmax, counts, ws = st["B"], st["E"], st["lg"], st["lmax"], st["counts"], st["ws"]
         if world > 1:  # counts, T and the bucket positions need every part's buckets
             kernels.rollout_merge(lg, B, lmax, ws, rank, world, counts)
         actions, fwd = kernels.rollout_sort(lg, B, lmax, ws, rank, world)
-        if st.pop("fill_after_sort", False):
+        fas = st.pop("fill_after_sort", False)
+        if fas == "inline":  # (pipelined lane: the fill in order after the sort)
+            st["rewards"] = env.fill_rewards(st["removed"], st["counts"], st["alpha"])
+        elif fas:
             self._fork_fill(st)
         t_dev = kernels.rollout_finish(lg, B, lmax, counts, ws, actions, fwd, rank, world)
         if "join" in st:  # the fill's stream (rollout_begin) rejoins before anything reads its outputs

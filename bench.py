@@ -30,6 +30,7 @@ rank 0.
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config c4|c2|c3] [--batch B]
 """
 import argparse
+import contextlib
 import json
 import math
 import os
@@ -444,14 +445,15 @@ def main():
     from gflownet_spai_amd.distributed import LineGather
     gather = LineGather(n, align=LINE_ALIGN) if do_assemble[0] else None
 
-    def assemble(log):
+    def assemble(log, m=None):
         if not do_assemble[0]:
             return
+        if m is None:
+            m = env.last_m  # columns: [B, this shard's lines, W] of EVERY candidate; slices: the same B on every rank
         if shard == "samples":  # global rewards everywhere, the best candidate's M on rank 0
             from gflownet_spai_amd.distributed import select_best_samples
-            assembled["r"], assembled["best"], assembled["m"] = select_best_samples(log.rewards, env.last_m)
+            assembled["r"], assembled["best"], assembled["m"] = select_best_samples(log.rewards, m)
             return
-        m = env.last_m  # columns: [B, this shard's lines, W] of EVERY candidate; slices: the same B on every rank
         if args.assemble == "best":  # the candidate with the highest reward: the preconditioner kept
             gather.start(m, rows=torch.argmax(log.rewards_all).view(1))
         else:
@@ -517,84 +519,128 @@ def main():
                 model.pipeline_join()
             torch.cuda.current_stream(dev).wait_stream(side)
             barrier()
-            st = {"s0": s0}
-            program, pool, run = [], None, []
-            cur = torch.cuda.current_stream(dev)
+            # --pipeline with a split (columns): two copies of the step's program, each captured on its
+            # own stream with its own buffers and memory pool, replayed alternately on two stream
+            # lanes; step k+1 waits only for step k's select (the Philox stream counter), so its
+            # select and bitmap pack run beside step k's exchange, fill and reductions.  The
+            # collectives stay eager and are issued in the same order on every rank.
+            xpipe = dist_on and args.pipeline and split is not None
 
-            def capture(run):
-                """One graph of consecutive device phases; its program entry keeps the first phase's
-                stream order (kind "side": replayed on the model's side stream, forked from the
-                current one; "join": after the side stream's work)."""
-                nonlocal pool
-                kind = run[0][1]
-                g = torch.cuda.CUDAGraph()
-                if dist_on:  # no collective of the previous eager phase still in flight on RCCL's stream
-                    torch.cuda.synchronize()
-                # a side segment runs beside later main segments: its own memory pool (graphs that
-                # share a pool may reuse each other's freed blocks, safe only when replayed in order)
-                gp = None if kind == "side" else pool
-                # thread_local: a HIP call from an RCCL helper thread cannot invalidate this capture
-                with torch.cuda.graph(g, pool=gp, capture_error_mode="thread_local" if dist_on else "global"):
-                    for f, _k in run:
-                        f(st)
-                    model.pipeline_join()  # (a pipelined step's lanes rejoin inside its capture)
-                if kind != "side":
-                    pool = g.pool()
-                if kind == "side":
-                    sstream = model._side_stream(dev)
+            def build(st, cs):
+                program, pool_, run = [], [None], []
 
-                    def rep():
-                        sstream.wait_stream(cur)
-                        with torch.cuda.stream(sstream):
+                def capture(run):
+                    """One graph of consecutive device phases; its program entry keeps the first phase's
+                    stream order (kind "side": replayed on the model's side stream, forked from the
+                    current one; "join": after the side stream's work)."""
+                    kind = run[0][1]
+                    g = torch.cuda.CUDAGraph()
+                    if dist_on:  # no collective of the previous eager phase still in flight on RCCL's stream
+                        torch.cuda.synchronize()
+                    # a side segment runs beside later main segments: its own memory pool (graphs that
+                    # share a pool may reuse each other's freed blocks, safe only when replayed in order)
+                    gp = None if kind == "side" else pool_[0]
+                    # thread_local: a HIP call from an RCCL helper thread cannot invalidate this capture
+                    with torch.cuda.graph(g, pool=gp, stream=cs,
+                                          capture_error_mode="thread_local" if dist_on else "global"):
+                        for f, _k in run:
+                            f(st)
+                        model.pipeline_join()  # (a pipelined step's lanes rejoin inside its capture)
+                    if kind != "side":
+                        pool_[0] = g.pool()
+                    if kind == "side":
+                        sstream = model._side_stream(dev)
+
+                        def rep():
+                            sstream.wait_stream(torch.cuda.current_stream(dev))
+                            with torch.cuda.stream(sstream):
+                                g.replay()
+                        return rep
+                    if kind == "join":
+                        sstream = model._side_stream(dev)
+
+                        def rep():
+                            torch.cuda.current_stream(dev).wait_stream(sstream)
                             g.replay()
-                    return rep
-                if kind == "join":
-                    sstream = model._side_stream(dev)
+                        return rep
+                    return g.replay
 
-                    def rep():
-                        cur.wait_stream(sstream)
-                        g.replay()
-                    return rep
-                return g.replay
+                # segments: maximal runs of device phases, cut at every collective, around every "side"
+                # phase and before every "join" phase
+                for fn, kind in phases + [(None, True)]:
+                    if fn is not None and kind is not True and kind != "side" and not (kind == "join" and run):
+                        run.append((fn, kind))
+                        continue
+                    if run:
+                        program.append(("graph:" + "+".join(f.__name__.strip("_") for f, _k in run), capture(run)))
+                        run = []
+                    if fn is None:
+                        break
+                    if kind is True:
+                        fn(st)  # a collective, eagerly (allocates its persistent buffers before the next capture)
+                        program.append((fn.__name__.strip("_"), lambda f=fn, st=st: f(st)))
+                    elif kind == "side":
+                        program.append(("graph(side):" + fn.__name__.strip("_"), capture([(fn, kind)])))
+                    else:  # "join" opens the next segment
+                        run.append((fn, kind))
+                return program, pool_[0]
 
-            # segments: maximal runs of device phases, cut at every collective, around every "side"
-            # phase and before every "join" phase
-            for fn, kind in phases + [(None, True)]:
-                if fn is not None and kind is not True and kind != "side" and not (kind == "join" and run):
-                    run.append((fn, kind))
-                    continue
-                if run:
-                    program.append(("graph:" + "+".join(f.__name__.strip("_") for f, _k in run), capture(run)))
-                    run = []
-                if fn is None:
-                    break
-                if kind is True:
-                    fn(st)  # a collective, eagerly (allocates its persistent buffers before the next capture)
-                    program.append((fn.__name__.strip("_"), lambda f=fn: f(st)))
-                elif kind == "side":
-                    program.append(("graph(side):" + fn.__name__.strip("_"), capture([(fn, kind)])))
-                else:  # "join" opens the next segment
-                    run.append((fn, kind))
-            glog = st["log"]
+            progs = []
+            for bt in (["A", "B"] if xpipe else [""]):
+                stp = {"s0": s0, "bt": bt}
+                program, pool = build(stp, torch.cuda.Stream(dev) if xpipe else None)
+                # (this program's Log, M and residual: what its replays write)
+                progs.append({"program": program, "log": stp["log"], "m": env.last_m, "res": env.last_residual,
+                              "lane": torch.cuda.Stream(dev, priority=-1) if xpipe else None})
+            glog = progs[0]["log"]
+            pstate = {"i": 0, "sel": None, "last": progs[0], "pending": None}
 
             def step(host=None):
-                for name, p in program:
-                    if host is None:
-                        p()
-                    else:  # host issue time per program entry (diagnostic pass)
-                        t = time.perf_counter()
-                        p()
-                        host.setdefault(name, []).append(time.perf_counter() - t)
-                if host is None:
-                    assemble(glog)
-                else:
-                    t = time.perf_counter()
-                    assemble(glog)
+                pr = progs[pstate["i"]]
+                pstate["i"] = (pstate["i"] + 1) % len(progs)
+                ln = pr["lane"]
+                ctx = contextlib.nullcontext()
+                if ln is not None:  # fork the lane after the previous step's select (via the caller's stream)
+                    c = torch.cuda.current_stream(dev)
+                    if pstate["sel"] is not None:
+                        c.wait_event(pstate["sel"])
+                    ln.wait_stream(c)
+                    ctx = torch.cuda.stream(ln)
+                with ctx:
+                    for i, (name, p) in enumerate(pr["program"]):
+                        if host is None:
+                            p()
+                        else:  # host issue time per program entry (diagnostic pass)
+                            t = time.perf_counter()
+                            p()
+                            host.setdefault(name, []).append(time.perf_counter() - t)
+                        if ln is not None and i == 0:  # the select phase: what the next step waits for
+                            ev = torch.cuda.Event()
+                            ev.record(ln)
+                            pstate["sel"] = ev
+                t = time.perf_counter()
+                if ln is None:
+                    with ctx:
+                        assemble(pr["log"], pr["m"])
+                else:  # the PREVIOUS step's M gather, on its own lane after this step's program: RCCL runs
+                    # its collectives in issue order, so this step's bitmap all_to_all goes first
+                    flush_assemble()
+                    pstate["pending"] = pr
+                if host is not None:
                     host.setdefault("assemble", []).append(time.perf_counter() - t)
-                return glog
+                pstate["last"] = pr
+                return pr["log"]
+
+            def flush_assemble():
+                pr = pstate.get("pending")
+                if pr is not None:
+                    with torch.cuda.stream(pr["lane"]):
+                        assemble(pr["log"], pr["m"])
+                    pstate["pending"] = None
 
             for _ in range(max(1, args.warmup)):
                 log = step()
+            flush_assemble()
             # a step without collectives (one GPU): spg consecutive steps in ONE graph, so the
             # ~12 us between two graph launches is paid once per spg steps (every step is still a
             # whole sample_states: its own select, sort, fill and Log, its own Philox stream id)
@@ -616,6 +662,9 @@ def main():
             step = eager_step
             spg = 1
 
+            def flush_assemble():
+                pass
+
         def steps(k):  # k timed steps: the remainder as single steps, then whole multi-step graphs
             out = None
             if spg > 1:
@@ -632,14 +681,16 @@ def main():
         barrier()
         t0 = time.perf_counter()
         log = steps(args.steps)
+        flush_assemble()
         if gather is not None:
             gather.wait()
         barrier()
         dt = (time.perf_counter() - t0) / args.steps
         dt_noasm = dt
         if args.dump and rank == 0:  # the last timed step: its stream id, every candidate's reward, M
+            res = pstate["last"]["res"] if use_graph and spg == 1 else env.last_residual
             dump = {"stream_id": model.rollouts - 1, "rewards_all": log.rewards_all.double().cpu(),
-                    "residual": env.last_residual.double().cpu(), "shard": shard, "world": world}
+                    "residual": res.double().cpu(), "shard": shard, "world": world}
             if gather is not None and args.assemble != "none":
                 dump["m_assembled"] = gather.result().cpu()
             torch.save(dump, args.dump)
@@ -648,6 +699,7 @@ def main():
             barrier()
             t0 = time.perf_counter()
             log = steps(args.steps)
+            flush_assemble()
             barrier()
             dt_noasm = (time.perf_counter() - t0) / args.steps
             do_assemble[0] = True
@@ -656,6 +708,7 @@ def main():
             host = {}
             for _ in range(k_eager):
                 step(host)
+            flush_assemble()
             if gather is not None:
                 gather.wait()
             barrier()
@@ -715,7 +768,7 @@ def main():
             "ms_per_step_without_assembly": dt_noasm * 1e3,
             "graph": use_graph,
             "steps_per_graph": spg,
-            "pipeline": bool(args.pipeline and not dist_on),
+            "pipeline": bool(args.pipeline and (not dist_on or split is not None)),
             "ms_per_step_eager": dt_eager * 1e3,
             "final_residual_fro": float(res[0]),
             "final_residual_fro_mean": float(res.mean()),

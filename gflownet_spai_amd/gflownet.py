@@ -465,7 +465,7 @@ class GFlowNet(nn.Module):
         words = (E + 31) // 32
         logits, alpha, lg, lmax, _ = self._logits(s0, defer_max=True)
         dev = lg.device
-        sel = self._buf("select", (bl * words + bl,), torch.int32, dev)
+        sel = self._buf("select" + st.get("bt", ""), (bl * words + bl,), torch.int32, dev)
         removed, counts, ws = kernels.rollout_select(lg, bl, lmax, self.seed, 0, self.sample_base + rank * bl,
                                                      self._counter(dev), out=sel)
         if isinstance(lmax, kernels.PendingMax):
@@ -477,9 +477,9 @@ class GFlowNet(nn.Module):
         rank, world, _ = st["part"]
         bl, dev = st["B"], st["dev"]
         plan = self.env.pack_plan(world)
-        send = self._buf("send", (plan.send_words(bl),), torch.int32, dev)
+        send = self._buf("send" + st.get("bt", ""), (plan.send_words(bl),), torch.int32, dev)
         kernels.bitmap_pack(st["removed"], st["counts"], plan, out=send)  # line-major packed bits per destination
-        recv = self._buf("recv", (world * bl, plan.wq[rank] + 1), torch.int32, dev)
+        recv = self._buf("recv" + st.get("bt", ""), (world * bl, plan.wq[rank] + 1), torch.int32, dev)
         st.update(send=send, recv=recv, plan=plan)
 
     def _c_send(self, st: dict) -> None:

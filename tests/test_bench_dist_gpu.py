@@ -56,3 +56,37 @@ def test_bench_columns_step_under_rccl_matches_one_gpu(tmp_path, fill):
     assert torch.equal(genv.last_residual.double().cpu(), d["residual"])
     best = int(torch.argmax(log.rewards_all))
     assert torch.equal(genv.last_m[best].cpu(), d["m_assembled"][0])
+
+
+def test_bench_columns_two_ranks_gloo_pipelined_matches_one_gpu(tmp_path):
+    """The multi-rank flow of the driver's scaling run on the one GPU: two ranks (gloo,
+    host-staged collectives, both on GPU 0), the columns split with its two alternating graph
+    programs (--pipeline, the default) and the deferred M gather.  Rank 0 dumps the last timed
+    step: every one of the 2 x 8 candidates' rewards and the assembled best M must equal one GPU
+    rolling out all 16 candidates at that stream id, bit for bit."""
+    dump = tmp_path / "cols2.pt"
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--config", "c2", "--gpus", "2", "--backend", "gloo",
+           "--share-gpu", "--steps", "4", "--warmup", "1", "--no-cpu-baseline", "--dump", str(dump)]
+    r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    import json
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["world_size"] == 2 and line["pipeline"] is True
+    d = torch.load(dump, weights_only=True)
+    assert d["shard"] == "columns" and d["world"] == 2
+
+    sys.path.insert(0, ROOT)
+    import bench
+    from gflownet_spai_amd import GFlowNet, PreconditionerEnv
+    A, P = bench.config_matrices("c2")
+    n = A.shape[0]
+    dev = torch.device("cuda", 0)
+    genv = PreconditionerEnv(n, P, A, side="AM", fill="qr", keep_m=True, device=dev)
+    with torch.no_grad():
+        model = GFlowNet(bench.make_policy(genv, P, dev), None, genv, mode="throughput", seed=1234)
+        model.rollouts = int(d["stream_id"])
+        log = model.sample_states([P] * 16, return_log=True)
+    assert torch.equal(log.rewards_all.double().cpu(), d["rewards_all"])
+    best = int(torch.argmax(log.rewards_all))
+    assert torch.equal(genv.last_m[best].cpu(), d["m_assembled"][0])

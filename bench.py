@@ -22,8 +22,13 @@ torch.distributed.run), DESIGN.md §6:
       rewards and one reduce of the best candidate's M to rank 0.
   --shard candidates (weak scaling): --batch candidates per rank, no collective.
 The timed steps replay HIP graphs of every maximal run of collective-free phases
-(GFlowNet.rollout_phases; one GPU: one graph per step), the collectives run eagerly between
-them; the Philox stream id lives on the device, so every replay draws a fresh rollout.  The
+(GFlowNet.rollout_phases; one GPU: up to --steps-per-graph whole steps per graph), the
+collectives run eagerly between them; the Philox stream id lives on the device, so every replay
+draws a fresh rollout.  --pipeline (default): consecutive steps alternate between two stream
+lanes and step k+1 waits only for step k's select, so its policy and select run beside step k's
+sort, fill and padding (one GPU: GFlowNet(pipeline=True); the columns split: two copies of its
+program with their own buffers); every step still does all of its work, with the same bits as
+steps run one after the other (tests/test_pipeline_gpu.py, tests/test_bench_dist_gpu.py).  The
 per-phase HIP-event timings come from an eager pass of the same step.  Prints ONE JSON line on
 rank 0.
 
